@@ -1,0 +1,226 @@
+"""Headline benchmark: GP posterior + acquisition grid-points/sec at N training points.
+
+One "step" = one planning tick over this rank's shard of the grid (SURVEY.md
+3.1 without ROS): the fused predictive sweep (K* generated in registers,
+V = sf2 L^-1 K*^T on f32 MFMA, mean alongside), ComputeSets in f64, the masked
+argmax of the confidence width over the safe set, and the cross-rank key
+reduction (one RCCL all-gather of 16-byte keys when N > 1).  Inputs (query
+coordinates) are resident in HBM before timing starts; mu/sd/lo/hi/S are
+written to HBM every step.  The fit (RBF fill + rocSOLVER potrf + strtri +
+operand pack) runs once, replicated on every rank, and is reported separately.
+
+Default workload = BASELINE.json configs[3] (C4: N=16384, 1000x1000 grid),
+the north-star target size, on 1 GPU; with --gpus P the same 10^6-point grid
+is split into P contiguous row blocks (strong scaling).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4]
+  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--config", default="C4", choices=["C2", "C3", "C4"])
+    p.add_argument("--n", type=int, default=None, help="override N")
+    p.add_argument("--grid", type=int, default=None, help="override grid side")
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-outputs", action="store_true", help="skip writing mu/sd/lo/hi/S (argmax only)")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    from safe_bayesian_optimization_amd import TerrainMapper, synthetic
+    from safe_bayesian_optimization_amd import _native as N
+    from safe_bayesian_optimization_amd.dist import allreduce_key, shard_range
+    from safe_bayesian_optimization_amd.terrain import CONFIGS
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n, gw, gh = CONFIGS[a.config]
+    if a.n:
+        n = a.n
+    if a.grid:
+        gw = gh = a.grid
+    wl = synthetic(n, gw, gh, seed=0, name=a.config)
+    m_total = wl.qx.size
+    if a.scaling == "weak":
+        lo, hi = 0, m_total
+        m_all = m_total * world
+    else:
+        lo, hi = shard_range(m_total, rank, world)
+        m_all = m_total
+    m = hi - lo
+
+    stream = torch.cuda.current_stream(dev)
+    gm = TerrainMapper(local, wl.hyper)
+    gm.ctx.set_stream(stream)
+    lib = N.lib()
+
+    f32 = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
+    X, Y, OBS = f32(wl.x), f32(wl.y), f32(wl.obs)
+    qx, qy = f32(wl.qx[lo:hi]), f32(wl.qy[lo:hi])
+    if a.no_outputs:
+        outs = {}
+    else:
+        outs = dict(mu=torch.empty(m, dtype=torch.float32, device=dev), sd=torch.empty(m, dtype=torch.float32, device=dev),
+                    lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
+                    safe=torch.empty(m, dtype=torch.uint8, device=dev))
+    key = torch.empty(2, dtype=torch.int64, device=dev)
+
+    # ---- fit (replicated), timed separately; fill roofline from HIP events
+    lib.sbo_profile(gm.ctx.handle, 1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gm.fit(X, Y, OBS)
+    torch.cuda.synchronize()
+    fit_ms = (time.perf_counter() - t0) * 1e3
+    import ctypes
+    pm, pl, fm, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_int64()
+    lib.sbo_profile_read(gm.ctx.handle, ctypes.byref(pm), ctypes.byref(pl), ctypes.byref(fm), ctypes.byref(fl))
+    fill_ms = fm.value / max(fl.value, 1)
+    fill_bytes = 4.0 * n * n + 8.0 * n
+
+    def step():
+        gm.tick(qx, qy, wl.beta, wl.f_min, score=N.SCORE_WIDTH, index_offset=lo, outputs=outs, key_out=key,
+                async_=True)
+        return allreduce_key(key)
+
+    for _ in range(a.warmup):
+        step()
+    lib.sbo_profile(gm.ctx.handle, 1)   # reset: time only the K measured launches
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    best = None
+    for _ in range(a.steps):
+        best = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lib.sbo_profile_read(gm.ctx.handle, ctypes.byref(pm), ctypes.byref(pl), ctypes.byref(fm), ctypes.byref(fl))
+    lib.sbo_profile(gm.ctx.handle, 0)
+    pred_ms = pm.value / max(pl.value, 1)
+    if world > 1:
+        t = torch.tensor([elapsed, pred_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, pred_ms_max = float(t[0]), float(t[1])
+    else:
+        pred_ms_max = pred_ms
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = elapsed * 1e3 / a.steps
+    value = m_all * a.steps / elapsed
+    flops_launch = float(n) * float(n) * m          # N^2 flop per grid point
+    achieved = flops_launch / (pred_ms * 1e-3) / 1e12
+    fill_gbs = fill_bytes / (fill_ms * 1e-3) / 1e9 if fill_ms > 0 else None
+
+    cpu = None
+    if world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(gm, wl, a.cpu_seconds)
+
+    line = {
+        "metric": "GP posterior+acq grid-points/sec at N train pts; 1/2/4/8 GPU",
+        "value": value,
+        "unit": "grid-points/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": a.scaling,
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SplitMix64 smooth field + N(0,sn2) noise, BASELINE configs, no terrain.csv)",
+        "config": {"workload": a.config, "n_train": n, "grid": [gw, gh], "M": m_total,
+                   "M_per_rank": m, "beta": wl.beta, "f_min": round(wl.f_min, 6),
+                   "hyper": [wl.hyper.length_scale, wl.hyper.sigma_f, wl.hyper.noise_level],
+                   "parallelism": f"m-shard{world}" if world > 1 else "single", "outputs_written": not a.no_outputs},
+        "roofline": {"kernel": "predict_kernel (V = sf2 L^-1 K*^T, f32 MFMA 32x32x2)", "bound": "mfma",
+                     "achieved": achieved, "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_F32_MFMA_TFLOPS, "traffic": None,
+                     "avg_launch_ms": pred_ms, "max_rank_launch_ms": pred_ms_max,
+                     "algorithmic_flops_per_launch": flops_launch},
+        "fill_roofline": {"kernel": "rbf_fill_kernel", "bound": "hbm", "achieved": fill_gbs, "peak": PEAK_HBM_GBS,
+                          "unit": "GB/s", "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None,
+                          "avg_launch_ms": fill_ms, "algorithmic_bytes": fill_bytes},
+        "fit_ms": fit_ms,
+        "argmax": {"index": best[1], "score": best[0]},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(gm, wl, budget_s):
+    """The oracle's f32 predictive path (blocked TRSM, OpenMP) + ComputeSets +
+    argmax on a contiguous sample of the grid, given the device factor; points/s
+    extrapolated linearly (the M axis is embarrassingly parallel)."""
+    from oracle import oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    O.set_threads(threads)
+    L, alpha = gm.factor()
+    Lcm = np.ascontiguousarray(L.T)          # column-major buffer of the lower factor
+    del L
+    h = wl.hyper
+    x, y = wl.x.astype(np.float32), wl.y.astype(np.float32)
+
+    def run(k):
+        qx = wl.qx[:k].astype(np.float32)
+        qy = wl.qy[:k].astype(np.float32)
+        t0 = time.perf_counter()
+        mu, var = O.predict_f32(Lcm, alpha, x, y, qx, qy, h.length_scale, h.sf2, h.prior_mean)
+        lo_, hi_, s_ = O.compute_sets(mu, np.sqrt(np.maximum(var, 0)), wl.beta, wl.f_min)
+        O.argmax(hi_ - lo_, s_)
+        return time.perf_counter() - t0
+
+    k = 64 * threads
+    t = run(k)
+    k2 = int(min(wl.qx.size, max(k, k * max(budget_s - t, 0.0) / max(t, 1e-6))))
+    k2 = max(64, (k2 // 64) * 64)
+    t2 = run(k2)
+    return {"value": k2 / t2, "unit": "grid-points/s", "cores": threads, "kind": "port",
+            "sample": f"{k2} contiguous grid points of {wl.name} (N={wl.x.size}), f32 blocked TRSM predictive + "
+                      f"ComputeSets + argmax, given the device L/alpha; {t2:.1f} s wall"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,190 @@
+/*
+ * sbo.h -- C ABI of the MI355X safe-BO planning-tick library (libsbo.so).
+ *
+ * The reference has no plugin/FFI API for this path.  Its
+ * boundary is (i) the GetTerrainMapWithUncertainty service between the
+ * external GP mapper and the node, consumed at
+ * src/safe_bayesian_optimization_node.cpp:576-647 (request resolution[2] f32
+ * :580-581; response success, message, n_width_cells, n_height_cells,
+ * x_coords[], y_coords[], values[] (= mu), uncertainties[] (= sigma)
+ * :606-644), and (ii) the node's private calls ComputeSets() (:399-416),
+ * FindSafetyContourIndices() (:418-497) and GetNextSubgoal() (:499-550).
+ * Each entry point below names the reference interface it replaces.
+ *
+ * Conventions (mirroring the reference, :129-177, :503-506, :1503):
+ *   - the caller owns every buffer; no exceptions cross this boundary;
+ *   - one context per thread; a context is not thread-safe;
+ *   - calls are synchronous with respect to the context's HIP stream unless
+ *     SBO_ASYNC is passed (then results are ready when the stream drains);
+ *   - array pointers are host pointers unless SBO_DEVICE_PTRS is passed, in
+ *     which case EVERY array argument of that call is a device pointer;
+ *   - coordinates are SoA (all x, then all y), like the column-major
+ *     Eigen::Matrix<double,Dynamic,2> D_ (:132);
+ *   - "no subgoal" is -1 (:503-506).
+ */
+#ifndef SBO_H_
+#define SBO_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBO_API __attribute__((visibility("default")))
+
+typedef enum sbo_status {
+    SBO_OK = 0,
+    SBO_E_INVAL = 1,    /* bad argument (null pointer, n <= 0, bad hyper-parameter) */
+    SBO_E_NOT_SPD = 2,  /* rocSOLVER potrf info > 0: K not positive definite */
+    SBO_E_DEVICE = 3,   /* HIP / rocBLAS / rocSOLVER runtime error */
+    SBO_E_OOM = 4,      /* device allocation failed */
+    SBO_E_EMPTY = 5,    /* nothing to operate on (no fit yet, empty input) */
+    SBO_E_STATE = 6     /* call out of order (e.g. predict before fit) */
+} sbo_status;
+
+/* flags */
+#define SBO_DEVICE_PTRS 0x1u  /* all array arguments are device pointers */
+#define SBO_ASYNC 0x2u        /* do not synchronise the stream before returning */
+
+/* GP hyper-parameters (config/lpsc.yaml:35-37: noise_level 0.1,
+ * length_scale 0.4, sigma_f 1.0).  noise_level is a noise VARIANCE. */
+typedef struct sbo_hyper {
+    double length_scale;
+    double sigma_f;
+    double noise_level;
+    double prior_mean;
+} sbo_hyper;
+
+/* Acquisition score for the grid argmax (a10). */
+typedef enum sbo_score {
+    SBO_SCORE_WIDTH = 0,  /* Q(:,1) - Q(:,0), the width GetNextSubgoal ranks (:516) */
+    SBO_SCORE_UCB = 1     /* Q(:,1) = mu + beta*sigma */
+} sbo_score;
+
+/* Result of a masked argmax: highest score, lowest global index on ties.
+ * idx = -1 when no point is eligible.  Keys from different shards combine
+ * with sbo_key_combine (this is what crosses ranks). */
+typedef struct sbo_key {
+    double score;
+    int64_t idx;
+} sbo_key;
+
+typedef struct sbo_ctx sbo_ctx;
+
+/* Library / context ------------------------------------------------------ */
+SBO_API const char *sbo_version(void);
+SBO_API const char *sbo_status_string(sbo_status s);
+/* Replaces the node's service client (:75-77): binds a HIP device.  */
+SBO_API sbo_status sbo_create(int device, sbo_ctx **out);
+SBO_API void sbo_destroy(sbo_ctx *ctx);
+/* Run on the caller's HIP stream (hipStream_t), e.g. torch's current stream.
+ * NULL restores the context's own stream. */
+SBO_API sbo_status sbo_set_stream(sbo_ctx *ctx, void *hip_stream);
+SBO_API const char *sbo_last_error(const sbo_ctx *ctx);
+
+/* GP mapper (the external terrain_mapping_node, a1+a2) -------------------
+ * Fit the posterior to n measurements (x, y, obs): RBF fill (HIP kernel),
+ * rocSOLVER spotrf, alpha by spotrs, L^-1 by strtri, and packing of the
+ * predictive operand.  Replaces the mapper's fit behind the service. */
+SBO_API sbo_status sbo_fit(sbo_ctx *ctx, const float *x, const float *y, const float *obs,
+                           int64_t n, sbo_hyper hyper, uint32_t flags);
+
+/* Streaming update (C5): append b measurements with a block Cholesky update
+ * (L21 = K21 L11^-T, L22 = chol(K22 - L21 L21^T)), then re-solve alpha.
+ * Replaces a full re-fit on each spatial_data_size change (:552-566). */
+SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, const float *obs,
+                              int64_t b, uint32_t flags);
+
+/* Number of training points currently fitted (0 before sbo_fit). */
+SBO_API int64_t sbo_num_train(const sbo_ctx *ctx);
+
+/* Predict (a3+a4): posterior mean and latent std at m query points
+ * (the service's values[] and uncertainties[], :642-643).  mu/sd may be NULL
+ * to skip that output. */
+SBO_API sbo_status sbo_predict(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m,
+                               float *mu, float *sd, uint32_t flags);
+
+/* ComputeSets() (:399-416) == ComputeConfidenceIntervals + UpdateSafeSet:
+ *   c = beta*sd;  lo = mu - c;  hi = mu + c;  safe = lo > f_min
+ * evaluated in IEEE double exactly as the node's Eigen code (no FMA).
+ * lo/hi are Q_.col(0)/Q_.col(1) (f64), safe is S_ (1 byte per point). */
+SBO_API sbo_status sbo_compute_sets(sbo_ctx *ctx, const float *mu, const float *sd, int64_t m,
+                                    double beta, double f_min, double *lo, double *hi,
+                                    uint8_t *safe, uint32_t flags);
+
+/* Grid acquisition argmax (a10): argmax of score over mask (mask may be NULL),
+ * lowest index on ties, NaN never wins.  index_offset is added to local
+ * indices (the first global row of this rank's shard). */
+SBO_API sbo_status sbo_argmax(sbo_ctx *ctx, const double *score, const uint8_t *mask, int64_t m,
+                              int64_t index_offset, sbo_key *out, uint32_t flags);
+
+/* The whole planning tick on one shard of the grid, fused on the device:
+ * predict -> ComputeSets -> masked argmax of `score` over the safe set.
+ * Output arrays may be NULL to skip writing them (the key is always produced).
+ * This is the headline step measured by bench.py. */
+SBO_API sbo_status sbo_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m,
+                            double beta, double f_min, sbo_score score, int64_t index_offset,
+                            float *mu, float *sd, double *lo, double *hi, uint8_t *safe,
+                            sbo_key *out, uint32_t flags);
+
+/* Combine two shard keys (the cross-rank reduction of sbo_tick / sbo_argmax). */
+SBO_API sbo_key sbo_key_combine(sbo_key a, sbo_key b);
+
+/* Host-side node logic (no device needed) ---------------------------------
+ * FindSafetyContourIndices() (:418-497): rasterise safe into a
+ * height x width image with the node's int-truncated bounds, trace external
+ * contours (cv::findContours RETR_EXTERNAL, CHAIN_APPROX_NONE restated) and
+ * map contour pixels back to grid indices (last writer wins, duplicates kept).
+ * Dx/Dy are D_.col(0)/D_.col(1) (f64).  Writes at most out_cap indices,
+ * stores the total in *count; returns SBO_E_INVAL if out_cap was too small. */
+SBO_API sbo_status sbo_find_safety_contour_indices(const double *Dx, const double *Dy,
+                                                   const uint8_t *safe, int64_t m,
+                                                   int width_cells, int height_cells,
+                                                   int32_t *out, int64_t out_cap, int64_t *count);
+
+/* GetNextSubgoal() (:499-550): frontier, distance sort to the goal, top
+ * max(1, F/4), strict-> argmax of Q(:,1)-Q(:,0).  Returns the grid index or -1. */
+SBO_API int64_t sbo_next_subgoal(const double *Dx, const double *Dy, const double *lo,
+                                 const double *hi, const uint8_t *safe, int64_t m,
+                                 int width_cells, int height_cells, double goal_x, double goal_y);
+
+/* Raw border follower used by the frontier: img is height x width u8
+ * row-major; points (x,y) pairs; start[c]..start[c+1] bound contour c.
+ * Returns the number of contours, or -1 if a capacity was exceeded. */
+SBO_API int64_t sbo_find_contours_external(const uint8_t *img, int width, int height,
+                                           int32_t *pts, int64_t pts_cap,
+                                           int64_t *start, int64_t contours_cap);
+
+/* Staged-parity accessors (tests) ----------------------------------------
+ * RBF fill alone (a1): writes the n x n column-major K (lda = n). */
+SBO_API sbo_status sbo_rbf_fill(sbo_ctx *ctx, const float *x, const float *y, int64_t n,
+                                sbo_hyper hyper, float *K, uint32_t flags);
+/* Copy out the current factor L (n x n column-major, lower; upper part
+ * zeroed) and alpha (n). */
+SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t flags);
+
+/* Options.  SBO_OPT_INVERSE_BITS (32 | 64, default 64): precision in which
+ * L^-1 is computed before sf2 * L^-1 is rounded to f32 for the predictive
+ * sweep (64 = widen L, rocsolver_dtrtri; 32 = rocsolver_strtri).  Takes
+ * effect at the next sbo_fit / sbo_append. */
+#define SBO_OPT_INVERSE_BITS 1
+SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
+
+/* Test accessor: the packed predictive operand A = sf2 * L^-1 unpacked into a
+ * dense n x n ROW-major f32 host array (upper triangle left untouched). */
+SBO_API sbo_status sbo_get_inverse(sbo_ctx *ctx, float *Linv);
+
+/* Kernel timing (bench.py): when enabled, hipEvents are recorded on the
+ * context's stream around every predictive-sweep and RBF-fill launch.
+ * sbo_profile(ctx, 1) enables and resets; sbo_profile_read sums the elapsed
+ * device time of the launches recorded so far (it synchronises on them). */
+SBO_API sbo_status sbo_profile(sbo_ctx *ctx, int enable);
+SBO_API sbo_status sbo_profile_read(sbo_ctx *ctx, double *predict_ms, int64_t *predict_launches,
+                                    double *fill_ms, int64_t *fill_launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SBO_H_ */

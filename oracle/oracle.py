@@ -1,0 +1,218 @@
+"""ctypes front-end for the CPU oracle (``liboracle.so``).
+
+TEST INFRASTRUCTURE ONLY: the parity checker for the MI355X library.  Only
+``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of
+``bench.py`` import this module.  The product package never imports it.
+
+Every function restates a reference code path (see ``sbo_oracle.c`` for the
+file:line citations) or the GP math contract of SURVEY.md section 7.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+_i64 = ctypes.c_int64
+_dbl = ctypes.c_double
+
+
+def build() -> str:
+    """Compile liboracle.so in place (gcc only)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.orc_set_threads.argtypes = [ctypes.c_int]
+        L.orc_get_threads.restype = ctypes.c_int
+        L.orc_rbf_fill.argtypes = [_f64p, _f64p, _i64, _dbl, _dbl, _dbl, _f64p]
+        L.orc_rbf_fill_f32in.argtypes = [_f32p, _f32p, _i64, _dbl, _dbl, _dbl, _f64p]
+        L.orc_rbf_fill_f32.argtypes = [_f32p, _f32p, _i64, ctypes.c_float, ctypes.c_float,
+                                       ctypes.c_float, _f32p]
+        L.orc_cholesky.argtypes = [_f64p, _i64]
+        L.orc_cholesky.restype = _i64
+        L.orc_chol_solve.argtypes = [_f64p, _i64, _f64p, _f64p]
+        L.orc_predict.argtypes = [_f64p, _f64p, _f64p, _f64p, _i64, _dbl, _dbl, _dbl,
+                                  _f64p, _f64p, _i64, _f64p, _f64p]
+        L.orc_predict_f32.argtypes = [_f32p, _f32p, _f32p, _f32p, _i64, _dbl, _dbl, _dbl,
+                                      _f32p, _f32p, _i64, _f32p, _f32p]
+        L.orc_compute_sets.argtypes = [_f64p, _f64p, _i64, _dbl, _dbl, _f64p, _f64p, _u8p]
+        L.orc_argmax.argtypes = [_f64p, ctypes.c_void_p, _i64, ctypes.POINTER(_dbl)]
+        L.orc_argmax.restype = _i64
+        L.orc_find_contours_external.argtypes = [_u8p, ctypes.c_int, ctypes.c_int,
+                                                 _i32p, _i64, _i64p, _i64]
+        L.orc_find_contours_external.restype = _i64
+        L.orc_find_safety_contour_indices.argtypes = [_f64p, _f64p, _u8p, _i64,
+                                                      ctypes.c_int, ctypes.c_int, _i32p, _i64]
+        L.orc_find_safety_contour_indices.restype = _i64
+        L.orc_next_subgoal.argtypes = [_f64p, _f64p, _f64p, _f64p, _u8p, _i64,
+                                       ctypes.c_int, ctypes.c_int, _dbl, _dbl]
+        L.orc_next_subgoal.restype = _i64
+        _lib = L
+    return _lib
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def set_threads(n: int) -> None:
+    lib().orc_set_threads(int(n))
+
+
+def get_threads() -> int:
+    return int(lib().orc_get_threads())
+
+
+# ---------------------------------------------------------------- GP (a1-a4)
+def rbf_fill(x, y, ell=0.4, sf2=1.0, sn2=0.1):
+    """K = sf2 exp(-d^2/2l^2) + sn2 I, column-major (returned as K[j, i])."""
+    x = _c(x, np.float64); y = _c(y, np.float64)
+    n = x.size
+    K = np.empty(n * n, np.float64)
+    lib().orc_rbf_fill(x, y, n, ell, sf2, sn2, K)
+    return K.reshape(n, n)  # symmetric: row/col major identical
+
+
+def rbf_fill_f32in(x, y, ell=0.4, sf2=1.0, sn2=0.1):
+    x = _c(x, np.float32); y = _c(y, np.float32)
+    n = x.size
+    K = np.empty(n * n, np.float64)
+    lib().orc_rbf_fill_f32in(x, y, n, ell, sf2, sn2, K)
+    return K.reshape(n, n)
+
+
+def rbf_fill_f32(x, y, ell=0.4, sf2=1.0, sn2=0.1):
+    """The device fill's f32 formulation (column-major == row-major, symmetric)."""
+    x = _c(x, np.float32); y = _c(y, np.float32)
+    n = x.size
+    K = np.empty(n * n, np.float32)
+    lib().orc_rbf_fill_f32(x, y, n, ell, sf2, sn2, K)
+    return K.reshape(n, n)
+
+
+def cholesky(K):
+    """Lower Cholesky factor (column-major buffer returned as an (n, n) array
+    A with A[j, i] = L[i, j]; use ``lower_from_colmajor`` for L)."""
+    n = K.shape[0]
+    A = np.array(K, dtype=np.float64, order="C").reshape(-1).copy()
+    info = lib().orc_cholesky(A, n)
+    if info:
+        raise np.linalg.LinAlgError(f"oracle cholesky: leading minor {info} not SPD")
+    return A.reshape(n, n)
+
+
+def lower_from_colmajor(A):
+    """(n, n) array holding a column-major buffer -> dense lower L (row-major)."""
+    return np.tril(A.T)
+
+
+def colmajor_from_lower(L):
+    return np.ascontiguousarray(np.asarray(L, np.float64).T)
+
+
+def chol_solve(Acm, b):
+    n = Acm.shape[0]
+    out = np.empty(n, np.float64)
+    lib().orc_chol_solve(np.ascontiguousarray(Acm, np.float64).reshape(-1), n, _c(b, np.float64), out)
+    return out
+
+
+def fit(x, y, obs, ell=0.4, sf2=1.0, sn2=0.1, m0=0.0):
+    """fp64 GP fit: returns (Lcm, alpha) with Lcm column-major (see cholesky)."""
+    K = rbf_fill(x, y, ell, sf2, sn2)
+    Lcm = cholesky(K)
+    alpha = chol_solve(Lcm, _c(obs, np.float64) - m0)
+    return Lcm, alpha
+
+
+def predict(Lcm, alpha, x, y, qx, qy, ell=0.4, sf2=1.0, m0=0.0):
+    """fp64 posterior mean and latent variance at the query points."""
+    n = alpha.size
+    qx = _c(qx, np.float64); qy = _c(qy, np.float64)
+    m = qx.size
+    mu = np.empty(m, np.float64); var = np.empty(m, np.float64)
+    lib().orc_predict(np.ascontiguousarray(Lcm, np.float64).reshape(-1), _c(alpha, np.float64),
+                      _c(x, np.float64), _c(y, np.float64), n, ell, sf2, m0, qx, qy, m, mu, var)
+    return mu, var
+
+
+def predict_f32(Lcm, alpha, x, y, qx, qy, ell=0.4, sf2=1.0, m0=0.0):
+    n = alpha.size
+    qx = _c(qx, np.float32); qy = _c(qy, np.float32)
+    m = qx.size
+    mu = np.empty(m, np.float32); var = np.empty(m, np.float32)
+    lib().orc_predict_f32(np.ascontiguousarray(Lcm, np.float32).reshape(-1), _c(alpha, np.float32),
+                          _c(x, np.float32), _c(y, np.float32), n, ell, sf2, m0, qx, qy, m, mu, var)
+    return mu, var
+
+
+# ------------------------------------------------------- acquisition (a6-a10)
+def compute_sets(mu, sd, beta, f_min):
+    """ComputeConfidenceIntervals + UpdateSafeSet (node.cpp:409-416)."""
+    mu = _c(mu, np.float64); sd = _c(sd, np.float64)
+    m = mu.size
+    lo = np.empty(m, np.float64); hi = np.empty(m, np.float64); s = np.empty(m, np.uint8)
+    lib().orc_compute_sets(mu, sd, m, float(beta), float(f_min), lo, hi, s)
+    return lo, hi, s
+
+
+def argmax(score, mask=None):
+    score = _c(score, np.float64)
+    val = _dbl(0.0)
+    if mask is not None:
+        mask = _c(mask, np.uint8)
+        ptr = mask.ctypes.data_as(ctypes.c_void_p)
+    else:
+        ptr = None
+    idx = lib().orc_argmax(score, ptr, score.size, ctypes.byref(val))
+    return int(idx), float(val.value)
+
+
+def find_contours_external(img):
+    """cv::findContours(img, RETR_EXTERNAL, CHAIN_APPROX_NONE) restated.
+    Returns a list of (k, 2) int arrays of (x, y) points, OpenCV order."""
+    img = _c(img, np.uint8)
+    h, w = img.shape
+    pcap = 8 * w * h + 16
+    ccap = w * h + 1
+    pts = np.empty(2 * pcap, np.int32)
+    st = np.empty(ccap + 1, np.int64)
+    nc = lib().orc_find_contours_external(img, w, h, pts, pcap, st, ccap)
+    if nc < 0:
+        raise RuntimeError("oracle contour capacity exceeded")
+    pts = pts.reshape(-1, 2)
+    return [pts[st[c]:st[c + 1]].copy() for c in range(nc)]
+
+
+def find_safety_contour_indices(Dx, Dy, safe, width, height):
+    Dx = _c(Dx, np.float64); Dy = _c(Dy, np.float64); safe = _c(safe, np.uint8)
+    cap = 8 * width * height + 16
+    out = np.empty(cap, np.int32)
+    n = lib().orc_find_safety_contour_indices(Dx, Dy, safe, Dx.size, int(width), int(height), out, cap)
+    if n < 0:
+        raise RuntimeError("oracle frontier capacity exceeded")
+    return out[:n].copy()
+
+
+def next_subgoal(Dx, Dy, lo, hi, safe, width, height, gx=0.0, gy=0.0):
+    return int(lib().orc_next_subgoal(_c(Dx, np.float64), _c(Dy, np.float64), _c(lo, np.float64),
+                                      _c(hi, np.float64), _c(safe, np.uint8), len(Dx),
+                                      int(width), int(height), float(gx), float(gy)))

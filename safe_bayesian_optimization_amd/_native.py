@@ -1,0 +1,135 @@
+"""ctypes binding of libsbo.so (the C ABI declared in include/sbo.h).
+
+The library is built in-tree (``make -C safe_bayesian_optimization_amd``) and
+loaded from ``safe_bayesian_optimization_amd/lib/libsbo.so``.  There is no
+fallback: if the library is missing or fails to load, every entry point
+raises.  torch (when importable) is imported first so that libsbo.so binds to
+the same HIP runtime instance torch uses (identical SONAMEs).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "lib", "libsbo.so")
+
+SBO_DEVICE_PTRS = 0x1
+SBO_ASYNC = 0x2
+SCORE_WIDTH = 0
+SCORE_UCB = 1
+
+STATUS = {0: "SBO_OK", 1: "SBO_E_INVAL", 2: "SBO_E_NOT_SPD", 3: "SBO_E_DEVICE", 4: "SBO_E_OOM",
+          5: "SBO_E_EMPTY", 6: "SBO_E_STATE"}
+
+# Every symbol include/sbo.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "sbo_version", "sbo_status_string", "sbo_create", "sbo_destroy", "sbo_set_stream", "sbo_last_error",
+    "sbo_fit", "sbo_append", "sbo_num_train", "sbo_predict", "sbo_compute_sets", "sbo_argmax", "sbo_tick",
+    "sbo_key_combine", "sbo_find_safety_contour_indices", "sbo_next_subgoal", "sbo_find_contours_external",
+    "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
+)
+SBO_OPT_INVERSE_BITS = 1
+
+
+class SboError(RuntimeError):
+    def __init__(self, status: int, message: str = ""):
+        self.status = status
+        super().__init__(f"{STATUS.get(status, status)}: {message}")
+
+
+class NotSPDError(SboError):
+    pass
+
+
+class sbo_hyper(ctypes.Structure):
+    _fields_ = [("length_scale", ctypes.c_double), ("sigma_f", ctypes.c_double),
+                ("noise_level", ctypes.c_double), ("prior_mean", ctypes.c_double)]
+
+
+class sbo_key(ctypes.Structure):
+    _fields_ = [("score", ctypes.c_double), ("idx", ctypes.c_int64)]
+
+
+_lib = None
+
+
+def build(jobs: int = 8) -> str:
+    subprocess.run(["make", "-s", "-j", str(jobs), "-C", _PKG], check=True)
+    return LIB_PATH
+
+
+def lib():
+    """Load libsbo.so (raises if it is missing: no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:  # share torch's HIP runtime when both live in one process
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libsbo.so not built: {LIB_PATH} (run `make -C {_PKG}` or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i64, u32, dbl, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32, ctypes.c_double, ctypes.c_int
+    st = ctypes.c_int
+    L.sbo_version.restype = ctypes.c_char_p
+    L.sbo_status_string.argtypes = [st]
+    L.sbo_status_string.restype = ctypes.c_char_p
+    L.sbo_create.argtypes = [i32, ctypes.POINTER(vp)]
+    L.sbo_create.restype = st
+    L.sbo_destroy.argtypes = [vp]
+    L.sbo_destroy.restype = None
+    L.sbo_set_stream.argtypes = [vp, vp]
+    L.sbo_set_stream.restype = st
+    L.sbo_last_error.argtypes = [vp]
+    L.sbo_last_error.restype = ctypes.c_char_p
+    L.sbo_fit.argtypes = [vp, vp, vp, vp, i64, sbo_hyper, u32]
+    L.sbo_fit.restype = st
+    L.sbo_append.argtypes = [vp, vp, vp, vp, i64, u32]
+    L.sbo_append.restype = st
+    L.sbo_num_train.argtypes = [vp]
+    L.sbo_num_train.restype = i64
+    L.sbo_predict.argtypes = [vp, vp, vp, i64, vp, vp, u32]
+    L.sbo_predict.restype = st
+    L.sbo_compute_sets.argtypes = [vp, vp, vp, i64, dbl, dbl, vp, vp, vp, u32]
+    L.sbo_compute_sets.restype = st
+    L.sbo_argmax.argtypes = [vp, vp, vp, i64, i64, ctypes.POINTER(sbo_key), u32]
+    L.sbo_argmax.restype = st
+    L.sbo_tick.argtypes = [vp, vp, vp, i64, dbl, dbl, i32, i64, vp, vp, vp, vp, vp, vp, u32]
+    L.sbo_tick.restype = st
+    L.sbo_key_combine.argtypes = [sbo_key, sbo_key]
+    L.sbo_key_combine.restype = sbo_key
+    L.sbo_find_safety_contour_indices.argtypes = [vp, vp, vp, i64, i32, i32, vp, i64, ctypes.POINTER(i64)]
+    L.sbo_find_safety_contour_indices.restype = st
+    L.sbo_next_subgoal.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, dbl, dbl]
+    L.sbo_next_subgoal.restype = i64
+    L.sbo_find_contours_external.argtypes = [vp, i32, i32, vp, i64, vp, i64]
+    L.sbo_find_contours_external.restype = i64
+    L.sbo_rbf_fill.argtypes = [vp, vp, vp, i64, sbo_hyper, vp, u32]
+    L.sbo_rbf_fill.restype = st
+    L.sbo_get_factor.argtypes = [vp, vp, vp, u32]
+    L.sbo_get_factor.restype = st
+    L.sbo_set_option.argtypes = [vp, i32, i64]
+    L.sbo_set_option.restype = st
+    L.sbo_get_inverse.argtypes = [vp, vp]
+    L.sbo_get_inverse.restype = st
+    L.sbo_profile.argtypes = [vp, i32]
+    L.sbo_profile.restype = st
+    L.sbo_profile_read.argtypes = [vp, ctypes.POINTER(dbl), ctypes.POINTER(i64), ctypes.POINTER(dbl),
+                                   ctypes.POINTER(i64)]
+    L.sbo_profile_read.restype = st
+    _lib = L
+    return L
+
+
+def check(status: int, ctx=None) -> None:
+    if status == 0:
+        return
+    msg = ""
+    if ctx is not None:
+        msg = lib().sbo_last_error(ctx).decode(errors="replace")
+    if status == 2:
+        raise NotSPDError(status, msg)
+    raise SboError(status, msg)

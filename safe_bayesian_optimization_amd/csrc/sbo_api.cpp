@@ -1,0 +1,613 @@
+// sbo_api.cpp -- the extern "C" entry points of libsbo.so (include/sbo.h).
+//
+// Host orchestration of the GP mapper (fit / append / predict) and the
+// node's acquisition (ComputeSets, grid argmax).  Device work runs on the
+// context's stream: HIP kernels from kernels.hip, rocSOLVER for the
+// factorisation.  No exception crosses the C boundary.
+#include <rocsolver/rocsolver.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "sbo_internal.hpp"
+
+using sbo::DevBuf;
+
+namespace {
+
+constexpr const char *kVersion = "sbo-mi355x 0.1.0";
+
+#define SBO_HIP(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);               \
+            return e_ == hipErrorOutOfMemory ? SBO_E_OOM : SBO_E_DEVICE;                \
+        }                                                                               \
+    } while (0)
+
+#define SBO_BLAS(expr)                                                                  \
+    do {                                                                                \
+        rocblas_status s_ = (expr);                                                     \
+        if (s_ != rocblas_status_success) {                                             \
+            ctx->err = std::string(#expr) + ": " + rocblas_status_to_string(s_);        \
+            return s_ == rocblas_status_memory_error ? SBO_E_OOM : SBO_E_DEVICE;        \
+        }                                                                               \
+    } while (0)
+
+#define SBO_CHECK(cond, code, msg)                                                      \
+    do {                                                                                \
+        if (!(cond)) {                                                                  \
+            ctx->err = (msg);                                                           \
+            return (code);                                                              \
+        }                                                                               \
+    } while (0)
+
+bool dev(uint32_t flags) { return (flags & SBO_DEVICE_PTRS) != 0; }
+
+sbo_status finish(sbo_ctx *ctx, uint32_t flags) {
+    if (flags & SBO_ASYNC) return SBO_OK;
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    return SBO_OK;
+}
+
+sbo_status check_hyper(sbo_ctx *ctx, const sbo_hyper &h) {
+    SBO_CHECK(std::isfinite(h.length_scale) && h.length_scale > 0.0, SBO_E_INVAL,
+              "length_scale must be > 0");
+    SBO_CHECK(std::isfinite(h.sigma_f) && h.sigma_f > 0.0, SBO_E_INVAL, "sigma_f must be > 0");
+    SBO_CHECK(std::isfinite(h.noise_level) && h.noise_level >= 0.0, SBO_E_INVAL,
+              "noise_level must be >= 0");
+    SBO_CHECK(std::isfinite(h.prior_mean), SBO_E_INVAL, "prior_mean must be finite");
+    return SBO_OK;
+}
+
+// Copy an input array into a device buffer (D2D or H2D).
+sbo_status stage_in(sbo_ctx *ctx, void *dst, const void *src, size_t bytes, uint32_t flags) {
+    if (bytes == 0) return SBO_OK;
+    SBO_HIP(hipMemcpyAsync(dst, src, bytes, dev(flags) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                           ctx->stream));
+    return SBO_OK;
+}
+
+// Sub-allocator over one scratch buffer (16-B aligned pieces).
+struct Carve {
+    char *base;
+    size_t off = 0;
+    explicit Carve(void *b) : base(static_cast<char *>(b)) {}
+    template <class T> T *take(size_t count) {
+        T *p = reinterpret_cast<T *>(base + off);
+        off += (count * sizeof(T) + 255) & ~size_t(255);
+        return p;
+    }
+    static size_t need(size_t count, size_t sz) { return (count * sz + 255) & ~size_t(255); }
+};
+
+// Event bracket around one launch when profiling is on.
+hipEvent_t take_event(sbo_ctx *ctx) {
+    if (!ctx->ev_pool.empty()) {
+        hipEvent_t e = ctx->ev_pool.back();
+        ctx->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+struct Bracket {
+    sbo_ctx *ctx;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> *list;
+    hipEvent_t a = nullptr, b = nullptr;
+    Bracket(sbo_ctx *c, std::vector<std::pair<hipEvent_t, hipEvent_t>> &l) : ctx(c), list(&l) {
+        if (!ctx->prof) return;
+        a = take_event(ctx);
+        b = take_event(ctx);
+        if (a) (void)hipEventRecord(a, ctx->stream);
+    }
+    ~Bracket() {
+        if (!ctx->prof || !a || !b) return;
+        (void)hipEventRecord(b, ctx->stream);
+        list->emplace_back(a, b);
+    }
+};
+
+void recycle_events(sbo_ctx *ctx) {
+    for (auto *l : {&ctx->ev_predict, &ctx->ev_fill}) {
+        for (auto &p : *l) {
+            ctx->ev_pool.push_back(p.first);
+            ctx->ev_pool.push_back(p.second);
+        }
+        l->clear();
+    }
+}
+
+// Rebuild alpha, L^-1 and the packed predictive operand from the current L.
+sbo_status refresh_operand(sbo_ctx *ctx) {
+    const int64_t n = ctx->n, ld = ctx->cap;
+    const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
+    float *L = ctx->L.as<float>();
+    float *alpha = ctx->alpha.as<float>();
+    rocblas_int *info = ctx->info.as<rocblas_int>();
+
+    // alpha = K^-1 (y - m0)
+    SBO_HIP(sbo::launch_sub_scalar(ctx->stream, ctx->obs.as<float>(), (float)ctx->hyper.prior_mean, n, alpha));
+    SBO_BLAS(rocsolver_spotrs(ctx->blas, rocblas_fill_lower, (rocblas_int)n, 1, L, (rocblas_int)ld, alpha,
+                              (rocblas_int)n));
+
+    // L^-1 (lower, non-unit) in the workspace.  Default: widen L to f64 and
+    // invert with dtrtri (f64 MFMA), then round sf2 * L^-1 to f32 once while
+    // packing -- the f32 strtri path adds its own inversion error on top of the
+    // f32 representation error (SBO_OPT_INVERSE_BITS = 32 selects it).
+    const int64_t npad = sbo::round_up(n, sbo::kBM);
+    const int64_t nI = npad / sbo::kBM;
+    SBO_HIP(ctx->aug.reserve(sizeof(float) * (size_t)sbo::total_tiles(nI) * sbo::kTileFloats));
+    SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
+    rocblas_int hinfo = 0;
+    if (ctx->inverse_bits == 64) {
+        SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)n * (size_t)n));
+        double *Li = ctx->Linv.as<double>();
+        SBO_HIP(sbo::launch_widen_lower(ctx->stream, L, ld, n, Li));
+        SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
+                                  (rocblas_int)n, info));
+        SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, n, n, npad, sf2, ctx->x.as<float>(), ctx->y.as<float>(),
+                                         alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
+    } else {
+        SBO_HIP(ctx->Linv.reserve(sizeof(float) * (size_t)ld * (size_t)n));
+        float *Li = ctx->Linv.as<float>();
+        SBO_HIP(hipMemcpyAsync(Li, L, sizeof(float) * (size_t)ld * (size_t)n, hipMemcpyDeviceToDevice, ctx->stream));
+        SBO_BLAS(rocsolver_strtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
+                                  (rocblas_int)ld, info));
+        SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, ld, n, npad, sf2, ctx->x.as<float>(), ctx->y.as<float>(),
+                                         alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
+    }
+    SBO_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    SBO_CHECK(hinfo == 0, SBO_E_NOT_SPD, "trtri: singular factor (info=" + std::to_string(hinfo) + ")");
+    ctx->npad = npad;
+    ctx->fitted = true;
+    return SBO_OK;
+}
+
+// Factor K in L (already filled, lda = cap) and refresh the operand.
+sbo_status factor_and_refresh(sbo_ctx *ctx) {
+    rocblas_int *info = ctx->info.as<rocblas_int>();
+    SBO_BLAS(rocsolver_spotrf(ctx->blas, rocblas_fill_lower, (rocblas_int)ctx->n, ctx->L.as<float>(),
+                              (rocblas_int)ctx->cap, info));
+    rocblas_int hinfo = 0;
+    SBO_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    if (hinfo != 0) {
+        ctx->fitted = false;
+        ctx->err = "spotrf: leading minor " + std::to_string(hinfo) + " not positive definite";
+        return SBO_E_NOT_SPD;
+    }
+    return refresh_operand(ctx);
+}
+
+// Predictive sweep + acquisition over m queries already on the device.
+sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, double beta, double f_min,
+                    int score_kind, int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
+                    uint8_t *safe, sbo_key *key_dev) {
+    const int64_t nI = ctx->npad / sbo::kBM;
+    const int64_t ldp = sbo::round_up(m, 64);
+    SBO_HIP(ctx->part.reserve(sizeof(float) * (size_t)nI * (size_t)ldp));
+    SBO_HIP(ctx->mean.reserve(sizeof(float) * (size_t)ldp));
+    const int64_t nb = sbo::acq_blocks(m);
+    SBO_HIP(ctx->keys.reserve(sizeof(sbo_key) * (size_t)(nb + 1)));
+    sbo_key *bkeys = ctx->keys.as<sbo_key>();
+    {
+        Bracket br(ctx, ctx->ev_predict);
+        SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(), ctx->npad, qx, qy,
+                                    m, ldp, (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean,
+                                    ctx->part.as<float>(), ctx->mean.as<float>()));
+    }
+    const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
+    SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<float>(), ctx->mean.as<float>(), (int)nI, ldp, m, sf2,
+                                beta, f_min, score_kind, index_offset, mu, sd, lo, hi, safe, bkeys, 1));
+    SBO_HIP(sbo::launch_reduce_keys(ctx->stream, bkeys, nb, key_dev ? key_dev : bkeys + nb));
+    return SBO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+SBO_API const char *sbo_version(void) { return kVersion; }
+
+SBO_API const char *sbo_status_string(sbo_status s) {
+    switch (s) {
+        case SBO_OK: return "SBO_OK";
+        case SBO_E_INVAL: return "SBO_E_INVAL";
+        case SBO_E_NOT_SPD: return "SBO_E_NOT_SPD";
+        case SBO_E_DEVICE: return "SBO_E_DEVICE";
+        case SBO_E_OOM: return "SBO_E_OOM";
+        case SBO_E_EMPTY: return "SBO_E_EMPTY";
+        case SBO_E_STATE: return "SBO_E_STATE";
+    }
+    return "SBO_E_UNKNOWN";
+}
+
+SBO_API sbo_status sbo_create(int device, sbo_ctx **out) {
+    if (!out) return SBO_E_INVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return SBO_E_DEVICE;
+    sbo_ctx *ctx = new (std::nothrow) sbo_ctx();
+    if (!ctx) return SBO_E_OOM;
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        rocblas_create_handle(&ctx->blas) != rocblas_status_success ||
+        hipHostMalloc(reinterpret_cast<void **>(&ctx->host_key), sizeof(sbo_key)) != hipSuccess ||
+        ctx->info.reserve(256) != hipSuccess) {
+        sbo_destroy(ctx);
+        return SBO_E_DEVICE;
+    }
+    ctx->stream = ctx->own_stream;
+    rocblas_set_stream(ctx->blas, ctx->stream);
+    *out = ctx;
+    return SBO_OK;
+}
+
+SBO_API void sbo_destroy(sbo_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    recycle_events(ctx);
+    for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->blas) rocblas_destroy_handle(ctx->blas);
+    if (ctx->host_key) (void)hipHostFree(ctx->host_key);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+}
+
+SBO_API sbo_status sbo_set_stream(sbo_ctx *ctx, void *hip_stream) {
+    if (!ctx) return SBO_E_INVAL;
+    ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+    SBO_BLAS(rocblas_set_stream(ctx->blas, ctx->stream));
+    return SBO_OK;
+}
+
+SBO_API const char *sbo_last_error(const sbo_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+SBO_API int64_t sbo_num_train(const sbo_ctx *ctx) { return ctx && ctx->fitted ? ctx->n : 0; }
+
+SBO_API sbo_status sbo_fit(sbo_ctx *ctx, const float *x, const float *y, const float *obs, int64_t n,
+                           sbo_hyper hyper, uint32_t flags) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(x && y && obs, SBO_E_INVAL, "sbo_fit: null input");
+    SBO_CHECK(n > 0, SBO_E_EMPTY, "sbo_fit: n must be > 0");
+    SBO_CHECK(n < (int64_t)1 << 30, SBO_E_INVAL, "sbo_fit: n too large");
+    if (sbo_status st = check_hyper(ctx, hyper)) return st;
+    SBO_HIP(hipSetDevice(ctx->device));
+    ctx->fitted = false;
+    ctx->hyper = hyper;
+    ctx->n = n;
+    ctx->cap = n;
+    SBO_HIP(ctx->x.reserve(sizeof(float) * n));
+    SBO_HIP(ctx->y.reserve(sizeof(float) * n));
+    SBO_HIP(ctx->obs.reserve(sizeof(float) * n));
+    SBO_HIP(ctx->alpha.reserve(sizeof(float) * n));
+    SBO_HIP(ctx->L.reserve(sizeof(float) * (size_t)n * (size_t)n));
+    if (sbo_status st = stage_in(ctx, ctx->x.as<float>(), x, sizeof(float) * n, flags)) return st;
+    if (sbo_status st = stage_in(ctx, ctx->y.as<float>(), y, sizeof(float) * n, flags)) return st;
+    if (sbo_status st = stage_in(ctx, ctx->obs.as<float>(), obs, sizeof(float) * n, flags)) return st;
+    const float sf2 = (float)(hyper.sigma_f * hyper.sigma_f);
+    {
+        Bracket br(ctx, ctx->ev_fill);
+        SBO_HIP(sbo::launch_rbf_fill(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, ctx->x.as<float>(),
+                                     ctx->y.as<float>(), n, n, (float)hyper.length_scale, sf2,
+                                     (float)hyper.noise_level, true, ctx->L.as<float>()));
+    }
+    if (sbo_status st = factor_and_refresh(ctx)) return st;
+    return finish(ctx, flags);
+}
+
+SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, const float *obs, int64_t b,
+                              uint32_t flags) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(ctx->fitted, SBO_E_STATE, "sbo_append: call sbo_fit first");
+    SBO_CHECK(x && y && obs, SBO_E_INVAL, "sbo_append: null input");
+    SBO_CHECK(b >= 0, SBO_E_INVAL, "sbo_append: b must be >= 0");
+    if (b == 0) return SBO_OK;
+    SBO_HIP(hipSetDevice(ctx->device));
+    const int64_t n0 = ctx->n, n1 = n0 + b;
+    SBO_CHECK(n1 < (int64_t)1 << 30, SBO_E_INVAL, "sbo_append: n too large");
+    const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
+
+    // grow storage (geometric) preserving the factor
+    if (n1 > ctx->cap) {
+        const int64_t ncap = std::max<int64_t>(n1, sbo::round_up(ctx->cap + ctx->cap / 2, 256));
+        DevBuf nx, ny, no, nL;
+        SBO_HIP(nx.reserve(sizeof(float) * ncap));
+        SBO_HIP(ny.reserve(sizeof(float) * ncap));
+        SBO_HIP(no.reserve(sizeof(float) * ncap));
+        SBO_HIP(nL.reserve(sizeof(float) * (size_t)ncap * (size_t)ncap));
+        SBO_HIP(hipMemcpyAsync(nx.as<float>(), ctx->x.as<float>(), sizeof(float) * n0, hipMemcpyDeviceToDevice, ctx->stream));
+        SBO_HIP(hipMemcpyAsync(ny.as<float>(), ctx->y.as<float>(), sizeof(float) * n0, hipMemcpyDeviceToDevice, ctx->stream));
+        SBO_HIP(hipMemcpyAsync(no.as<float>(), ctx->obs.as<float>(), sizeof(float) * n0, hipMemcpyDeviceToDevice, ctx->stream));
+        SBO_HIP(hipMemcpy2DAsync(nL.as<float>(), sizeof(float) * ncap, ctx->L.as<float>(), sizeof(float) * ctx->cap,
+                                 sizeof(float) * n0, n0, hipMemcpyDeviceToDevice, ctx->stream));
+        SBO_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->x.swap(nx);
+        ctx->y.swap(ny);
+        ctx->obs.swap(no);
+        ctx->L.swap(nL);
+        ctx->cap = ncap;
+        SBO_HIP(ctx->alpha.reserve(sizeof(float) * ncap));
+    }
+    const int64_t ld = ctx->cap;
+    if (sbo_status st = stage_in(ctx, ctx->x.as<float>() + n0, x, sizeof(float) * b, flags)) return st;
+    if (sbo_status st = stage_in(ctx, ctx->y.as<float>() + n0, y, sizeof(float) * b, flags)) return st;
+    if (sbo_status st = stage_in(ctx, ctx->obs.as<float>() + n0, obs, sizeof(float) * b, flags)) return st;
+
+    // Block Cholesky update of the lower factor (column-major, lda = ld):
+    //   [L11  0 ]   K21 = k(Xnew, X)  -> L21 = K21 L11^-T        (trsm)
+    //   [L21 L22]   K22 = k(Xnew, Xnew) + sn2 I - L21 L21^T      (syrk)
+    //               L22 = chol(K22)                              (potrf)
+    float *L = ctx->L.as<float>();
+    float *xs = ctx->x.as<float>(), *ys = ctx->y.as<float>();
+    const float ell = (float)ctx->hyper.length_scale, sn2 = (float)ctx->hyper.noise_level;
+    float *L21 = L + n0;                  // rows n0.., columns 0..n0-1
+    float *L22 = L + n0 + n0 * ld;        // rows n0.., columns n0..
+    SBO_HIP(sbo::launch_rbf_fill(ctx->stream, xs + n0, ys + n0, b, xs, ys, n0, ld, ell, sf2, sn2, false, L21));
+    SBO_HIP(sbo::launch_rbf_fill(ctx->stream, xs + n0, ys + n0, b, xs + n0, ys + n0, b, ld, ell, sf2, sn2, true, L22));
+    const float one = 1.0f, minus_one = -1.0f;
+    SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
+    SBO_BLAS(rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                           rocblas_diagonal_non_unit, (rocblas_int)b, (rocblas_int)n0, &one, L, (rocblas_int)ld, L21,
+                           (rocblas_int)ld));
+    SBO_BLAS(rocblas_ssyrk(ctx->blas, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)b, (rocblas_int)n0,
+                           &minus_one, L21, (rocblas_int)ld, &one, L22, (rocblas_int)ld));
+    rocblas_int *info = ctx->info.as<rocblas_int>();
+    SBO_BLAS(rocsolver_spotrf(ctx->blas, rocblas_fill_lower, (rocblas_int)b, L22, (rocblas_int)ld, info));
+    rocblas_int hinfo = 0;
+    SBO_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    if (hinfo != 0) {
+        ctx->fitted = false;
+        ctx->err = "sbo_append: updated block not positive definite (info=" + std::to_string(hinfo) + ")";
+        return SBO_E_NOT_SPD;
+    }
+    ctx->n = n1;
+    if (sbo_status st = refresh_operand(ctx)) return st;
+    return finish(ctx, flags);
+}
+
+SBO_API sbo_status sbo_predict(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, float *mu, float *sd,
+                               uint32_t flags) {
+    return sbo_tick(ctx, qx, qy, m, 0.0, 0.0, SBO_SCORE_WIDTH, 0, mu, sd, nullptr, nullptr, nullptr, nullptr,
+                    flags);
+}
+
+SBO_API sbo_status sbo_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, double beta, double f_min,
+                            sbo_score score, int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
+                            uint8_t *safe, sbo_key *out, uint32_t flags) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(ctx->fitted, SBO_E_STATE, "sbo_tick: call sbo_fit first");
+    SBO_CHECK(qx && qy, SBO_E_INVAL, "sbo_tick: null query coordinates");
+    SBO_CHECK(m > 0, SBO_E_EMPTY, "sbo_tick: m must be > 0");
+    SBO_CHECK(score == SBO_SCORE_WIDTH || score == SBO_SCORE_UCB, SBO_E_INVAL, "sbo_tick: bad score kind");
+    SBO_CHECK(std::isfinite(beta) && !std::isnan(f_min), SBO_E_INVAL, "sbo_tick: beta/f_min must be finite");
+    SBO_HIP(hipSetDevice(ctx->device));
+    if (dev(flags)) {
+        if (sbo_status st = run_tick(ctx, qx, qy, m, beta, f_min, (int)score, index_offset, mu, sd, lo, hi, safe,
+                                     out))
+            return st;
+        return finish(ctx, flags);
+    }
+    // host pointers: stage through device scratch
+    const size_t need = Carve::need(m, 4) * 4 + Carve::need(m, 8) * 2 + Carve::need(m, 1) + Carve::need(1, sizeof(sbo_key));
+    SBO_HIP(ctx->hq.reserve(need));
+    Carve c(ctx->hq.as<void>());
+    float *dqx = c.take<float>(m), *dqy = c.take<float>(m), *dmu = c.take<float>(m), *dsd = c.take<float>(m);
+    double *dlo = c.take<double>(m), *dhi = c.take<double>(m);
+    uint8_t *dsafe = c.take<uint8_t>(m);
+    sbo_key *dkey = c.take<sbo_key>(1);
+    SBO_HIP(hipMemcpyAsync(dqx, qx, sizeof(float) * m, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(dqy, qy, sizeof(float) * m, hipMemcpyHostToDevice, ctx->stream));
+    if (sbo_status st = run_tick(ctx, dqx, dqy, m, beta, f_min, (int)score, index_offset, mu ? dmu : nullptr,
+                                 sd ? dsd : nullptr, lo ? dlo : nullptr, hi ? dhi : nullptr,
+                                 safe ? dsafe : nullptr, dkey))
+        return st;
+    if (mu) SBO_HIP(hipMemcpyAsync(mu, dmu, sizeof(float) * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (sd) SBO_HIP(hipMemcpyAsync(sd, dsd, sizeof(float) * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (lo) SBO_HIP(hipMemcpyAsync(lo, dlo, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (hi) SBO_HIP(hipMemcpyAsync(hi, dhi, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (safe) SBO_HIP(hipMemcpyAsync(safe, dsafe, m, hipMemcpyDeviceToHost, ctx->stream));
+    if (out) SBO_HIP(hipMemcpyAsync(ctx->host_key, dkey, sizeof(sbo_key), hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    if (out) *out = *ctx->host_key;
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_compute_sets(sbo_ctx *ctx, const float *mu, const float *sd, int64_t m, double beta,
+                                    double f_min, double *lo, double *hi, uint8_t *safe, uint32_t flags) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(mu && sd, SBO_E_INVAL, "sbo_compute_sets: null mu/sd");
+    SBO_CHECK(m >= 0, SBO_E_INVAL, "sbo_compute_sets: m must be >= 0");
+    if (m == 0) return SBO_OK;
+    SBO_HIP(hipSetDevice(ctx->device));
+    if (dev(flags)) {
+        SBO_HIP(sbo::launch_sets(ctx->stream, mu, sd, m, beta, f_min, lo, hi, safe));
+        return finish(ctx, flags);
+    }
+    const size_t need = Carve::need(m, 4) * 2 + Carve::need(m, 8) * 2 + Carve::need(m, 1);
+    SBO_HIP(ctx->hq.reserve(need));
+    Carve c(ctx->hq.as<void>());
+    float *dmu = c.take<float>(m), *dsd = c.take<float>(m);
+    double *dlo = c.take<double>(m), *dhi = c.take<double>(m);
+    uint8_t *ds = c.take<uint8_t>(m);
+    SBO_HIP(hipMemcpyAsync(dmu, mu, sizeof(float) * m, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(dsd, sd, sizeof(float) * m, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(sbo::launch_sets(ctx->stream, dmu, dsd, m, beta, f_min, lo ? dlo : nullptr, hi ? dhi : nullptr,
+                             safe ? ds : nullptr));
+    if (lo) SBO_HIP(hipMemcpyAsync(lo, dlo, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (hi) SBO_HIP(hipMemcpyAsync(hi, dhi, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (safe) SBO_HIP(hipMemcpyAsync(safe, ds, m, hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_argmax(sbo_ctx *ctx, const double *score, const uint8_t *mask, int64_t m,
+                              int64_t index_offset, sbo_key *out, uint32_t flags) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(score && out, SBO_E_INVAL, "sbo_argmax: null score/out");
+    SBO_CHECK(m >= 0, SBO_E_INVAL, "sbo_argmax: m must be >= 0");
+    SBO_HIP(hipSetDevice(ctx->device));
+    if (m == 0) {
+        const sbo_key none{0.0, -1};
+        if (dev(flags)) {
+            SBO_HIP(hipMemcpyAsync(out, &none, sizeof(none), hipMemcpyHostToDevice, ctx->stream));
+            return finish(ctx, flags);
+        }
+        *out = none;
+        return SBO_OK;
+    }
+    const int64_t nb = sbo::acq_blocks(m);
+    SBO_HIP(ctx->keys.reserve(sizeof(sbo_key) * (size_t)(nb + 1)));
+    sbo_key *bk = ctx->keys.as<sbo_key>();
+    if (dev(flags)) {
+        SBO_HIP(sbo::launch_argmax_blocks(ctx->stream, score, mask, m, index_offset, bk));
+        SBO_HIP(sbo::launch_reduce_keys(ctx->stream, bk, nb, out));
+        return finish(ctx, flags);
+    }
+    const size_t need = Carve::need(m, 8) + Carve::need(m, 1);
+    SBO_HIP(ctx->hq.reserve(need));
+    Carve c(ctx->hq.as<void>());
+    double *ds = c.take<double>(m);
+    uint8_t *dm = c.take<uint8_t>(m);
+    SBO_HIP(hipMemcpyAsync(ds, score, sizeof(double) * m, hipMemcpyHostToDevice, ctx->stream));
+    if (mask) SBO_HIP(hipMemcpyAsync(dm, mask, m, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(sbo::launch_argmax_blocks(ctx->stream, ds, mask ? dm : nullptr, m, index_offset, bk));
+    SBO_HIP(sbo::launch_reduce_keys(ctx->stream, bk, nb, bk + nb));
+    SBO_HIP(hipMemcpyAsync(ctx->host_key, bk + nb, sizeof(sbo_key), hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    *out = *ctx->host_key;
+    return SBO_OK;
+}
+
+SBO_API sbo_key sbo_key_combine(sbo_key a, sbo_key b) {
+    if (a.idx < 0) return b;
+    if (b.idx < 0) return a;
+    if (a.score > b.score) return a;
+    if (b.score > a.score) return b;
+    return a.idx <= b.idx ? a : b;
+}
+
+SBO_API sbo_status sbo_rbf_fill(sbo_ctx *ctx, const float *x, const float *y, int64_t n, sbo_hyper hyper, float *K,
+                                uint32_t flags) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(x && y && K, SBO_E_INVAL, "sbo_rbf_fill: null argument");
+    SBO_CHECK(n > 0, SBO_E_EMPTY, "sbo_rbf_fill: n must be > 0");
+    if (sbo_status st = check_hyper(ctx, hyper)) return st;
+    SBO_HIP(hipSetDevice(ctx->device));
+    const float sf2 = (float)(hyper.sigma_f * hyper.sigma_f);
+    if (dev(flags)) {
+        Bracket br(ctx, ctx->ev_fill);
+        SBO_HIP(sbo::launch_rbf_fill(ctx->stream, x, y, n, x, y, n, n, (float)hyper.length_scale, sf2,
+                                     (float)hyper.noise_level, true, K));
+        return finish(ctx, flags);
+    }
+    const size_t need = Carve::need(n, 4) * 2 + Carve::need((size_t)n * n, 4);
+    SBO_HIP(ctx->hq.reserve(need));
+    Carve c(ctx->hq.as<void>());
+    float *dx = c.take<float>(n), *dy = c.take<float>(n), *dK = c.take<float>((size_t)n * n);
+    SBO_HIP(hipMemcpyAsync(dx, x, sizeof(float) * n, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(dy, y, sizeof(float) * n, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(sbo::launch_rbf_fill(ctx->stream, dx, dy, n, dx, dy, n, n, (float)hyper.length_scale, sf2,
+                                 (float)hyper.noise_level, true, dK));
+    SBO_HIP(hipMemcpyAsync(K, dK, sizeof(float) * (size_t)n * n, hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t flags) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(ctx->fitted, SBO_E_STATE, "sbo_get_factor: call sbo_fit first");
+    SBO_HIP(hipSetDevice(ctx->device));
+    const int64_t n = ctx->n;
+    const hipMemcpyKind k = dev(flags) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (L) {
+        if (dev(flags)) {
+            SBO_HIP(sbo::launch_copy_lower(ctx->stream, ctx->L.as<float>(), ctx->cap, n, L, n));
+        } else {
+            SBO_HIP(ctx->hq.reserve(sizeof(float) * (size_t)n * n));
+            SBO_HIP(sbo::launch_copy_lower(ctx->stream, ctx->L.as<float>(), ctx->cap, n, ctx->hq.as<float>(), n));
+            SBO_HIP(hipMemcpyAsync(L, ctx->hq.as<float>(), sizeof(float) * (size_t)n * n, k, ctx->stream));
+        }
+    }
+    if (alpha) SBO_HIP(hipMemcpyAsync(alpha, ctx->alpha.as<float>(), sizeof(float) * n, k, ctx->stream));
+    if (!dev(flags)) {
+        SBO_HIP(hipStreamSynchronize(ctx->stream));
+        return SBO_OK;
+    }
+    return finish(ctx, flags);
+}
+
+SBO_API sbo_status sbo_profile(sbo_ctx *ctx, int enable) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    recycle_events(ctx);
+    ctx->prof = enable != 0;
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_profile_read(sbo_ctx *ctx, double *predict_ms, int64_t *predict_launches, double *fill_ms,
+                                    int64_t *fill_launches) {
+    if (!ctx) return SBO_E_INVAL;
+    auto sum = [&](const std::vector<std::pair<hipEvent_t, hipEvent_t>> &l, double *ms, int64_t *cnt) -> sbo_status {
+        double t = 0.0;
+        for (const auto &p : l) {
+            SBO_HIP(hipEventSynchronize(p.second));
+            float e = 0.f;
+            SBO_HIP(hipEventElapsedTime(&e, p.first, p.second));
+            t += e;
+        }
+        if (ms) *ms = t;
+        if (cnt) *cnt = (int64_t)l.size();
+        return SBO_OK;
+    };
+    if (sbo_status st = sum(ctx->ev_predict, predict_ms, predict_launches)) return st;
+    return sum(ctx->ev_fill, fill_ms, fill_launches);
+}
+
+SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
+    if (!ctx) return SBO_E_INVAL;
+    switch (option) {
+        case SBO_OPT_INVERSE_BITS:
+            SBO_CHECK(value == 32 || value == 64, SBO_E_INVAL, "SBO_OPT_INVERSE_BITS must be 32 or 64");
+            ctx->inverse_bits = (int)value;
+            return SBO_OK;
+    }
+    ctx->err = "unknown option " + std::to_string(option);
+    return SBO_E_INVAL;
+}
+
+SBO_API sbo_status sbo_get_inverse(sbo_ctx *ctx, float *Linv) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(ctx->fitted && Linv, SBO_E_STATE, "sbo_get_inverse: call sbo_fit first");
+    SBO_HIP(hipSetDevice(ctx->device));
+    const int64_t n = ctx->n, npad = ctx->npad;
+    // unpack the packed operand tiles (rows of sf2 * L^-1) on the host
+    const int64_t nI = npad / sbo::kBM;
+    const size_t tiles = (size_t)sbo::total_tiles(nI);
+    std::vector<float> h(tiles * sbo::kTileFloats);
+    SBO_HIP(hipMemcpyAsync(h.data(), ctx->aug.as<float>(), sizeof(float) * h.size(), hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    for (int64_t I = 0; I < nI; ++I)
+        for (int64_t kb = 0; kb < (I + 1) * sbo::kTilesPerRowBlockStep; ++kb) {
+            const float *t = h.data() + (sbo::tile_start(I) + kb) * sbo::kTileFloats;
+            for (int k = 0; k < sbo::kBK; ++k)
+                for (int r = 0; r < sbo::kBM; ++r) {
+                    const int64_t row = I * sbo::kBM + r, col = kb * sbo::kBK + k;
+                    if (row < n && col < n) Linv[row * n + col] = t[k * sbo::kBM + r];
+                }
+        }
+    return SBO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,151 @@
+// sbo_internal.hpp -- context state, device buffers and kernel launchers of
+// libsbo.so.  Not part of the public ABI (include/sbo.h is).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/sbo.h"
+
+namespace sbo {
+
+// ---------------------------------------------------------------- geometry
+// Predictive operand tiling (see DESIGN.md "predictive sweep").
+//   BM rows of A = sf2 * L^-1 per workgroup, BN queries per workgroup
+//   (4 waves x 32), BK training points per LDS stage.
+constexpr int kBM = 128;
+constexpr int kBN = 128;
+constexpr int kBK = 32;
+constexpr int kTileFloats = kBM * kBK;           // one packed [BK][BM] tile
+constexpr int kTilesPerRowBlockStep = kBM / kBK;  // k-tiles added per row block
+constexpr int kAcqThreads = 256;
+
+__host__ __device__ inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// First packed tile of row block I: sum_{I'<I} (I'+1)*(BM/BK).
+__host__ __device__ inline int64_t tile_start(int64_t I) { return kTilesPerRowBlockStep * I * (I + 1) / 2; }
+inline int64_t total_tiles(int64_t nI) { return tile_start(nI); }
+
+// ----------------------------------------------------------- device buffer
+class DevBuf {
+public:
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    // Grow-only; contents are NOT preserved on growth.
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap_) return hipSuccess;
+        release();
+        hipError_t e = hipMalloc(&ptr_, bytes);
+        if (e != hipSuccess) { ptr_ = nullptr; return e; }
+        cap_ = bytes;
+        return hipSuccess;
+    }
+    void release() {
+        if (ptr_) (void)hipFree(ptr_);
+        ptr_ = nullptr;
+        cap_ = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(ptr_); }
+    void swap(DevBuf &o) {
+        std::swap(ptr_, o.ptr_);
+        std::swap(cap_, o.cap_);
+    }
+    size_t capacity() const { return cap_; }
+
+private:
+    void *ptr_ = nullptr;
+    size_t cap_ = 0;
+};
+
+}  // namespace sbo
+
+struct sbo_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    rocblas_handle blas = nullptr;
+    std::string err;
+
+    // fitted model
+    int64_t n = 0;       // training points
+    int64_t cap = 0;     // allocated leading dimension of L (>= n, for appends)
+    sbo_hyper hyper{0.4, 1.0, 0.1, 0.0};
+    bool fitted = false;
+
+    sbo::DevBuf x, y, obs;       // training data, f32, capacity cap
+    sbo::DevBuf L;               // lower Cholesky factor, column-major, lda = cap
+    sbo::DevBuf Linv;            // workspace: L^-1 (strtri f32, lda = cap, or dtrtri f64, lda = n)
+    int inverse_bits = 64;       // SBO_OPT_INVERSE_BITS: precision of the L^-1 computation
+    sbo::DevBuf alpha;           // K^-1 (y - m0), length cap
+    sbo::DevBuf aug;             // packed sf2 * L^-1 tiles
+    sbo::DevBuf kcoord;          // per k-tile: x[BK], y[BK], sf2*alpha[BK]
+    sbo::DevBuf info;            // rocSOLVER info
+    sbo::DevBuf scratch;         // append workspace
+    int64_t npad = 0;            // rows/cols of the packed operand (multiple of BM)
+
+    // per-call staging
+    sbo::DevBuf part, mean;      // predictive partial sums [nI][ldp], mean [ldp]
+    sbo::DevBuf hq;              // host-input staging (queries, mu/sd, ...)
+    sbo::DevBuf hout;            // host-output staging
+    sbo::DevBuf keys;            // per-block argmax keys + final key
+    sbo_key *host_key = nullptr; // pinned readback
+
+    // kernel timing (sbo_profile)
+    bool prof = false;
+    std::vector<hipEvent_t> ev_pool;               // free events
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_predict, ev_fill;
+
+    bool fail(const std::string &m) { err = m; return false; }
+};
+
+namespace sbo {
+
+// ---------------------------------------------------------- kernel launchers
+// All launchers enqueue on `s` and return hipGetLastError().
+// K[i + j*ld] = sf2 exp(-|a_i - b_j|^2 / 2l^2) (+ sn2 on i == j when diag).
+hipError_t launch_rbf_fill(hipStream_t s, const float *xa, const float *ya, int64_t ma, const float *xb,
+                           const float *yb, int64_t mb, int64_t ld, float ell, float sf2, float sn2, bool diag,
+                           float *K);
+hipError_t launch_sub_scalar(hipStream_t s, const float *in, float v, int64_t n, float *out);
+hipError_t launch_copy_lower(hipStream_t s, const float *src, int64_t ld_src, int64_t n,
+                             float *dst, int64_t ld_dst);
+// Pack A = sf2 * L^-1 (from an f32 or f64 inverse, lower, column-major) into
+// [BK][BM] tiles, plus per-k coordinates and sf2 * alpha.
+hipError_t launch_pack_operand(hipStream_t s, const float *Linv, int64_t ld, int64_t n, int64_t npad,
+                               double sf2, const float *x, const float *y, const float *alpha, float *aug,
+                               float *kcoord);
+hipError_t launch_pack_operand(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad,
+                               double sf2, const float *x, const float *y, const float *alpha, float *aug,
+                               float *kcoord);
+// dst (n x n, ld n, f64) = lower(src), upper zeroed.
+hipError_t launch_widen_lower(hipStream_t s, const float *src, int64_t ld_src, int64_t n, double *dst);
+// Predictive sweep: part[I][q] = sum over rows of block I of (sf2 L^-1 k_q)^2,
+// mean[q] = m0 + sf2 alpha^T k_q.
+hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, int64_t npad,
+                          const float *qx, const float *qy, int64_t m, int64_t ldp,
+                          float ell, float m0, float *part, float *mean);
+// Acquisition over predictive partials (fused reduce + sets + block argmax).
+hipError_t launch_acquire(hipStream_t s, const float *part, const float *mean, int nI, int64_t ldp,
+                          int64_t m, float sf2, double beta, double f_min, int score_kind,
+                          int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
+                          uint8_t *safe, sbo_key *block_keys, int do_sets);
+// ComputeSets from given mu/sd (staged API).
+hipError_t launch_sets(hipStream_t s, const float *mu, const float *sd, int64_t m, double beta,
+                       double f_min, double *lo, double *hi, uint8_t *safe);
+// Masked argmax over f64 scores -> block keys.
+hipError_t launch_argmax_blocks(hipStream_t s, const double *score, const uint8_t *mask, int64_t m,
+                                int64_t index_offset, sbo_key *block_keys);
+// Reduce nblocks keys into *out (device pointer).
+hipError_t launch_reduce_keys(hipStream_t s, const sbo_key *keys, int64_t nblocks, sbo_key *out);
+
+inline int64_t acq_blocks(int64_t m) { return (m + kAcqThreads - 1) / kAcqThreads; }
+
+}  // namespace sbo

@@ -1,0 +1,224 @@
+"""GP terrain mapper on MI355X -- the host-side mirror of the external
+``terrain_mapping_node`` that serves ``get_terrain_map_with_uncertainty`` to
+the reference node (launch/safe_bayesian_optimization.launch.py:111-117,
+hyper-parameters config/lpsc.yaml:35-37, client
+src/safe_bayesian_optimization_node.cpp:75-77, request/response :576-644).
+
+Everything numeric runs in libsbo.so (HIP kernels + rocSOLVER); this module
+only marshals arrays.  Inputs may be numpy arrays (host) or torch tensors on
+the GPU (zero-copy, passed as device pointers).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as N
+from .terrain import Hyper
+
+
+def _is_dev(a) -> bool:
+    return hasattr(a, "is_cuda") and bool(a.is_cuda)
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if _is_dev(a):
+        return ctypes.c_void_p(a.data_ptr())
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _host(a, dt):
+    return np.ascontiguousarray(np.asarray(a), dtype=dt)
+
+
+def _prep(arrs, dt_np, dt_torch_name):
+    """Make every input the same kind: all device (contiguous, right dtype) or all host."""
+    if all(_is_dev(a) for a in arrs):
+        import torch
+        dt = getattr(torch, dt_torch_name)
+        return [a.contiguous().to(dt) for a in arrs], N.SBO_DEVICE_PTRS
+    if any(_is_dev(a) for a in arrs):
+        raise TypeError("mix of device tensors and host arrays")
+    return [_host(a, dt_np) for a in arrs], 0
+
+
+def _to_hyper(h: Hyper) -> N.sbo_hyper:
+    return N.sbo_hyper(float(h.length_scale), float(h.sigma_f), float(h.noise_level), float(h.prior_mean))
+
+
+@dataclass
+class TerrainMapResponse:
+    """Fields of GetTerrainMapWithUncertainty::Response in the order the node
+    reads them (node.cpp:607-644)."""
+    success: bool
+    message: str
+    n_width_cells: int
+    n_height_cells: int
+    x_coords: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    y_coords: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    values: np.ndarray = field(default_factory=lambda: np.zeros(0))          # mu
+    uncertainties: np.ndarray = field(default_factory=lambda: np.zeros(0))   # sigma
+
+
+class Context:
+    """Owns one sbo_ctx (one per thread, bound to a device)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = N.lib()
+        h = ctypes.c_void_p()
+        N.check(self._lib.sbo_create(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def set_stream(self, stream) -> None:
+        """Bind to a HIP stream (a torch.cuda.Stream, a raw handle int, or None)."""
+        raw = getattr(stream, "cuda_stream", stream)
+        N.check(self._lib.sbo_set_stream(self.handle, ctypes.c_void_p(raw) if raw else None), self.handle)
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.sbo_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, status: int) -> None:
+        N.check(status, self.handle)
+
+
+class TerrainMapper:
+    """GP posterior over a terrain grid (a1-a4) on one GPU."""
+
+    def __init__(self, device: int = 0, hyper: Hyper | None = None, ctx: Context | None = None):
+        self.ctx = ctx or Context(device)
+        self.hyper = hyper or Hyper()
+        self._lib = N.lib()
+        self._bounds = None
+
+    # -------------------------------------------------------------- fitting
+    def fit(self, x, y, obs, *, async_: bool = False) -> None:
+        (x, y, obs), fl = _prep([x, y, obs], np.float32, "float32")
+        if async_:
+            fl |= N.SBO_ASYNC
+        n = int(x.numel() if _is_dev(x) else x.size)
+        self._bounds = ((float(x.min()), float(x.max())), (float(y.min()), float(y.max()))) if n else None
+        self.ctx.check(self._lib.sbo_fit(self.ctx.handle, _ptr(x), _ptr(y), _ptr(obs), n,
+                                         _to_hyper(self.hyper), fl))
+
+    def append(self, x, y, obs) -> None:
+        (x, y, obs), fl = _prep([x, y, obs], np.float32, "float32")
+        b = int(x.numel() if _is_dev(x) else x.size)
+        self.ctx.check(self._lib.sbo_append(self.ctx.handle, _ptr(x), _ptr(y), _ptr(obs), b, fl))
+
+    @property
+    def n(self) -> int:
+        return int(self._lib.sbo_num_train(self.ctx.handle))
+
+    # ----------------------------------------------------------- prediction
+    def predict(self, qx, qy, *, out=None, async_: bool = False):
+        """Posterior mean and latent std at the queries (f32)."""
+        (qx, qy), fl = _prep([qx, qy], np.float32, "float32")
+        if async_:
+            fl |= N.SBO_ASYNC
+        m = int(qx.numel() if _is_dev(qx) else qx.size)
+        if out is None:
+            if fl & N.SBO_DEVICE_PTRS:
+                import torch
+                mu = torch.empty(m, dtype=torch.float32, device=qx.device)
+                sd = torch.empty_like(mu)
+            else:
+                mu = np.empty(m, np.float32)
+                sd = np.empty(m, np.float32)
+        else:
+            mu, sd = out
+        self.ctx.check(self._lib.sbo_predict(self.ctx.handle, _ptr(qx), _ptr(qy), m, _ptr(mu), _ptr(sd), fl))
+        return mu, sd
+
+    def tick(self, qx, qy, beta: float, f_min: float, *, score: int = N.SCORE_WIDTH, index_offset: int = 0,
+             outputs: dict | None = None, key_out=None, async_: bool = False):
+        """Fused predict -> ComputeSets -> masked argmax (the headline step).
+
+        ``outputs`` may hold preallocated mu/sd/lo/hi/safe arrays (None entries
+        are skipped).  Host mode returns an ``sbo_key``; device mode writes the
+        16-byte key into ``key_out`` (a device tensor) and returns it."""
+        (qx, qy), fl = _prep([qx, qy], np.float32, "float32")
+        if async_:
+            fl |= N.SBO_ASYNC
+        m = int(qx.numel() if _is_dev(qx) else qx.size)
+        o = outputs or {}
+        if fl & N.SBO_DEVICE_PTRS:
+            if key_out is None:
+                import torch
+                key_out = torch.empty(2, dtype=torch.int64, device=qx.device)
+            kp = ctypes.cast(ctypes.c_void_p(key_out.data_ptr()), ctypes.POINTER(N.sbo_key))
+            self.ctx.check(self._lib.sbo_tick(self.ctx.handle, _ptr(qx), _ptr(qy), m, float(beta), float(f_min),
+                                              int(score), int(index_offset), _ptr(o.get("mu")), _ptr(o.get("sd")),
+                                              _ptr(o.get("lo")), _ptr(o.get("hi")), _ptr(o.get("safe")), kp, fl))
+            return key_out
+        key = N.sbo_key()
+        self.ctx.check(self._lib.sbo_tick(self.ctx.handle, _ptr(qx), _ptr(qy), m, float(beta), float(f_min),
+                                          int(score), int(index_offset), _ptr(o.get("mu")), _ptr(o.get("sd")),
+                                          _ptr(o.get("lo")), _ptr(o.get("hi")), _ptr(o.get("safe")),
+                                          ctypes.byref(key), fl))
+        return key
+
+    # --------------------------------------------------------- test access
+    def factor(self):
+        """(L, alpha): L dense lower (row-major numpy f32), alpha f32."""
+        n = self.n
+        Lcm = np.empty(n * n, np.float32)
+        a = np.empty(n, np.float32)
+        self.ctx.check(self._lib.sbo_get_factor(self.ctx.handle, _ptr(Lcm), _ptr(a), 0))
+        return Lcm.reshape(n, n).T.copy(), a
+
+    def rbf_fill(self, x, y):
+        (x, y), fl = _prep([x, y], np.float32, "float32")
+        n = int(x.numel() if _is_dev(x) else x.size)
+        if fl & N.SBO_DEVICE_PTRS:
+            import torch
+            K = torch.empty(n * n, dtype=torch.float32, device=x.device)
+        else:
+            K = np.empty(n * n, np.float32)
+        self.ctx.check(self._lib.sbo_rbf_fill(self.ctx.handle, _ptr(x), _ptr(y), n, _to_hyper(self.hyper),
+                                              _ptr(K), fl))
+        return K.reshape(n, n)
+
+    # ------------------------------------------------------------- service
+    def get_terrain_map_with_uncertainty(self, resolution, x_range=None, y_range=None) -> TerrainMapResponse:
+        """Serve the node's request (resolution[2] f32, node.cpp:580-581).
+
+        The mapper's grid rule is not in the reference (the service "will
+        calculate dimensions from data bounds", :583-586).  Here the grid spans
+        the training-data bounds (or the given ranges) with
+        n = floor(extent / resolution) + 1 cells per axis, stored row-major
+        (y outer, x inner).  Parity of this rule is unpinned."""
+        if self.n == 0 or self._bounds is None:
+            return TerrainMapResponse(False, "no measurements", 0, 0)
+        rx, ry = (float(np.float32(r)) for r in resolution)
+        if not (rx > 0 and ry > 0):
+            return TerrainMapResponse(False, "resolution must be > 0", 0, 0)
+        x0, x1 = x_range if x_range is not None else self._bounds[0]
+        y0, y1 = y_range if y_range is not None else self._bounds[1]
+        w = int(np.floor((x1 - x0) / rx)) + 1
+        h = int(np.floor((y1 - y0) / ry)) + 1
+        gx = x0 + rx * np.arange(w)
+        gy = y0 + ry * np.arange(h)
+        QY, QX = np.meshgrid(gy, gx, indexing="ij")
+        return self.grid_response(QX.reshape(-1), QY.reshape(-1), w, h)
+
+    def grid_response(self, qx, qy, width: int, height: int) -> TerrainMapResponse:
+        mu, sd = self.predict(qx, qy)
+        return TerrainMapResponse(True, f"{width}x{height} grid, N={self.n}", int(width), int(height),
+                                  np.asarray(qx, np.float64), np.asarray(qy, np.float64),
+                                  np.asarray(mu), np.asarray(sd))
+
+    def close(self) -> None:
+        self.ctx.close()
