@@ -142,10 +142,9 @@ __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__r
 // Accuracy: a single f32 MFMA chain over all N training points accumulates
 // ~sqrt(N) roundings on large cancelling terms (2.2e-5 normwise variance
 // error at N = 8192, measured on the device and emulated on the host).  The
-// chain is therefore cut after every k-tile (BK = 32 k): each tile's MFMA
+// chain is therefore cut after every k-tile (BK = 64 k): each tile's MFMA
 // chain starts from a zero accumulator and its result is added into an f64
-// outer accumulator (emulated: 3.5e-6 at N = 8192, 9e-6 on an ill-conditioned
-// l = 0.7 / sn2 = 0.05 case where a plain f32 strsm is at 2.7e-5).
+// outer accumulator (2 VALU per accumulator register per tile).
 constexpr int kStageFloats = kTileFloats + 3 * kBK;
 
 template <bool MEAN>
@@ -159,9 +158,9 @@ __device__ __forceinline__ void predict_body(const float *__restrict__ tiles,
     const int row = lane & 31;
 
     // LDS-DMA staging (global_load_lds_dwordx4): each wave instruction moves
-    // 1 KiB, lane-linear; no staging registers.  A stage = the 16 KiB [BK][BM]
-    // tile (4 instructions per wave) + 384 B of per-k coordinates (wave 0,
-    // lanes 0-23).
+    // 1 KiB, lane-linear; no staging registers.  A stage = the 32 KiB [BK][BM]
+    // tile (8 instructions per wave) + 768 B of per-k coordinates (wave 0,
+    // lanes 0-47).
     const int wave = tid >> 6;
     typedef __attribute__((address_space(3))) void lds_void;
     const char *gA = reinterpret_cast<const char *>(tiles) + wave * 1024 + lane * 16;
@@ -172,7 +171,7 @@ __device__ __forceinline__ void predict_body(const float *__restrict__ tiles,
     do {                                                                                            \
         const char *s_ = gA + (int64_t)(kb) * kTileBytes;                                           \
         char *d_ = lA + (buf) * kStageBytes;                                                        \
-        _Pragma("unroll") for (int j = 0; j < 4; ++j)                                               \
+        _Pragma("unroll") for (int j = 0; j < kTileBytes / 4096; ++j)                               \
             __builtin_amdgcn_global_load_lds((const void *)(s_ + j * 4096), (lds_void *)(d_ + j * 4096), \
                                              16, 0, 0);                                             \
         if (wave == 0 && lane < kCBytes / 16)                                                       \

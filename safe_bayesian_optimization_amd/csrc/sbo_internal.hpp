@@ -21,7 +21,7 @@ namespace sbo {
 //   (4 waves x 32), BK training points per LDS stage.
 constexpr int kBM = 128;
 constexpr int kBN = 128;
-constexpr int kBK = 32;
+constexpr int kBK = 64;
 constexpr int kTileFloats = kBM * kBK;           // one packed [BK][BM] tile
 constexpr int kTilesPerRowBlockStep = kBM / kBK;  // k-tiles added per row block
 constexpr int kAcqThreads = 256;

@@ -44,3 +44,12 @@ def test_null_context_is_rejected_without_device():
     lib = N.lib()
     assert lib.sbo_fit(None, None, None, None, 0, N.sbo_hyper(0.4, 1, 0.1, 0), 0) == 1
     assert lib.sbo_tick(None, None, None, 0, 2.0, 0.0, 0, 0, None, None, None, None, None, None, 0) == 1
+
+
+def test_cpp_node_driver_builds_and_links():
+    """tools/sbo_tick_main.cpp (the C++ node mirror over include/sbo_node.hpp) links to libsbo."""
+    import subprocess
+    exe = os.path.join(ROOT, "safe_bayesian_optimization_amd", "lib", "sbo_tick_main")
+    assert os.path.exists(exe)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr

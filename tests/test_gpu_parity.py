@@ -313,3 +313,30 @@ def test_c3_properties(dev):
     assert nrel(mu.cpu().numpy()[sel], omu) < REL_TOL
     assert nrel(sdn[sel].astype(np.float64) ** 2, ovar) < REL_TOL
     gm.close()
+
+
+def test_cpp_node_driver_tick(mapper):
+    """The C++ host path (include/sbo_node.hpp) reproduces the Python workload
+    bit for bit (same SplitMix64 inputs) and its fused-tick argmax equals the
+    node-path argmax; its subgoal equals the Python OptimizerCore's."""
+    import json
+    import os
+    import subprocess
+    from safe_bayesian_optimization_amd import OptimizerCore
+    from safe_bayesian_optimization_amd.gp import TerrainMapResponse
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "safe_bayesian_optimization_amd", "lib", "sbo_tick_main")
+    r = subprocess.run([exe, "1500", "120", "90", "3", "1.5", "2.0"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    wl = synthetic(1500, 120, 90, seed=3)
+    assert abs(out["f_min"] - wl.f_min) <= 1e-12 * max(1.0, abs(wl.f_min))
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    mu, sd = gm.predict(wl.qx, wl.qy)
+    node = OptimizerCore(2.0, out["f_min"], ctx=mapper.ctx)
+    node.goal_point_callback(1.5, 2.0)
+    node.process_terrain_map(TerrainMapResponse(True, "", 120, 90, wl.qx, wl.qy, mu, sd))
+    assert int(node.S_.sum()) == out["safe"]
+    assert node.GetNextSubgoal() == out["subgoal"]
+    assert node.FindSafetyContourIndices().size == out["frontier"]

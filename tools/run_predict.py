@@ -1,0 +1,42 @@
+"""Fit once and run K planning ticks on cuda:0 (profiling driver for rocprofv3)."""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--config", default="C2")
+    p.add_argument("--n", type=int)
+    p.add_argument("--grid", type=int)
+    p.add_argument("--ticks", type=int, default=3)
+    a = p.parse_args()
+    import torch
+    from safe_bayesian_optimization_amd import TerrainMapper, synthetic
+    from safe_bayesian_optimization_amd.terrain import CONFIGS
+    n, gw, gh = CONFIGS[a.config]
+    n = a.n or n
+    if a.grid:
+        gw = gh = a.grid
+    wl = synthetic(n, gw, gh, seed=0)
+    dev = torch.device("cuda:0")
+    t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
+    gm = TerrainMapper(0, wl.hyper)
+    gm.fit(t(wl.x), t(wl.y), t(wl.obs))
+    qx, qy = t(wl.qx), t(wl.qy)
+    m = qx.numel()
+    outs = dict(mu=torch.empty(m, device=dev), sd=torch.empty(m, device=dev),
+                lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
+                safe=torch.empty(m, dtype=torch.uint8, device=dev))
+    for _ in range(a.ticks):
+        gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs)
+    torch.cuda.synchronize()
+    print("done", n, m)
+
+
+if __name__ == "__main__":
+    main()
