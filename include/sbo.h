@@ -161,7 +161,7 @@ SBO_API int64_t sbo_find_contours_external(const uint8_t *img, int width, int he
 SBO_API sbo_status sbo_rbf_fill(sbo_ctx *ctx, const float *x, const float *y, int64_t n,
                                 sbo_hyper hyper, float *K, uint32_t flags);
 /* Copy out the current factor L (n x n column-major, lower; upper part
- * zeroed) and alpha (n). */
+ * zeroed) and alpha (n), both in the internal training order (sbo_get_order). */
 SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t flags);
 
 /* Options.  SBO_OPT_INVERSE_BITS (32 | 64, default 64): precision in which
@@ -169,7 +169,23 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * sweep (64 = widen L, rocsolver_dtrtri; 32 = rocsolver_strtri).  Takes
  * effect at the next sbo_fit / sbo_append. */
 #define SBO_OPT_INVERSE_BITS 1
+/* SBO_OPT_SPATIAL_ORDER (0 | 1, default 1): store the training points in
+ * Morton order (sbo_fit sorts all points, sbo_append sorts each batch), so
+ * every 64-point k-tile of the predictive sweep is spatially compact.  The
+ * posterior does not depend on the order; sbo_get_factor returns the factor
+ * of the internally ordered K and sbo_get_order the caller's index of each
+ * internal row.  Takes effect at the next sbo_fit / sbo_append. */
+#define SBO_OPT_SPATIAL_ORDER 2
+/* SBO_OPT_TILE_SKIP (0 | 1, default 1): skip k-tiles whose K* block is
+ * exactly +0.0 in f32 for every query of a workgroup (bounding boxes farther
+ * apart than the exp2 underflow radius).  Results are bitwise identical to
+ * the dense sweep. */
+#define SBO_OPT_TILE_SKIP 3
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
+
+/* order[i] = the caller's index (position in the sbo_fit / sbo_append
+ * inputs, appends numbered after the fit) of internal training row i. */
+SBO_API sbo_status sbo_get_order(const sbo_ctx *ctx, int64_t *order);
 
 /* Test accessor: the packed predictive operand A = sf2 * L^-1 unpacked into a
  * dense n x n ROW-major f32 host array (upper triangle left untouched). */
@@ -182,6 +198,9 @@ SBO_API sbo_status sbo_get_inverse(sbo_ctx *ctx, float *Linv);
 SBO_API sbo_status sbo_profile(sbo_ctx *ctx, int enable);
 SBO_API sbo_status sbo_profile_read(sbo_ctx *ctx, double *predict_ms, int64_t *predict_launches,
                                     double *fill_ms, int64_t *fill_launches);
+/* MFMA flops the predictive sweep actually executed since sbo_profile(ctx, 1)
+ * (2*BM*BN*BK per multiplied tile; skipped exactly-zero tiles excluded). */
+SBO_API sbo_status sbo_profile_work(sbo_ctx *ctx, double *predict_flops);
 
 #ifdef __cplusplus
 }

@@ -126,6 +126,20 @@ __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__r
     c[2 * kBK + o] = in ? sf2 * alpha[k] : 0.0f;
 }
 
+// Bounding box of each k-tile's valid training points: (xmin, xmax, ymin, ymax);
+// a tile with no valid point gets an empty box (+inf, -inf, +inf, -inf).
+__global__ void tile_box_kernel(const float *__restrict__ x, const float *__restrict__ y, int64_t n,
+                                int64_t ntiles, float4 *__restrict__ kbox) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+    for (int64_t k = t * kBK; k < (t + 1) * kBK && k < n; ++k) {
+        x0 = fminf(x0, x[k]); x1 = fmaxf(x1, x[k]);
+        y0 = fminf(y0, y[k]); y1 = fmaxf(y1, y[k]);
+    }
+    kbox[t] = make_float4(x0, x1, y0, y1);
+}
+
 // ---------------------------------------------------------- a3+a4 predict
 // Workgroup (I, qb): rows [I*BM, I*BM+BM) of A = sf2 L^-1 and the BN = 128
 // queries [qb*BN, qb*BN+BN).  Wave w owns queries qb*BN + 32w + (l&31) and all
@@ -136,8 +150,16 @@ __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__r
 // B-fragment map -- so K* never touches LDS or HBM: one exp2 per lane per
 // four MFMAs.  The A tile [BK][BM] is staged through LDS (double buffered,
 // one barrier per stage); lanes 0-31 / 32-63 read consecutive rows of
-// adjacent k (conflict-free ds_read_b32).  The mean rides along in the last
-// row block (every k visited) as an f64 FMA per k pair.
+// adjacent k (conflict-free).  The mean rides along in the last row block
+// (every k visited) as an f64 FMA per k pair.
+//
+// Exact tile skipping: a k-tile whose bounding box is farther from the
+// workgroup's query bounding box than the f32 underflow radius
+// (c*d^2 < -160, i.e. |d| > 14.9 l) contributes K* == +0.0 to every product,
+// so it adds exactly nothing to any accumulator.  Each workgroup first
+// compacts the list of k-tiles it needs (ascending, so the surviving
+// accumulation order is unchanged and results are bitwise identical to the
+// dense sweep) and only stages and multiplies those.
 //
 // Accuracy: a single f32 MFMA chain over all N training points accumulates
 // ~sqrt(N) roundings on large cancelling terms (2.2e-5 normwise variance
@@ -146,11 +168,13 @@ __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__r
 // chain starts from a zero accumulator and its result is added into an f64
 // outer accumulator (2 VALU per accumulator register per tile).
 constexpr int kStageFloats = kTileFloats + 3 * kBK;
+constexpr int kMaxList = 2048;  // k-tiles a workgroup can list (N <= 131072); beyond: dense
+constexpr int kSmemFloats = 2 * kStageFloats + kMaxList + 32;
 
 template <bool MEAN>
 __device__ __forceinline__ void predict_body(const float *__restrict__ tiles,
-                                             const float *__restrict__ kc, int nkb, float xq,
-                                             float yq, float cexp, float *smem,
+                                             const float *__restrict__ kc, const int *tlist,
+                                             int cnt, float xq, float yq, float cexp, float *smem,
                                              double (&outer)[4][16], double &mu) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -183,13 +207,14 @@ __device__ __forceinline__ void predict_body(const float *__restrict__ tiles,
 
     f32x16 acc[4];
     const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (cnt == 0) return;
 
-    SBO_STAGE(0, 0);
+    SBO_STAGE(tlist ? tlist[0] : 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int kb = 0; kb < nkb; ++kb) {
-        const int cur = kb & 1;
-        if (kb + 1 < nkb) SBO_STAGE(kb + 1, cur ^ 1);
+    for (int i = 0; i < cnt; ++i) {
+        const int cur = i & 1;
+        if (i + 1 < cnt) SBO_STAGE(tlist ? tlist[i + 1] : i + 1, cur ^ 1);
         const float *sA = smem + cur * kStageFloats;
         const float *sC = sA + kTileFloats;
 #pragma unroll
@@ -213,25 +238,84 @@ __device__ __forceinline__ void predict_body(const float *__restrict__ tiles,
 #undef SBO_STAGE
 }
 
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
 __global__ __launch_bounds__(256, 2) void predict_kernel(const float *__restrict__ aug,
-                                                         const float *__restrict__ kcoord, int nI,
+                                                         const float *__restrict__ kcoord,
+                                                         const float4 *__restrict__ kbox, int nI,
                                                          int nQ, const float *__restrict__ qx,
                                                          const float *__restrict__ qy, int64_t m,
-                                                         int64_t ldp, float cexp, float m0,
-                                                         float *__restrict__ part,
-                                                         float *__restrict__ mean) {
-    __shared__ __attribute__((aligned(16))) float smem[2 * kStageFloats];
+                                                         int64_t ldp, float cexp, float skip_d2,
+                                                         float m0, float *__restrict__ part,
+                                                         float *__restrict__ mean,
+                                                         unsigned long long *__restrict__ tiles_done) {
+    __shared__ __attribute__((aligned(16))) float smem[kSmemFloats];
+    int *tlist = reinterpret_cast<int *>(smem + 2 * kStageFloats);
+    float *wbox = smem + 2 * kStageFloats + kMaxList;       // [4 waves][4]
+    int *wcnt = reinterpret_cast<int *>(wbox + 16);         // [4 waves]
     const int64_t bid = blockIdx.x;
     const int I = nI - 1 - (int)(bid / nQ);  // heaviest row blocks first
     const int64_t qb = bid % nQ;
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
     const int nkb = (I + 1) * kTilesPerRowBlockStep;
     const float *tiles = aug + tile_start(I) * kTileFloats;
 
     const int64_t q = qb * kBN + wave * 32 + (lane & 31);
     const int64_t qc = q < m ? q : m - 1;
     const float xq = qx[qc], yq = qy[qc];
+
+    // ---- list the k-tiles this workgroup needs (ascending)
+    int cnt = nkb;
+    const int *list = nullptr;
+    if (skip_d2 > 0.0f && nkb <= kMaxList) {
+        const float bx0 = wave_min(xq), bx1 = wave_max(xq), by0 = wave_min(yq), by1 = wave_max(yq);
+        if (lane == 0) {
+            wbox[wave * 4 + 0] = bx0; wbox[wave * 4 + 1] = bx1;
+            wbox[wave * 4 + 2] = by0; wbox[wave * 4 + 3] = by1;
+        }
+        __syncthreads();
+        float qx0 = wbox[0], qx1 = wbox[1], qy0 = wbox[2], qy1 = wbox[3];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            qx0 = fminf(qx0, wbox[w * 4 + 0]); qx1 = fmaxf(qx1, wbox[w * 4 + 1]);
+            qy0 = fminf(qy0, wbox[w * 4 + 2]); qy1 = fmaxf(qy1, wbox[w * 4 + 3]);
+        }
+        int base = 0;
+        for (int t0 = 0; t0 < nkb; t0 += 256) {
+            const int t = t0 + tid;
+            bool keep = false;
+            if (t < nkb) {
+                const float4 b = kbox[t];  // (xmin, xmax, ymin, ymax); empty tile = (+inf, -inf, ..)
+                const float dx = fmaxf(0.0f, fmaxf(b.x - qx1, qx0 - b.y));
+                const float dy = fmaxf(0.0f, fmaxf(b.z - qy1, qy0 - b.w));
+                keep = fmaf(dy, dy, dx * dx) <= skip_d2;
+            }
+            const unsigned long long bal = __ballot(keep);
+            const int before = __popcll(bal & ((1ull << lane) - 1ull));
+            __syncthreads();  // previous chunk's wcnt reads are done
+            if (lane == 0) wcnt[wave] = __popcll(bal);
+            __syncthreads();
+            int off = base;
+            for (int w = 0; w < wave; ++w) off += wcnt[w];
+            if (keep) tlist[off + before] = t;
+            base += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        }
+        __syncthreads();
+        cnt = base;
+        list = tlist;
+    }
+    if (tid == 0 && tiles_done) atomicAdd(tiles_done, (unsigned long long)cnt);  // executed-work counter
 
     double outer[4][16];
 #pragma unroll
@@ -242,9 +326,9 @@ __global__ __launch_bounds__(256, 2) void predict_kernel(const float *__restrict
 
     const bool last = (I == nI - 1);
     if (last)
-        predict_body<true>(tiles, kcoord, nkb, xq, yq, cexp, smem, outer, mu);
+        predict_body<true>(tiles, kcoord, list, cnt, xq, yq, cexp, smem, outer, mu);
     else
-        predict_body<false>(tiles, kcoord, nkb, xq, yq, cexp, smem, outer, mu);
+        predict_body<false>(tiles, kcoord, list, cnt, xq, yq, cexp, smem, outer, mu);
 
     // epilogue: column sums of V^2 over this block's rows; lanes l and l+32 hold
     // the two row halves of column l&31 of each 32x32 accumulator
@@ -432,16 +516,26 @@ hipError_t launch_widen_lower(hipStream_t s, const float *src, int64_t ld_src, i
     return hipGetLastError();
 }
 
-hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, int64_t npad,
-                          const float *qx, const float *qy, int64_t m, int64_t ldp, float ell, float m0,
-                          float *part, float *mean) {
+hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int64_t n, int64_t npad, float4 *kbox) {
+    const int64_t nt = npad / kBK;
+    hipLaunchKernelGGL(tile_box_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, x, y, n, nt, kbox);
+    return hipGetLastError();
+}
+
+hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox, int64_t npad,
+                          const float *qx, const float *qy, int64_t m, int64_t ldp, float ell, float m0, bool skip,
+                          float *part, float *mean, unsigned long long *tiles_done) {
     const int nI = (int)(npad / kBM);
     const int64_t nQ = (m + kBN - 1) / kBN;
-    const float cexp = (float)(-1.0 / (2.0 * (double)ell * (double)ell * 0.69314718055994530942));
+    const double ce = -1.0 / (2.0 * (double)ell * (double)ell * 0.69314718055994530942);
+    const float cexp = (float)ce;
+    // k-tiles farther than this squared distance give c*d^2 < -160: exp2 is
+    // exactly +0.0 in f32 (0.1% margin over the kernel's own rounding)
+    const float skip_d2 = skip ? (float)(160.0 / -ce * 1.001) : -1.0f;
     const int64_t blocks = (int64_t)nI * nQ;
     if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(predict_kernel, dim3((unsigned)blocks), dim3(256), 0, s, aug, kcoord, nI,
-                       (int)nQ, qx, qy, m, ldp, cexp, m0, part, mean);
+    hipLaunchKernelGGL(predict_kernel, dim3((unsigned)blocks), dim3(256), 0, s, aug, kcoord, kbox, nI, (int)nQ, qx,
+                       qy, m, ldp, cexp, skip_d2, m0, part, mean, tiles_done);
     return hipGetLastError();
 }
 

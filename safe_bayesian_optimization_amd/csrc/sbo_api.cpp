@@ -65,11 +65,58 @@ sbo_status check_hyper(sbo_ctx *ctx, const sbo_hyper &h) {
     return SBO_OK;
 }
 
-// Copy an input array into a device buffer (D2D or H2D).
-sbo_status stage_in(sbo_ctx *ctx, void *dst, const void *src, size_t bytes, uint32_t flags) {
-    if (bytes == 0) return SBO_OK;
-    SBO_HIP(hipMemcpyAsync(dst, src, bytes, dev(flags) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                           ctx->stream));
+// 32-bit Morton (Z-order) code of a point quantised to 16 bits per axis.
+uint32_t morton2(uint32_t a, uint32_t b) {
+    auto spread = [](uint32_t v) {
+        v &= 0xFFFFu;
+        v = (v | (v << 8)) & 0x00FF00FFu;
+        v = (v | (v << 4)) & 0x0F0F0F0Fu;
+        v = (v | (v << 2)) & 0x33333333u;
+        v = (v | (v << 1)) & 0x55555555u;
+        return v;
+    };
+    return spread(a) | (spread(b) << 1);
+}
+
+// Copy `count` measurements into the context's training buffers at `dst`,
+// in Morton order when ctx->spatial_order (so every 64-point k-tile is
+// spatially compact and far tiles can be skipped exactly), and record the
+// caller's index of each internal row in ctx->order.
+sbo_status stage_training(sbo_ctx *ctx, const float *x, const float *y, const float *obs, int64_t count,
+                          int64_t dst, int64_t index_base, uint32_t flags) {
+    std::vector<float> hx(count), hy(count), ho(count);
+    const hipMemcpyKind k = dev(flags) ? hipMemcpyDeviceToHost : hipMemcpyHostToHost;
+    SBO_HIP(hipMemcpyAsync(hx.data(), x, sizeof(float) * count, k, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(hy.data(), y, sizeof(float) * count, k, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(ho.data(), obs, sizeof(float) * count, k, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<int64_t> perm(count);
+    for (int64_t i = 0; i < count; ++i) perm[i] = i;
+    if (ctx->spatial_order && count > 1) {
+        const auto mx = std::minmax_element(hx.begin(), hx.end());
+        const auto my = std::minmax_element(hy.begin(), hy.end());
+        const double x0 = *mx.first, sx = std::max(1e-30, (double)*mx.second - x0);
+        const double y0 = *my.first, sy = std::max(1e-30, (double)*my.second - y0);
+        std::vector<uint32_t> code(count);
+        for (int64_t i = 0; i < count; ++i) {
+            const double u = std::min(1.0, std::max(0.0, (hx[i] - x0) / sx));
+            const double v = std::min(1.0, std::max(0.0, (hy[i] - y0) / sy));
+            code[i] = std::isfinite(u) && std::isfinite(v) ? morton2((uint32_t)(u * 65535.0), (uint32_t)(v * 65535.0)) : 0;
+        }
+        std::stable_sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return code[a] < code[b]; });
+    }
+    std::vector<float> px(count), py(count), po(count);
+    for (int64_t i = 0; i < count; ++i) {
+        px[i] = hx[perm[i]];
+        py[i] = hy[perm[i]];
+        po[i] = ho[perm[i]];
+    }
+    SBO_HIP(hipMemcpyAsync(ctx->x.as<float>() + dst, px.data(), sizeof(float) * count, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(ctx->y.as<float>() + dst, py.data(), sizeof(float) * count, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(ctx->obs.as<float>() + dst, po.data(), sizeof(float) * count, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->order.resize((size_t)dst);
+    for (int64_t i = 0; i < count; ++i) ctx->order.push_back(index_base + perm[i]);
     return SBO_OK;
 }
 
@@ -164,6 +211,8 @@ sbo_status refresh_operand(sbo_ctx *ctx) {
         SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, ld, n, npad, sf2, ctx->x.as<float>(), ctx->y.as<float>(),
                                          alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
     }
+    SBO_HIP(ctx->kbox.reserve(sizeof(float4) * (size_t)(npad / sbo::kBK)));
+    SBO_HIP(sbo::launch_tile_boxes(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, npad, ctx->kbox.as<float4>()));
     SBO_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
     SBO_CHECK(hinfo == 0, SBO_E_NOT_SPD, "trtri: singular factor (info=" + std::to_string(hinfo) + ")");
@@ -201,9 +250,11 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     sbo_key *bkeys = ctx->keys.as<sbo_key>();
     {
         Bracket br(ctx, ctx->ev_predict);
-        SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(), ctx->npad, qx, qy,
-                                    m, ldp, (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean,
-                                    ctx->part.as<float>(), ctx->mean.as<float>()));
+        SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(),
+                                    ctx->kbox.as<float4>(), ctx->npad, qx, qy, m, ldp,
+                                    (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, ctx->tile_skip,
+                                    ctx->part.as<float>(), ctx->mean.as<float>(),
+                                    ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr));
     }
     const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
     SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<float>(), ctx->mean.as<float>(), (int)nI, ldp, m, sf2,
@@ -292,9 +343,7 @@ SBO_API sbo_status sbo_fit(sbo_ctx *ctx, const float *x, const float *y, const f
     SBO_HIP(ctx->obs.reserve(sizeof(float) * n));
     SBO_HIP(ctx->alpha.reserve(sizeof(float) * n));
     SBO_HIP(ctx->L.reserve(sizeof(float) * (size_t)n * (size_t)n));
-    if (sbo_status st = stage_in(ctx, ctx->x.as<float>(), x, sizeof(float) * n, flags)) return st;
-    if (sbo_status st = stage_in(ctx, ctx->y.as<float>(), y, sizeof(float) * n, flags)) return st;
-    if (sbo_status st = stage_in(ctx, ctx->obs.as<float>(), obs, sizeof(float) * n, flags)) return st;
+    if (sbo_status st = stage_training(ctx, x, y, obs, n, 0, 0, flags)) return st;
     const float sf2 = (float)(hyper.sigma_f * hyper.sigma_f);
     {
         Bracket br(ctx, ctx->ev_fill);
@@ -340,9 +389,7 @@ SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, cons
         SBO_HIP(ctx->alpha.reserve(sizeof(float) * ncap));
     }
     const int64_t ld = ctx->cap;
-    if (sbo_status st = stage_in(ctx, ctx->x.as<float>() + n0, x, sizeof(float) * b, flags)) return st;
-    if (sbo_status st = stage_in(ctx, ctx->y.as<float>() + n0, y, sizeof(float) * b, flags)) return st;
-    if (sbo_status st = stage_in(ctx, ctx->obs.as<float>() + n0, obs, sizeof(float) * b, flags)) return st;
+    if (sbo_status st = stage_training(ctx, x, y, obs, b, n0, n0, flags)) return st;
 
     // Block Cholesky update of the lower factor (column-major, lda = ld):
     //   [L11  0 ]   K21 = k(Xnew, X)  -> L21 = K21 L11^-T        (trsm)
@@ -553,6 +600,20 @@ SBO_API sbo_status sbo_profile(sbo_ctx *ctx, int enable) {
     SBO_HIP(hipStreamSynchronize(ctx->stream));
     recycle_events(ctx);
     ctx->prof = enable != 0;
+    SBO_HIP(ctx->counters.reserve(64));
+    SBO_HIP(hipMemsetAsync(ctx->counters.as<void>(), 0, 64, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_profile_work(sbo_ctx *ctx, double *predict_flops) {
+    if (!ctx || !predict_flops) return SBO_E_INVAL;
+    unsigned long long t = 0;
+    if (ctx->counters.capacity()) {
+        SBO_HIP(hipMemcpyAsync(&t, ctx->counters.as<void>(), sizeof(t), hipMemcpyDeviceToHost, ctx->stream));
+        SBO_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    *predict_flops = 2.0 * sbo::kBM * sbo::kBN * sbo::kBK * (double)t;
     return SBO_OK;
 }
 
@@ -582,9 +643,22 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             SBO_CHECK(value == 32 || value == 64, SBO_E_INVAL, "SBO_OPT_INVERSE_BITS must be 32 or 64");
             ctx->inverse_bits = (int)value;
             return SBO_OK;
+        case SBO_OPT_SPATIAL_ORDER:
+            ctx->spatial_order = value != 0;
+            return SBO_OK;
+        case SBO_OPT_TILE_SKIP:
+            ctx->tile_skip = value != 0;
+            return SBO_OK;
     }
     ctx->err = "unknown option " + std::to_string(option);
     return SBO_E_INVAL;
+}
+
+SBO_API sbo_status sbo_get_order(const sbo_ctx *ctx, int64_t *order) {
+    if (!ctx || !order) return SBO_E_INVAL;
+    if (!ctx->fitted) return SBO_E_STATE;
+    std::copy(ctx->order.begin(), ctx->order.begin() + ctx->n, order);
+    return SBO_OK;
 }
 
 SBO_API sbo_status sbo_get_inverse(sbo_ctx *ctx, float *Linv) {

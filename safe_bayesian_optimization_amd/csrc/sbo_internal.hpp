@@ -84,6 +84,10 @@ struct sbo_ctx {
     sbo::DevBuf L;               // lower Cholesky factor, column-major, lda = cap
     sbo::DevBuf Linv;            // workspace: L^-1 (strtri f32, lda = cap, or dtrtri f64, lda = n)
     int inverse_bits = 64;       // SBO_OPT_INVERSE_BITS: precision of the L^-1 computation
+    bool spatial_order = true;   // SBO_OPT_SPATIAL_ORDER: Morton-order the training points
+    bool tile_skip = true;       // SBO_OPT_TILE_SKIP: skip exactly-zero K* tiles
+    std::vector<int64_t> order;  // internal row -> caller's training index
+    sbo::DevBuf kbox;            // per k-tile bounding boxes (float4)
     sbo::DevBuf alpha;           // K^-1 (y - m0), length cap
     sbo::DevBuf aug;             // packed sf2 * L^-1 tiles
     sbo::DevBuf kcoord;          // per k-tile: x[BK], y[BK], sf2*alpha[BK]
@@ -102,6 +106,7 @@ struct sbo_ctx {
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;               // free events
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_predict, ev_fill;
+    sbo::DevBuf counters;                          // [0]: predictive tiles multiplied
 
     bool fail(const std::string &m) { err = m; return false; }
 };
@@ -129,9 +134,15 @@ hipError_t launch_pack_operand(hipStream_t s, const double *Linv, int64_t ld, in
 hipError_t launch_widen_lower(hipStream_t s, const float *src, int64_t ld_src, int64_t n, double *dst);
 // Predictive sweep: part[I][q] = sum over rows of block I of (sf2 L^-1 k_q)^2,
 // mean[q] = m0 + sf2 alpha^T k_q.
-hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, int64_t npad,
-                          const float *qx, const float *qy, int64_t m, int64_t ldp,
-                          float ell, float m0, float *part, float *mean);
+// skip: drop k-tiles whose K* block is exactly zero (bitwise-identical result).
+// tiles_done (may be null): += number of (BM x BN x BK) tiles multiplied.
+hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox,
+                          int64_t npad, const float *qx, const float *qy, int64_t m, int64_t ldp,
+                          float ell, float m0, bool skip, float *part, float *mean,
+                          unsigned long long *tiles_done);
+// Per k-tile bounding boxes of the (internally ordered) training points.
+hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int64_t n, int64_t npad,
+                             float4 *kbox);
 // Acquisition over predictive partials (fused reduce + sets + block argmax).
 hipError_t launch_acquire(hipStream_t s, const float *part, const float *mean, int nI, int64_t ldp,
                           int64_t m, float sf2, double beta, double f_min, int score_kind,

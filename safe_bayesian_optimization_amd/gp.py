@@ -171,8 +171,18 @@ class TerrainMapper:
         return key
 
     # --------------------------------------------------------- test access
+    def order(self) -> np.ndarray:
+        """Caller's training index of each internal row (the factor's order)."""
+        o = np.empty(self.n, np.int64)
+        self.ctx.check(self._lib.sbo_get_order(self.ctx.handle, _ptr(o)))
+        return o
+
+    def set_option(self, option: int, value: int) -> None:
+        self.ctx.check(self._lib.sbo_set_option(self.ctx.handle, int(option), int(value)))
+
     def factor(self):
-        """(L, alpha): L dense lower (row-major numpy f32), alpha f32."""
+        """(L, alpha) in the internal training order (see ``order()``):
+        L dense lower (row-major numpy f32), alpha f32."""
         n = self.n
         Lcm = np.empty(n * n, np.float32)
         a = np.empty(n, np.float32)

@@ -56,12 +56,15 @@ def ulp_diff(a, b):
 
 
 def oracle_given_factor(gm, wl, qx=None, qy=None):
+    """fp64 oracle prediction from the device's own factor (in its internal
+    training order, gm.order())."""
     L, alpha = gm.factor()
+    o = gm.order()
     Lcm = O.colmajor_from_lower(L.astype(np.float64))
     qx = wl.qx if qx is None else qx
     qy = wl.qy if qy is None else qy
     h = wl.hyper
-    return O.predict(Lcm, alpha.astype(np.float64), f32(wl.x), f32(wl.y), f32(qx), f32(qy),
+    return O.predict(Lcm, alpha.astype(np.float64), f32(wl.x)[o], f32(wl.y)[o], f32(qx), f32(qy),
                      h.length_scale, h.sf2, h.prior_mean)
 
 
@@ -91,12 +94,14 @@ def test_cholesky_backward_error(mapper, n):
     wl = synthetic(n, 8, seed=n + 1)
     mapper.fit(wl.x, wl.y, wl.obs)
     L, alpha = mapper.factor()
-    K = O.rbf_fill_f32in(f32(wl.x), f32(wl.y))
+    o = mapper.order()
+    assert np.array_equal(np.sort(o), np.arange(n))
+    K = O.rbf_fill_f32in(f32(wl.x)[o], f32(wl.y)[o])
     L64 = L.astype(np.float64)
     be = np.linalg.norm(L64 @ L64.T - K) / np.linalg.norm(K)
     assert be <= 10 * n * EPS32, be
     # alpha solves K alpha = y - m0 to f32 accuracy
-    r = K @ alpha.astype(np.float64) - wl.obs
+    r = K @ alpha.astype(np.float64) - wl.obs[o]
     assert np.linalg.norm(r) / np.linalg.norm(wl.obs) < 1e-3
 
 
@@ -135,7 +140,8 @@ def test_predict_nondefault_hyper(mapper):
     # accurate as it, and within 1e-5 whenever that is.
     import scipy.linalg as sla
     L, _ = gm.factor()
-    xs, ys, qx, qy = (f32(v).astype(np.float64) for v in (wl.x, wl.y, wl.qx, wl.qy))
+    o = gm.order()
+    xs, ys, qx, qy = (f32(v).astype(np.float64) for v in (wl.x[o], wl.y[o], wl.qx, wl.qy))
     Ks = (h.sf2 * np.exp(-((xs[:, None] - qx[None, :]) ** 2 + (ys[:, None] - qy[None, :]) ** 2)
                          / (2 * h.length_scale ** 2))).astype(np.float32)
     V = sla.solve_triangular(L, Ks, lower=True).astype(np.float64)
@@ -263,6 +269,40 @@ def test_tick_empty_safe_set(mapper):
     mapper.fit(wl.x, wl.y, wl.obs)
     k = mapper.tick(wl.qx, wl.qy, wl.beta, 1e9)
     assert k.idx == -1
+
+
+# --------------------------------------------------------- exact tile skipping
+def test_tile_skip_is_bitwise_exact(dev, mapper):
+    """N = 8192 over a 32 l domain: far k-tiles are skipped; mu, sd and the key
+    must be bitwise identical to the dense sweep (SBO_OPT_TILE_SKIP = 0)."""
+    wl = synthetic(8192, 200, 160, seed=21)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    res = {}
+    for skip in (1, 0):
+        gm.set_option(N.SBO_OPT_TILE_SKIP, skip)
+        m = wl.qx.size
+        out = dict(mu=np.empty(m, np.float32), sd=np.empty(m, np.float32))
+        k = gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
+        res[skip] = (out["mu"], out["sd"], k.idx, k.score)
+    gm.set_option(N.SBO_OPT_TILE_SKIP, 1)
+    assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
+    assert res[0][2:] == res[1][2:]
+
+
+def test_spatial_order_does_not_change_the_posterior(mapper):
+    wl = synthetic(3000, 64, 48, seed=22)
+    out = {}
+    for order in (1, 0):
+        gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+        gm.set_option(N.SBO_OPT_SPATIAL_ORDER, order)
+        gm.fit(wl.x, wl.y, wl.obs)
+        if not order:
+            assert np.array_equal(gm.order(), np.arange(3000))
+        out[order] = gm.predict(wl.qx, wl.qy)
+    gm.set_option(N.SBO_OPT_SPATIAL_ORDER, 1)
+    assert nrel(out[1][0], out[0][0].astype(np.float64)) < 1e-5
+    assert nrel(out[1][1].astype(np.float64) ** 2, out[0][1].astype(np.float64) ** 2) < 1e-5
 
 
 # ---------------------------------------------------------------- (C5) append
