@@ -523,15 +523,16 @@ hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int6
 }
 
 hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox, int64_t npad,
-                          const float *qx, const float *qy, int64_t m, int64_t ldp, float ell, float m0, bool skip,
+                          const float *qx, const float *qy, int64_t m, int64_t ldp, float ell, float m0, int skip_log2,
                           float *part, float *mean, unsigned long long *tiles_done) {
     const int nI = (int)(npad / kBM);
     const int64_t nQ = (m + kBN - 1) / kBN;
     const double ce = -1.0 / (2.0 * (double)ell * (double)ell * 0.69314718055994530942);
     const float cexp = (float)ce;
-    // k-tiles farther than this squared distance give c*d^2 < -160: exp2 is
-    // exactly +0.0 in f32 (0.1% margin over the kernel's own rounding)
-    const float skip_d2 = skip ? (float)(160.0 / -ce * 1.001) : -1.0f;
+    // k-tiles farther than this squared distance give c*d^2 < -skip_log2, i.e.
+    // every K* entry < 2^-skip_log2 (0.1% margin over the kernel's rounding);
+    // skip_log2 >= 150 means every such entry is exactly +0.0 in f32
+    const float skip_d2 = skip_log2 > 0 ? (float)((double)skip_log2 / -ce * 1.001) : -1.0f;
     const int64_t blocks = (int64_t)nI * nQ;
     if (blocks > 0x7fffffff) return hipErrorInvalidValue;
     hipLaunchKernelGGL(predict_kernel, dim3((unsigned)blocks), dim3(256), 0, s, aug, kcoord, kbox, nI, (int)nQ, qx,

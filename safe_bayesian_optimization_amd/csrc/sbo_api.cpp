@@ -252,7 +252,7 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         Bracket br(ctx, ctx->ev_predict);
         SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(),
                                     ctx->kbox.as<float4>(), ctx->npad, qx, qy, m, ldp,
-                                    (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, ctx->tile_skip,
+                                    (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, ctx->skip_log2,
                                     ctx->part.as<float>(), ctx->mean.as<float>(),
                                     ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr));
     }
@@ -647,7 +647,9 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->spatial_order = value != 0;
             return SBO_OK;
         case SBO_OPT_TILE_SKIP:
-            ctx->tile_skip = value != 0;
+            SBO_CHECK(value == 0 || (value >= 16 && value <= 1000), SBO_E_INVAL,
+                      "SBO_OPT_TILE_SKIP must be 0 (dense) or a cutoff exponent in [16, 1000]");
+            ctx->skip_log2 = (int)value;
             return SBO_OK;
     }
     ctx->err = "unknown option " + std::to_string(option);

@@ -85,7 +85,7 @@ struct sbo_ctx {
     sbo::DevBuf Linv;            // workspace: L^-1 (strtri f32, lda = cap, or dtrtri f64, lda = n)
     int inverse_bits = 64;       // SBO_OPT_INVERSE_BITS: precision of the L^-1 computation
     bool spatial_order = true;   // SBO_OPT_SPATIAL_ORDER: Morton-order the training points
-    bool tile_skip = true;       // SBO_OPT_TILE_SKIP: skip exactly-zero K* tiles
+    int skip_log2 = 64;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-skip_log2
     std::vector<int64_t> order;  // internal row -> caller's training index
     sbo::DevBuf kbox;            // per k-tile bounding boxes (float4)
     sbo::DevBuf alpha;           // K^-1 (y - m0), length cap
@@ -134,11 +134,12 @@ hipError_t launch_pack_operand(hipStream_t s, const double *Linv, int64_t ld, in
 hipError_t launch_widen_lower(hipStream_t s, const float *src, int64_t ld_src, int64_t n, double *dst);
 // Predictive sweep: part[I][q] = sum over rows of block I of (sf2 L^-1 k_q)^2,
 // mean[q] = m0 + sf2 alpha^T k_q.
-// skip: drop k-tiles whose K* block is exactly zero (bitwise-identical result).
+// skip_log2 > 0: drop k-tiles whose every K* entry is < 2^-skip_log2 (exactly
+// zero, and a bitwise-identical result, for skip_log2 >= 150); 0: dense.
 // tiles_done (may be null): += number of (BM x BN x BK) tiles multiplied.
 hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox,
                           int64_t npad, const float *qx, const float *qy, int64_t m, int64_t ldp,
-                          float ell, float m0, bool skip, float *part, float *mean,
+                          float ell, float m0, int skip_log2, float *part, float *mean,
                           unsigned long long *tiles_done);
 // Per k-tile bounding boxes of the (internally ordered) training points.
 hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int64_t n, int64_t npad,
