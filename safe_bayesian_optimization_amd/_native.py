@@ -34,6 +34,7 @@ EXPORTS = (
 SBO_OPT_INVERSE_BITS = 1
 SBO_OPT_SPATIAL_ORDER = 2
 SBO_OPT_TILE_SKIP = 3
+SBO_OPT_QUERY_ORDER = 4
 
 
 class SboError(RuntimeError):

@@ -387,8 +387,9 @@ __device__ __forceinline__ void compute_sets_one(float mu, float sd, double beta
 __global__ __launch_bounds__(kAcqThreads) void acquire_kernel(
     const float *__restrict__ part, const float *__restrict__ mean, int nI, int64_t ldp, int64_t m,
     float sf2, double beta, double f_min, int score_kind, int64_t index_offset,
-    float *__restrict__ mu_out, float *__restrict__ sd_out, double *__restrict__ lo_out,
-    double *__restrict__ hi_out, uint8_t *__restrict__ safe_out, sbo_key *__restrict__ keys) {
+    const int32_t *__restrict__ perm, float *__restrict__ mu_out, float *__restrict__ sd_out,
+    double *__restrict__ lo_out, double *__restrict__ hi_out, uint8_t *__restrict__ safe_out,
+    sbo_key *__restrict__ keys) {
     const int64_t i = (int64_t)blockIdx.x * kAcqThreads + threadIdx.x;
     double bs = 0.0;
     int64_t bi = -1;
@@ -399,16 +400,17 @@ __global__ __launch_bounds__(kAcqThreads) void acquire_kernel(
         float var = vd > 0.0 ? (float)vd : 0.0f;
         const float sd = __fsqrt_rn(var);
         const float mu = mean[i];
-        if (mu_out) mu_out[i] = mu;
-        if (sd_out) sd_out[i] = sd;
+        const int64_t o = perm ? (int64_t)perm[i] : i;  // caller's index of sweep position i
+        if (mu_out) mu_out[o] = mu;
+        if (sd_out) sd_out[o] = sd;
         double lo, hi;
         bool safe;
         compute_sets_one(mu, sd, beta, f_min, lo, hi, safe);
-        if (lo_out) lo_out[i] = lo;
-        if (hi_out) hi_out[i] = hi;
-        if (safe_out) safe_out[i] = safe ? 1 : 0;
+        if (lo_out) lo_out[o] = lo;
+        if (hi_out) hi_out[o] = hi;
+        if (safe_out) safe_out[o] = safe ? 1 : 0;
         const double score = score_kind == SBO_SCORE_UCB ? hi : __dsub_rn(hi, lo);
-        if (safe && score == score) { bs = score; bi = index_offset + i; }
+        if (safe && score == score) { bs = score; bi = index_offset + o; }
     }
     block_reduce_key(bs, bi, keys + blockIdx.x);
 }
@@ -542,10 +544,10 @@ hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, 
 
 hipError_t launch_acquire(hipStream_t s, const float *part, const float *mean, int nI, int64_t ldp,
                           int64_t m, float sf2, double beta, double f_min, int score_kind,
-                          int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
-                          uint8_t *safe, sbo_key *block_keys, int /*do_sets*/) {
+                          int64_t index_offset, const int32_t *perm, float *mu, float *sd, double *lo,
+                          double *hi, uint8_t *safe, sbo_key *block_keys) {
     hipLaunchKernelGGL(acquire_kernel, dim3((unsigned)acq_blocks(m)), dim3(kAcqThreads), 0, s, part, mean,
-                       nI, ldp, m, sf2, beta, f_min, score_kind, index_offset, mu, sd, lo, hi, safe,
+                       nI, ldp, m, sf2, beta, f_min, score_kind, index_offset, perm, mu, sd, lo, hi, safe,
                        block_keys);
     return hipGetLastError();
 }

@@ -117,6 +117,16 @@ sbo_status stage_training(sbo_ctx *ctx, const float *x, const float *y, const fl
     SBO_HIP(hipStreamSynchronize(ctx->stream));
     ctx->order.resize((size_t)dst);
     for (int64_t i = 0; i < count; ++i) ctx->order.push_back(index_base + perm[i]);
+    // running bounding box of all training points (query Morton frame)
+    const auto mx = std::minmax_element(hx.begin(), hx.end());
+    const auto my = std::minmax_element(hy.begin(), hy.end());
+    if (dst == 0) {
+        ctx->bbox[0] = *mx.first; ctx->bbox[1] = *mx.second;
+        ctx->bbox[2] = *my.first; ctx->bbox[3] = *my.second;
+    } else {
+        ctx->bbox[0] = std::min(ctx->bbox[0], *mx.first); ctx->bbox[1] = std::max(ctx->bbox[1], *mx.second);
+        ctx->bbox[2] = std::min(ctx->bbox[2], *my.first); ctx->bbox[3] = std::max(ctx->bbox[3], *my.second);
+    }
     return SBO_OK;
 }
 
@@ -248,6 +258,18 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     const int64_t nb = sbo::acq_blocks(m);
     SBO_HIP(ctx->keys.reserve(sizeof(sbo_key) * (size_t)(nb + 1)));
     sbo_key *bkeys = ctx->keys.as<sbo_key>();
+    // sweep the queries in Morton order (compact 128-query blocks skip more k-tiles)
+    const int32_t *perm = nullptr;
+    if (ctx->query_order && ctx->skip_log2 > 0 && m > sbo::kBN) {
+        const size_t wb = sbo::query_order_bytes(m);
+        SBO_HIP(ctx->qwork.reserve(wb));
+        int32_t *p = nullptr;
+        float *sx = nullptr, *sy = nullptr;
+        SBO_HIP(sbo::launch_query_order(ctx->stream, qx, qy, m, ctx->bbox, ctx->qwork.as<void>(), wb, &p, &sx, &sy));
+        perm = p;
+        qx = sx;
+        qy = sy;
+    }
     {
         Bracket br(ctx, ctx->ev_predict);
         SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(),
@@ -258,7 +280,7 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     }
     const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
     SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<float>(), ctx->mean.as<float>(), (int)nI, ldp, m, sf2,
-                                beta, f_min, score_kind, index_offset, mu, sd, lo, hi, safe, bkeys, 1));
+                                beta, f_min, score_kind, index_offset, perm, mu, sd, lo, hi, safe, bkeys));
     SBO_HIP(sbo::launch_reduce_keys(ctx->stream, bkeys, nb, key_dev ? key_dev : bkeys + nb));
     return SBO_OK;
 }
@@ -645,6 +667,9 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             return SBO_OK;
         case SBO_OPT_SPATIAL_ORDER:
             ctx->spatial_order = value != 0;
+            return SBO_OK;
+        case SBO_OPT_QUERY_ORDER:
+            ctx->query_order = value != 0;
             return SBO_OK;
         case SBO_OPT_TILE_SKIP:
             SBO_CHECK(value == 0 || (value >= 16 && value <= 1000), SBO_E_INVAL,

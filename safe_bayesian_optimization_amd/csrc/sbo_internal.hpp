@@ -87,6 +87,9 @@ struct sbo_ctx {
     bool spatial_order = true;   // SBO_OPT_SPATIAL_ORDER: Morton-order the training points
     int skip_log2 = 64;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-skip_log2
     std::vector<int64_t> order;  // internal row -> caller's training index
+    float bbox[4] = {0.f, 0.f, 0.f, 0.f};  // training bounding box (x0, x1, y0, y1)
+    bool query_order = true;     // SBO_OPT_QUERY_ORDER: sweep queries in Morton order
+    sbo::DevBuf qwork;           // query ordering workspace
     sbo::DevBuf kbox;            // per k-tile bounding boxes (float4)
     sbo::DevBuf alpha;           // K^-1 (y - m0), length cap
     sbo::DevBuf aug;             // packed sf2 * L^-1 tiles
@@ -145,10 +148,18 @@ hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, 
 hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int64_t n, int64_t npad,
                              float4 *kbox);
 // Acquisition over predictive partials (fused reduce + sets + block argmax).
+// perm (may be null): sweep position i holds caller query perm[i]; outputs and
+// key indices are written in the caller's order.
 hipError_t launch_acquire(hipStream_t s, const float *part, const float *mean, int nI, int64_t ldp,
                           int64_t m, float sf2, double beta, double f_min, int score_kind,
-                          int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
-                          uint8_t *safe, sbo_key *block_keys, int do_sets);
+                          int64_t index_offset, const int32_t *perm, float *mu, float *sd, double *lo,
+                          double *hi, uint8_t *safe, sbo_key *block_keys);
+// Morton ordering of the queries (query_order.hip): workspace of
+// query_order_bytes(m); returns the permutation and the gathered coordinates
+// (all inside the workspace).
+size_t query_order_bytes(int64_t m);
+hipError_t launch_query_order(hipStream_t s, const float *qx, const float *qy, int64_t m, const float bbox[4],
+                              void *work, size_t work_bytes, int32_t **perm, float **sqx, float **sqy);
 // ComputeSets from given mu/sd (staged API).
 hipError_t launch_sets(hipStream_t s, const float *mu, const float *sd, int64_t m, double beta,
                        double f_min, double *lo, double *hi, uint8_t *safe);
