@@ -176,21 +176,29 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * of the internally ordered K and sbo_get_order the caller's index of each
  * internal row.  Takes effect at the next sbo_fit / sbo_append. */
 #define SBO_OPT_SPATIAL_ORDER 2
-/* SBO_OPT_TILE_SKIP (0 | L in [16, 1000], default 64): skip a k-tile for a
- * workgroup of queries when the two bounding boxes are so far apart that
- * every K* entry of the block is below 2^-L (|d| > l * sqrt(2 L ln 2)).
- * L >= 150: those entries are exactly +0.0 in f32 and the result is bitwise
- * identical to the dense sweep (0).  L = 64 (default): the dropped mass is
- * < 2^-64 * ||sf2 L^-1||_1 per V entry, ~1e-17 relative, orders of magnitude
- * below f32 rounding; outputs differ from the dense sweep in at most the last
- * bit of a vanishing fraction of points (tested). */
+/* SBO_OPT_TILE_SKIP (-1 | 0 | L in [16, 1000], default -1): skip a k-tile
+ * for a workgroup of queries when the two bounding boxes are so far apart
+ * that every K* entry of the block is below 2^-L (|d| > l sqrt(2 L ln 2)).
+ * 0: dense sweep.  L >= 150: the dropped entries are exactly +0.0 in f32 and
+ * the result is bitwise identical to the dense sweep.  -1 (auto): L is the
+ * smallest exponent whose worst-case effect -- 2^-L max_i |(sf2 L^-1)_i|_1 on
+ * any V entry, hence 2 sqrt(N sf2) times that on sigma^2, and
+ * 2^-L |sf2 alpha|_1 on any mean -- stays below 2^-27 sf2 (resp. 2^-27
+ * sqrt(sf2)), computed from the fitted factor (sbo_get_skip reports it). */
 #define SBO_OPT_TILE_SKIP 3
 /* SBO_OPT_QUERY_ORDER (0 | 1, default 1): sweep the queries of a tick in
  * Morton order (device radix sort, ~0.1 ms per 10^6 points) so each
  * workgroup's 128 queries are spatially compact and skip more k-tiles;
  * outputs and argmax indices stay in the caller's order. */
 #define SBO_OPT_QUERY_ORDER 4
+/* SBO_OPT_KERNEL_VARIANT (A/B builds of the predictive kernel): 0 = f64
+ * cross-tile accumulator, 2 waves/SIMD (default); 1 = f32 accumulator,
+ * 2 waves/SIMD; 2 = f32 accumulator, 3 waves/SIMD. */
+#define SBO_OPT_KERNEL_VARIANT 5
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
+
+/* The K* tile cutoff in effect (auto or fixed) and the norms it was derived from. */
+SBO_API sbo_status sbo_get_skip(const sbo_ctx *ctx, int *cutoff_log2, double *max_row_l1, double *alpha_l1);
 
 /* order[i] = the caller's index (position in the sbo_fit / sbo_append
  * inputs, appends numbered after the fit) of internal training row i. */

@@ -29,12 +29,13 @@ EXPORTS = (
     "sbo_fit", "sbo_append", "sbo_num_train", "sbo_predict", "sbo_compute_sets", "sbo_argmax", "sbo_tick",
     "sbo_key_combine", "sbo_find_safety_contour_indices", "sbo_next_subgoal", "sbo_find_contours_external",
     "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
-    "sbo_get_order", "sbo_profile_work",
+    "sbo_get_order", "sbo_profile_work", "sbo_get_skip",
 )
 SBO_OPT_INVERSE_BITS = 1
 SBO_OPT_SPATIAL_ORDER = 2
 SBO_OPT_TILE_SKIP = 3
 SBO_OPT_QUERY_ORDER = 4
+SBO_OPT_KERNEL_VARIANT = 5
 
 
 class SboError(RuntimeError):
@@ -117,6 +118,8 @@ def lib():
     L.sbo_get_factor.restype = st
     L.sbo_set_option.argtypes = [vp, i32, i64]
     L.sbo_set_option.restype = st
+    L.sbo_get_skip.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(dbl), ctypes.POINTER(dbl)]
+    L.sbo_get_skip.restype = st
     L.sbo_get_order.argtypes = [vp, vp]
     L.sbo_get_order.restype = st
     L.sbo_get_inverse.argtypes = [vp, vp]

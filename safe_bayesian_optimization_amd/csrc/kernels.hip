@@ -126,6 +126,17 @@ __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__r
     c[2 * kBK + o] = in ? sf2 * alpha[k] : 0.0f;
 }
 
+// Row 1-norms of the packed operand: block I, thread r sums |A[I*BM + r][:]|.
+__global__ __launch_bounds__(kBM) void row_l1_kernel(const float *__restrict__ aug, double *__restrict__ row_l1) {
+    const int64_t I = blockIdx.x;
+    const int r = threadIdx.x;
+    const float *t = aug + tile_start(I) * kTileFloats;
+    const int64_t nk = (I + 1) * kBM;  // k-tiles 0..2(I+1)-1, each [BK][BM]
+    double s = 0.0;
+    for (int64_t k = 0; k < nk; ++k) s += fabs((double)t[k * kBM + r]);
+    row_l1[I * kBM + r] = s;
+}
+
 // Bounding box of each k-tile's valid training points: (xmin, xmax, ymin, ymax);
 // a tile with no valid point gets an empty box (+inf, -inf, +inf, -inf).
 __global__ void tile_box_kernel(const float *__restrict__ x, const float *__restrict__ y, int64_t n,
@@ -171,11 +182,11 @@ constexpr int kStageFloats = kTileFloats + 3 * kBK;
 constexpr int kMaxList = 2048;  // k-tiles a workgroup can list (N <= 131072); beyond: dense
 constexpr int kSmemFloats = 2 * kStageFloats + kMaxList + 32;
 
-template <bool MEAN>
+template <bool MEAN, class OT>
 __device__ __forceinline__ void predict_body(const float *__restrict__ tiles,
                                              const float *__restrict__ kc, const int *tlist,
                                              int cnt, float xq, float yq, float cexp, float *smem,
-                                             double (&outer)[4][16], double &mu) {
+                                             OT (&outer)[4][16], double &mu) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int half = lane >> 5;
@@ -231,7 +242,7 @@ __device__ __forceinline__ void predict_body(const float *__restrict__ tiles,
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) outer[rb][r] += (double)acc[rb][r];
+            for (int r = 0; r < 16; ++r) outer[rb][r] += (OT)acc[rb][r];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -249,7 +260,10 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
-__global__ __launch_bounds__(256, 2) void predict_kernel(const float *__restrict__ aug,
+// OT: outer (cross-tile) accumulator type; W: waves per SIMD the register
+// budget is fitted to (f64 outer needs 2; f32 outer can run 3).
+template <class OT, int W>
+__global__ __launch_bounds__(256, W) void predict_kernel(const float *__restrict__ aug,
                                                          const float *__restrict__ kcoord,
                                                          const float4 *__restrict__ kbox, int nI,
                                                          int nQ, const float *__restrict__ qx,
@@ -317,18 +331,18 @@ __global__ __launch_bounds__(256, 2) void predict_kernel(const float *__restrict
     }
     if (tid == 0 && tiles_done) atomicAdd(tiles_done, (unsigned long long)cnt);  // executed-work counter
 
-    double outer[4][16];
+    OT outer[4][16];
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) outer[rb][r] = 0.0;
+        for (int r = 0; r < 16; ++r) outer[rb][r] = (OT)0;
     double mu = 0.0;
 
     const bool last = (I == nI - 1);
     if (last)
-        predict_body<true>(tiles, kcoord, list, cnt, xq, yq, cexp, smem, outer, mu);
+        predict_body<true, OT>(tiles, kcoord, list, cnt, xq, yq, cexp, smem, outer, mu);
     else
-        predict_body<false>(tiles, kcoord, list, cnt, xq, yq, cexp, smem, outer, mu);
+        predict_body<false, OT>(tiles, kcoord, list, cnt, xq, yq, cexp, smem, outer, mu);
 
     // epilogue: column sums of V^2 over this block's rows; lanes l and l+32 hold
     // the two row halves of column l&31 of each 32x32 accumulator
@@ -336,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void predict_kernel(const float *__restrict
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s = fma(outer[rb][r], outer[rb][r], s);
+        for (int r = 0; r < 16; ++r) s = fma((double)outer[rb][r], (double)outer[rb][r], s);
     s += __shfl_xor(s, 32);
     mu += __shfl_xor(mu, 32);
     if (lane < 32 && q < m) {
@@ -518,6 +532,11 @@ hipError_t launch_widen_lower(hipStream_t s, const float *src, int64_t ld_src, i
     return hipGetLastError();
 }
 
+hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, double *row_l1) {
+    hipLaunchKernelGGL(row_l1_kernel, dim3((unsigned)(npad / kBM)), dim3(kBM), 0, s, aug, row_l1);
+    return hipGetLastError();
+}
+
 hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int64_t n, int64_t npad, float4 *kbox) {
     const int64_t nt = npad / kBK;
     hipLaunchKernelGGL(tile_box_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, x, y, n, nt, kbox);
@@ -526,7 +545,7 @@ hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int6
 
 hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox, int64_t npad,
                           const float *qx, const float *qy, int64_t m, int64_t ldp, float ell, float m0, int skip_log2,
-                          float *part, float *mean, unsigned long long *tiles_done) {
+                          float *part, float *mean, unsigned long long *tiles_done, int variant) {
     const int nI = (int)(npad / kBM);
     const int64_t nQ = (m + kBN - 1) / kBN;
     const double ce = -1.0 / (2.0 * (double)ell * (double)ell * 0.69314718055994530942);
@@ -537,8 +556,13 @@ hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, 
     const float skip_d2 = skip_log2 > 0 ? (float)((double)skip_log2 / -ce * 1.001) : -1.0f;
     const int64_t blocks = (int64_t)nI * nQ;
     if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(predict_kernel, dim3((unsigned)blocks), dim3(256), 0, s, aug, kcoord, kbox, nI, (int)nQ, qx,
-                       qy, m, ldp, cexp, skip_d2, m0, part, mean, tiles_done);
+#define SBO_PREDICT_ARGS aug, kcoord, kbox, nI, (int)nQ, qx, qy, m, ldp, cexp, skip_d2, m0, part, mean, tiles_done
+    switch (variant) {
+        case 1: hipLaunchKernelGGL((predict_kernel<float, 2>), dim3((unsigned)blocks), dim3(256), 0, s, SBO_PREDICT_ARGS); break;
+        case 2: hipLaunchKernelGGL((predict_kernel<float, 3>), dim3((unsigned)blocks), dim3(256), 0, s, SBO_PREDICT_ARGS); break;
+        default: hipLaunchKernelGGL((predict_kernel<double, 2>), dim3((unsigned)blocks), dim3(256), 0, s, SBO_PREDICT_ARGS); break;
+    }
+#undef SBO_PREDICT_ARGS
     return hipGetLastError();
 }
 

@@ -221,6 +221,30 @@ sbo_status refresh_operand(sbo_ctx *ctx) {
         SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, ld, n, npad, sf2, ctx->x.as<float>(), ctx->y.as<float>(),
                                          alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
     }
+    // Error budget of the K* tile cutoff (SBO_OPT_TILE_SKIP = -1, auto): a
+    // dropped block has every entry < 2^-L, so each V_i moves by at most
+    // 2^-L max_i |A_i|_1 and each mean by at most 2^-L |sf2 alpha|_1.  With
+    // |V|_2 <= sf2^(1/2), |d sigma^2| <= 2 sf2^(1/2) sqrt(N) max|dV_i|.  L is the
+    // smallest exponent that keeps both below 2^-27 (~7.5e-9) of sf2 / sf2^(1/2).
+    {
+        SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)npad));
+        SBO_HIP(sbo::launch_row_l1(ctx->stream, ctx->aug.as<float>(), npad, ctx->scratch.as<double>()));
+        std::vector<double> rl1((size_t)npad);
+        std::vector<float> ha((size_t)n);
+        SBO_HIP(hipMemcpyAsync(rl1.data(), ctx->scratch.as<double>(), sizeof(double) * npad, hipMemcpyDeviceToHost,
+                               ctx->stream));
+        SBO_HIP(hipMemcpyAsync(ha.data(), alpha, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+        SBO_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->max_row_l1 = *std::max_element(rl1.begin(), rl1.end());
+        double al1 = 0.0;
+        for (float v : ha) al1 += std::fabs((double)v);
+        ctx->alpha_l1 = al1 * sf2;
+        const double tol = std::ldexp(1.0, -27), sf = std::sqrt(sf2);
+        const double need_v = 2.0 * std::sqrt((double)n) * ctx->max_row_l1 / (tol * sf);
+        const double need_m = ctx->alpha_l1 / (tol * sf);
+        const double l2 = std::log2(std::max({need_v, need_m, 1.0}));
+        ctx->auto_skip_log2 = std::isfinite(l2) ? std::min(160, std::max(24, (int)std::ceil(l2))) : 160;
+    }
     SBO_HIP(ctx->kbox.reserve(sizeof(float4) * (size_t)(npad / sbo::kBK)));
     SBO_HIP(sbo::launch_tile_boxes(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, npad, ctx->kbox.as<float4>()));
     SBO_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, ctx->stream));
@@ -260,7 +284,8 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     sbo_key *bkeys = ctx->keys.as<sbo_key>();
     // sweep the queries in Morton order (compact 128-query blocks skip more k-tiles)
     const int32_t *perm = nullptr;
-    if (ctx->query_order && ctx->skip_log2 > 0 && m > sbo::kBN) {
+    const int skip_log2 = ctx->skip_log2 < 0 ? ctx->auto_skip_log2 : ctx->skip_log2;
+    if (ctx->query_order && skip_log2 > 0 && m > sbo::kBN) {
         const size_t wb = sbo::query_order_bytes(m);
         SBO_HIP(ctx->qwork.reserve(wb));
         int32_t *p = nullptr;
@@ -274,9 +299,10 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         Bracket br(ctx, ctx->ev_predict);
         SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(),
                                     ctx->kbox.as<float4>(), ctx->npad, qx, qy, m, ldp,
-                                    (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, ctx->skip_log2,
+                                    (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, skip_log2,
                                     ctx->part.as<float>(), ctx->mean.as<float>(),
-                                    ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr));
+                                    ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr,
+                                    ctx->kernel_variant));
     }
     const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
     SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<float>(), ctx->mean.as<float>(), (int)nI, ldp, m, sf2,
@@ -671,14 +697,26 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
         case SBO_OPT_QUERY_ORDER:
             ctx->query_order = value != 0;
             return SBO_OK;
+        case SBO_OPT_KERNEL_VARIANT:
+            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be 0, 1 or 2");
+            ctx->kernel_variant = (int)value;
+            return SBO_OK;
         case SBO_OPT_TILE_SKIP:
-            SBO_CHECK(value == 0 || (value >= 16 && value <= 1000), SBO_E_INVAL,
-                      "SBO_OPT_TILE_SKIP must be 0 (dense) or a cutoff exponent in [16, 1000]");
+            SBO_CHECK(value == -1 || value == 0 || (value >= 16 && value <= 1000), SBO_E_INVAL,
+                      "SBO_OPT_TILE_SKIP must be -1 (auto), 0 (dense) or a cutoff exponent in [16, 1000]");
             ctx->skip_log2 = (int)value;
             return SBO_OK;
     }
     ctx->err = "unknown option " + std::to_string(option);
     return SBO_E_INVAL;
+}
+
+SBO_API sbo_status sbo_get_skip(const sbo_ctx *ctx, int *cutoff_log2, double *max_row_l1, double *alpha_l1) {
+    if (!ctx) return SBO_E_INVAL;
+    if (cutoff_log2) *cutoff_log2 = ctx->skip_log2 < 0 ? ctx->auto_skip_log2 : ctx->skip_log2;
+    if (max_row_l1) *max_row_l1 = ctx->max_row_l1;
+    if (alpha_l1) *alpha_l1 = ctx->alpha_l1;
+    return SBO_OK;
 }
 
 SBO_API sbo_status sbo_get_order(const sbo_ctx *ctx, int64_t *order) {

@@ -85,10 +85,14 @@ struct sbo_ctx {
     sbo::DevBuf Linv;            // workspace: L^-1 (strtri f32, lda = cap, or dtrtri f64, lda = n)
     int inverse_bits = 64;       // SBO_OPT_INVERSE_BITS: precision of the L^-1 computation
     bool spatial_order = true;   // SBO_OPT_SPATIAL_ORDER: Morton-order the training points
-    int skip_log2 = 64;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-skip_log2
+    int skip_log2 = -1;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-L (-1: auto)
+    int auto_skip_log2 = 160;    // L from the error budget, computed at fit (see refresh_operand)
+    double max_row_l1 = 0.0;     // max_i sum_j |A_ij|, A = sf2 L^-1
+    double alpha_l1 = 0.0;       // sum_j |sf2 alpha_j|
     std::vector<int64_t> order;  // internal row -> caller's training index
     float bbox[4] = {0.f, 0.f, 0.f, 0.f};  // training bounding box (x0, x1, y0, y1)
     bool query_order = true;     // SBO_OPT_QUERY_ORDER: sweep queries in Morton order
+    int kernel_variant = 0;      // SBO_OPT_KERNEL_VARIANT: predictive kernel build (A/B)
     sbo::DevBuf qwork;           // query ordering workspace
     sbo::DevBuf kbox;            // per k-tile bounding boxes (float4)
     sbo::DevBuf alpha;           // K^-1 (y - m0), length cap
@@ -143,7 +147,9 @@ hipError_t launch_widen_lower(hipStream_t s, const float *src, int64_t ld_src, i
 hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox,
                           int64_t npad, const float *qx, const float *qy, int64_t m, int64_t ldp,
                           float ell, float m0, int skip_log2, float *part, float *mean,
-                          unsigned long long *tiles_done);
+                          unsigned long long *tiles_done, int variant);
+// row_l1[i] = sum_j |A_ij| over the packed operand (f64), i < npad.
+hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, double *row_l1);
 // Per k-tile bounding boxes of the (internally ordered) training points.
 hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int64_t n, int64_t npad,
                              float4 *kbox);

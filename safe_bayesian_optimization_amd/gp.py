@@ -177,6 +177,12 @@ class TerrainMapper:
         self.ctx.check(self._lib.sbo_get_order(self.ctx.handle, _ptr(o)))
         return o
 
+    def skip_info(self):
+        """(cutoff exponent L in effect, max_i |A_i|_1, |sf2 alpha|_1)."""
+        L, r, a = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+        self.ctx.check(self._lib.sbo_get_skip(self.ctx.handle, ctypes.byref(L), ctypes.byref(r), ctypes.byref(a)))
+        return L.value, r.value, a.value
+
     def set_option(self, option: int, value: int) -> None:
         self.ctx.check(self._lib.sbo_set_option(self.ctx.handle, int(option), int(value)))
 

@@ -272,21 +272,33 @@ def test_tick_empty_safe_set(mapper):
 
 
 # --------------------------------------------------------- exact tile skipping
-def test_tile_skip_exact_and_negligible(dev, mapper):
+def test_tile_skip_exact_and_bounded(dev, mapper):
     """N = 8192 over a 32 l domain.  Cutoff 2^-160 (entries exactly +0.0):
-    mu, sd and the key bitwise identical to the dense sweep.  Default cutoff
-    2^-64: at most 1 ulp on a vanishing fraction of points, same argmax."""
+    mu, sd and the key bitwise identical to the dense sweep.  Cutoff 2^-64:
+    at most 1 ulp on a vanishing fraction of points.  Auto cutoff (default):
+    within its stated error budget (2^-27 sf2 on sigma^2, 2^-27 sf on mu)
+    of the dense sweep, same argmax."""
     wl = synthetic(8192, 200, 160, seed=21)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
     gm.fit(wl.x, wl.y, wl.obs)
     res = {}
     m = wl.qx.size
-    for cut in (0, 160, 64):
+    for cut in (0, 160, 64, -1):
         gm.set_option(N.SBO_OPT_TILE_SKIP, cut)
         out = dict(mu=np.empty(m, np.float32), sd=np.empty(m, np.float32))
         k = gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
         res[cut] = (out["mu"], out["sd"], k.idx, k.score)
-    gm.set_option(N.SBO_OPT_TILE_SKIP, 64)
+    gm.set_option(N.SBO_OPT_TILE_SKIP, -1)
+    L, rl1, al1 = gm.skip_info()
+    print(f"auto cutoff 2^-{L} (max row l1 {rl1:.3g}, |sf2 alpha|_1 {al1:.3g})")
+    assert 24 <= L < 64
+    budget = 2.0 ** -27
+    dmu = np.abs(res[-1][0].astype(np.float64) - res[0][0]).max()
+    dvar = np.abs(res[-1][1].astype(np.float64) ** 2 - res[0][1].astype(np.float64) ** 2).max()
+    ulp = np.finfo(np.float32).eps
+    assert dmu <= budget + 2 * ulp * np.abs(res[0][0]).max()   # f32 output rounding on top
+    assert dvar <= budget + 4 * ulp
+    assert res[-1][2] == res[0][2]
     assert np.array_equal(res[0][0], res[160][0]) and np.array_equal(res[0][1], res[160][1])
     assert res[0][2:] == res[160][2:]
     for a, b in ((res[0][0], res[64][0]), (res[0][1], res[64][1])):

@@ -32,14 +32,16 @@ def diag(wl, nq=2048):
         gm.fit(x, y, wl.obs.astype(np.float32))
         mu, sd = gm.predict(qx, qy)
         L, alpha = gm.factor()
+        o = gm.order()  # factor rows are in the library's internal (Morton) order
         n = L.shape[0]
-        omu, ovar = O.predict(O.colmajor_from_lower(L.astype(np.float64)), alpha.astype(np.float64), x, y, qx, qy,
+        xo, yo = x[o], y[o]
+        omu, ovar = O.predict(O.colmajor_from_lower(L.astype(np.float64)), alpha.astype(np.float64), xo, yo, qx, qy,
                               h.length_scale, h.sf2, h.prior_mean)
         A = np.zeros((n, n), np.float32)
         gm.ctx.check(N.lib().sbo_get_inverse(gm.ctx.handle, A.ctypes.data))
         A = np.tril(A).astype(np.float64)
         inv_err = np.abs(A @ L.astype(np.float64) / h.sf2 - np.eye(n)).max()
-        xs, ys = x.astype(np.float64), y.astype(np.float64)
+        xs, ys = xo.astype(np.float64), yo.astype(np.float64)
         E = np.exp(-((xs[:, None] - qx[None, :].astype(np.float64)) ** 2 + (ys[:, None] - qy[None, :].astype(np.float64)) ** 2)
                    / (2 * h.length_scale ** 2))
         V = A @ E
