@@ -6,19 +6,23 @@ V = sf2 L^-1 K*^T on f32 MFMA, mean alongside), ComputeSets in f64, the masked
 argmax of the confidence width over the safe set, and the cross-rank key
 reduction (one RCCL all-gather of 16-byte keys when N > 1).  Inputs (query
 coordinates) are resident in HBM before timing starts; mu/sd/lo/hi/S are
-written to HBM every step.  The fit (RBF fill + rocSOLVER potrf + strtri +
+written to HBM every step.  The fit (RBF fill + rocSOLVER potrf + dtrtri +
 operand pack) runs once, replicated on every rank, and is reported separately.
 
 Default workload = BASELINE.json configs[3] (C4: N=16384, 1000x1000 grid),
 the north-star target size, on 1 GPU; with --gpus P the same 10^6-point grid
-is split into P contiguous row blocks (strong scaling).
+is split into P contiguous row blocks (strong scaling).  --config C5 runs the
+streaming loop instead (configs[4]: 50 iterations, N 1000 -> 8000 by
+incremental Cholesky appends, 512x512 grid, 1 GPU): a step is one append +
+one tick.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -31,6 +35,8 @@ sys.path.insert(0, ROOT)
 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "GP posterior+acq grid-points/sec at N train pts; 1/2/4/8 GPU"
+DATA = "synthetic (SplitMix64 smooth field + N(0,sn2) noise in BASELINE config shapes; terrain.csv is a missing blob)"
 
 
 def parse():
@@ -38,14 +44,33 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--config", default="C4", choices=["C2", "C3", "C4"])
+    p.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
     p.add_argument("--n", type=int, default=None, help="override N")
     p.add_argument("--grid", type=int, default=None, help="override grid side")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    p.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-outputs", action="store_true", help="skip writing mu/sd/lo/hi/S (argmax only)")
     return p.parse_args()
+
+
+class Prof:
+    """Kernel timing recorded by libsbo on the launch stream (sbo_profile)."""
+
+    def __init__(self, lib, handle):
+        self.lib, self.h = lib, handle
+
+    def reset(self, on=True):
+        self.lib.sbo_profile(self.h, 1 if on else 0)
+
+    def read(self):
+        pm, pl, fm, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_int64()
+        self.lib.sbo_profile_read(self.h, ctypes.byref(pm), ctypes.byref(pl), ctypes.byref(fm), ctypes.byref(fl))
+        w = ctypes.c_double()
+        self.lib.sbo_profile_work(self.h, ctypes.byref(w))
+        return dict(predict_ms=pm.value, predict_launches=pl.value, fill_ms=fm.value, fill_launches=fl.value,
+                    predict_flops=w.value)
 
 
 def main():
@@ -53,22 +78,52 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from safe_bayesian_optimization_amd import TerrainMapper, synthetic
-    from safe_bayesian_optimization_amd import _native as N
-    from safe_bayesian_optimization_amd.dist import allreduce_key, shard_range
-    from safe_bayesian_optimization_amd.terrain import CONFIGS
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.backend)
+    try:
+        if a.config == "C5":
+            line = run_streaming(a, dev, world, rank)
+        else:
+            line = run_sweep(a, dev, world, rank)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+    finally:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+
+
+def _max_over_ranks(vals, dev, world, backend):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return vals
+    t = torch.tensor(vals, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.cpu()]
+
+
+def run_sweep(a, dev, world, rank):
+    import torch
+    import torch.distributed as dist
+
+    from safe_bayesian_optimization_amd import TerrainMapper, synthetic
+    from safe_bayesian_optimization_amd import _native as N
+    from safe_bayesian_optimization_amd.dist import allreduce_key, shard_range
+    from safe_bayesian_optimization_amd.gp import _to_hyper
+    from safe_bayesian_optimization_amd.terrain import CONFIGS
 
     n, gw, gh = CONFIGS[a.config]
-    if a.n:
-        n = a.n
+    n = a.n or n
     if a.grid:
         gw = gh = a.grid
     wl = synthetic(n, gw, gh, seed=0, name=a.config)
@@ -82,53 +137,49 @@ def main():
     m = hi - lo
 
     stream = torch.cuda.current_stream(dev)
-    gm = TerrainMapper(local, wl.hyper)
+    gm = TerrainMapper(dev.index, wl.hyper)
     gm.ctx.set_stream(stream)
     lib = N.lib()
+    prof = Prof(lib, gm.ctx.handle)
 
     f32 = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
     X, Y, OBS = f32(wl.x), f32(wl.y), f32(wl.obs)
     qx, qy = f32(wl.qx[lo:hi]), f32(wl.qy[lo:hi])
-    if a.no_outputs:
-        outs = {}
-    else:
-        outs = dict(mu=torch.empty(m, dtype=torch.float32, device=dev), sd=torch.empty(m, dtype=torch.float32, device=dev),
-                    lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
-                    safe=torch.empty(m, dtype=torch.uint8, device=dev))
+    outs = {} if a.no_outputs else dict(
+        mu=torch.empty(m, dtype=torch.float32, device=dev), sd=torch.empty(m, dtype=torch.float32, device=dev),
+        lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
+        safe=torch.empty(m, dtype=torch.uint8, device=dev))
     key = torch.empty(2, dtype=torch.int64, device=dev)
 
-    # ---- fit (replicated), timed separately; fill roofline from HIP events
-    lib.sbo_profile(gm.ctx.handle, 1)
+    # ---- fit (replicated on every rank), timed separately
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     gm.fit(X, Y, OBS)
     torch.cuda.synchronize()
     fit_ms = (time.perf_counter() - t0) * 1e3
-    import ctypes
-    pm, pl, fm, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_int64()
-    # RBF fill (a1) alone, warm: the first launch inside fit also pays the
-    # code-object load, so time 3 more launches into a scratch K
+    cutoff, row_l1, alpha_l1 = gm.skip_info()
+
+    # ---- RBF fill (a1) alone, warm (the fill inside fit also paid the code-object load)
     Kbuf = torch.empty(n * n, dtype=torch.float32, device=dev)
-    from safe_bayesian_optimization_amd.gp import _to_hyper
     fill_args = (gm.ctx.handle, ctypes.c_void_p(X.data_ptr()), ctypes.c_void_p(Y.data_ptr()), n,
                  _to_hyper(wl.hyper), ctypes.c_void_p(Kbuf.data_ptr()), N.SBO_DEVICE_PTRS | N.SBO_ASYNC)
     gm.ctx.check(lib.sbo_rbf_fill(*fill_args))
-    lib.sbo_profile(gm.ctx.handle, 1)
+    prof.reset()
     for _ in range(3):
         gm.ctx.check(lib.sbo_rbf_fill(*fill_args))
-    lib.sbo_profile_read(gm.ctx.handle, ctypes.byref(pm), ctypes.byref(pl), ctypes.byref(fm), ctypes.byref(fl))
-    fill_ms = fm.value / max(fl.value, 1)
+    pr = prof.read()
+    fill_ms = pr["fill_ms"] / max(pr["fill_launches"], 1)
     fill_bytes = 4.0 * n * n + 8.0 * n
     del Kbuf
 
     def step():
         gm.tick(qx, qy, wl.beta, wl.f_min, score=N.SCORE_WIDTH, index_offset=lo, outputs=outs, key_out=key,
                 async_=True)
-        return allreduce_key(key)
+        return allreduce_key(key if a.backend == "nccl" else key.cpu())
 
     for _ in range(a.warmup):
         step()
-    lib.sbo_profile(gm.ctx.handle, 1)   # reset: time only the K measured launches
+    prof.reset()   # time only the K measured launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -140,65 +191,41 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    lib.sbo_profile_read(gm.ctx.handle, ctypes.byref(pm), ctypes.byref(pl), ctypes.byref(fm), ctypes.byref(fl))
-    work = ctypes.c_double()
-    lib.sbo_profile_work(gm.ctx.handle, ctypes.byref(work))
-    lib.sbo_profile(gm.ctx.handle, 0)
-    pred_ms = pm.value / max(pl.value, 1)
-    exec_flops_launch = work.value / max(pl.value, 1)
-    if world > 1:
-        t = torch.tensor([elapsed, pred_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, pred_ms_max = float(t[0]), float(t[1])
-    else:
-        pred_ms_max = pred_ms
-
+    pr = prof.read()
+    prof.reset(False)
+    pred_ms = pr["predict_ms"] / max(pr["predict_launches"], 1)
+    exec_flops_launch = pr["predict_flops"] / max(pr["predict_launches"], 1)
+    elapsed, pred_ms_max = _max_over_ranks([elapsed, pred_ms], dev, world, a.backend)
     if rank != 0:
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
+        return None
 
     ms_per_step = elapsed * 1e3 / a.steps
     value = m_all * a.steps / elapsed
-    # Algorithmic work of one launch: the MFMA products that are not identically
-    # zero -- 2*BM*BN*BK per k-tile a workgroup multiplies (counted on the
-    # device); k-tiles whose K* block underflows to +0.0 are skipped exactly.
-    # The dense reference figure N^2 flop per grid point is
-    # reported beside it as a throughput equivalent.
+    # Algorithmic work of one launch: the MFMA products that are not dropped --
+    # 2*BM*BN*BK per k-tile a workgroup multiplies (counted on the device).
+    # k-tiles whose every K* entry is below the error-budgeted cutoff 2^-L are
+    # skipped.  The dense figure N^2 flop per grid point
+    #  is reported beside it as a throughput equivalent.
     dense_flops_launch = float(n) * float(n) * m
     achieved = exec_flops_launch / (pred_ms * 1e-3) / 1e12
-    dense_equiv = dense_flops_launch / (pred_ms * 1e-3) / 1e12
     fill_gbs = fill_bytes / (fill_ms * 1e-3) / 1e9 if fill_ms > 0 else None
-
-    cpu = None
-    if world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(gm, wl, a.cpu_seconds)
-
-    line = {
-        "metric": "GP posterior+acq grid-points/sec at N train pts; 1/2/4/8 GPU",
-        "value": value,
-        "unit": "grid-points/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": ms_per_step,
-        "higher_is_better": True,
-        "scaling": a.scaling,
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (SplitMix64 smooth field + N(0,sn2) noise, BASELINE configs, no terrain.csv)",
-        "config": {"workload": a.config, "n_train": n, "grid": [gw, gh], "M": m_total,
-                   "M_per_rank": m, "beta": wl.beta, "f_min": round(wl.f_min, 6),
+    cpu = cpu_baseline(gm, wl, a.cpu_seconds) if world == 1 and not a.no_cpu else None
+    return {
+        "metric": METRIC, "value": value, "unit": "grid-points/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": a.scaling,
+        "vs_baseline": None, "dtype": "f32", "data": DATA,
+        "config": {"workload": a.config, "n_train": n, "grid": [gw, gh], "M": m_total, "M_per_rank": m,
+                   "beta": wl.beta, "f_min": round(wl.f_min, 6),
                    "hyper": [wl.hyper.length_scale, wl.hyper.sigma_f, wl.hyper.noise_level],
-                   "parallelism": f"m-shard{world}" if world > 1 else "single", "outputs_written": not a.no_outputs},
+                   "kstar_cutoff_log2": cutoff, "parallelism": f"m-shard{world}" if world > 1 else "single",
+                   "outputs_written": not a.no_outputs},
         "roofline": {"kernel": "predict_kernel (V = sf2 L^-1 K*^T, f32 MFMA 32x32x2)", "bound": "mfma",
                      "achieved": achieved, "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F32_MFMA_TFLOPS, "traffic": None,
                      "avg_launch_ms": pred_ms, "max_rank_launch_ms": pred_ms_max,
                      "algorithmic_flops_per_launch": exec_flops_launch,
                      "dense_flops_per_launch": dense_flops_launch,
-                     "dense_equivalent_tflops": dense_equiv},
+                     "dense_equivalent_tflops": dense_flops_launch / (pred_ms * 1e-3) / 1e12},
         "fill_roofline": {"kernel": "rbf_fill_kernel", "bound": "hbm", "achieved": fill_gbs, "peak": PEAK_HBM_GBS,
                           "unit": "GB/s", "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None,
                           "avg_launch_ms": fill_ms, "algorithmic_bytes": fill_bytes},
@@ -206,16 +233,86 @@ def main():
         "argmax": {"index": best[1], "score": best[0]},
         "cpu_baseline": cpu,
     }
-    print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+
+
+def run_streaming(a, dev, world, rank):
+    """C5: 50 iterations, N 1000 -> 8000 by sbo_append, 512x512 grid."""
+    import torch
+
+    from safe_bayesian_optimization_amd import TerrainMapper, synthetic
+    from safe_bayesian_optimization_amd import _native as N
+    from safe_bayesian_optimization_amd.dist import key_tensor_to_pairs
+    if world != 1:
+        raise SystemExit("C5 is a single-GPU streaming configuration")
+    n_end, n0, iters, g = 8000, 1000, 50, a.grid or 512
+    wl = synthetic(n_end, g, g, seed=0, name="C5")
+    chunks = np.linspace(n0, n_end, iters + 1).round().astype(int)
+    stream = torch.cuda.current_stream(dev)
+    gm = TerrainMapper(dev.index, wl.hyper)
+    gm.ctx.set_stream(stream)
+    prof = Prof(N.lib(), gm.ctx.handle)
+    f32 = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
+    X, Y, OBS = f32(wl.x), f32(wl.y), f32(wl.obs)
+    qx, qy = f32(wl.qx), f32(wl.qy)
+    m = qx.numel()
+    outs = dict(mu=torch.empty(m, device=dev), sd=torch.empty(m, device=dev),
+                lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
+                safe=torch.empty(m, dtype=torch.uint8, device=dev))
+    key = torch.empty(2, dtype=torch.int64, device=dev)
+
+    def loop():
+        gm.fit(X[:n0], Y[:n0], OBS[:n0])
+        t_app = t_tick = 0.0
+        last = None
+        for i in range(iters):
+            a0, a1 = chunks[i], chunks[i + 1]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            gm.append(X[a0:a1], Y[a0:a1], OBS[a0:a1])
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs, key_out=key)
+            last = key.cpu()
+            t_tick += time.perf_counter() - t1
+            t_app += t1 - t0
+        return t_app, t_tick, last
+
+    for _ in range(a.warmup):
+        loop()
+    prof.reset()
+    reps = max(1, a.steps // iters)
+    t0 = time.perf_counter()
+    t_app = t_tick = 0.0
+    last = None
+    for _ in range(reps):
+        ta, tt, last = loop()
+        t_app += ta
+        t_tick += tt
+    elapsed = time.perf_counter() - t0
+    pr = prof.read()
+    prof.reset(False)
+    steps = reps * iters
+    pred_ms = pr["predict_ms"] / max(pr["predict_launches"], 1)
+    achieved = pr["predict_flops"] / max(pr["predict_launches"], 1) / (pred_ms * 1e-3) / 1e12
+    (s, i), = key_tensor_to_pairs(last)
+    return {
+        "metric": METRIC, "value": m * steps / elapsed, "unit": "grid-points/s", "n_gpus": 1, "steps": steps,
+        "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": DATA,
+        "config": {"workload": "C5", "n_train": [n0, n_end], "iterations": iters, "grid": [g, g], "M": m,
+                   "parallelism": "single", "step": "sbo_append (block Cholesky) + sbo_tick (includes one fit per loop)"},
+        "roofline": {"kernel": "predict_kernel", "bound": "mfma", "achieved": achieved,
+                     "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_F32_MFMA_TFLOPS,
+                     "traffic": None, "avg_launch_ms": pred_ms},
+        "append_ms_avg": t_app * 1e3 / steps, "tick_ms_avg": t_tick * 1e3 / steps,
+        "argmax": {"index": i, "score": s}, "cpu_baseline": None,
+    }
 
 
 def cpu_baseline(gm, wl, budget_s):
-    """The oracle's f32 predictive path (blocked TRSM, OpenMP) + ComputeSets +
-    argmax on a contiguous sample of the grid, given the device factor; points/s
-    extrapolated linearly (the M axis is embarrassingly parallel)."""
+    """The oracle's f32 predictive path (dense blocked TRSM, OpenMP) +
+    ComputeSets + argmax on a contiguous sample of the grid, given the device
+    factor; points/s extrapolated linearly (the M axis is embarrassingly parallel)."""
     from oracle import oracle as O
     threads = min(16, os.cpu_count() or 1)
     O.set_threads(threads)
@@ -241,8 +338,8 @@ def cpu_baseline(gm, wl, budget_s):
     k2 = max(64, (k2 // 64) * 64)
     t2 = run(k2)
     return {"value": k2 / t2, "unit": "grid-points/s", "cores": threads, "kind": "port",
-            "sample": f"{k2} contiguous grid points of {wl.name} (N={wl.x.size}), f32 blocked TRSM predictive + "
-                      f"ComputeSets + argmax, given the device L/alpha; {t2:.1f} s wall"}
+            "sample": f"{k2} contiguous grid points of {wl.name} (N={wl.x.size}), f32 dense blocked TRSM predictive "
+                      f"+ ComputeSets + argmax (oracle, OpenMP), given the device L/alpha; {t2:.1f} s wall"}
 
 
 if __name__ == "__main__":
