@@ -210,6 +210,7 @@ def run_sweep(a, dev, world, rank):
     achieved = exec_flops_launch / (pred_ms * 1e-3) / 1e12
     fill_gbs = fill_bytes / (fill_ms * 1e-3) / 1e9 if fill_ms > 0 else None
     cpu = cpu_baseline(gm, wl, a.cpu_seconds) if world == 1 and not a.no_cpu else None
+    traffic, traffic_src = pmc_traffic(a.config, n, m_total, m)
     return {
         "metric": METRIC, "value": value, "unit": "grid-points/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": a.scaling,
@@ -221,7 +222,7 @@ def run_sweep(a, dev, world, rank):
                    "outputs_written": not a.no_outputs},
         "roofline": {"kernel": "predict_kernel (V = sf2 L^-1 K*^T, f32 MFMA 32x32x2)", "bound": "mfma",
                      "achieved": achieved, "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_F32_MFMA_TFLOPS, "traffic": None,
+                     "frac": achieved / PEAK_F32_MFMA_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
                      "avg_launch_ms": pred_ms, "max_rank_launch_ms": pred_ms_max,
                      "algorithmic_flops_per_launch": exec_flops_launch,
                      "dense_flops_per_launch": dense_flops_launch,
@@ -307,6 +308,22 @@ def run_streaming(a, dev, world, rank):
         "append_ms_avg": t_app * 1e3 / steps, "tick_ms_avg": t_tick * 1e3 / steps,
         "argmax": {"index": i, "score": s}, "cpu_baseline": None,
     }
+
+
+def pmc_traffic(config, n, m_total, m):
+    """HBM bytes per predict launch from the newest committed PMC summary of
+    this config (tools/collect_pmc.sh: separate FETCH_SIZE / WRITE_SIZE
+    rocprofv3 passes, gfx950 FETCH_SIZE x2), scaled to this rank's shard."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{config}.json")))
+    if not files or m_total == 0:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+        t = d["predict_kernel"]["traffic_bytes"] * m / m_total
+        return t, f"{os.path.relpath(files[-1], ROOT)} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
+    except Exception:
+        return None, None
 
 
 def cpu_baseline(gm, wl, budget_s):

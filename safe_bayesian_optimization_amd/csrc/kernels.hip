@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void pack_operand_kernel(const T *__restrict__
     if (kb >= (I + 1) * kTilesPerRowBlockStep) return;
     float *tile = aug + (tile_start(I) + kb) * kTileFloats;
     for (int e = threadIdx.x; e < kTileFloats; e += 256) {
-        const int k = e / kBM, r = e % kBM;
+        const int k = e / kBM, r = ((e & 3) << 5) | ((e >> 2) & 31);  // inverse of tile_offset
         const int64_t row = I * kBM + r, col = kb * kBK + k;
         float v = 0.0f;
         if (row < n && col < n && col <= row) v = (float)(sf2 * Linv[row + col * ld]);
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(kBM) void row_l1_kernel(const float *__restrict__ a
     const float *t = aug + tile_start(I) * kTileFloats;
     const int64_t nk = (I + 1) * kBM;  // k-tiles 0..2(I+1)-1, each [BK][BM]
     double s = 0.0;
-    for (int64_t k = 0; k < nk; ++k) s += fabs((double)t[k * kBM + r]);
+    for (int64_t k = 0; k < nk; ++k) s += fabs((double)t[(k / kBK) * kTileFloats + tile_offset((int)(k % kBK), r)]);
     row_l1[I * kBM + r] = s;
 }
 
@@ -226,18 +226,35 @@ __device__ __forceinline__ void predict_body(const float *__restrict__ tiles,
     for (int i = 0; i < cnt; ++i) {
         const int cur = i & 1;
         if (i + 1 < cnt) SBO_STAGE(tlist ? tlist[i + 1] : i + 1, cur ^ 1);
-        const float *sA = smem + cur * kStageFloats;
-        const float *sC = sA + kTileFloats;
+        // per-lane bases; every k step is a constant offset from them (LDS
+        // immediate offsets, no per-step address registers)
+        const float4 *pa = reinterpret_cast<const float4 *>(smem + cur * kStageFloats) + half * 32 + row;
+        const float *pc = smem + cur * kStageFloats + kTileFloats + half;
+        // software pipeline: the A operands (one ds_read_b128 = the four row
+        // blocks, tile_offset layout) and K* of k step p+1 are fetched and
+        // evaluated while the four MFMAs of step p run
+        float4 a_cur = pa[0];
+        float b_cur;
+        {
+            const float dx = pc[0] - xq, dy = pc[kBK] - yq;
+            b_cur = fast_exp2(cexp * fmaf(dy, dy, dx * dx));
+        }
 #pragma unroll
         for (int p = 0; p < kBK / 2; ++p) {
-            const int k = 2 * p + half;
-            const float dx = sC[k] - xq, dy = sC[kBK + k] - yq;
-            const float b = fast_exp2(cexp * fmaf(dy, dy, dx * dx));
-            if (MEAN) mu = fma((double)sC[2 * kBK + k], (double)b, mu);
-#pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
-                acc[rb] = __builtin_amdgcn_mfma_f32_32x32x2f32(sA[k * kBM + rb * 32 + row], b,
-                                                               p == 0 ? zero : acc[rb], 0, 0, 0);
+            float4 a_nxt = a_cur;
+            float b_nxt = b_cur;
+            if (p + 1 < kBK / 2) {
+                a_nxt = pa[(p + 1) * 64];
+                const float dx = pc[2 * (p + 1)] - xq, dy = pc[kBK + 2 * (p + 1)] - yq;
+                b_nxt = fast_exp2(cexp * fmaf(dy, dy, dx * dx));
+            }
+            if (MEAN) mu = fma((double)pc[2 * kBK + 2 * p], (double)b_cur, mu);
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur.x, b_cur, p == 0 ? zero : acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur.y, b_cur, p == 0 ? zero : acc[1], 0, 0, 0);
+            acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur.z, b_cur, p == 0 ? zero : acc[2], 0, 0, 0);
+            acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur.w, b_cur, p == 0 ? zero : acc[3], 0, 0, 0);
+            a_cur = a_nxt;
+            b_cur = b_nxt;
         }
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)

@@ -743,7 +743,7 @@ SBO_API sbo_status sbo_get_inverse(sbo_ctx *ctx, float *Linv) {
             for (int k = 0; k < sbo::kBK; ++k)
                 for (int r = 0; r < sbo::kBM; ++r) {
                     const int64_t row = I * sbo::kBM + r, col = kb * sbo::kBK + k;
-                    if (row < n && col < n) Linv[row * n + col] = t[k * sbo::kBM + r];
+                    if (row < n && col < n) Linv[row * n + col] = t[sbo::tile_offset(k, r)];
                 }
         }
     return SBO_OK;

@@ -31,6 +31,10 @@ __host__ __device__ inline int64_t round_up(int64_t v, int64_t m) { return (v + 
 // First packed tile of row block I: sum_{I'<I} (I'+1)*(BM/BK).
 __host__ __device__ inline int64_t tile_start(int64_t I) { return kTilesPerRowBlockStep * I * (I + 1) / 2; }
 inline int64_t total_tiles(int64_t nI) { return tile_start(nI); }
+// Element offset inside a packed [BK][BM] tile of A[row][k] (row < BM, k < BK):
+// the four 32-row MFMA blocks of one row are adjacent, so one ds_read_b128 per
+// lane fetches the A operands of all four MFMAs of a k step.
+__host__ __device__ constexpr int tile_offset(int k, int row) { return (k * 32 + (row & 31)) * 4 + (row >> 5); }
 
 // ----------------------------------------------------------- device buffer
 class DevBuf {
