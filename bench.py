@@ -33,7 +33,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA peak (spec, 2.4 GHz)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = "GP posterior+acq grid-points/sec at N train pts; 1/2/4/8 GPU"
 DATA = "synthetic (SplitMix64 smooth field + N(0,sn2) noise in BASELINE config shapes; terrain.csv is a missing blob)"
@@ -220,7 +220,7 @@ def run_sweep(a, dev, world, rank):
                    "hyper": [wl.hyper.length_scale, wl.hyper.sigma_f, wl.hyper.noise_level],
                    "kstar_cutoff_log2": cutoff, "parallelism": f"m-shard{world}" if world > 1 else "single",
                    "outputs_written": not a.no_outputs},
-        "roofline": {"kernel": "predict_kernel (V = sf2 L^-1 K*^T, f32 MFMA 32x32x2)", "bound": "mfma",
+        "roofline": {"kernel": "predict_kernel (V = sf2 L^-1 K*^T, f32 MFMA 16x16x4)", "bound": "mfma",
                      "achieved": achieved, "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F32_MFMA_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
                      "avg_launch_ms": pred_ms, "max_rank_launch_ms": pred_ms_max,

@@ -191,10 +191,14 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * workgroup's 128 queries are spatially compact and skip more k-tiles;
  * outputs and argmax indices stay in the caller's order. */
 #define SBO_OPT_QUERY_ORDER 4
-/* SBO_OPT_KERNEL_VARIANT (A/B builds of the predictive kernel): 0 = f64
- * cross-tile accumulator, 2 waves/SIMD (default); 1 = f32 accumulator,
- * 2 waves/SIMD; 2 = f32 accumulator, 3 waves/SIMD. */
+/* SBO_OPT_KERNEL_VARIANT (A/B builds of the predictive kernel): 0 = f32
+ * cross-tile accumulator (default); 1 = f64 cross-tile accumulator (same
+ * accuracy at N = 16384, 5 % slower: tools/variant_accuracy.py). */
 #define SBO_OPT_KERNEL_VARIANT 5
+/* SBO_OPT_ROW_CHUNK: row blocks (256 rows each) one predictive workgroup
+ * walks for its 128 queries; 0 = default (1: row-block-major grid, A tiles
+ * shared in L2 by the concurrently running workgroups). */
+#define SBO_OPT_ROW_CHUNK 6
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The K* tile cutoff in effect (auto or fixed) and the norms it was derived from. */

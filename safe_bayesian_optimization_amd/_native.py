@@ -36,6 +36,7 @@ SBO_OPT_SPATIAL_ORDER = 2
 SBO_OPT_TILE_SKIP = 3
 SBO_OPT_QUERY_ORDER = 4
 SBO_OPT_KERNEL_VARIANT = 5
+SBO_OPT_ROW_CHUNK = 6
 
 
 class SboError(RuntimeError):

@@ -12,6 +12,8 @@
 //
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit,
 // so the f64 acquisition arithmetic is the node's plain IEEE double sequence.
+#include <algorithm>
+
 #include "sbo_internal.hpp"
 
 namespace sbo {
@@ -98,7 +100,9 @@ __global__ __launch_bounds__(256) void pack_operand_kernel(const T *__restrict__
     if (kb >= (I + 1) * kTilesPerRowBlockStep) return;
     float *tile = aug + (tile_start(I) + kb) * kTileFloats;
     for (int e = threadIdx.x; e < kTileFloats; e += 256) {
-        const int k = e / kBM, r = ((e & 3) << 5) | ((e >> 2) & 31);  // inverse of tile_offset
+        // inverse of tile_offset: e = ((jj*BK + k)*16 + r)*4 + j3, row = 64 jj + 16 j3 + r
+        const int j3 = e & 3, r16 = (e >> 2) & 15, k = (e >> 6) & (kBK - 1), jj = e >> 12;
+        const int r = jj * 64 + j3 * 16 + r16;
         const int64_t row = I * kBM + r, col = kb * kBK + k;
         float v = 0.0f;
         if (row < n && col < n && col <= row) v = (float)(sf2 * Linv[row + col * ld]);
@@ -152,118 +156,117 @@ __global__ void tile_box_kernel(const float *__restrict__ x, const float *__rest
 }
 
 // ---------------------------------------------------------- a3+a4 predict
-// Workgroup (I, qb): rows [I*BM, I*BM+BM) of A = sf2 L^-1 and the BN = 128
-// queries [qb*BN, qb*BN+BN).  Wave w owns queries qb*BN + 32w + (l&31) and all
-// BM = 128 rows as four 32-row blocks: four accumulators of
-// v_mfma_f32_32x32x2_f32 (exact f32, 64 FLOP/clk/SIMD, independent so the
-// 64-cycle dependent latency never stalls issue).  The B operand K*[k][q] is
-// generated per lane -- lane l holds k = l>>5, q = l&31, exactly the MFMA
-// B-fragment map -- so K* never touches LDS or HBM: one exp2 per lane per
-// four MFMAs.  The A tile [BK][BM] is staged through LDS (double buffered,
-// one barrier per stage); lanes 0-31 / 32-63 read consecutive rows of
-// adjacent k (conflict-free).  The mean rides along in the last row block
-// (every k visited) as an f64 FMA per k pair.
+// Workgroup (qb, chunk): the BN = 128 queries [qb*BN, qb*BN+BN) against the
+// row blocks I of one chunk, each I = rows [I*BM, I*BM+BM) of A = sf2 L^-1
+// (BM = 256).  Eight waves, two per SIMD; wave w owns the 16 queries
+// qb*BN + 16w + (l&15) and ALL 256 rows of the current row block as sixteen
+// 16-row blocks: sixteen accumulators of v_mfma_f32_16x16x4_f32 (exact f32,
+// 64 FLOP/clk/SIMD).  The B operand K*[k][q] is generated per lane -- lane l
+// holds k = l>>4, q = l&15, exactly the MFMA B-fragment map -- so K* never
+// touches LDS or HBM.
 //
-// Exact tile skipping: a k-tile whose bounding box is farther from the
-// workgroup's query bounding box than the f32 underflow radius
-// (c*d^2 < -160, i.e. |d| > 14.9 l) contributes K* == +0.0 to every product,
-// so it adds exactly nothing to any accumulator.  Each workgroup first
-// compacts the list of k-tiles it needs (ascending, so the surviving
-// accumulation order is unchanged and results are bitwise identical to the
-// dense sweep) and only stages and multiplies those.
+// Why this shape: on gfx950 the VALU work of a wave does not overlap the
+// matrix pipe (measured, tools/mfma_probe.hip: four 32x32x2 MFMAs per K*
+// value run at 86 % of peak, sixteen 16x16x4 MFMAs per K* value at 91 %), so
+// the K* chain (2 sub, mul, fma, mul, exp) must be amortised over as many
+// MFMAs as the register file allows.  256 rows x 16 queries per wave is 64
+// accumulator registers plus 64 (f32) or 128 (f64) for the cross-tile sum,
+// which leaves two waves per SIMD.
+//
+// The A tile [BK = 64][BM = 256] is staged through LDS by LDS-DMA (double
+// buffered, one barrier per stage).  tile_offset puts the four A operands of
+// row blocks 4jj..4jj+3 of one (k, row&15) side by side, so a k step is four
+// conflict-free ds_read_b128 per lane.  The mean rides along in the last row
+// block (every k visited) as an f64 FMA per k step.
+//
+// Tile skipping: a k-tile whose bounding box is farther from the
+// workgroup's query bounding box than the cutoff radius contributes K* <
+// 2^-L to every product (exactly +0.0 for L >= 150: c*d^2 < -150 underflows).
+// Each workgroup compacts, once, the ascending list of k-tiles its queries
+// need; row block I multiplies the prefix of that list below its diagonal
+// (t < 4(I+1)), so the surviving accumulation order is the dense order and
+// results are bitwise identical to the dense sweep at L >= 150.  The cutoff
+// L comes from an error budget (sbo_api.cpp).  One workgroup walks all row
+// blocks of its chunk as one flat stream of (row block, k-tile) items, so
+// the list is built once per chunk, the LDS-DMA pipeline runs across row
+// block boundaries, and row blocks with an empty prefix cost nothing.
 //
 // Accuracy: a single f32 MFMA chain over all N training points accumulates
 // ~sqrt(N) roundings on large cancelling terms (2.2e-5 normwise variance
-// error at N = 8192, measured on the device and emulated on the host).  The
-// chain is therefore cut after every k-tile (BK = 64 k): each tile's MFMA
-// chain starts from a zero accumulator and its result is added into an f64
-// outer accumulator (2 VALU per accumulator register per tile).
+// error at N = 8192, measured).  Each k-tile's chain therefore starts from
+// zero and is added into an outer accumulator; the K* evaluation error
+// (f32 coordinate differences and exp2), amplified by A, dominates what is
+// left (tools/variant_accuracy.py: 7e-6 at N = 16384 for either outer type).
 constexpr int kStageFloats = kTileFloats + 3 * kBK;
-constexpr int kMaxList = 2048;  // k-tiles a workgroup can list (N <= 131072); beyond: dense
-constexpr int kSmemFloats = 2 * kStageFloats + kMaxList + 32;
+constexpr int kMaxList = 2048;   // k-tiles a workgroup can list (N <= 131072); beyond: dense
+constexpr int kMaxChunk = 128;   // row blocks per workgroup chunk
+constexpr int kPredictWaves = kBN / 16;
+constexpr int kPredictThreads = 64 * kPredictWaves;
+constexpr int kSmemFloats = 2 * kStageFloats + kMaxList + 4 * kPredictWaves + kPredictWaves + kMaxChunk;
+constexpr int kSteps = kBK / 4;          // 16x16x4 k steps per tile
+constexpr int kRowBlocks = kBM / 16;     // 16-row MFMA blocks per wave
 
-template <bool MEAN, class OT>
-__device__ __forceinline__ void predict_body(const float *__restrict__ tiles,
-                                             const float *__restrict__ kc, const int *tlist,
-                                             int cnt, float xq, float yq, float cexp, float *smem,
-                                             OT (&outer)[4][16], double &mu) {
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int half = lane >> 5;
-    const int row = lane & 31;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-    // LDS-DMA staging (global_load_lds_dwordx4): each wave instruction moves
-    // 1 KiB, lane-linear; no staging registers.  A stage = the 32 KiB [BK][BM]
-    // tile (8 instructions per wave) + 768 B of per-k coordinates (wave 0,
-    // lanes 0-47).
-    const int wave = tid >> 6;
-    typedef __attribute__((address_space(3))) void lds_void;
-    const char *gA = reinterpret_cast<const char *>(tiles) + wave * 1024 + lane * 16;
-    const char *gC = reinterpret_cast<const char *>(kc) + lane * 16;
-    char *lA = reinterpret_cast<char *>(smem) + wave * 1024;
-    constexpr int kTileBytes = kTileFloats * 4, kStageBytes = kStageFloats * 4, kCBytes = 3 * kBK * 4;
-#define SBO_STAGE(kb, buf)                                                                          \
-    do {                                                                                            \
-        const char *s_ = gA + (int64_t)(kb) * kTileBytes;                                           \
-        char *d_ = lA + (buf) * kStageBytes;                                                        \
-        _Pragma("unroll") for (int j = 0; j < kTileBytes / 4096; ++j)                               \
-            __builtin_amdgcn_global_load_lds((const void *)(s_ + j * 4096), (lds_void *)(d_ + j * 4096), \
-                                             16, 0, 0);                                             \
-        if (wave == 0 && lane < kCBytes / 16)                                                       \
-            __builtin_amdgcn_global_load_lds((const void *)(gC + (int64_t)(kb) * kCBytes),          \
-                                             (lds_void *)(reinterpret_cast<char *>(smem) +          \
-                                                          (buf) * kStageBytes + kTileBytes),        \
-                                             16, 0, 0);                                             \
-    } while (0)
-
-    f32x16 acc[4];
-    const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (cnt == 0) return;
-
-    SBO_STAGE(tlist ? tlist[0] : 0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int i = 0; i < cnt; ++i) {
-        const int cur = i & 1;
-        if (i + 1 < cnt) SBO_STAGE(tlist ? tlist[i + 1] : i + 1, cur ^ 1);
-        // per-lane bases; every k step is a constant offset from them (LDS
-        // immediate offsets, no per-step address registers)
-        const float4 *pa = reinterpret_cast<const float4 *>(smem + cur * kStageFloats) + half * 32 + row;
-        const float *pc = smem + cur * kStageFloats + kTileFloats + half;
-        // software pipeline: the A operands (one ds_read_b128 = the four row
-        // blocks, tile_offset layout) and K* of k step p+1 are fetched and
-        // evaluated while the four MFMAs of step p run
-        float4 a_cur = pa[0];
-        float b_cur;
-        {
-            const float dx = pc[0] - xq, dy = pc[kBK] - yq;
-            b_cur = fast_exp2(cexp * fmaf(dy, dy, dx * dx));
-        }
+// The sixteen k steps of one staged tile: acc = A_tile * K*_tile (fresh
+// chain), mean += sf2 alpha^T K* when MEAN.
+//
+// Software pipeline, pinned with scheduling fences (left alone, the compiler
+// minimises registers by issuing each A read right before its MFMA and then
+// waiting on it): step p first issues the LDS reads of the A operands of
+// step p+1 (four ds_read_b128 = the sixteen row blocks, tile_offset layout)
+// and of the coordinates of step p+2, then evaluates K* of step p+1 from
+// coordinates read one step earlier, beside the sixteen MFMAs of step p.  No
+// MFMA or exp waits on a read issued in its own step.
+template <bool MEAN>
+__device__ __forceinline__ void tile_steps(const float4 *__restrict__ pa, const float *__restrict__ pc, float xq,
+                                           float yq, float cexp, f32x4 (&acc)[kRowBlocks], double &mu) {
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    float4 a_cur[4];
 #pragma unroll
-        for (int p = 0; p < kBK / 2; ++p) {
-            float4 a_nxt = a_cur;
-            float b_nxt = b_cur;
-            if (p + 1 < kBK / 2) {
-                a_nxt = pa[(p + 1) * 64];
-                const float dx = pc[2 * (p + 1)] - xq, dy = pc[kBK + 2 * (p + 1)] - yq;
-                b_nxt = fast_exp2(cexp * fmaf(dy, dy, dx * dx));
-            }
-            if (MEAN) mu = fma((double)pc[2 * kBK + 2 * p], (double)b_cur, mu);
-            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur.x, b_cur, p == 0 ? zero : acc[0], 0, 0, 0);
-            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur.y, b_cur, p == 0 ? zero : acc[1], 0, 0, 0);
-            acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur.z, b_cur, p == 0 ? zero : acc[2], 0, 0, 0);
-            acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur.w, b_cur, p == 0 ? zero : acc[3], 0, 0, 0);
-            a_cur = a_nxt;
-            b_cur = b_nxt;
-        }
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) outer[rb][r] += (OT)acc[rb][r];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+    for (int jj = 0; jj < 4; ++jj) a_cur[jj] = pa[jj * 1024];
+    float b_cur;
+    {
+        const float dx = pc[0] - xq, dy = pc[kBK] - yq;
+        b_cur = fast_exp2(cexp * fmaf(dy, dy, dx * dx));
     }
-#undef SBO_STAGE
+    float x1 = pc[4], y1 = pc[kBK + 4];
+#pragma unroll
+    for (int p = 0; p < kSteps; ++p) {
+        float4 a_nxt[4];
+        float x2 = x1, y2 = y1;
+        if (p + 1 < kSteps) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) a_nxt[jj] = pa[jj * 1024 + (p + 1) * 64];
+        }
+        if (p + 2 < kSteps) {
+            x2 = pc[4 * (p + 2)];
+            y2 = pc[kBK + 4 * (p + 2)];
+        }
+        const float alpha = MEAN ? pc[2 * kBK + 4 * p] : 0.0f;
+        __builtin_amdgcn_sched_barrier(0);
+        float b_nxt = b_cur;
+        if (p + 1 < kSteps) {
+            const float dx = x1 - xq, dy = y1 - yq;
+            b_nxt = fast_exp2(cexp * fmaf(dy, dy, dx * dx));
+        }
+        if (MEAN) mu = fma((double)alpha, (double)b_cur, mu);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            acc[4 * jj + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].x, b_cur, p == 0 ? zero : acc[4 * jj + 0], 0, 0, 0);
+            acc[4 * jj + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].y, b_cur, p == 0 ? zero : acc[4 * jj + 1], 0, 0, 0);
+            acc[4 * jj + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].z, b_cur, p == 0 ? zero : acc[4 * jj + 2], 0, 0, 0);
+            acc[4 * jj + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].w, b_cur, p == 0 ? zero : acc[4 * jj + 3], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (p + 1 < kSteps) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) a_cur[jj] = a_nxt[jj];
+        }
+        x1 = x2;
+        y1 = y2;
+        b_cur = b_nxt;
+    }
 }
 
 __device__ __forceinline__ float wave_min(float v) {
@@ -277,34 +280,38 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
-// OT: outer (cross-tile) accumulator type; W: waves per SIMD the register
-// budget is fitted to (f64 outer needs 2; f32 outer can run 3).
-template <class OT, int W>
-__global__ __launch_bounds__(256, W) void predict_kernel(const float *__restrict__ aug,
-                                                         const float *__restrict__ kcoord,
-                                                         const float4 *__restrict__ kbox, int nI,
-                                                         int nQ, const float *__restrict__ qx,
-                                                         const float *__restrict__ qy, int64_t m,
-                                                         int64_t ldp, float cexp, float skip_d2,
-                                                         float m0, float *__restrict__ part,
-                                                         float *__restrict__ mean,
-                                                         unsigned long long *__restrict__ tiles_done) {
+// OT: outer (cross-tile) accumulator type.  Grid: nQ query blocks x nC row
+// block chunks of G row blocks.
+template <class OT>
+__global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
+    const float *__restrict__ aug, const float *__restrict__ kcoord, const float4 *__restrict__ kbox, int nI, int nC,
+    int G, const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp, float cexp,
+    float skip_d2, float m0, float *__restrict__ part, float *__restrict__ mean,
+    unsigned long long *__restrict__ tiles_done) {
     __shared__ __attribute__((aligned(16))) float smem[kSmemFloats];
     int *tlist = reinterpret_cast<int *>(smem + 2 * kStageFloats);
-    float *wbox = smem + 2 * kStageFloats + kMaxList;       // [4 waves][4]
-    int *wcnt = reinterpret_cast<int *>(wbox + 16);         // [4 waves]
+    float *wbox = smem + 2 * kStageFloats + kMaxList;               // [waves][4]
+    int *wcnt = reinterpret_cast<int *>(wbox + 4 * kPredictWaves);  // [waves]
+    int *rcnt = wcnt + kPredictWaves;                               // [G] list prefix per row block
+    // chunk-major, heaviest chunk first; consecutive workgroups take
+    // consecutive (Morton-adjacent) query blocks of one chunk.  Workgroups go
+    // to the 8 XCDs round-robin by index, so every XCD sees every chunk.
+    const int64_t nQ = (m + kBN - 1) / kBN;
     const int64_t bid = blockIdx.x;
-    const int I = nI - 1 - (int)(bid / nQ);  // heaviest row blocks first
     const int64_t qb = bid % nQ;
+    const int chunk = nC - 1 - (int)(bid / nQ);
+    const int I0 = chunk * G, I1 = min(I0 + G, nI);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int nkb = (I + 1) * kTilesPerRowBlockStep;
-    const float *tiles = aug + tile_start(I) * kTileFloats;
+    const int g = lane >> 4;   // k within the step
+    const int r = lane & 15;   // row within a 16-row block / query within the wave
+    const int nkb = I1 * kTilesPerRowBlockStep;
 
-    const int64_t q = qb * kBN + wave * 32 + (lane & 31);
+    const int64_t q = qb * kBN + wave * 16 + r;
     const int64_t qc = q < m ? q : m - 1;
     const float xq = qx[qc], yq = qy[qc];
+    const bool writer = lane < 16 && q < m;
 
     // ---- list the k-tiles this workgroup needs (ascending)
     int cnt = nkb;
@@ -318,12 +325,12 @@ __global__ __launch_bounds__(256, W) void predict_kernel(const float *__restrict
         __syncthreads();
         float qx0 = wbox[0], qx1 = wbox[1], qy0 = wbox[2], qy1 = wbox[3];
 #pragma unroll
-        for (int w = 1; w < 4; ++w) {
+        for (int w = 1; w < kPredictWaves; ++w) {
             qx0 = fminf(qx0, wbox[w * 4 + 0]); qx1 = fmaxf(qx1, wbox[w * 4 + 1]);
             qy0 = fminf(qy0, wbox[w * 4 + 2]); qy1 = fmaxf(qy1, wbox[w * 4 + 3]);
         }
         int base = 0;
-        for (int t0 = 0; t0 < nkb; t0 += 256) {
+        for (int t0 = 0; t0 < nkb; t0 += kPredictThreads) {
             const int t = t0 + tid;
             bool keep = false;
             if (t < nkb) {
@@ -337,43 +344,146 @@ __global__ __launch_bounds__(256, W) void predict_kernel(const float *__restrict
             __syncthreads();  // previous chunk's wcnt reads are done
             if (lane == 0) wcnt[wave] = __popcll(bal);
             __syncthreads();
-            int off = base;
-            for (int w = 0; w < wave; ++w) off += wcnt[w];
+            int off = base, tot = 0;
+#pragma unroll
+            for (int w = 0; w < kPredictWaves; ++w) {
+                off += w < wave ? wcnt[w] : 0;
+                tot += wcnt[w];
+            }
             if (keep) tlist[off + before] = t;
-            base += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+            base += tot;
         }
-        __syncthreads();
         cnt = base;
         list = tlist;
+        __syncthreads();
     }
-    if (tid == 0 && tiles_done) atomicAdd(tiles_done, (unsigned long long)cnt);  // executed-work counter
+    // ---- list prefix of each row block of the chunk: entries t < 4(I+1)
+    for (int i = tid; i < I1 - I0; i += kPredictThreads) {
+        const int lim = (I0 + i + 1) * kTilesPerRowBlockStep;
+        int n = lim < cnt ? lim : cnt;
+        if (list) {  // ascending list: lower bound of lim
+            int lo = 0, hi = cnt;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (list[mid] < lim) lo = mid + 1; else hi = mid;
+            }
+            n = lo;
+        }
+        rcnt[i] = n;
+    }
+    __syncthreads();
+    if (tid == 0 && tiles_done) {  // executed-work counter
+        unsigned long long tot = 0;
+        for (int i = 0; i < I1 - I0; ++i) tot += (unsigned long long)rcnt[i];
+        atomicAdd(tiles_done, tot);
+    }
+    // row blocks with an empty prefix contribute exactly zero
+    for (int I = I0; I < I1; ++I)
+        if (rcnt[I - I0] == 0 && writer) {
+            part[(int64_t)I * ldp + q] = 0.0f;
+            if (I == nI - 1) mean[q] = m0;
+        }
 
-    OT outer[4][16];
+    // ---- the sweep: a flat stream of (row block, k-tile) items
+    // LDS-DMA staging (global_load_lds_dwordx4): each wave instruction moves
+    // 1 KiB, lane-linear, no staging registers.  A stage = the 64 KiB [BK][BM]
+    // tile (8 instructions per wave) + 768 B of per-k coordinates (wave 0).
+    // The DMA is issued from inline asm so that hipcc does not see an LDS
+    // write in flight: with a compiler-visible one pending it drains every
+    // ds_read wait to lgkmcnt(0) (waiting on reads issued one instruction
+    // earlier) instead of counting.  The stage is retired by the explicit
+    // vmcnt(0) + barrier at the end of each item.
+    typedef __attribute__((address_space(3))) char lds_char;
+    constexpr int kTileBytes = kTileFloats * 4, kStageBytes = kStageFloats * 4, kCBytes = 3 * kBK * 4;
+    constexpr int kWaveStride = kTileBytes / kPredictWaves;  // bytes per wave per stage
+    const char *gA = reinterpret_cast<const char *>(aug) + wave * 1024 + lane * 16;
+    const char *gC = reinterpret_cast<const char *>(kcoord) + lane * 16;
+    const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
+    const uint32_t lds_wave = lds_smem + (uint32_t)__builtin_amdgcn_readfirstlane(wave) * 1024u;
+#define SBO_DMA16(gsrc, ldst)                                                                           \
+    do {                                                                                                \
+        uint32_t keep_;                                                                                 \
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t" \
+                     "s_mov_b32 m0, %0"                                                                 \
+                     : "=&s"(keep_)                                                                     \
+                     : "v"(gsrc), "s"(ldst)                                                             \
+                     : "memory");                                                                       \
+    } while (0)
+#define SBO_STAGE(I_, t_, buf)                                                                          \
+    do {                                                                                                \
+        const char *s_ = gA + (tile_start(I_) + (t_)) * (int64_t)kTileBytes;                           \
+        const uint32_t d_ = lds_wave + (uint32_t)(buf) * kStageBytes;                                   \
+        _Pragma("unroll") for (int j = 0; j < kWaveStride / 1024; ++j)                                  \
+            SBO_DMA16(s_ + j * kPredictWaves * 1024, d_ + (uint32_t)(j * kPredictWaves * 1024));        \
+        if (wave == 0 && lane < kCBytes / 16)                                                           \
+            SBO_DMA16(gC + (int64_t)(t_) * kCBytes, lds_smem + (uint32_t)((buf) * kStageBytes + kTileBytes)); \
+    } while (0)
+
+    int I = I0;
+    while (I < I1 && rcnt[I - I0] == 0) ++I;
+    if (I >= I1) return;
+    SBO_STAGE(I, list ? list[0] : 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    OT outer[kRowBlocks][4];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
+    for (int rb = 0; rb < kRowBlocks; ++rb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) outer[rb][r] = (OT)0;
+        for (int e = 0; e < 4; ++e) outer[rb][e] = (OT)0;
     double mu = 0.0;
-
-    const bool last = (I == nI - 1);
-    if (last)
-        predict_body<true, OT>(tiles, kcoord, list, cnt, xq, yq, cexp, smem, outer, mu);
-    else
-        predict_body<false, OT>(tiles, kcoord, list, cnt, xq, yq, cexp, smem, outer, mu);
-
-    // epilogue: column sums of V^2 over this block's rows; lanes l and l+32 hold
-    // the two row halves of column l&31 of each 32x32 accumulator
-    double s = 0.0;
+    f32x4 acc[kRowBlocks];
+    int j = 0, cur = 0;
+    for (;;) {
+        const int n = rcnt[I - I0];
+        // next item: (I, j+1), or the first tile of the next non-empty row block
+        int In = I, jn = j + 1;
+        if (jn >= n) {
+            jn = 0;
+            do ++In; while (In < I1 && rcnt[In - I0] == 0);
+        }
+        const bool more = In < I1;
+        if (more) SBO_STAGE(In, list ? list[jn] : jn, cur ^ 1);
+        // per-lane bases; every k step is a constant offset from them
+        const float4 *pa = reinterpret_cast<const float4 *>(smem + cur * kStageFloats) + g * 16 + r;
+        const float *pc = smem + cur * kStageFloats + kTileFloats + g;
+        if (I == nI - 1)
+            tile_steps<true>(pa, pc, xq, yq, cexp, acc, mu);
+        else
+            tile_steps<false>(pa, pc, xq, yq, cexp, acc, mu);
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
+        for (int rb = 0; rb < kRowBlocks; ++rb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s = fma((double)outer[rb][r], (double)outer[rb][r], s);
-    s += __shfl_xor(s, 32);
-    mu += __shfl_xor(mu, 32);
-    if (lane < 32 && q < m) {
-        part[(int64_t)I * ldp + q] = (float)s;
-        if (last) mean[q] = (float)((double)m0 + mu);
+            for (int e = 0; e < 4; ++e) outer[rb][e] += (OT)acc[rb][e];
+        if (j == n - 1) {
+            // row block done: column sums of V^2 over its rows; lanes l, l+16,
+            // l+32, l+48 hold four row quarters of column l&15 of every block
+            double s = 0.0;
+#pragma unroll
+            for (int rb = 0; rb < kRowBlocks; ++rb)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    s = fma((double)outer[rb][e], (double)outer[rb][e], s);
+                    outer[rb][e] = (OT)0;
+                }
+            s += __shfl_xor(s, 16);
+            s += __shfl_xor(s, 32);
+            if (writer) part[(int64_t)I * ldp + q] = (float)s;
+            if (I == nI - 1) {
+                mu += __shfl_xor(mu, 16);
+                mu += __shfl_xor(mu, 32);
+                if (writer) mean[q] = (float)((double)m0 + mu);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (!more) break;
+        I = In;
+        j = jn;
+        cur ^= 1;
     }
+#undef SBO_STAGE
+#undef SBO_DMA16
 }
 
 // ------------------------------------------------------ a6+a7+a10 acquire
@@ -562,7 +672,7 @@ hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int6
 
 hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox, int64_t npad,
                           const float *qx, const float *qy, int64_t m, int64_t ldp, float ell, float m0, int skip_log2,
-                          float *part, float *mean, unsigned long long *tiles_done, int variant) {
+                          float *part, float *mean, unsigned long long *tiles_done, int variant, int row_chunk) {
     const int nI = (int)(npad / kBM);
     const int64_t nQ = (m + kBN - 1) / kBN;
     const double ce = -1.0 / (2.0 * (double)ell * (double)ell * 0.69314718055994530942);
@@ -571,13 +681,21 @@ hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, 
     // every K* entry < 2^-skip_log2 (0.1% margin over the kernel's rounding);
     // skip_log2 >= 150 means every such entry is exactly +0.0 in f32
     const float skip_d2 = skip_log2 > 0 ? (float)((double)skip_log2 / -ce * 1.001) : -1.0f;
-    const int64_t blocks = (int64_t)nI * nQ;
+    // Row blocks per workgroup (chunk).  Default 1: the grid is row-block
+    // major, so the workgroups running at any moment all read row block I's
+    // A tiles and share them in L2 -- 18 GB of HBM fetch per C4 sweep,
+    // against 577 GB when each workgroup walks every row block for its
+    // queries (same time: the sweep is MFMA-bound either way; measured with
+    // rocprofv3 FETCH_SIZE).
+    const int G = row_chunk > 0 ? std::min(row_chunk, nI) : 1;
+    const int nC = (nI + G - 1) / G;
+    if (G > kMaxChunk) return hipErrorInvalidValue;
+    const int64_t blocks = nQ * nC;
     if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-#define SBO_PREDICT_ARGS aug, kcoord, kbox, nI, (int)nQ, qx, qy, m, ldp, cexp, skip_d2, m0, part, mean, tiles_done
+#define SBO_PREDICT_ARGS aug, kcoord, kbox, nI, nC, G, qx, qy, m, ldp, cexp, skip_d2, m0, part, mean, tiles_done
     switch (variant) {
-        case 1: hipLaunchKernelGGL((predict_kernel<float, 2>), dim3((unsigned)blocks), dim3(256), 0, s, SBO_PREDICT_ARGS); break;
-        case 2: hipLaunchKernelGGL((predict_kernel<float, 3>), dim3((unsigned)blocks), dim3(256), 0, s, SBO_PREDICT_ARGS); break;
-        default: hipLaunchKernelGGL((predict_kernel<double, 2>), dim3((unsigned)blocks), dim3(256), 0, s, SBO_PREDICT_ARGS); break;
+        case 1: hipLaunchKernelGGL((predict_kernel<double>), dim3((unsigned)blocks), dim3(kPredictThreads), 0, s, SBO_PREDICT_ARGS); break;
+        default: hipLaunchKernelGGL((predict_kernel<float>), dim3((unsigned)blocks), dim3(kPredictThreads), 0, s, SBO_PREDICT_ARGS); break;
     }
 #undef SBO_PREDICT_ARGS
     return hipGetLastError();

@@ -302,7 +302,7 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
                                     (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, skip_log2,
                                     ctx->part.as<float>(), ctx->mean.as<float>(),
                                     ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr,
-                                    ctx->kernel_variant));
+                                    ctx->kernel_variant, ctx->row_chunk));
     }
     const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
     SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<float>(), ctx->mean.as<float>(), (int)nI, ldp, m, sf2,
@@ -697,8 +697,12 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
         case SBO_OPT_QUERY_ORDER:
             ctx->query_order = value != 0;
             return SBO_OK;
+        case SBO_OPT_ROW_CHUNK:
+            SBO_CHECK(value >= 0 && value <= 128, SBO_E_INVAL, "SBO_OPT_ROW_CHUNK must be in [0, 128]");
+            ctx->row_chunk = (int)value;
+            return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
-            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be 0, 1 or 2");
+            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be 0 or 1");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
         case SBO_OPT_TILE_SKIP:

@@ -18,8 +18,8 @@ namespace sbo {
 // ---------------------------------------------------------------- geometry
 // Predictive operand tiling (see DESIGN.md "predictive sweep").
 //   BM rows of A = sf2 * L^-1 per workgroup, BN queries per workgroup
-//   (4 waves x 32), BK training points per LDS stage.
-constexpr int kBM = 128;
+//   (8 waves x 16), BK training points per LDS stage.
+constexpr int kBM = 256;
 constexpr int kBN = 128;
 constexpr int kBK = 64;
 constexpr int kTileFloats = kBM * kBK;           // one packed [BK][BM] tile
@@ -31,10 +31,14 @@ __host__ __device__ inline int64_t round_up(int64_t v, int64_t m) { return (v + 
 // First packed tile of row block I: sum_{I'<I} (I'+1)*(BM/BK).
 __host__ __device__ inline int64_t tile_start(int64_t I) { return kTilesPerRowBlockStep * I * (I + 1) / 2; }
 inline int64_t total_tiles(int64_t nI) { return tile_start(nI); }
-// Element offset inside a packed [BK][BM] tile of A[row][k] (row < BM, k < BK):
-// the four 32-row MFMA blocks of one row are adjacent, so one ds_read_b128 per
-// lane fetches the A operands of all four MFMAs of a k step.
-__host__ __device__ constexpr int tile_offset(int k, int row) { return (k * 32 + (row & 31)) * 4 + (row >> 5); }
+// Element offset inside a packed [BK][BM] tile of A[row][k] (row < BM, k < BK).
+// The MFMA is 16x16x4: lane (k&3, row&15) of a k step needs A of the sixteen
+// 16-row blocks of its row; blocks 4jj..4jj+3 sit side by side, so four
+// conflict-free ds_read_b128 per lane fetch the A operands of all sixteen
+// MFMAs of a step.
+__host__ __device__ constexpr int tile_offset(int k, int row) {
+    return (((row >> 6) * kBK + k) * 16 + (row & 15)) * 4 + ((row >> 4) & 3);
+}
 
 // ----------------------------------------------------------- device buffer
 class DevBuf {
@@ -97,6 +101,7 @@ struct sbo_ctx {
     float bbox[4] = {0.f, 0.f, 0.f, 0.f};  // training bounding box (x0, x1, y0, y1)
     bool query_order = true;     // SBO_OPT_QUERY_ORDER: sweep queries in Morton order
     int kernel_variant = 0;      // SBO_OPT_KERNEL_VARIANT: predictive kernel build (A/B)
+    int row_chunk = 0;           // SBO_OPT_ROW_CHUNK: row blocks per predictive workgroup (0: auto)
     sbo::DevBuf qwork;           // query ordering workspace
     sbo::DevBuf kbox;            // per k-tile bounding boxes (float4)
     sbo::DevBuf alpha;           // K^-1 (y - m0), length cap
@@ -151,7 +156,7 @@ hipError_t launch_widen_lower(hipStream_t s, const float *src, int64_t ld_src, i
 hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox,
                           int64_t npad, const float *qx, const float *qy, int64_t m, int64_t ldp,
                           float ell, float m0, int skip_log2, float *part, float *mean,
-                          unsigned long long *tiles_done, int variant);
+                          unsigned long long *tiles_done, int variant, int row_chunk);
 // row_l1[i] = sum_j |A_ij| over the packed operand (f64), i < npad.
 hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, double *row_l1);
 // Per k-tile bounding boxes of the (internally ordered) training points.

@@ -307,6 +307,33 @@ def test_tile_skip_exact_and_bounded(dev, mapper):
     assert res[0][2] == res[64][2]
 
 
+def test_row_chunk_and_outer_variant(mapper):
+    """Workgroup decomposition does not change the arithmetic: every row
+    block's accumulation order is the same whether a workgroup walks 1, 3 or
+    all row blocks (bitwise equal, empty prefixes and a ragged last chunk
+    included).  The f64 cross-tile accumulator (variant 1) agrees with the
+    f32 default to the contract tolerance."""
+    wl = synthetic(5000, 90, 70, seed=23)   # npad 5120 = 20 row blocks
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    res = {}
+    for chunk in (0, 1, 3, 20):
+        gm.set_option(N.SBO_OPT_ROW_CHUNK, chunk)
+        res[chunk] = gm.predict(wl.qx, wl.qy)
+    gm.set_option(N.SBO_OPT_ROW_CHUNK, 0)
+    for chunk in (1, 3, 20):
+        assert np.array_equal(res[chunk][0], res[0][0]) and np.array_equal(res[chunk][1], res[0][1])
+    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 1)
+    mu64, sd64 = gm.predict(wl.qx, wl.qy)
+    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 0)
+    assert nrel(mu64, res[0][0].astype(np.float64)) < 1e-6   # the mean is f64-accumulated in both
+    assert nrel(sd64.astype(np.float64) ** 2, res[0][1].astype(np.float64) ** 2) < 1e-5
+    with pytest.raises(N.SboError):
+        gm.set_option(N.SBO_OPT_ROW_CHUNK, 129)
+    with pytest.raises(N.SboError):
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 2)
+
+
 def test_spatial_order_does_not_change_the_posterior(mapper):
     wl = synthetic(3000, 64, 48, seed=22)
     out = {}

@@ -14,6 +14,7 @@ def main():
     p.add_argument("--n", type=int)
     p.add_argument("--grid", type=int)
     p.add_argument("--ticks", type=int, default=3)
+    p.add_argument("--opt", nargs="*", default=[], help="NAME=VALUE library options (e.g. SBO_OPT_TILE_SKIP=0)")
     a = p.parse_args()
     import torch
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
@@ -26,6 +27,10 @@ def main():
     dev = torch.device("cuda:0")
     t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
     gm = TerrainMapper(0, wl.hyper)
+    from safe_bayesian_optimization_amd import _native as N
+    for kv in a.opt:
+        k, v = kv.split("=")
+        gm.set_option(getattr(N, k), int(v))
     gm.fit(t(wl.x), t(wl.y), t(wl.obs))
     qx, qy = t(wl.qx), t(wl.qy)
     m = qx.numel()
