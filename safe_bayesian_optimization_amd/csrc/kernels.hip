@@ -93,9 +93,9 @@ __global__ void copy_lower_kernel(const float *__restrict__ src, int64_t lds, in
 // grid.x = k-tiles of the longest row block, grid.y = row block I.
 template <class T>
 __global__ __launch_bounds__(256) void pack_operand_kernel(const T *__restrict__ Linv,
-                                                           int64_t ld, int64_t n, T sf2,
+                                                           int64_t ld, int64_t n, T sf2, int64_t I0,
                                                            float *__restrict__ aug) {
-    const int64_t I = blockIdx.y;
+    const int64_t I = I0 + blockIdx.y;
     const int64_t kb = blockIdx.x;
     if (kb >= (I + 1) * kTilesPerRowBlockStep) return;
     float *tile = aug + (tile_start(I) + kb) * kTileFloats;
@@ -110,11 +110,12 @@ __global__ __launch_bounds__(256) void pack_operand_kernel(const T *__restrict__
     }
 }
 
-__global__ void widen_lower_kernel(const float *__restrict__ src, int64_t lds, int64_t n,
-                                   double *__restrict__ dst) {
+// dst[i + j*ldd] = src[i + j*lds] (f32 -> f64), i < m, j < n; lower: zero above the diagonal.
+__global__ void widen_kernel(const float *__restrict__ src, int64_t lds, int64_t m, int lower,
+                             double *__restrict__ dst, int64_t ldd) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t j = blockIdx.y;
-    if (i < n) dst[i + j * n] = i >= j ? (double)src[i + j * lds] : 0.0;
+    if (i < m) dst[i + j * ldd] = (!lower || i >= j) ? (double)src[i + j * lds] : 0.0;
 }
 
 __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__restrict__ y,
@@ -131,14 +132,33 @@ __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__r
 }
 
 // Row 1-norms of the packed operand: block I, thread r sums |A[I*BM + r][:]|.
-__global__ __launch_bounds__(kBM) void row_l1_kernel(const float *__restrict__ aug, double *__restrict__ row_l1) {
-    const int64_t I = blockIdx.x;
+// Row 1-norms of the packed operand, |A[I*BM + r][:]|_1: block (c, I)
+// sums row r over k-tiles [c*kRowL1Tiles, (c+1)*kRowL1Tiles) of row block I
+// and adds into row_l1 (zeroed by the launcher).
+constexpr int kRowL1Tiles = 4;
+__global__ __launch_bounds__(kBM) void row_l1_kernel(const float *__restrict__ aug, int64_t I0,
+                                                     double *__restrict__ row_l1) {
+    const int64_t I = I0 + blockIdx.y;
+    const int64_t kb0 = (int64_t)blockIdx.x * kRowL1Tiles;
+    const int64_t nkb = (I + 1) * kTilesPerRowBlockStep;
+    if (kb0 >= nkb) return;
     const int r = threadIdx.x;
-    const float *t = aug + tile_start(I) * kTileFloats;
-    const int64_t nk = (I + 1) * kBM;  // k-tiles 0..2(I+1)-1, each [BK][BM]
+    const float *t = aug + (tile_start(I) + kb0) * kTileFloats;
     double s = 0.0;
-    for (int64_t k = 0; k < nk; ++k) s += fabs((double)t[(k / kBK) * kTileFloats + tile_offset((int)(k % kBK), r)]);
-    row_l1[I * kBM + r] = s;
+    for (int64_t kb = 0; kb < kRowL1Tiles && kb0 + kb < nkb; ++kb)
+        for (int k = 0; k < kBK; ++k) s += fabs((double)t[kb * kTileFloats + tile_offset(k, r)]);
+    atomicAdd(row_l1 + I * kBM + r, s);
+}
+
+// d[i] = (double)in[i] - v
+__global__ void widen_sub_kernel(const float *__restrict__ in, double v, int64_t n, double *__restrict__ d) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) d[i] = (double)in[i] - v;
+}
+
+__global__ void narrow_kernel(const double *__restrict__ d, int64_t n, float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (float)d[i];
 }
 
 // Bounding box of each k-tile's valid training points: (xmin, xmax, ymin, ymax);
@@ -631,36 +651,58 @@ hipError_t launch_copy_lower(hipStream_t s, const float *src, int64_t ld_src, in
 }
 
 template <class T>
-hipError_t launch_pack_operand_t(hipStream_t s, const T *Linv, int64_t ld, int64_t n, int64_t npad, double sf2,
-                                 const float *x, const float *y, const float *alpha, float *aug, float *kcoord) {
+hipError_t launch_pack_operand_t(hipStream_t s, const T *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
+                                 double sf2, const float *x, const float *y, const float *alpha, float *aug,
+                                 float *kcoord) {
     const int64_t nI = npad / kBM;
-    hipLaunchKernelGGL(pack_operand_kernel<T>, dim3((unsigned)(nI * kTilesPerRowBlockStep), (unsigned)nI),
-                       dim3(256), 0, s, Linv, ld, n, (T)sf2, aug);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (I0 < nI) {
+        hipLaunchKernelGGL(pack_operand_kernel<T>, dim3((unsigned)(nI * kTilesPerRowBlockStep), (unsigned)(nI - I0)),
+                           dim3(256), 0, s, Linv, ld, n, (T)sf2, I0, aug);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(pack_kcoord_kernel, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, s, x, y,
                        alpha, n, npad, (float)sf2, kcoord);
     return hipGetLastError();
 }
 
-hipError_t launch_pack_operand(hipStream_t s, const float *Linv, int64_t ld, int64_t n, int64_t npad, double sf2,
-                               const float *x, const float *y, const float *alpha, float *aug, float *kcoord) {
-    return launch_pack_operand_t<float>(s, Linv, ld, n, npad, sf2, x, y, alpha, aug, kcoord);
+hipError_t launch_pack_operand(hipStream_t s, const float *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
+                               double sf2, const float *x, const float *y, const float *alpha, float *aug,
+                               float *kcoord) {
+    return launch_pack_operand_t<float>(s, Linv, ld, n, npad, I0, sf2, x, y, alpha, aug, kcoord);
 }
 
-hipError_t launch_pack_operand(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, double sf2,
-                               const float *x, const float *y, const float *alpha, float *aug, float *kcoord) {
-    return launch_pack_operand_t<double>(s, Linv, ld, n, npad, sf2, x, y, alpha, aug, kcoord);
+hipError_t launch_pack_operand(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
+                               double sf2, const float *x, const float *y, const float *alpha, float *aug,
+                               float *kcoord) {
+    return launch_pack_operand_t<double>(s, Linv, ld, n, npad, I0, sf2, x, y, alpha, aug, kcoord);
 }
 
-hipError_t launch_widen_lower(hipStream_t s, const float *src, int64_t ld_src, int64_t n, double *dst) {
-    hipLaunchKernelGGL(widen_lower_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)n), dim3(256), 0, s, src,
-                       ld_src, n, dst);
+hipError_t launch_widen(hipStream_t s, const float *src, int64_t ld_src, int64_t m, int64_t n, bool lower,
+                        double *dst, int64_t ld_dst) {
+    if (m <= 0 || n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(widen_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)n), dim3(256), 0, s, src, ld_src,
+                       m, lower ? 1 : 0, dst, ld_dst);
     return hipGetLastError();
 }
 
-hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, double *row_l1) {
-    hipLaunchKernelGGL(row_l1_kernel, dim3((unsigned)(npad / kBM)), dim3(kBM), 0, s, aug, row_l1);
+hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t I0, double *row_l1) {
+    const int64_t nI = npad / kBM;
+    if (I0 >= nI) return hipSuccess;
+    hipError_t e = hipMemsetAsync(row_l1 + I0 * kBM, 0, sizeof(double) * (size_t)((nI - I0) * kBM), s);
+    if (e != hipSuccess) return e;
+    const int64_t chunks = (nI * kTilesPerRowBlockStep + kRowL1Tiles - 1) / kRowL1Tiles;
+    hipLaunchKernelGGL(row_l1_kernel, dim3((unsigned)chunks, (unsigned)(nI - I0)), dim3(kBM), 0, s, aug, I0, row_l1);
+    return hipGetLastError();
+}
+
+hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d) {
+    hipLaunchKernelGGL(widen_sub_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, v, n, d);
+    return hipGetLastError();
+}
+
+hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out) {
+    hipLaunchKernelGGL(narrow_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, n, out);
     return hipGetLastError();
 }
 

@@ -182,43 +182,103 @@ void recycle_events(sbo_ctx *ctx) {
     }
 }
 
+// Grow a device buffer to `bytes`, keeping its first `keep` bytes.
+hipError_t grow_keep(sbo_ctx *ctx, DevBuf &buf, size_t bytes, size_t keep) {
+    if (bytes <= buf.capacity()) return hipSuccess;
+    DevBuf nb;
+    hipError_t e = nb.reserve(bytes);
+    if (e != hipSuccess) return e;
+    if (keep) {
+        e = hipMemcpyAsync(nb.as<void>(), buf.as<void>(), keep, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e != hipSuccess) return e;
+        e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) return e;
+    }
+    buf.swap(nb);
+    return hipSuccess;
+}
+
 // Rebuild alpha, L^-1 and the packed predictive operand from the current L.
-sbo_status refresh_operand(sbo_ctx *ctx) {
+// n_old > 0 (an append of rows n_old..n-1 to an unchanged leading factor):
+// with the f64 inverse of the leading block kept from the last refresh, only
+// the new rows of L^-1 are computed,
+//     [L11  0 ]^-1   [ L11^-1                  0     ]
+//     [L21 L22]    = [ -L22^-1 L21 L11^-1   L22^-1 ]
+// (one b x b dtrtri and two dtrmm, O(b n^2) instead of O(n^3)), and only the
+// row blocks that hold new rows are repacked.  alpha, the per-k coordinates
+// and the tile boxes are rebuilt in full (O(n^2) and O(n)).
+sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     const int64_t n = ctx->n, ld = ctx->cap;
     const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
     float *L = ctx->L.as<float>();
     float *alpha = ctx->alpha.as<float>();
     rocblas_int *info = ctx->info.as<rocblas_int>();
 
-    // alpha = K^-1 (y - m0)
-    SBO_HIP(sbo::launch_sub_scalar(ctx->stream, ctx->obs.as<float>(), (float)ctx->hyper.prior_mean, n, alpha));
-    SBO_BLAS(rocsolver_spotrs(ctx->blas, rocblas_fill_lower, (rocblas_int)n, 1, L, (rocblas_int)ld, alpha,
-                              (rocblas_int)n));
-
-    // L^-1 (lower, non-unit) in the workspace.  Default: widen L to f64 and
-    // invert with dtrtri (f64 MFMA), then round sf2 * L^-1 to f32 once while
-    // packing -- the f32 strtri path adds its own inversion error on top of the
-    // f32 representation error (SBO_OPT_INVERSE_BITS = 32 selects it).
+    // L^-1 (lower, non-unit).  Default: widen L to f64 and invert with dtrtri
+    // (f64 MFMA), then round sf2 * L^-1 to f32 once while packing -- the f32
+    // strtri path adds its own inversion error on top of the f32
+    // representation error (SBO_OPT_INVERSE_BITS = 32 selects it).
     const int64_t npad = sbo::round_up(n, sbo::kBM);
     const int64_t nI = npad / sbo::kBM;
-    SBO_HIP(ctx->aug.reserve(sizeof(float) * (size_t)sbo::total_tiles(nI) * sbo::kTileFloats));
+    const bool incr = n_old > 0 && ctx->inverse_bits == 64 && ctx->linv_n == n_old && ctx->npad > 0;
+    const int64_t I0 = incr ? n_old / sbo::kBM : 0;  // first row block holding new rows
+    const size_t old_tiles = incr ? (size_t)sbo::total_tiles(I0) : 0;
+    SBO_HIP(grow_keep(ctx, ctx->aug, sizeof(float) * (size_t)sbo::total_tiles(nI) * sbo::kTileFloats,
+                      sizeof(float) * old_tiles * sbo::kTileFloats));
     SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
     rocblas_int hinfo = 0;
     if (ctx->inverse_bits == 64) {
-        SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)n * (size_t)n));
         double *Li = ctx->Linv.as<double>();
-        SBO_HIP(sbo::launch_widen_lower(ctx->stream, L, ld, n, Li));
-        SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
-                                  (rocblas_int)n, info));
-        SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, n, n, npad, sf2, ctx->x.as<float>(), ctx->y.as<float>(),
-                                         alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
+        if (incr) {
+            const int64_t b = n - n_old;
+            const double one = 1.0, minus_one = -1.0;
+            double *T = Li + n_old;                      // rows n_old.., columns 0..n_old-1
+            double *L22i = Li + n_old + n_old * ld;      // rows n_old.., columns n_old..
+            SBO_HIP(sbo::launch_widen(ctx->stream, L + n_old, ld, b, n_old, false, T, ld));
+            SBO_HIP(sbo::launch_widen(ctx->stream, L + n_old + n_old * ld, ld, b, b, true, L22i, ld));
+            SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)b, L22i,
+                                      (rocblas_int)ld, info));
+            SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
+            // T = L21 L11^-1, then T = -L22^-1 T
+            SBO_BLAS(rocblas_dtrmm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_none,
+                                   rocblas_diagonal_non_unit, (rocblas_int)b, (rocblas_int)n_old, &one, Li,
+                                   (rocblas_int)ld, T, (rocblas_int)ld, T, (rocblas_int)ld));
+            SBO_BLAS(rocblas_dtrmm(ctx->blas, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none,
+                                   rocblas_diagonal_non_unit, (rocblas_int)b, (rocblas_int)n_old, &minus_one, L22i,
+                                   (rocblas_int)ld, T, (rocblas_int)ld, T, (rocblas_int)ld));
+        } else {
+            SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)ld * (size_t)ld));
+            Li = ctx->Linv.as<double>();
+            SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
+            SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
+                                      (rocblas_int)ld, info));
+        }
+        ctx->linv_n = n;
+        // alpha = K^-1 (y - m0) = L^-T L^-1 (y - m0), in f64 from the f64
+        // inverse: two triangular matrix-vector products (bandwidth-bound and
+        // parallel, unlike the two sequential triangular solves of spotrs)
+        SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max(npad, n)));
+        double *d = ctx->scratch.as<double>();
+        SBO_HIP(sbo::launch_widen_sub(ctx->stream, ctx->obs.as<float>(), ctx->hyper.prior_mean, n, d));
+        SBO_BLAS(rocblas_dtrmv(ctx->blas, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit,
+                               (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
+        SBO_BLAS(rocblas_dtrmv(ctx->blas, rocblas_fill_lower, rocblas_operation_transpose, rocblas_diagonal_non_unit,
+                               (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
+        SBO_HIP(sbo::launch_narrow(ctx->stream, d, n, alpha));
+        SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, ld, n, npad, I0, sf2, ctx->x.as<float>(),
+                                         ctx->y.as<float>(), alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
     } else {
+        ctx->linv_n = 0;
+        // alpha = K^-1 (y - m0) by the f32 triangular solves
+        SBO_HIP(sbo::launch_sub_scalar(ctx->stream, ctx->obs.as<float>(), (float)ctx->hyper.prior_mean, n, alpha));
+        SBO_BLAS(rocsolver_spotrs(ctx->blas, rocblas_fill_lower, (rocblas_int)n, 1, L, (rocblas_int)ld, alpha,
+                                  (rocblas_int)n));
         SBO_HIP(ctx->Linv.reserve(sizeof(float) * (size_t)ld * (size_t)n));
         float *Li = ctx->Linv.as<float>();
         SBO_HIP(hipMemcpyAsync(Li, L, sizeof(float) * (size_t)ld * (size_t)n, hipMemcpyDeviceToDevice, ctx->stream));
         SBO_BLAS(rocsolver_strtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
                                   (rocblas_int)ld, info));
-        SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, ld, n, npad, sf2, ctx->x.as<float>(), ctx->y.as<float>(),
+        SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, ld, n, npad, 0, sf2, ctx->x.as<float>(), ctx->y.as<float>(),
                                          alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
     }
     // Error budget of the K* tile cutoff (SBO_OPT_TILE_SKIP = -1, auto): a
@@ -226,16 +286,21 @@ sbo_status refresh_operand(sbo_ctx *ctx) {
     // 2^-L max_i |A_i|_1 and each mean by at most 2^-L |sf2 alpha|_1.  With
     // |V|_2 <= sf2^(1/2), |d sigma^2| <= 2 sf2^(1/2) sqrt(N) max|dV_i|.  L is the
     // smallest exponent that keeps both below 2^-27 (~7.5e-9) of sf2 / sf2^(1/2).
+    // Rows of earlier row blocks are unchanged by an append: only the repacked
+    // row blocks are re-measured.
     {
         SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)npad));
-        SBO_HIP(sbo::launch_row_l1(ctx->stream, ctx->aug.as<float>(), npad, ctx->scratch.as<double>()));
-        std::vector<double> rl1((size_t)npad);
+        SBO_HIP(sbo::launch_row_l1(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->scratch.as<double>()));
+        const int64_t r0 = I0 * sbo::kBM;
+        std::vector<double> rl1((size_t)(npad - r0));
         std::vector<float> ha((size_t)n);
-        SBO_HIP(hipMemcpyAsync(rl1.data(), ctx->scratch.as<double>(), sizeof(double) * npad, hipMemcpyDeviceToHost,
-                               ctx->stream));
+        SBO_HIP(hipMemcpyAsync(rl1.data(), ctx->scratch.as<double>() + r0, sizeof(double) * (npad - r0),
+                               hipMemcpyDeviceToHost, ctx->stream));
         SBO_HIP(hipMemcpyAsync(ha.data(), alpha, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
         SBO_HIP(hipStreamSynchronize(ctx->stream));
-        ctx->max_row_l1 = *std::max_element(rl1.begin(), rl1.end());
+        double mx = *std::max_element(rl1.begin(), rl1.end());
+        if (incr) mx = std::max(mx, ctx->max_row_l1);
+        ctx->max_row_l1 = mx;
         double al1 = 0.0;
         for (float v : ha) al1 += std::fabs((double)v);
         ctx->alpha_l1 = al1 * sf2;
@@ -249,6 +314,7 @@ sbo_status refresh_operand(sbo_ctx *ctx) {
     SBO_HIP(sbo::launch_tile_boxes(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, npad, ctx->kbox.as<float4>()));
     SBO_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
+    if (hinfo != 0) ctx->linv_n = 0;
     SBO_CHECK(hinfo == 0, SBO_E_NOT_SPD, "trtri: singular factor (info=" + std::to_string(hinfo) + ")");
     ctx->npad = npad;
     ctx->fitted = true;
@@ -386,6 +452,7 @@ SBO_API sbo_status sbo_fit(sbo_ctx *ctx, const float *x, const float *y, const f
     ctx->hyper = hyper;
     ctx->n = n;
     ctx->cap = n;
+    ctx->linv_n = 0;
     SBO_HIP(ctx->x.reserve(sizeof(float) * n));
     SBO_HIP(ctx->y.reserve(sizeof(float) * n));
     SBO_HIP(ctx->obs.reserve(sizeof(float) * n));
@@ -429,6 +496,17 @@ SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, cons
         SBO_HIP(hipMemcpy2DAsync(nL.as<float>(), sizeof(float) * ncap, ctx->L.as<float>(), sizeof(float) * ctx->cap,
                                  sizeof(float) * n0, n0, hipMemcpyDeviceToDevice, ctx->stream));
         SBO_HIP(hipStreamSynchronize(ctx->stream));
+        if (ctx->linv_n == n0 && ctx->inverse_bits == 64) {  // keep the f64 inverse for the incremental refresh
+            DevBuf nLi;
+            SBO_HIP(nLi.reserve(sizeof(double) * (size_t)ncap * (size_t)ncap));
+            SBO_HIP(hipMemcpy2DAsync(nLi.as<double>(), sizeof(double) * ncap, ctx->Linv.as<double>(),
+                                     sizeof(double) * ctx->cap, sizeof(double) * n0, n0, hipMemcpyDeviceToDevice,
+                                     ctx->stream));
+            SBO_HIP(hipStreamSynchronize(ctx->stream));
+            ctx->Linv.swap(nLi);
+        } else {
+            ctx->linv_n = 0;
+        }
         ctx->x.swap(nx);
         ctx->y.swap(ny);
         ctx->obs.swap(no);
@@ -468,7 +546,7 @@ SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, cons
         return SBO_E_NOT_SPD;
     }
     ctx->n = n1;
-    if (sbo_status st = refresh_operand(ctx)) return st;
+    if (sbo_status st = refresh_operand(ctx, n0)) return st;
     return finish(ctx, flags);
 }
 

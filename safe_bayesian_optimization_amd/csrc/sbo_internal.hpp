@@ -90,7 +90,8 @@ struct sbo_ctx {
 
     sbo::DevBuf x, y, obs;       // training data, f32, capacity cap
     sbo::DevBuf L;               // lower Cholesky factor, column-major, lda = cap
-    sbo::DevBuf Linv;            // workspace: L^-1 (strtri f32, lda = cap, or dtrtri f64, lda = n)
+    sbo::DevBuf Linv;            // L^-1 (strtri f32 workspace, or dtrtri f64 kept for appends), lda = cap
+    int64_t linv_n = 0;          // rows of the f64 L^-1 held in Linv (0: none; appends extend it)
     int inverse_bits = 64;       // SBO_OPT_INVERSE_BITS: precision of the L^-1 computation
     bool spatial_order = true;   // SBO_OPT_SPATIAL_ORDER: Morton-order the training points
     int skip_log2 = -1;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-L (-1: auto)
@@ -139,15 +140,17 @@ hipError_t launch_sub_scalar(hipStream_t s, const float *in, float v, int64_t n,
 hipError_t launch_copy_lower(hipStream_t s, const float *src, int64_t ld_src, int64_t n,
                              float *dst, int64_t ld_dst);
 // Pack A = sf2 * L^-1 (from an f32 or f64 inverse, lower, column-major) into
-// [BK][BM] tiles, plus per-k coordinates and sf2 * alpha.
-hipError_t launch_pack_operand(hipStream_t s, const float *Linv, int64_t ld, int64_t n, int64_t npad,
+// [BK][BM] tiles for row blocks I >= I0 (earlier row blocks are left as they
+// are), plus per-k coordinates and sf2 * alpha for all k.
+hipError_t launch_pack_operand(hipStream_t s, const float *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
                                double sf2, const float *x, const float *y, const float *alpha, float *aug,
                                float *kcoord);
-hipError_t launch_pack_operand(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad,
+hipError_t launch_pack_operand(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
                                double sf2, const float *x, const float *y, const float *alpha, float *aug,
                                float *kcoord);
-// dst (n x n, ld n, f64) = lower(src), upper zeroed.
-hipError_t launch_widen_lower(hipStream_t s, const float *src, int64_t ld_src, int64_t n, double *dst);
+// dst (m x n, f64, ld_dst) = src (f32, ld_src); lower: zero above the diagonal.
+hipError_t launch_widen(hipStream_t s, const float *src, int64_t ld_src, int64_t m, int64_t n, bool lower,
+                        double *dst, int64_t ld_dst);
 // Predictive sweep: part[I][q] = sum over rows of block I of (sf2 L^-1 k_q)^2,
 // mean[q] = m0 + sf2 alpha^T k_q.
 // skip_log2 > 0: drop k-tiles whose every K* entry is < 2^-skip_log2 (exactly
@@ -157,8 +160,11 @@ hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, 
                           int64_t npad, const float *qx, const float *qy, int64_t m, int64_t ldp,
                           float ell, float m0, int skip_log2, float *part, float *mean,
                           unsigned long long *tiles_done, int variant, int row_chunk);
-// row_l1[i] = sum_j |A_ij| over the packed operand (f64), i < npad.
-hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, double *row_l1);
+// d = (double)in - v;  out = (float)d
+hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);
+hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out);
+// row_l1[i] = sum_j |A_ij| over the packed operand (f64), rows of row blocks >= I0.
+hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t I0, double *row_l1);
 // Per k-tile bounding boxes of the (internally ordered) training points.
 hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int64_t n, int64_t npad,
                              float4 *kbox);

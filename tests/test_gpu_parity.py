@@ -367,6 +367,30 @@ def test_append_matches_refit(mapper):
     assert nrel(mu_a, mu_r) < 1e-4 and nrel(sd_a.astype(np.float64) ** 2, sd_r.astype(np.float64) ** 2) < 1e-4
 
 
+def test_append_incremental_inverse(mapper):
+    """Appends update L^-1 incrementally (new rows only, f64): the packed
+    operand must equal sf2 * inv(L) of the appended factor to f32 rounding --
+    single-point appends, an append that crosses a 256-row block boundary, and
+    one that grows the capacity."""
+    wl = synthetic(900, 30, 30, seed=31)
+    gm = TerrainMapper(0, ctx=mapper.ctx)
+    gm.fit(wl.x[:250], wl.y[:250], wl.obs[:250])
+    for a, b in ((250, 251), (251, 252), (252, 300), (300, 512), (512, 513), (513, 900)):
+        gm.append(wl.x[a:b], wl.y[a:b], wl.obs[a:b])
+    n = gm.n
+    assert n == 900
+    L, _ = gm.factor()
+    A = np.zeros((n, n), np.float32)
+    gm.ctx.check(N.lib().sbo_get_inverse(gm.ctx.handle, A.ctypes.data))
+    ref = wl.hyper.sf2 * np.linalg.inv(L.astype(np.float64))
+    err = np.abs(np.tril(A) - ref).max() / np.abs(ref).max()
+    print(f"incremental inverse: max rel err {err:.2e}")
+    assert err < 1e-6
+    mu, sd = gm.predict(wl.qx, wl.qy)
+    omu, ovar = oracle_given_factor(gm, wl)
+    assert nrel(mu, omu) < REL_TOL and nrel(sd.astype(np.float64) ** 2, ovar) < REL_TOL
+
+
 # ------------------------------------------------------ full-size properties
 def test_c3_properties(dev):
     """N=8192 with a 1024x1024 grid (C3): properties that hold at any size --
