@@ -149,6 +149,23 @@ SBO_API int64_t sbo_next_subgoal(const double *Dx, const double *Dy, const doubl
                                  const double *hi, const uint8_t *safe, int64_t m,
                                  int width_cells, int height_cells, double goal_x, double goal_y);
 
+/* The same two steps on device-resident grid data: with
+ * SBO_DEVICE_PTRS, Dx/Dy/lo/hi/safe are device arrays (e.g. the tick's own
+ * outputs); the O(M) raster -- bounds, pixel arithmetic, the last-writer
+ * maps -- runs on the GPU and only the width x height image crosses to the
+ * host for the border follow.  Results are identical to the host functions
+ * above for finite coordinates (non-finite ones: the device bounds ignore
+ * them).  Without the flag they call the host functions.  `out` is host
+ * memory; count receives the frontier size even when out_cap is too small
+ * (SBO_E_INVAL).  *index = -1 when there is no frontier. */
+SBO_API sbo_status sbo_frontier(sbo_ctx *ctx, const double *Dx, const double *Dy, const uint8_t *safe,
+                                int64_t m, int width_cells, int height_cells, int32_t *out,
+                                int64_t out_cap, int64_t *count, uint32_t flags);
+SBO_API sbo_status sbo_subgoal(sbo_ctx *ctx, const double *Dx, const double *Dy, const double *lo,
+                               const double *hi, const uint8_t *safe, int64_t m, int width_cells,
+                               int height_cells, double goal_x, double goal_y, int64_t *index,
+                               uint32_t flags);
+
 /* Raw border follower used by the frontier: img is height x width u8
  * row-major; points (x,y) pairs; start[c]..start[c+1] bound contour c.
  * Returns the number of contours, or -1 if a capacity was exceeded. */

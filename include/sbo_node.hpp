@@ -50,6 +50,26 @@ public:
     sbo_ctx *get() const { return ctx_; }
     std::string last_error() const { return sbo_last_error(ctx_); }
 
+    // FindSafetyContourIndices / GetNextSubgoal on device-resident grid data
+    // (e.g. the tick's own lo/hi/S outputs): GPU raster, host border follow.
+    std::vector<int32_t> frontier_device(const double *Dx, const double *Dy, const uint8_t *safe, int64_t m,
+                                         int width, int height) const {
+        int64_t count = 0;
+        std::vector<int32_t> out((size_t)8 * (size_t)std::max(width, 1) * (size_t)std::max(height, 1) + 16);
+        if (sbo_frontier(ctx_, Dx, Dy, safe, m, width, height, out.data(), (int64_t)out.size(), &count,
+                         SBO_DEVICE_PTRS) != SBO_OK)
+            throw std::runtime_error("sbo_frontier: " + last_error());
+        out.resize((size_t)count);
+        return out;
+    }
+    int64_t subgoal_device(const double *Dx, const double *Dy, const double *lo, const double *hi,
+                           const uint8_t *safe, int64_t m, int width, int height, double gx, double gy) const {
+        int64_t idx = -1;
+        if (sbo_subgoal(ctx_, Dx, Dy, lo, hi, safe, m, width, height, gx, gy, &idx, SBO_DEVICE_PTRS) != SBO_OK)
+            throw std::runtime_error("sbo_subgoal: " + last_error());
+        return idx;
+    }
+
 private:
     sbo_ctx *ctx_ = nullptr;
 };

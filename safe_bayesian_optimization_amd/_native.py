@@ -29,7 +29,7 @@ EXPORTS = (
     "sbo_fit", "sbo_append", "sbo_num_train", "sbo_predict", "sbo_compute_sets", "sbo_argmax", "sbo_tick",
     "sbo_key_combine", "sbo_find_safety_contour_indices", "sbo_next_subgoal", "sbo_find_contours_external",
     "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
-    "sbo_get_order", "sbo_profile_work", "sbo_get_skip",
+    "sbo_get_order", "sbo_profile_work", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
 )
 SBO_OPT_INVERSE_BITS = 1
 SBO_OPT_SPATIAL_ORDER = 2
@@ -111,6 +111,10 @@ def lib():
     L.sbo_find_safety_contour_indices.restype = st
     L.sbo_next_subgoal.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, dbl, dbl]
     L.sbo_next_subgoal.restype = i64
+    L.sbo_frontier.argtypes = [vp, vp, vp, vp, i64, i32, i32, vp, i64, ctypes.POINTER(i64), u32]
+    L.sbo_frontier.restype = st
+    L.sbo_subgoal.argtypes = [vp, vp, vp, vp, vp, vp, i64, i32, i32, dbl, dbl, ctypes.POINTER(i64), u32]
+    L.sbo_subgoal.restype = st
     L.sbo_find_contours_external.argtypes = [vp, i32, i32, vp, i64, vp, i64]
     L.sbo_find_contours_external.restype = i64
     L.sbo_rbf_fill.argtypes = [vp, vp, vp, i64, sbo_hyper, vp, u32]

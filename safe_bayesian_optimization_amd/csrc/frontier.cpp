@@ -24,7 +24,7 @@
 #include <utility>
 #include <vector>
 
-#include "../../include/sbo.h"
+#include "sbo_internal.hpp"
 
 namespace sbo {
 namespace {
@@ -142,6 +142,49 @@ void contours_external(const uint8_t *img, int w, int h, std::vector<Pt> &pts, s
     starts.push_back((int64_t)pts.size());
 }
 
+}  // namespace
+
+// Frontier pixels (y * width + x) in the node's order: contours in reverse
+// discovery order, every traversed pixel (duplicates kept).
+void trace_external_pixels(const uint8_t *img, int w, int h, std::vector<int32_t> &pix) {
+    std::vector<Pt> pts;
+    std::vector<int64_t> starts;
+    contours_external(img, w, h, pts, starts);
+    pix.clear();
+    pix.reserve(pts.size());
+    for (const Pt &p : pts) pix.push_back(p.y * w + p.x);
+}
+
+// GetNextSubgoal's selection (:508-550) over the frontier F with its
+// gathered coordinates and bounds: sort by distance to the goal (stable on
+// the frontier position), keep the nearest max(1, F/4), strict-> argmax of
+// hi - lo from -1.  Returns the position in F, or -1.
+int64_t select_subgoal(size_t nf, const double *fx, const double *fy, const double *flo, const double *fhi,
+                       double goal_x, double goal_y) {
+    if (nf == 0) return -1;  // "No frontier points found" (:503-506)
+    std::vector<double> width(nf);
+    std::vector<std::pair<double, size_t>> order(nf);
+    for (size_t i = 0; i < nf; ++i) {
+        width[i] = fhi[i] - flo[i];                     // Q(idx,1) - Q(idx,0) (:516)
+        const double dx = fx[i] - goal_x, dy = fy[i] - goal_y;
+        order[i] = {std::sqrt(dx * dx + dy * dy), i};  // rowwise().norm() (:522-523)
+    }
+    std::sort(order.begin(), order.end());              // distance, then frontier position (:526-530)
+    const size_t top = std::max<size_t>(1, nf / 4);     // (:533)
+    double best_w = -1.0;
+    int64_t best = -1;
+    for (size_t t = 0; t < top; ++t) {                  // strict > from -1.0 (:536-547)
+        const size_t fi = order[t].second;
+        if (width[fi] > best_w) {
+            best_w = width[fi];
+            best = (int64_t)fi;
+        }
+    }
+    return best;
+}
+
+namespace {
+
 // FindSafetyContourIndices (:418-497).
 void frontier_indices(const double *Dx, const double *Dy, const uint8_t *safe, int64_t m, int width, int height,
                       std::vector<int32_t> &out) {
@@ -219,28 +262,16 @@ SBO_API int64_t sbo_next_subgoal(const double *Dx, const double *Dy, const doubl
     if (m <= 0 || !Dx || !Dy || !lo || !hi || !safe) return -1;
     std::vector<int32_t> F;
     sbo::frontier_indices(Dx, Dy, safe, m, width_cells, height_cells, F);
-    if (F.empty()) return -1;  // "No frontier points found" (:503-506)
     const size_t nf = F.size();
-    std::vector<double> width(nf);
-    std::vector<std::pair<double, size_t>> order(nf);
+    std::vector<double> fx(nf), fy(nf), flo(nf), fhi(nf);
     for (size_t i = 0; i < nf; ++i) {
-        const int32_t idx = F[i];
-        width[i] = hi[idx] - lo[idx];                 // Q(idx,1) - Q(idx,0) (:516)
-        const double dx = Dx[idx] - goal_x, dy = Dy[idx] - goal_y;
-        order[i] = {std::sqrt(dx * dx + dy * dy), i};  // rowwise().norm() (:522-523)
+        fx[i] = Dx[F[i]];
+        fy[i] = Dy[F[i]];
+        flo[i] = lo[F[i]];
+        fhi[i] = hi[F[i]];
     }
-    std::sort(order.begin(), order.end());            // distance, then frontier position (:526-530)
-    const size_t top = std::max<size_t>(1, nf / 4);   // (:533)
-    double best_w = -1.0;
-    int64_t best = -1;
-    for (size_t t = 0; t < top; ++t) {                // strict > from -1.0 (:536-547)
-        const size_t fi = order[t].second;
-        if (width[fi] > best_w) {
-            best_w = width[fi];
-            best = (int64_t)fi;
-        }
-    }
-    return best >= 0 ? F[(size_t)best] : -1;
+    const int64_t b = sbo::select_subgoal(nf, fx.data(), fy.data(), flo.data(), fhi.data(), goal_x, goal_y);
+    return b >= 0 ? F[(size_t)b] : -1;
 }
 
 }  // extern "C"

@@ -832,3 +832,98 @@ SBO_API sbo_status sbo_get_inverse(sbo_ctx *ctx, float *Linv) {
 }
 
 }  // extern "C"
+
+// ----------------------------------------------------------- frontier 8(f)1
+namespace {
+
+// Device raster + host border following; F = frontier grid indices in the
+// node's order.  Returns SBO_OK with F filled (possibly empty).
+sbo_status device_frontier(sbo_ctx *ctx, const double *Dx, const double *Dy, const uint8_t *safe, int64_t m,
+                           int width, int height, const double *lo, const double *hi, std::vector<int32_t> &F,
+                           std::vector<double> &cols) {
+    F.clear();
+    cols.clear();
+    if (m <= 0 || width <= 0 || height <= 0) return SBO_OK;  // "D_ or S_ is empty" (:419-422)
+    SBO_CHECK(m <= INT32_MAX, SBO_E_INVAL, "frontier: m must fit int32 (grid indices)");
+    const int64_t npx = (int64_t)width * height;
+    SBO_HIP(ctx->fwork.reserve(sbo::frontier_work_bytes(m)));
+    SBO_HIP(ctx->fowner.reserve(sizeof(int32_t) * (size_t)npx));
+    SBO_HIP(ctx->fimg.reserve((size_t)npx));
+    SBO_HIP(sbo::launch_frontier_raster(ctx->stream, Dx, Dy, safe, m, width, height, ctx->fwork.as<void>(),
+                                        ctx->fowner.as<int32_t>(), ctx->fimg.as<uint8_t>()));
+    std::vector<uint8_t> img((size_t)npx);
+    SBO_HIP(hipMemcpyAsync(img.data(), ctx->fimg.as<uint8_t>(), (size_t)npx, hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<int32_t> pix;
+    sbo::trace_external_pixels(img.data(), width, height, pix);
+    const int64_t nf = (int64_t)pix.size();
+    if (nf == 0) return SBO_OK;
+    SBO_HIP(ctx->fpix.reserve(sizeof(int32_t) * (size_t)nf));
+    const size_t fbytes = (size_t)sbo::round_up((int64_t)sizeof(int32_t) * nf, 8);
+    SBO_HIP(ctx->fout.reserve(fbytes + 4 * sizeof(double) * (size_t)nf));
+    int32_t *dF = ctx->fout.as<int32_t>();
+    double *dcols = reinterpret_cast<double *>(ctx->fout.as<char>() + fbytes);
+    SBO_HIP(hipMemcpyAsync(ctx->fpix.as<int32_t>(), pix.data(), sizeof(int32_t) * nf, hipMemcpyHostToDevice,
+                           ctx->stream));
+    SBO_HIP(sbo::launch_frontier_gather(ctx->stream, ctx->fpix.as<int32_t>(), nf, ctx->fowner.as<int32_t>(), Dx, Dy,
+                                        lo, hi, dF, dcols));
+    F.resize((size_t)nf);
+    SBO_HIP(hipMemcpyAsync(F.data(), dF, sizeof(int32_t) * nf, hipMemcpyDeviceToHost, ctx->stream));
+    if (lo) {
+        cols.resize((size_t)(4 * nf));
+        SBO_HIP(hipMemcpyAsync(cols.data(), dcols, sizeof(double) * 4 * nf, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    return SBO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+SBO_API sbo_status sbo_frontier(sbo_ctx *ctx, const double *Dx, const double *Dy, const uint8_t *safe, int64_t m,
+                                int width_cells, int height_cells, int32_t *out, int64_t out_cap, int64_t *count,
+                                uint32_t flags) {
+    if (!ctx || !count) return SBO_E_INVAL;
+    *count = 0;
+    SBO_CHECK(m >= 0, SBO_E_INVAL, "sbo_frontier: m must be >= 0");
+    if (m == 0) return SBO_OK;
+    SBO_CHECK(Dx && Dy && safe, SBO_E_INVAL, "sbo_frontier: null input");
+    if (!dev(flags))
+        return sbo_find_safety_contour_indices(Dx, Dy, safe, m, width_cells, height_cells, out, out_cap, count);
+    SBO_HIP(hipSetDevice(ctx->device));
+    std::vector<int32_t> F;
+    std::vector<double> cols;
+    if (sbo_status st = device_frontier(ctx, Dx, Dy, safe, m, width_cells, height_cells, nullptr, nullptr, F, cols))
+        return st;
+    *count = (int64_t)F.size();
+    SBO_CHECK((int64_t)F.size() <= out_cap && (out || F.empty()), SBO_E_INVAL,
+              "sbo_frontier: out_cap too small (count holds the size)");
+    std::copy(F.begin(), F.end(), out);
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_subgoal(sbo_ctx *ctx, const double *Dx, const double *Dy, const double *lo, const double *hi,
+                               const uint8_t *safe, int64_t m, int width_cells, int height_cells, double goal_x,
+                               double goal_y, int64_t *index, uint32_t flags) {
+    if (!ctx || !index) return SBO_E_INVAL;
+    *index = -1;
+    SBO_CHECK(m >= 0, SBO_E_INVAL, "sbo_subgoal: m must be >= 0");
+    if (m == 0) return SBO_OK;
+    SBO_CHECK(Dx && Dy && lo && hi && safe, SBO_E_INVAL, "sbo_subgoal: null input");
+    if (!dev(flags)) {
+        *index = sbo_next_subgoal(Dx, Dy, lo, hi, safe, m, width_cells, height_cells, goal_x, goal_y);
+        return SBO_OK;
+    }
+    SBO_HIP(hipSetDevice(ctx->device));
+    std::vector<int32_t> F;
+    std::vector<double> cols;
+    if (sbo_status st = device_frontier(ctx, Dx, Dy, safe, m, width_cells, height_cells, lo, hi, F, cols)) return st;
+    const size_t nf = F.size();
+    const int64_t b = sbo::select_subgoal(nf, cols.data(), cols.data() + nf, cols.data() + 2 * nf,
+                                          cols.data() + 3 * nf, goal_x, goal_y);
+    *index = b >= 0 ? F[(size_t)b] : -1;
+    return SBO_OK;
+}
+
+}  // extern "C"

@@ -103,6 +103,7 @@ struct sbo_ctx {
     bool query_order = true;     // SBO_OPT_QUERY_ORDER: sweep queries in Morton order
     int kernel_variant = 0;      // SBO_OPT_KERNEL_VARIANT: predictive kernel build (A/B)
     int row_chunk = 0;           // SBO_OPT_ROW_CHUNK: row blocks per predictive workgroup (0: auto)
+    sbo::DevBuf fwork, fowner, fimg, fpix, fout;  // device frontier (sbo_frontier / sbo_subgoal)
     sbo::DevBuf qwork;           // query ordering workspace
     sbo::DevBuf kbox;            // per k-tile bounding boxes (float4)
     sbo::DevBuf alpha;           // K^-1 (y - m0), length cap
@@ -191,5 +192,26 @@ hipError_t launch_argmax_blocks(hipStream_t s, const double *score, const uint8_
 hipError_t launch_reduce_keys(hipStream_t s, const sbo_key *keys, int64_t nblocks, sbo_key *out);
 
 inline int64_t acq_blocks(int64_t m) { return (m + kAcqThreads - 1) / kAcqThreads; }
+
+// ------------------------------------------------------ frontier (8(f)1)
+// Device raster of FindSafetyContourIndices (:425-475): the node's
+// int-truncated bounds from a device min/max, each grid point's pixel
+// (scaled by width/height, out-of-range dropped), last writer (highest
+// index) wins -- atomicMax on a dense owner map, which replaces the node's
+// unordered_map (:468-475) -- and owner[k] = that point if it is safe, else
+// -1 (a pixel is foreground exactly when its last writer is safe).
+// img[k] = 1 on foreground pixels.  Workspace: frontier_work_bytes(m);
+// owner: width*height int32; img: width*height bytes.
+size_t frontier_work_bytes(int64_t m);
+hipError_t launch_frontier_raster(hipStream_t s, const double *Dx, const double *Dy, const uint8_t *safe, int64_t m,
+                                  int width, int height, void *work, int32_t *owner, uint8_t *img);
+// F[i] = owner[pix[i]]; when lo is non-null also out[c*nf + i] = (Dx, Dy, lo, hi)[F[i]].
+hipError_t launch_frontier_gather(hipStream_t s, const int32_t *pix, int64_t nf, const int32_t *owner,
+                                  const double *Dx, const double *Dy, const double *lo, const double *hi, int32_t *F,
+                                  double *out);
+// host side (frontier.cpp)
+void trace_external_pixels(const uint8_t *img, int w, int h, std::vector<int32_t> &pix);
+int64_t select_subgoal(size_t nf, const double *fx, const double *fy, const double *flo, const double *fhi,
+                       double goal_x, double goal_y);
 
 }  // namespace sbo

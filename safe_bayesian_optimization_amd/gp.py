@@ -79,6 +79,32 @@ class Context:
         raw = getattr(stream, "cuda_stream", stream)
         N.check(self._lib.sbo_set_stream(self.handle, ctypes.c_void_p(raw) if raw else None), self.handle)
 
+    # ------------------------------------------------- frontier, 8(f)1
+    def frontier(self, Dx, Dy, safe, width: int, height: int) -> np.ndarray:
+        """FindSafetyContourIndices (node.cpp:418-497).  Torch device tensors
+        (f64 coordinates, u8 mask) take the device raster; numpy arrays the
+        host restatement.  Returns the frontier grid indices (int32, host)."""
+        (Dx, Dy), fl = _prep([Dx, Dy], np.float64, "float64")
+        safe = safe.contiguous() if _is_dev(safe) else _host(safe, np.uint8)
+        m = int(Dx.numel() if _is_dev(Dx) else Dx.size)
+        cap = 8 * max(1, int(width)) * max(1, int(height)) + 16
+        out = np.empty(cap, np.int32)
+        cnt = ctypes.c_int64(0)
+        self.check(self._lib.sbo_frontier(self.handle, _ptr(Dx), _ptr(Dy), _ptr(safe), m, int(width), int(height),
+                                          ctypes.c_void_p(out.ctypes.data), cap, ctypes.byref(cnt), fl))
+        return out[:cnt.value].copy()
+
+    def subgoal(self, Dx, Dy, lo, hi, safe, width: int, height: int, gx: float = 0.0, gy: float = 0.0) -> int:
+        """GetNextSubgoal (node.cpp:499-550) on device tensors or host arrays;
+        -1 when there is no frontier."""
+        (Dx, Dy, lo, hi), fl = _prep([Dx, Dy, lo, hi], np.float64, "float64")
+        safe = safe.contiguous() if _is_dev(safe) else _host(safe, np.uint8)
+        m = int(Dx.numel() if _is_dev(Dx) else Dx.size)
+        idx = ctypes.c_int64(-1)
+        self.check(self._lib.sbo_subgoal(self.handle, _ptr(Dx), _ptr(Dy), _ptr(lo), _ptr(hi), _ptr(safe), m,
+                                         int(width), int(height), float(gx), float(gy), ctypes.byref(idx), fl))
+        return int(idx.value)
+
     def close(self) -> None:
         if getattr(self, "handle", None):
             self._lib.sbo_destroy(self.handle)
