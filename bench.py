@@ -209,6 +209,22 @@ def run_sweep(a, dev, world, rank):
     dense_flops_launch = float(n) * float(n) * m
     achieved = exec_flops_launch / (pred_ms * 1e-3) / 1e12
     fill_gbs = fill_bytes / (fill_ms * 1e-3) / 1e9 if fill_ms > 0 else None
+    # node-side selection on the tick's device outputs (8(f)1): frontier of S,
+    # nearest quarter to the goal, widest interval -- GetNextSubgoal
+    subgoal = None
+    if world == 1 and not a.no_outputs:
+        Dx = torch.as_tensor(wl.qx, dtype=torch.float64, device=dev)
+        Dy = torch.as_tensor(wl.qy, dtype=torch.float64, device=dev)
+        goal = (float(wl.qx.mean()), float(wl.qy.mean()))
+        sg = lambda: gm.ctx.subgoal(Dx, Dy, outs["lo"], outs["hi"], outs["safe"], gw, gh, *goal)  # noqa: E731
+        sg()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(3):
+            sidx = sg()
+        sub_ms = (time.perf_counter() - t1) * 1e3 / 3
+        subgoal = {"index": sidx, "ms": sub_ms, "goal": goal,
+                   "how": "sbo_subgoal: device raster/owner map, host border follow of the w x h image"}
     cpu = cpu_baseline(gm, wl, a.cpu_seconds) if world == 1 and not a.no_cpu else None
     traffic, traffic_src = pmc_traffic(a.config, n, m_total, m)
     return {
@@ -232,6 +248,7 @@ def run_sweep(a, dev, world, rank):
                           "avg_launch_ms": fill_ms, "algorithmic_bytes": fill_bytes},
         "fit_ms": fit_ms,
         "argmax": {"index": best[1], "score": best[0]},
+        "subgoal": subgoal,
         "cpu_baseline": cpu,
     }
 

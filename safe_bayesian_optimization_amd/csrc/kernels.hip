@@ -302,7 +302,7 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // OT: outer (cross-tile) accumulator type.  Grid: nQ query blocks x nC row
 // block chunks of G row blocks.
-template <class OT>
+template <class OT, int LOADERS = kPredictWaves / 2>
 __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     const float *__restrict__ aug, const float *__restrict__ kcoord, const float4 *__restrict__ kbox, int nI, int nC,
     int G, const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp, float cexp,
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     // ---- the sweep: a flat stream of (row block, k-tile) items
     // LDS-DMA staging (global_load_lds_dwordx4): each wave instruction moves
     // 1 KiB, lane-linear, no staging registers.  A stage = the 64 KiB [BK][BM]
-    // tile (8 instructions per wave) + 768 B of per-k coordinates (wave 0).
+    // tile (16 instructions per loader wave) + 768 B of per-k coordinates.
     // The DMA is issued from inline asm so that hipcc does not see an LDS
     // write in flight: with a compiler-visible one pending it drains every
     // ds_read wait to lgkmcnt(0) (waiting on reads issued one instruction
@@ -415,11 +415,16 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     // vmcnt(0) + barrier at the end of each item.
     typedef __attribute__((address_space(3))) char lds_char;
     constexpr int kTileBytes = kTileFloats * 4, kStageBytes = kStageFloats * 4, kCBytes = 3 * kBK * 4;
-    constexpr int kWaveStride = kTileBytes / kPredictWaves;  // bytes per wave per stage
-    const char *gA = reinterpret_cast<const char *>(aug) + wave * 1024 + lane * 16;
+    // Only the last LOADERS waves (one per SIMD) issue the stage, 16 pieces
+    // each; the first four go straight from the barrier into their MFMAs
+    // (1.8 % over every wave issuing 8, measured at C4).
+    constexpr int kWaveStride = kTileBytes / LOADERS;  // bytes per loader wave per stage
+    const int lw = wave - (kPredictWaves - LOADERS);    // loader index (< 0: not a loader)
+    const bool loader = lw >= 0;
+    const char *gA = reinterpret_cast<const char *>(aug) + (loader ? lw : 0) * 1024 + lane * 16;
     const char *gC = reinterpret_cast<const char *>(kcoord) + lane * 16;
     const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
-    const uint32_t lds_wave = lds_smem + (uint32_t)__builtin_amdgcn_readfirstlane(wave) * 1024u;
+    const uint32_t lds_wave = lds_smem + (uint32_t)__builtin_amdgcn_readfirstlane(loader ? lw : 0) * 1024u;
 #define SBO_DMA16(gsrc, ldst)                                                                           \
     do {                                                                                                \
         uint32_t keep_;                                                                                 \
@@ -431,11 +436,13 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     } while (0)
 #define SBO_STAGE(I_, t_, buf)                                                                          \
     do {                                                                                                \
-        const char *s_ = gA + (tile_start(I_) + (t_)) * (int64_t)kTileBytes;                           \
-        const uint32_t d_ = lds_wave + (uint32_t)(buf) * kStageBytes;                                   \
-        _Pragma("unroll") for (int j = 0; j < kWaveStride / 1024; ++j)                                  \
-            SBO_DMA16(s_ + j * kPredictWaves * 1024, d_ + (uint32_t)(j * kPredictWaves * 1024));        \
-        if (wave == 0 && lane < kCBytes / 16)                                                           \
+        if (loader) {                                                                                   \
+            const char *s_ = gA + (tile_start(I_) + (t_)) * (int64_t)kTileBytes;                       \
+            const uint32_t d_ = lds_wave + (uint32_t)(buf) * kStageBytes;                               \
+            _Pragma("unroll") for (int j = 0; j < kWaveStride / 1024; ++j)                              \
+                SBO_DMA16(s_ + j * LOADERS * 1024, d_ + (uint32_t)(j * LOADERS * 1024));                \
+        }                                                                                               \
+        if (lw == 0 && lane < kCBytes / 16)                                                             \
             SBO_DMA16(gC + (int64_t)(t_) * kCBytes, lds_smem + (uint32_t)((buf) * kStageBytes + kTileBytes)); \
     } while (0)
 

@@ -325,7 +325,19 @@ void run(bool zero, int blocks_per_cu) {
     ghz /= blocks;
     const double flops = (double)reps * blocks * 4 /*waves*/ * iters * (MIX < 0 ? 32 : MIX == 99 ? 256 : MIX == 98 ? 128 : 128) * 4096.0;  // spec: 4 consumer waves x 128
     const double tf = flops / (ms * 1e-3) / 1e12;
-    if (MIX >= 0) printf("mix %d ", MIX);
+    const char *what = "bare MFMA loop (4 x 32x32x2 per step, register operands)";
+    if (MIX == 98) what = "16x16x4: 16 MFMAs + 4 ds_read_b128 + K* chain per step (256 rows x 16 q / wave)";
+    else if (MIX == 99) what = "32x32x2: 8 MFMAs + 2 ds_read_b128 + K* chain per step (256 rows x 32 q / wave)";
+    else if (MIX >= 100) what = "specialised: MFMA-only waves 0-3 beside VALU-only (K* + ds_write) waves 4-7";
+    else if (MIX >= 0) {
+        static char buf[160];
+        snprintf(buf, sizeof buf, "32x32x2, 4 MFMAs per step%s%s%s%s", (MIX & 1) ? " + LDS reads" : "",
+                 (MIX & 2) ? " + K* VALU chain" : "", (MIX & 4) ? " with exp" : "", (MIX & 8) ? ", acc in AGPRs" : "");
+        what = buf;
+    }
+    printf("[%s%s] ", what, MIX >= 100 ? (MIX == 100 ? ", producers idle" : MIX == 102 ? ", 1 K* / 4 steps" :
+                                           MIX == 108 ? ", 1 K* / step" : ", 2 K* / step") : "");
+    if (MIX >= 100) ghz = 2.4;  // per-wave stamps are not a clock here (consumers finish first)
     printf("waves/SIMD %d (launch_bounds %d) %s: %.1f TF (%.1f%% of 157.3)  in-kernel clock %.3f GHz  => %.1f%% of clock-scaled peak\n",
            blocks_per_cu, W, zero ? "zero  " : "random", tf, tf / 157.3 * 100, ghz, tf / (157.3 * ghz / 2.4) * 100);
     CHECK(hipFree(in));

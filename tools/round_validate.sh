@@ -17,4 +17,7 @@ step bench_c5 600 python bench.py --config C5
 step prof_c4 600 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run --output-format csv -- python bench.py --no-cpu --steps 3
 step pmc_c4 900 bash tools/collect_pmc.sh C4 $TAG
 step pmc_c3 900 bash tools/collect_pmc.sh C3 $TAG
+step clock_c4 900 bash tools/pmc_clock.sh c4 --config C4 --ticks 2
+[ -x tools/mfma_probe.bin ] || hipcc -O3 --offload-arch=gfx950 tools/mfma_probe.hip -o tools/mfma_probe.bin
+step mfma_probe 300 ./tools/mfma_probe.bin
 echo done
