@@ -1,0 +1,38 @@
+"""Fit (a1 + a2) timing: first fit (allocations, code objects) vs warm refits,
+at C3/C4 sizes.   python tools/fit_timing.py [--n 16384] [--reps 3]"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--n", type=int, nargs="+", default=[8192, 16384])
+    p.add_argument("--reps", type=int, default=3)
+    a = p.parse_args()
+    import torch
+    from safe_bayesian_optimization_amd import TerrainMapper, synthetic
+    dev = torch.device("cuda:0")
+    for n in a.n:
+        wl = synthetic(n, 64, 64, seed=0)
+        t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
+        X, Y, O = t(wl.x), t(wl.y), t(wl.obs)
+        gm = TerrainMapper(0, wl.hyper)
+        ts = []
+        for _ in range(a.reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            gm.fit(X, Y, O)
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        print(f"N={n}: first fit {ts[0]:.1f} ms, warm refits {', '.join(f'{v:.1f}' for v in ts[1:])} ms", flush=True)
+        gm.close()
+
+
+if __name__ == "__main__":
+    main()
