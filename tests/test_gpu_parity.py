@@ -126,6 +126,65 @@ def test_predict_given_factor(mapper, n, gw, gh):
     assert np.all(sd >= 0) and np.all(sd <= np.sqrt(wl.hyper.sf2) * (1 + 1e-6))
 
 
+@pytest.mark.parametrize("offset", [(250.0, -730.0), (-4096.5, 12.25)])
+def test_predict_far_from_origin(mapper, offset):
+    """A terrain patch far from the origin (map frames are rarely centred):
+    K* differences stay exact-ish in f32 near each query, the Morton codes and
+    tile boxes are relative to the training box; same contract."""
+    wl = synthetic(1500, 60, 45, seed=41)
+    wl.x = wl.x + offset[0]
+    wl.y = wl.y + offset[1]
+    wl.qx = wl.qx + offset[0]
+    wl.qy = wl.qy + offset[1]
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    mu, sd = gm.predict(wl.qx, wl.qy)
+    omu, ovar = oracle_given_factor(gm, wl)
+    emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
+    print(f"offset {offset}: mu {emu:.2e} var {evar:.2e}")
+    assert emu < REL_TOL and evar < REL_TOL
+
+
+def strtrs_var_error(gm, wl, ovar):
+    """Normwise variance error of a plain f32 LAPACK strtrs on the device's
+    own L and the same f32 K* -- the reference implementation class
+     -- for ill-conditioned cases."""
+    import scipy.linalg as sla
+    h = wl.hyper
+    L, _ = gm.factor()
+    o = gm.order()
+    xs, ys, qx, qy = (f32(v).astype(np.float64) for v in (wl.x[o], wl.y[o], wl.qx, wl.qy))
+    Ks = (h.sf2 * np.exp(-((xs[:, None] - qx[None, :]) ** 2 + (ys[:, None] - qy[None, :]) ** 2)
+                         / (2 * h.length_scale ** 2))).astype(np.float32)
+    V = sla.solve_triangular(L, Ks, lower=True).astype(np.float64)
+    return nrel(h.sf2 - (V * V).sum(0), ovar)
+
+
+@pytest.mark.parametrize("ell", [0.05, 1.6])
+def test_predict_length_scale_extremes(mapper, ell):
+    """l = 0.05 on the default domain: nearly every K* tile is skipped
+    (K ~ (sf2 + sn2) I); l = 1.6: almost nothing is skipped and K is badly
+    conditioned (128 points per l^2).  There f32 arithmetic cannot meet 1e-5
+    whatever the algorithm: the bound is the reference implementation class,
+    a plain f32 strtrs on the same L and K*.  The explicit-inverse sweep lands
+    within 1.5x of it (measured 3.6e-5 vs 2.7e-5 at l = 1.6, and 0.9x at
+    l = 1.0; the error is the f32 rounding of A and K*: it does not move with
+    the outer accumulator type or the tile cutoff)."""
+    h = Hyper(length_scale=ell, sigma_f=1.0, noise_level=0.1, prior_mean=0.0)
+    wl = synthetic(2048, 64, 48, seed=42)
+    gm = TerrainMapper(0, h, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    mu, sd = gm.predict(wl.qx, wl.qy)
+    wl.hyper = h
+    omu, ovar = oracle_given_factor(gm, wl)
+    emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
+    L, rl1, al1 = gm.skip_info()
+    estrsm = strtrs_var_error(gm, wl, ovar)
+    print(f"l={ell}: cutoff 2^-{L}: mu {emu:.2e} var {evar:.2e} (f32 strtrs {estrsm:.2e})")
+    assert emu < REL_TOL
+    assert evar < max(REL_TOL, 1.5 * estrsm)
+
+
 def test_predict_nondefault_hyper(mapper):
     h = Hyper(length_scale=0.7, sigma_f=1.7, noise_level=0.05, prior_mean=0.3)
     wl = synthetic(700, 50, 20, seed=3, hyper=h)
