@@ -163,6 +163,35 @@ def run_sweep(a, dev, world, rank):
     gm.fit(X, Y, OBS)
     torch.cuda.synchronize()
     fit_ms = (time.perf_counter() - t0) * 1e3
+    # SURVEY.md 8(e) alternative: rank 0 fits, the packed predictive state is
+    # broadcast (RCCL) and imported elsewhere -- timed beside the replicated fit
+    fit_bcast = None
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        on_dev = a.backend == "nccl"
+        size = torch.zeros(1, dtype=torch.int64, device=dev if on_dev else "cpu")
+        if rank == 0:
+            gm.fit(X, Y, OBS)
+            blob = gm.export_state()
+            size[0] = blob.numel()
+        dist.broadcast(size, 0)
+        if rank != 0:
+            blob = torch.empty(int(size.item()), dtype=torch.uint8, device=dev)
+        if on_dev:
+            dist.broadcast(blob, 0)
+        else:
+            hb = blob.cpu()
+            dist.broadcast(hb, 0)
+            blob.copy_(hb)
+        if rank != 0:
+            gm.import_state(blob)
+        torch.cuda.synchronize()
+        dist.barrier()
+        fit_bcast = {"ms": (time.perf_counter() - t0) * 1e3, "state_bytes": int(size.item()),
+                     "how": "rank 0 sbo_fit + sbo_export_state, broadcast, sbo_import_state"}
+        del blob
     cutoff, row_l1, alpha_l1 = gm.skip_info()
 
     # ---- RBF fill (a1) alone, warm (the fill inside fit also paid the code-object load)
@@ -252,7 +281,7 @@ def run_sweep(a, dev, world, rank):
         "fill_roofline": {"kernel": "rbf_fill_kernel", "bound": "hbm", "achieved": fill_gbs, "peak": PEAK_HBM_GBS,
                           "unit": "GB/s", "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None,
                           "avg_launch_ms": fill_ms, "algorithmic_bytes": fill_bytes},
-        "fit_ms": fit_ms, "fit_first_ms": fit_first_ms,
+        "fit_ms": fit_ms, "fit_first_ms": fit_first_ms, "fit_broadcast": fit_bcast,
         "argmax": {"index": best[1], "score": best[0]},
         "subgoal": subgoal,
         "cpu_baseline": cpu,

@@ -166,6 +166,18 @@ SBO_API sbo_status sbo_subgoal(sbo_ctx *ctx, const double *Dx, const double *Dy,
                                int height_cells, double goal_x, double goal_y, int64_t *index,
                                uint32_t flags);
 
+/* Fitted predictive state as one device blob (fit on one
+ * rank, broadcast the operand to the others instead of refitting there).
+ * sbo_state_bytes gives the size (the packed sf2 L^-1 tiles dominate:
+ * ~2 N^2 B), sbo_export_state writes it into a caller device buffer,
+ * sbo_import_state restores it into another context on any device.  An
+ * imported context predicts, ticks and reports like the original (bitwise
+ * identical sweeps) but holds no factor: sbo_append / sbo_get_factor return
+ * SBO_E_STATE until the next sbo_fit. */
+SBO_API sbo_status sbo_state_bytes(sbo_ctx *ctx, int64_t *bytes);
+SBO_API sbo_status sbo_export_state(sbo_ctx *ctx, void *dev_buf, int64_t cap);
+SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t bytes);
+
 /* Raw border follower used by the frontier: img is height x width u8
  * row-major; points (x,y) pairs; start[c]..start[c+1] bound contour c.
  * Returns the number of contours, or -1 if a capacity was exceeded. */

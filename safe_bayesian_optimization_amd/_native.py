@@ -30,6 +30,7 @@ EXPORTS = (
     "sbo_key_combine", "sbo_find_safety_contour_indices", "sbo_next_subgoal", "sbo_find_contours_external",
     "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
     "sbo_get_order", "sbo_profile_work", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
+    "sbo_state_bytes", "sbo_export_state", "sbo_import_state",
 )
 SBO_OPT_INVERSE_BITS = 1
 SBO_OPT_SPATIAL_ORDER = 2
@@ -115,6 +116,12 @@ def lib():
     L.sbo_frontier.restype = st
     L.sbo_subgoal.argtypes = [vp, vp, vp, vp, vp, vp, i64, i32, i32, dbl, dbl, ctypes.POINTER(i64), u32]
     L.sbo_subgoal.restype = st
+    L.sbo_state_bytes.argtypes = [vp, ctypes.POINTER(i64)]
+    L.sbo_state_bytes.restype = st
+    L.sbo_export_state.argtypes = [vp, vp, i64]
+    L.sbo_export_state.restype = st
+    L.sbo_import_state.argtypes = [vp, vp, i64]
+    L.sbo_import_state.restype = st
     L.sbo_find_contours_external.argtypes = [vp, i32, i32, vp, i64, vp, i64]
     L.sbo_find_contours_external.restype = i64
     L.sbo_rbf_fill.argtypes = [vp, vp, vp, i64, sbo_hyper, vp, u32]

@@ -334,6 +334,7 @@ sbo_status factor_and_refresh(sbo_ctx *ctx) {
         ctx->err = "spotrf: leading minor " + std::to_string(hinfo) + " not positive definite";
         return SBO_E_NOT_SPD;
     }
+    ctx->has_factor = true;
     return refresh_operand(ctx);
 }
 
@@ -474,6 +475,7 @@ SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, cons
                               uint32_t flags) {
     if (!ctx) return SBO_E_INVAL;
     SBO_CHECK(ctx->fitted, SBO_E_STATE, "sbo_append: call sbo_fit first");
+    SBO_CHECK(ctx->has_factor, SBO_E_STATE, "sbo_append: imported predict-only state has no factor; refit");
     SBO_CHECK(x && y && obs, SBO_E_INVAL, "sbo_append: null input");
     SBO_CHECK(b >= 0, SBO_E_INVAL, "sbo_append: b must be >= 0");
     if (b == 0) return SBO_OK;
@@ -700,7 +702,7 @@ SBO_API sbo_status sbo_rbf_fill(sbo_ctx *ctx, const float *x, const float *y, in
 
 SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t flags) {
     if (!ctx) return SBO_E_INVAL;
-    SBO_CHECK(ctx->fitted, SBO_E_STATE, "sbo_get_factor: call sbo_fit first");
+    SBO_CHECK(ctx->fitted && ctx->has_factor, SBO_E_STATE, "sbo_get_factor: call sbo_fit first");
     SBO_HIP(hipSetDevice(ctx->device));
     const int64_t n = ctx->n;
     const hipMemcpyKind k = dev(flags) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -923,6 +925,116 @@ SBO_API sbo_status sbo_subgoal(sbo_ctx *ctx, const double *Dx, const double *Dy,
     const int64_t b = sbo::select_subgoal(nf, cols.data(), cols.data() + nf, cols.data() + 2 * nf,
                                           cols.data() + 3 * nf, goal_x, goal_y);
     *index = b >= 0 ? F[(size_t)b] : -1;
+    return SBO_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------- fitted state, 8(e)
+namespace {
+
+constexpr uint64_t kStateMagic = 0x3153544154534253ull;  // "SBSTATS1"
+
+struct StateHeader {
+    uint64_t magic;
+    int64_t n, npad;
+    double hyper[4];
+    double max_row_l1, alpha_l1;
+    float bbox[4];
+    int32_t auto_skip_log2, spatial_order;
+    int64_t off_order, off_aug, off_kcoord, off_kbox, total;
+};
+
+StateHeader state_layout(const sbo_ctx *ctx) {
+    StateHeader h{};
+    h.magic = kStateMagic;
+    h.n = ctx->n;
+    h.npad = ctx->npad;
+    h.hyper[0] = ctx->hyper.length_scale;
+    h.hyper[1] = ctx->hyper.sigma_f;
+    h.hyper[2] = ctx->hyper.noise_level;
+    h.hyper[3] = ctx->hyper.prior_mean;
+    h.max_row_l1 = ctx->max_row_l1;
+    h.alpha_l1 = ctx->alpha_l1;
+    for (int i = 0; i < 4; ++i) h.bbox[i] = ctx->bbox[i];
+    h.auto_skip_log2 = ctx->auto_skip_log2;
+    h.spatial_order = ctx->spatial_order ? 1 : 0;
+    const int64_t nt = ctx->npad / sbo::kBK;
+    h.off_order = 256;
+    h.off_aug = sbo::round_up(h.off_order + 8 * h.n, 256);
+    h.off_kcoord = sbo::round_up(h.off_aug + 4 * sbo::total_tiles(ctx->npad / sbo::kBM) * sbo::kTileFloats, 256);
+    h.off_kbox = sbo::round_up(h.off_kcoord + 4 * nt * 3 * sbo::kBK, 256);
+    h.total = sbo::round_up(h.off_kbox + 16 * nt, 256);
+    return h;
+}
+
+}  // namespace
+
+extern "C" {
+
+SBO_API sbo_status sbo_state_bytes(sbo_ctx *ctx, int64_t *bytes) {
+    if (!ctx || !bytes) return SBO_E_INVAL;
+    SBO_CHECK(ctx->fitted, SBO_E_STATE, "sbo_state_bytes: call sbo_fit first");
+    *bytes = state_layout(ctx).total;
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_export_state(sbo_ctx *ctx, void *dev_buf, int64_t cap) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(ctx->fitted, SBO_E_STATE, "sbo_export_state: call sbo_fit first");
+    const StateHeader h = state_layout(ctx);
+    SBO_CHECK(dev_buf && cap >= h.total, SBO_E_INVAL, "sbo_export_state: buffer smaller than sbo_state_bytes");
+    SBO_HIP(hipSetDevice(ctx->device));
+    char *b = static_cast<char *>(dev_buf);
+    const int64_t nt = ctx->npad / sbo::kBK;
+    SBO_HIP(hipMemcpyAsync(b, &h, sizeof(h), hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(b + h.off_order, ctx->order.data(), 8 * (size_t)h.n, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(b + h.off_aug, ctx->aug.as<void>(),
+                           4 * (size_t)sbo::total_tiles(ctx->npad / sbo::kBM) * sbo::kTileFloats,
+                           hipMemcpyDeviceToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(b + h.off_kcoord, ctx->kcoord.as<void>(), 4 * (size_t)nt * 3 * sbo::kBK,
+                           hipMemcpyDeviceToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(b + h.off_kbox, ctx->kbox.as<void>(), 16 * (size_t)nt, hipMemcpyDeviceToDevice,
+                           ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));  // the header and order live on this host stack
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t bytes) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(dev_buf && bytes >= (int64_t)sizeof(StateHeader), SBO_E_INVAL, "sbo_import_state: bad buffer");
+    SBO_HIP(hipSetDevice(ctx->device));
+    const char *b = static_cast<const char *>(dev_buf);
+    StateHeader h;
+    SBO_HIP(hipMemcpyAsync(&h, b, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    SBO_CHECK(h.magic == kStateMagic && h.total <= bytes && h.n > 0 && h.npad == sbo::round_up(h.n, sbo::kBM),
+              SBO_E_INVAL, "sbo_import_state: not an sbo state blob (or truncated)");
+    ctx->fitted = false;
+    ctx->has_factor = false;
+    ctx->linv_n = 0;
+    const int64_t nt = h.npad / sbo::kBK;
+    const size_t aug_bytes = 4 * (size_t)sbo::total_tiles(h.npad / sbo::kBM) * sbo::kTileFloats;
+    SBO_HIP(ctx->aug.reserve(aug_bytes));
+    SBO_HIP(ctx->kcoord.reserve(4 * (size_t)nt * 3 * sbo::kBK));
+    SBO_HIP(ctx->kbox.reserve(16 * (size_t)nt));
+    ctx->order.resize((size_t)h.n);
+    SBO_HIP(hipMemcpyAsync(ctx->order.data(), b + h.off_order, 8 * (size_t)h.n, hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(ctx->aug.as<void>(), b + h.off_aug, aug_bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(ctx->kcoord.as<void>(), b + h.off_kcoord, 4 * (size_t)nt * 3 * sbo::kBK,
+                           hipMemcpyDeviceToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(ctx->kbox.as<void>(), b + h.off_kbox, 16 * (size_t)nt, hipMemcpyDeviceToDevice,
+                           ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->n = h.n;
+    ctx->npad = h.npad;
+    ctx->hyper = sbo_hyper{h.hyper[0], h.hyper[1], h.hyper[2], h.hyper[3]};
+    ctx->max_row_l1 = h.max_row_l1;
+    ctx->alpha_l1 = h.alpha_l1;
+    for (int i = 0; i < 4; ++i) ctx->bbox[i] = h.bbox[i];
+    ctx->auto_skip_log2 = h.auto_skip_log2;
+    ctx->spatial_order = h.spatial_order != 0;
+    ctx->fitted = true;
     return SBO_OK;
 }
 

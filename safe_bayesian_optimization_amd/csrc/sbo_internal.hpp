@@ -87,6 +87,7 @@ struct sbo_ctx {
     int64_t cap = 0;     // allocated leading dimension of L (>= n, for appends)
     sbo_hyper hyper{0.4, 1.0, 0.1, 0.0};
     bool fitted = false;
+    bool has_factor = false;     // false after sbo_import_state: predict-only (no L to append to)
 
     sbo::DevBuf x, y, obs;       // training data, f32, capacity cap
     sbo::DevBuf L;               // lower Cholesky factor, column-major, lda = cap

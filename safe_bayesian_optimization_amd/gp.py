@@ -212,6 +212,21 @@ class TerrainMapper:
     def set_option(self, option: int, value: int) -> None:
         self.ctx.check(self._lib.sbo_set_option(self.ctx.handle, int(option), int(value)))
 
+    def export_state(self):
+        """The fitted predictive state as a torch uint8 device tensor
+        (broadcast it; ``import_state`` on another rank)."""
+        import torch
+        nb = ctypes.c_int64(0)
+        self.ctx.check(self._lib.sbo_state_bytes(self.ctx.handle, ctypes.byref(nb)))
+        buf = torch.empty(nb.value, dtype=torch.uint8, device=f"cuda:{self.ctx.device}")
+        self.ctx.check(self._lib.sbo_export_state(self.ctx.handle, ctypes.c_void_p(buf.data_ptr()), nb.value))
+        return buf
+
+    def import_state(self, buf) -> None:
+        """Adopt a state exported by another context (predict-only until the next fit)."""
+        self.ctx.check(self._lib.sbo_import_state(self.ctx.handle, ctypes.c_void_p(buf.data_ptr()),
+                                                  int(buf.numel())))
+
     def factor(self):
         """(L, alpha) in the internal training order (see ``order()``):
         L dense lower (row-major numpy f32), alpha f32."""

@@ -507,3 +507,39 @@ def test_cpp_node_driver_tick(mapper):
     assert int(node.S_.sum()) == out["safe"]
     assert node.GetNextSubgoal() == out["subgoal"]
     assert node.FindSafetyContourIndices().size == out["frontier"]
+
+
+# ------------------------------------------- 8(e) fitted-state broadcast
+def test_state_export_import(dev, mapper):
+    """Fit once, export the predictive state, import it into a fresh context:
+    the imported context's tick is bitwise identical (same operand, same
+    order, same cutoff), it refuses appends and factor reads (no factor
+    travels), and a corrupted or truncated blob is rejected."""
+    wl = synthetic(3000, 80, 60, seed=51)
+    a = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    a.fit(wl.x, wl.y, wl.obs)
+    blob = a.export_state()
+    ka = a.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=dict(mu=np.empty(wl.qx.size, np.float32),
+                                                               sd=np.empty(wl.qx.size, np.float32)))
+    mua, sda = a.predict(wl.qx, wl.qy)
+    b = TerrainMapper(0, wl.hyper)
+    b.import_state(blob)
+    assert b.n == 3000 and np.array_equal(b.order(), a.order())
+    assert b.skip_info() == a.skip_info()
+    mub, sdb = b.predict(wl.qx, wl.qy)
+    assert np.array_equal(mua, mub) and np.array_equal(sda, sdb)
+    kb = b.tick(wl.qx, wl.qy, wl.beta, wl.f_min)
+    assert (kb.idx, kb.score) == (ka.idx, ka.score)
+    with pytest.raises(N.SboError):
+        b.append(wl.x[:5], wl.y[:5], wl.obs[:5])
+    with pytest.raises(N.SboError):
+        b.factor()
+    with pytest.raises(N.SboError):
+        b.import_state(blob[:1024])
+    bad = blob.clone()
+    bad[:8] = 0
+    with pytest.raises(N.SboError):
+        b.import_state(bad)
+    b.fit(wl.x, wl.y, wl.obs)      # a refit restores the full state
+    b.append(wl.x[:5] + 0.01, wl.y[:5], wl.obs[:5])
+    b.close()
