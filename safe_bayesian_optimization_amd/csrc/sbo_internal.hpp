@@ -94,7 +94,7 @@ struct sbo_ctx {
     sbo::DevBuf Linv;            // L^-1 (strtri f32 workspace, or dtrtri f64 kept for appends), lda = cap
     int64_t linv_n = 0;          // rows of the f64 L^-1 held in Linv (0: none; appends extend it)
     int inverse_bits = 64;       // SBO_OPT_INVERSE_BITS: precision of the L^-1 computation
-    bool spatial_order = true;   // SBO_OPT_SPATIAL_ORDER: Morton-order the training points
+    int spatial_order = 1;       // SBO_OPT_SPATIAL_ORDER: 0 caller order, 1 Hilbert, 2 Morton
     int skip_log2 = -1;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-L (-1: auto)
     int auto_skip_log2 = 160;    // L from the error budget, computed at fit (see refresh_operand)
     double max_row_l1 = 0.0;     // max_i sum_j |A_ij|, A = sf2 L^-1

