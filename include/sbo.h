@@ -214,8 +214,9 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * the result is bitwise identical to the dense sweep.  -1 (auto): L is the
  * smallest exponent whose worst-case effect -- 2^-L max_i |(sf2 L^-1)_i|_1 on
  * any V entry, hence 2 sqrt(N sf2) times that on sigma^2, and
- * 2^-L |sf2 alpha|_1 on any mean -- stays below 2^-27 sf2 (resp. 2^-27
- * sqrt(sf2)), computed from the fitted factor (sbo_get_skip reports it). */
+ * 2^-L |sf2 alpha|_1 on any mean -- stays below 2^-B sf2 (resp. 2^-B
+ * sqrt(sf2)), B = SBO_OPT_SKIP_BUDGET, computed from the fitted factor
+ * (sbo_get_skip reports it). */
 #define SBO_OPT_TILE_SKIP 3
 /* SBO_OPT_QUERY_ORDER (0 | 1, default 1): sweep the queries of a tick in
  * Morton order (device radix sort, ~0.1 ms per 10^6 points) so each
@@ -230,6 +231,13 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * walks for its 128 queries; 0 = default (1: row-block-major grid, A tiles
  * shared in L2 by the concurrently running workgroups). */
 #define SBO_OPT_ROW_CHUNK 6
+/* SBO_OPT_SKIP_BUDGET (B in [10, 60], default 22): the automatic K* cutoff
+ * (SBO_OPT_TILE_SKIP = -1) keeps its worst-case error below 2^-B sf2 on any
+ * variance and 2^-B sf2^(1/2) on any mean (2^-22 = 2.4e-7: under 3 % of the
+ * 1e-5 contract; the measured effect at B = 20..27 is below the f32
+ * rounding of the sweep itself).  Takes effect at the next sbo_fit /
+ * sbo_append. */
+#define SBO_OPT_SKIP_BUDGET 7
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The K* tile cutoff in effect (auto or fixed) and the norms it was derived from. */

@@ -38,6 +38,7 @@ SBO_OPT_TILE_SKIP = 3
 SBO_OPT_QUERY_ORDER = 4
 SBO_OPT_KERNEL_VARIANT = 5
 SBO_OPT_ROW_CHUNK = 6
+SBO_OPT_SKIP_BUDGET = 7
 
 
 class SboError(RuntimeError):

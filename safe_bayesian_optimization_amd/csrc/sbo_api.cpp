@@ -313,7 +313,8 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     // dropped block has every entry < 2^-L, so each V_i moves by at most
     // 2^-L max_i |A_i|_1 and each mean by at most 2^-L |sf2 alpha|_1.  With
     // |V|_2 <= sf2^(1/2), |d sigma^2| <= 2 sf2^(1/2) sqrt(N) max|dV_i|.  L is the
-    // smallest exponent that keeps both below 2^-27 (~7.5e-9) of sf2 / sf2^(1/2).
+    // smallest exponent that keeps both below 2^-B of sf2 / sf2^(1/2), B =
+    // SBO_OPT_SKIP_BUDGET.
     // Rows of earlier row blocks are unchanged by an append: only the repacked
     // row blocks are re-measured.
     {
@@ -332,7 +333,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         double al1 = 0.0;
         for (float v : ha) al1 += std::fabs((double)v);
         ctx->alpha_l1 = al1 * sf2;
-        const double tol = std::ldexp(1.0, -27), sf = std::sqrt(sf2);
+        const double tol = std::ldexp(1.0, -ctx->skip_budget), sf = std::sqrt(sf2);
         const double need_v = 2.0 * std::sqrt((double)n) * ctx->max_row_l1 / (tol * sf);
         const double need_m = ctx->alpha_l1 / (tol * sf);
         const double l2 = std::log2(std::max({need_v, need_m, 1.0}));
@@ -805,6 +806,10 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             return SBO_OK;
         case SBO_OPT_QUERY_ORDER:
             ctx->query_order = value != 0;
+            return SBO_OK;
+        case SBO_OPT_SKIP_BUDGET:
+            SBO_CHECK(value >= 10 && value <= 60, SBO_E_INVAL, "SBO_OPT_SKIP_BUDGET must be in [10, 60]");
+            ctx->skip_budget = (int)value;
             return SBO_OK;
         case SBO_OPT_ROW_CHUNK:
             SBO_CHECK(value >= 0 && value <= 128, SBO_E_INVAL, "SBO_OPT_ROW_CHUNK must be in [0, 128]");

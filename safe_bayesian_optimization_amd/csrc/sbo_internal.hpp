@@ -97,6 +97,7 @@ struct sbo_ctx {
     int spatial_order = 1;       // SBO_OPT_SPATIAL_ORDER: 0 caller order, 1 Hilbert, 2 Morton
     int skip_log2 = -1;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-L (-1: auto)
     int auto_skip_log2 = 160;    // L from the error budget, computed at fit (see refresh_operand)
+    int skip_budget = 22;        // SBO_OPT_SKIP_BUDGET: the auto cutoff keeps the skip error below 2^-B
     double max_row_l1 = 0.0;     // max_i sum_j |A_ij|, A = sf2 L^-1
     double alpha_l1 = 0.0;       // sum_j |sf2 alpha_j|
     std::vector<int64_t> order;  // internal row -> caller's training index

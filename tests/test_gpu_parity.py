@@ -337,7 +337,8 @@ def test_tile_skip_exact_and_bounded(dev, mapper):
     """N = 8192 over a 32 l domain.  Cutoff 2^-160 (entries exactly +0.0):
     mu, sd and the key bitwise identical to the dense sweep.  Cutoff 2^-64:
     at most 1 ulp on a vanishing fraction of points.  Auto cutoff (default):
-    within its stated error budget (2^-27 sf2 on sigma^2, 2^-27 sf on mu)
+    within its stated error budget (2^-B sf2 on sigma^2, 2^-B sf on mu, B =
+    SBO_OPT_SKIP_BUDGET, default 22; also checked at B = 27)
     of the dense sweep, same argmax."""
     wl = synthetic(8192, 200, 160, seed=21)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
@@ -352,14 +353,23 @@ def test_tile_skip_exact_and_bounded(dev, mapper):
     gm.set_option(N.SBO_OPT_TILE_SKIP, -1)
     L, rl1, al1 = gm.skip_info()
     print(f"auto cutoff 2^-{L} (max row l1 {rl1:.3g}, |sf2 alpha|_1 {al1:.3g})")
-    assert 24 <= L < 64
-    budget = 2.0 ** -27
-    dmu = np.abs(res[-1][0].astype(np.float64) - res[0][0]).max()
-    dvar = np.abs(res[-1][1].astype(np.float64) ** 2 - res[0][1].astype(np.float64) ** 2).max()
+    assert 20 <= L < 64
     ulp = np.finfo(np.float32).eps
-    assert dmu <= budget + 2 * ulp * np.abs(res[0][0]).max()   # f32 output rounding on top
-    assert dvar <= budget + 4 * ulp
-    assert res[-1][2] == res[0][2]
+
+    def within(r, B):
+        dmu = np.abs(r[0].astype(np.float64) - res[0][0]).max()
+        dvar = np.abs(r[1].astype(np.float64) ** 2 - res[0][1].astype(np.float64) ** 2).max()
+        assert dmu <= 2.0 ** -B + 2 * ulp * np.abs(res[0][0]).max()   # f32 output rounding on top
+        assert dvar <= 2.0 ** -B + 4 * ulp
+        assert r[2] == res[0][2]
+    within(res[-1], 22)
+    gm.set_option(N.SBO_OPT_SKIP_BUDGET, 27)          # a stricter budget, refit: a larger L
+    gm.fit(wl.x, wl.y, wl.obs)
+    out = dict(mu=np.empty(m, np.float32), sd=np.empty(m, np.float32))
+    k = gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
+    assert gm.skip_info()[0] > L
+    within((out["mu"], out["sd"], k.idx, k.score), 27)
+    gm.set_option(N.SBO_OPT_SKIP_BUDGET, 22)
     assert np.array_equal(res[0][0], res[160][0]) and np.array_equal(res[0][1], res[160][1])
     assert res[0][2:] == res[160][2:]
     for a, b in ((res[0][0], res[64][0]), (res[0][1], res[64][1])):

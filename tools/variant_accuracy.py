@@ -23,7 +23,7 @@ def nrel(a, b):
     return float(np.abs(np.asarray(a, np.float64) - b).max() / np.abs(b).max())
 
 
-def run(n, variants, nq, skip):
+def run(n, variants, nq, skip, budget=None):
     wl = synthetic(n, 1000, 1000, seed=0)
     h = wl.hyper
     rng = np.random.default_rng(1)
@@ -32,6 +32,8 @@ def run(n, variants, nq, skip):
     qx, qy = wl.qx[sel].astype(np.float32), wl.qy[sel].astype(np.float32)
     gm = TerrainMapper(0, h)
     gm.set_option(N.SBO_OPT_TILE_SKIP, skip)
+    if budget is not None:
+        gm.set_option(N.SBO_OPT_SKIP_BUDGET, budget)
     gm.fit(wl.x.astype(np.float32), wl.y.astype(np.float32), wl.obs.astype(np.float32))
     A = np.zeros((n, n), np.float32)
     gm.ctx.check(N.lib().sbo_get_inverse(gm.ctx.handle, A.ctypes.data))
@@ -42,12 +44,16 @@ def run(n, variants, nq, skip):
                  (ys[:, None] - qy[None, :].astype(np.float64)) ** 2) / (2 * h.length_scale ** 2))
     V = A @ E
     hvar = h.sf2 - (V * V).sum(0)
+    Lf, alpha = gm.factor()
+    hmu = h.prior_mean + h.sf2 * (E.T @ alpha.astype(np.float64))
     del A, E, V
     for v in variants:
         gm.set_option(N.SBO_OPT_KERNEL_VARIANT, v)
         mu, sd = gm.predict(qx, qy)
         var = sd.astype(np.float64) ** 2
-        print(f"N={n} skip={skip} variant {v}: var vs host f64 sweep {nrel(var, hvar):.2e}", flush=True)
+        L = gm.skip_info()[0]
+        print(f"N={n} skip={skip} budget={budget} (L={L}) variant {v}: var vs host f64 sweep {nrel(var, hvar):.2e}"
+              f"  mu vs host f64 {nrel(mu, hmu):.2e}", flush=True)
     gm.close()
 
 
@@ -57,9 +63,11 @@ def main():
     p.add_argument("--variants", type=int, nargs="+", default=[0, 1])
     p.add_argument("--nq", type=int, default=1024)
     p.add_argument("--skip", type=int, default=-1)
+    p.add_argument("--budget", type=int, nargs="*", default=[None])
     a = p.parse_args()
     for n in a.n:
-        run(n, a.variants, a.nq, a.skip)
+        for b in a.budget:
+            run(n, a.variants, a.nq, a.skip, b)
 
 
 if __name__ == "__main__":
