@@ -150,6 +150,26 @@ __global__ __launch_bounds__(kBM) void row_l1_kernel(const float *__restrict__ a
     atomicAdd(row_l1 + I * kBM + r, s);
 }
 
+// Per packed tile: log2 of the largest row sum of |A| over its 64 k (one
+// workgroup per tile, thread r = row r).
+__global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
+                                                        float *__restrict__ lgn) {
+    __shared__ double red[kBM / 64];
+    const int64_t tile = t0 + blockIdx.x;
+    const float *t = aug + tile * kTileFloats;
+    const int r = threadIdx.x;
+    double s = 0.0;
+    for (int k = 0; k < kBK; ++k) s += fabs((double)t[tile_offset(k, r)]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s = fmax(s, __shfl_xor(s, o));
+    if ((r & 63) == 0) red[r >> 6] = s;
+    __syncthreads();
+    if (r == 0) {
+        for (int w = 1; w < kBM / 64; ++w) s = fmax(s, red[w]);
+        lgn[tile] = s > 0.0 ? (float)log2(s) : -1000.0f;
+    }
+}
+
 // d[i] = (double)in[i] - v
 __global__ void widen_sub_kernel(const float *__restrict__ in, double v, int64_t n, double *__restrict__ d) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -306,7 +326,8 @@ template <class OT, int LOADERS = kPredictWaves / 2>
 __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     const float *__restrict__ aug, const float *__restrict__ kcoord, const float4 *__restrict__ kbox, int nI, int nC,
     int G, const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp, float cexp,
-    float skip_d2, float m0, float *__restrict__ part, float *__restrict__ mean,
+    float skip_d2, float skip_d2_mean, const float *__restrict__ lgn, float lg_tau_v, float m0,
+    float *__restrict__ part, float *__restrict__ mean,
     unsigned long long *__restrict__ tiles_done) {
     __shared__ __attribute__((aligned(16))) float smem[kSmemFloats];
     int *tlist = reinterpret_cast<int *>(smem + 2 * kStageFloats);
@@ -337,6 +358,11 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     int cnt = nkb;
     const int *list = nullptr;
     if (skip_d2 > 0.0f && nkb <= kMaxList) {
+        const bool mean_block = (I1 == nI);  // the chunk holding the last row block also accumulates the mean
+        const float lg_tau_I = lg_tau_v - __log2f((float)nkb) - 0.05f;  // budget share per tile (5 % slack)
+        // tile-norm test per row block: one row block per workgroup only (a
+        // chunk shares one list, and the norms differ between its row blocks)
+        const float *lgn_I = (lgn && I1 - I0 == 1) ? lgn + tile_start(I0) : nullptr;
         const float bx0 = wave_min(xq), bx1 = wave_max(xq), by0 = wave_min(yq), by1 = wave_max(yq);
         if (lane == 0) {
             wbox[wave * 4 + 0] = bx0; wbox[wave * 4 + 1] = bx1;
@@ -357,7 +383,11 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
                 const float4 b = kbox[t];  // (xmin, xmax, ymin, ymax); empty tile = (+inf, -inf, ..)
                 const float dx = fmaxf(0.0f, fmaxf(b.x - qx1, qx0 - b.y));
                 const float dy = fmaxf(0.0f, fmaxf(b.z - qy1, qy0 - b.w));
-                keep = fmaf(dy, dy, dx * dx) <= skip_d2;
+                const float d2 = fmaf(dy, dy, dx * dx);
+                keep = d2 <= skip_d2;
+                // largest possible contribution of tile t to a V entry of row block I1-1
+                if (keep && lgn_I) keep = fmaf(cexp, d2 * 1.001f, lgn_I[t]) > lg_tau_I;
+                if (!keep && mean_block) keep = d2 <= skip_d2_mean;
             }
             const unsigned long long bal = __ballot(keep);
             const int before = __popcll(bal & ((1ull << lane) - 1ull));
@@ -703,6 +733,14 @@ hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t 
     return hipGetLastError();
 }
 
+hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float *lgn) {
+    const int64_t nI = npad / kBM;
+    const int64_t t0 = tile_start(I0), t1 = tile_start(nI);
+    if (t1 <= t0) return hipSuccess;
+    hipLaunchKernelGGL(tile_norm_kernel, dim3((unsigned)(t1 - t0)), dim3(kBM), 0, s, aug, t0, lgn);
+    return hipGetLastError();
+}
+
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d) {
     hipLaunchKernelGGL(widen_sub_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, v, n, d);
     return hipGetLastError();
@@ -720,16 +758,18 @@ hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int6
 }
 
 hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox, int64_t npad,
-                          const float *qx, const float *qy, int64_t m, int64_t ldp, float ell, float m0, int skip_log2,
-                          float *part, float *mean, unsigned long long *tiles_done, int variant, int row_chunk) {
+                          const float *qx, const float *qy, int64_t m, int64_t ldp, float ell, float m0,
+                          const SkipPlan &skip, float *part, float *mean, unsigned long long *tiles_done, int variant,
+                          int row_chunk) {
     const int nI = (int)(npad / kBM);
     const int64_t nQ = (m + kBN - 1) / kBN;
     const double ce = -1.0 / (2.0 * (double)ell * (double)ell * 0.69314718055994530942);
     const float cexp = (float)ce;
-    // k-tiles farther than this squared distance give c*d^2 < -skip_log2, i.e.
-    // every K* entry < 2^-skip_log2 (0.1% margin over the kernel's rounding);
-    // skip_log2 >= 150 means every such entry is exactly +0.0 in f32
-    const float skip_d2 = skip_log2 > 0 ? (float)((double)skip_log2 / -ce * 1.001) : -1.0f;
+    // k-tiles farther than this squared distance give c*d^2 < -L, i.e.
+    // every K* entry < 2^-L (0.1% margin over the kernel's rounding);
+    // L >= 150 means every such entry is exactly +0.0 in f32
+    const float skip_d2 = skip.L > 0 ? (float)((double)skip.L / -ce * 1.001) : -1.0f;
+    const float skip_d2_mean = skip.L > 0 && skip.L_mean > skip.L ? (float)((double)skip.L_mean / -ce * 1.001) : skip_d2;
     // Row blocks per workgroup (chunk).  Default 1: the grid is row-block
     // major, so the workgroups running at any moment all read row block I's
     // A tiles and share them in L2 -- 18 GB of HBM fetch per C4 sweep,
@@ -741,7 +781,8 @@ hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, 
     if (G > kMaxChunk) return hipErrorInvalidValue;
     const int64_t blocks = nQ * nC;
     if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-#define SBO_PREDICT_ARGS aug, kcoord, kbox, nI, nC, G, qx, qy, m, ldp, cexp, skip_d2, m0, part, mean, tiles_done
+#define SBO_PREDICT_ARGS aug, kcoord, kbox, nI, nC, G, qx, qy, m, ldp, cexp, skip_d2, skip_d2_mean, skip.lgn, \
+        skip.lg_tau_v, m0, part, mean, tiles_done
     switch (variant) {
         case 1: hipLaunchKernelGGL((predict_kernel<double>), dim3((unsigned)blocks), dim3(kPredictThreads), 0, s, SBO_PREDICT_ARGS); break;
         default: hipLaunchKernelGGL((predict_kernel<float>), dim3((unsigned)blocks), dim3(kPredictThreads), 0, s, SBO_PREDICT_ARGS); break;

@@ -309,17 +309,25 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, ld, n, npad, 0, sf2, ctx->x.as<float>(), ctx->y.as<float>(),
                                          alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
     }
-    // Error budget of the K* tile cutoff (SBO_OPT_TILE_SKIP = -1, auto): a
-    // dropped block has every entry < 2^-L, so each V_i moves by at most
-    // 2^-L max_i |A_i|_1 and each mean by at most 2^-L |sf2 alpha|_1.  With
-    // |V|_2 <= sf2^(1/2), |d sigma^2| <= 2 sf2^(1/2) sqrt(N) max|dV_i|.  L is the
-    // smallest exponent that keeps both below 2^-B of sf2 / sf2^(1/2), B =
-    // SBO_OPT_SKIP_BUDGET.
-    // Rows of earlier row blocks are unchanged by an append: only the repacked
-    // row blocks are re-measured.
+    // Error budget of the automatic K* tile cutoff (SBO_OPT_TILE_SKIP = -1),
+    // B = SBO_OPT_SKIP_BUDGET.  For a V entry: |dsigma^2| <= 2 sf2^(1/2)
+    // sqrt(N) max|dV_i| (|V|_2 <= sf2^(1/2)), so each V_i may move by
+    // tau_v = 2^-B sf2^(1/2) / (2 sqrt(N)).  Half of it goes to tiles whose
+    // every K* entry is below 2^-L (moves V_i by at most 2^-L |A_i|_1 <=
+    // 2^-L max_i |A_i|_1); the other half to tiles dropped by the tile-norm
+    // test: a row block I keeps tile t only if n_It 2^(c d^2) exceeds
+    // (tau_v/2) / 4(I+1), n_It = the tile's largest row sum of |A| -- far
+    // from row block I's own points A decays by orders of magnitude, so most
+    // (row block, query block) pairs that are far apart run no tile at all.
+    // The mean (last row block) drops only tiles below 2^-L_mean, with
+    // 2^-L_mean |sf2 alpha|_1 <= 2^-B sf2^(1/2).  Rows of earlier row blocks
+    // are unchanged by an append: only the repacked row blocks are measured.
     {
         SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)npad));
         SBO_HIP(sbo::launch_row_l1(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->scratch.as<double>()));
+        SBO_HIP(grow_keep(ctx, ctx->tile_lgn, sizeof(float) * (size_t)sbo::total_tiles(nI),
+                          sizeof(float) * old_tiles));
+        SBO_HIP(sbo::launch_tile_norms(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->tile_lgn.as<float>()));
         const int64_t r0 = I0 * sbo::kBM;
         std::vector<double> rl1((size_t)(npad - r0));
         std::vector<float> ha((size_t)n);
@@ -334,10 +342,14 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         for (float v : ha) al1 += std::fabs((double)v);
         ctx->alpha_l1 = al1 * sf2;
         const double tol = std::ldexp(1.0, -ctx->skip_budget), sf = std::sqrt(sf2);
-        const double need_v = 2.0 * std::sqrt((double)n) * ctx->max_row_l1 / (tol * sf);
-        const double need_m = ctx->alpha_l1 / (tol * sf);
-        const double l2 = std::log2(std::max({need_v, need_m, 1.0}));
-        ctx->auto_skip_log2 = std::isfinite(l2) ? std::min(160, std::max(24, (int)std::ceil(l2))) : 160;
+        const double tau_v = tol * sf / (2.0 * std::sqrt((double)n)) * 0.99;  // 1 % for the dV^2 term
+        auto cut = [](double need) {
+            const double l2 = std::log2(std::max(need, 1.0));
+            return std::isfinite(l2) ? std::min(160, std::max(16, (int)std::ceil(l2))) : 160;
+        };
+        ctx->auto_skip_log2 = cut(ctx->max_row_l1 / (0.5 * tau_v));
+        ctx->auto_skip_mean_log2 = cut(ctx->alpha_l1 / (tol * sf));
+        ctx->lg_tau_v = (float)std::log2(0.5 * tau_v);
     }
     SBO_HIP(ctx->kbox.reserve(sizeof(float4) * (size_t)(npad / sbo::kBK)));
     SBO_HIP(sbo::launch_tile_boxes(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, npad, ctx->kbox.as<float4>()));
@@ -380,8 +392,16 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     sbo_key *bkeys = ctx->keys.as<sbo_key>();
     // sweep the queries in Morton order (compact 128-query blocks skip more k-tiles)
     const int32_t *perm = nullptr;
-    const int skip_log2 = ctx->skip_log2 < 0 ? ctx->auto_skip_log2 : ctx->skip_log2;
-    if (ctx->query_order && skip_log2 > 0 && m > sbo::kBN) {
+    sbo::SkipPlan plan;
+    if (ctx->skip_log2 < 0) {
+        plan.L = ctx->auto_skip_log2;
+        plan.L_mean = ctx->auto_skip_mean_log2;
+        plan.lgn = ctx->tile_lgn.as<float>();
+        plan.lg_tau_v = ctx->lg_tau_v;
+    } else {
+        plan.L = ctx->skip_log2;
+    }
+    if (ctx->query_order && plan.L > 0 && m > sbo::kBN) {
         const size_t wb = sbo::query_order_bytes(m);
         SBO_HIP(ctx->qwork.reserve(wb));
         int32_t *p = nullptr;
@@ -395,7 +415,7 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         Bracket br(ctx, ctx->ev_predict);
         SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(),
                                     ctx->kbox.as<float4>(), ctx->npad, qx, qy, m, ldp,
-                                    (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, skip_log2,
+                                    (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan,
                                     ctx->part.as<float>(), ctx->mean.as<float>(),
                                     ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr,
                                     ctx->kernel_variant, ctx->row_chunk));
@@ -967,7 +987,7 @@ SBO_API sbo_status sbo_subgoal(sbo_ctx *ctx, const double *Dx, const double *Dy,
 // ------------------------------------------------- fitted state, 8(e)
 namespace {
 
-constexpr uint64_t kStateMagic = 0x3153544154534253ull;  // "SBSTATS1"
+constexpr uint64_t kStateMagic = 0x3253544154534253ull;  // "SBSTATS2"
 
 struct StateHeader {
     uint64_t magic;
@@ -975,8 +995,9 @@ struct StateHeader {
     double hyper[4];
     double max_row_l1, alpha_l1;
     float bbox[4];
-    int32_t auto_skip_log2, spatial_order;
-    int64_t off_order, off_aug, off_kcoord, off_kbox, total;
+    int32_t auto_skip_log2, spatial_order, auto_skip_mean_log2;
+    float lg_tau_v;
+    int64_t off_order, off_aug, off_kcoord, off_kbox, off_lgn, total;
 };
 
 StateHeader state_layout(const sbo_ctx *ctx) {
@@ -992,13 +1013,16 @@ StateHeader state_layout(const sbo_ctx *ctx) {
     h.alpha_l1 = ctx->alpha_l1;
     for (int i = 0; i < 4; ++i) h.bbox[i] = ctx->bbox[i];
     h.auto_skip_log2 = ctx->auto_skip_log2;
+    h.auto_skip_mean_log2 = ctx->auto_skip_mean_log2;
+    h.lg_tau_v = ctx->lg_tau_v;
     h.spatial_order = ctx->spatial_order;
     const int64_t nt = ctx->npad / sbo::kBK;
     h.off_order = 256;
     h.off_aug = sbo::round_up(h.off_order + 8 * h.n, 256);
     h.off_kcoord = sbo::round_up(h.off_aug + 4 * sbo::total_tiles(ctx->npad / sbo::kBM) * sbo::kTileFloats, 256);
     h.off_kbox = sbo::round_up(h.off_kcoord + 4 * nt * 3 * sbo::kBK, 256);
-    h.total = sbo::round_up(h.off_kbox + 16 * nt, 256);
+    h.off_lgn = sbo::round_up(h.off_kbox + 16 * nt, 256);
+    h.total = sbo::round_up(h.off_lgn + 4 * sbo::total_tiles(ctx->npad / sbo::kBM), 256);
     return h;
 }
 
@@ -1030,6 +1054,8 @@ SBO_API sbo_status sbo_export_state(sbo_ctx *ctx, void *dev_buf, int64_t cap) {
                            hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipMemcpyAsync(b + h.off_kbox, ctx->kbox.as<void>(), 16 * (size_t)nt, hipMemcpyDeviceToDevice,
                            ctx->stream));
+    SBO_HIP(hipMemcpyAsync(b + h.off_lgn, ctx->tile_lgn.as<void>(),
+                           4 * (size_t)sbo::total_tiles(ctx->npad / sbo::kBM), hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));  // the header and order live on this host stack
     return SBO_OK;
 }
@@ -1052,6 +1078,7 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
     SBO_HIP(ctx->aug.reserve(aug_bytes));
     SBO_HIP(ctx->kcoord.reserve(4 * (size_t)nt * 3 * sbo::kBK));
     SBO_HIP(ctx->kbox.reserve(16 * (size_t)nt));
+    SBO_HIP(ctx->tile_lgn.reserve(4 * (size_t)sbo::total_tiles(h.npad / sbo::kBM)));
     ctx->order.resize((size_t)h.n);
     SBO_HIP(hipMemcpyAsync(ctx->order.data(), b + h.off_order, 8 * (size_t)h.n, hipMemcpyDeviceToHost, ctx->stream));
     SBO_HIP(hipMemcpyAsync(ctx->aug.as<void>(), b + h.off_aug, aug_bytes, hipMemcpyDeviceToDevice, ctx->stream));
@@ -1059,6 +1086,8 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
                            hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipMemcpyAsync(ctx->kbox.as<void>(), b + h.off_kbox, 16 * (size_t)nt, hipMemcpyDeviceToDevice,
                            ctx->stream));
+    SBO_HIP(hipMemcpyAsync(ctx->tile_lgn.as<void>(), b + h.off_lgn, 4 * (size_t)sbo::total_tiles(h.npad / sbo::kBM),
+                           hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
     ctx->n = h.n;
     ctx->npad = h.npad;
@@ -1067,6 +1096,8 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
     ctx->alpha_l1 = h.alpha_l1;
     for (int i = 0; i < 4; ++i) ctx->bbox[i] = h.bbox[i];
     ctx->auto_skip_log2 = h.auto_skip_log2;
+    ctx->auto_skip_mean_log2 = h.auto_skip_mean_log2;
+    ctx->lg_tau_v = h.lg_tau_v;
     ctx->spatial_order = h.spatial_order;
     ctx->fitted = true;
     return SBO_OK;

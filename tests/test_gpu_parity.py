@@ -388,10 +388,14 @@ def test_row_chunk_and_outer_variant(mapper):
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
     gm.fit(wl.x, wl.y, wl.obs)
     res = {}
+    # a fixed distance cutoff: the tile-norm test of the auto cutoff is per row
+    # block, so chunks of several row blocks keep a (harmless) superset there
+    gm.set_option(N.SBO_OPT_TILE_SKIP, 40)
     for chunk in (0, 1, 3, 20):
         gm.set_option(N.SBO_OPT_ROW_CHUNK, chunk)
         res[chunk] = gm.predict(wl.qx, wl.qy)
     gm.set_option(N.SBO_OPT_ROW_CHUNK, 0)
+    gm.set_option(N.SBO_OPT_TILE_SKIP, -1)
     for chunk in (1, 3, 20):
         assert np.array_equal(res[chunk][0], res[0][0]) and np.array_equal(res[chunk][1], res[0][1])
     gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 1)
