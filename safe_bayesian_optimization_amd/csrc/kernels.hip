@@ -150,23 +150,39 @@ __global__ __launch_bounds__(kBM) void row_l1_kernel(const float *__restrict__ a
     atomicAdd(row_l1 + I * kBM + r, s);
 }
 
-// Per packed tile: log2 of the largest row sum of |A| over its 64 k (one
-// workgroup per tile, thread r = row r).
+// Per packed tile: log2 of a bound on the tile's 2-norm gain, nu with
+// |A_It k|_2 <= nu max|k| for every 64-vector k:  nu = min(16 max_r |A_r|_1,
+// 8 |A_It|_F)  (|.|_2 <= sqrt(256) |.|_inf, resp. |A k|_2 <= |A|_F |k|_2 and
+// |k|_2 <= 8 max|k|).  One workgroup per tile, thread r = row r, f64 sums.
 __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
                                                         float *__restrict__ lgn) {
-    __shared__ double red[kBM / 64];
+    __shared__ double red[2][kBM / 64];
     const int64_t tile = t0 + blockIdx.x;
     const float *t = aug + tile * kTileFloats;
     const int r = threadIdx.x;
-    double s = 0.0;
-    for (int k = 0; k < kBK; ++k) s += fabs((double)t[tile_offset(k, r)]);
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < kBK; ++k) {
+        const double a = (double)t[tile_offset(k, r)];
+        s += fabs(a);
+        q = fma(a, a, q);
+    }
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s = fmax(s, __shfl_xor(s, o));
-    if ((r & 63) == 0) red[r >> 6] = s;
+    for (int o = 32; o >= 1; o >>= 1) {
+        s = fmax(s, __shfl_xor(s, o));
+        q += __shfl_xor(q, o);
+    }
+    if ((r & 63) == 0) {
+        red[0][r >> 6] = s;
+        red[1][r >> 6] = q;
+    }
     __syncthreads();
     if (r == 0) {
-        for (int w = 1; w < kBM / 64; ++w) s = fmax(s, red[w]);
-        lgn[tile] = s > 0.0 ? (float)log2(s) : -1000.0f;
+        for (int w = 1; w < kBM / 64; ++w) {
+            s = fmax(s, red[0][w]);
+            q += red[1][w];
+        }
+        const double nu = fmin(16.0 * s, 8.0 * sqrt(q));
+        lgn[tile] = nu > 0.0 ? (float)log2(nu) + 1e-5f : -1000.0f;  // rounded up
     }
 }
 
@@ -243,6 +259,10 @@ constexpr int kMaxChunk = 128;   // row blocks per workgroup chunk
 constexpr int kPredictWaves = kBN / 16;
 constexpr int kPredictThreads = 64 * kPredictWaves;
 constexpr int kSmemFloats = 2 * kStageFloats + kMaxList + 4 * kPredictWaves + kPredictWaves + kMaxChunk;
+constexpr int kBudgetFloor = 40;        // bounds below 2^-40 of the budget share bin 0
+constexpr int kBinsPerBit = 4;
+constexpr int kBudgetBins = kBudgetFloor * kBinsPerBit + 2;
+static_assert(kBudgetBins * 8 <= kStageFloats * 4, "budget bins alias stage 0");
 constexpr int kSteps = kBK / 4;          // 16x16x4 k steps per tile
 constexpr int kRowBlocks = kBM / 16;     // 16-row MFMA blocks per wave
 
@@ -359,15 +379,17 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     const int *list = nullptr;
     if (skip_d2 > 0.0f && nkb <= kMaxList) {
         const bool mean_block = (I1 == nI);  // the chunk holding the last row block also accumulates the mean
-        const float lg_tau_I = lg_tau_v - __log2f((float)nkb) - 0.05f;  // budget share per tile (5 % slack)
-        // tile-norm test per row block: one row block per workgroup only (a
-        // chunk shares one list, and the norms differ between its row blocks)
+        // budgeted test (one row block per workgroup only: a chunk shares one
+        // list, and the norms differ between its row blocks)
         const float *lgn_I = (lgn && I1 - I0 == 1) ? lgn + tile_start(I0) : nullptr;
         const float bx0 = wave_min(xq), bx1 = wave_max(xq), by0 = wave_min(yq), by1 = wave_max(yq);
         if (lane == 0) {
             wbox[wave * 4 + 0] = bx0; wbox[wave * 4 + 1] = bx1;
             wbox[wave * 4 + 2] = by0; wbox[wave * 4 + 3] = by1;
         }
+        unsigned long long *bins = reinterpret_cast<unsigned long long *>(smem);  // stage 0 is free until the sweep
+        if (lgn_I)
+            for (int i = tid; i < kBudgetBins; i += kPredictThreads) bins[i] = 0ull;
         __syncthreads();
         float qx0 = wbox[0], qx1 = wbox[1], qy0 = wbox[2], qy1 = wbox[3];
 #pragma unroll
@@ -375,18 +397,73 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
             qx0 = fminf(qx0, wbox[w * 4 + 0]); qx1 = fmaxf(qx1, wbox[w * 4 + 1]);
             qy0 = fminf(qy0, wbox[w * 4 + 2]); qy1 = fmaxf(qy1, wbox[w * 4 + 3]);
         }
+        auto box_d2 = [&](int t) {
+            const float4 b = kbox[t];  // (xmin, xmax, ymin, ymax); empty tile = (+inf, -inf, ..)
+            const float dx = fmaxf(0.0f, fmaxf(b.x - qx1, qx0 - b.y));
+            const float dy = fmaxf(0.0f, fmaxf(b.z - qy1, qy0 - b.w));
+            return fmaf(dy, dy, dx * dx);
+        };
+        // log2 of tile t's largest possible share of |dV_I|_2, relative to the
+        // row block's budget, and its budget bin (0: negligible, kBudgetBins-1:
+        // over budget on its own, never dropped)
+        auto bin_of = [&](float d2, int t, float &rel) {
+            rel = fmaf(cexp, d2 * 1.001f, lgn_I[t]) - lg_tau_v + 0.01f;
+            const float f = (rel + (float)kBudgetFloor) * (float)kBinsPerBit + 1.0f;
+            return f < 0.0f ? 0 : (f >= (float)(kBudgetBins - 1) ? kBudgetBins - 1 : (int)f);
+        };
+        int drop_max = -1;  // budget bins 0..drop_max are dropped
+        if (lgn_I) {
+            // greedy, smallest bins first: the largest prefix of bins whose
+            // summed bounds (fixed point 2^32 = the budget, each term rounded
+            // up, integer adds = order-independent) stay within the budget
+            for (int t = tid; t < nkb; t += kPredictThreads) {
+                float rel;
+                const int bi = bin_of(box_d2(t), t, rel);
+                if (bi < kBudgetBins - 1)
+                    atomicAdd(bins + bi, (unsigned long long)ceilf(exp2f(rel + 32.0f) * 1.0001f) + 1ull);
+            }
+            __syncthreads();
+            if (wave == 0) {
+                constexpr int per = (kBudgetBins + 63) / 64;
+                unsigned long long v[per], run = 0;
+#pragma unroll
+                for (int j = 0; j < per; ++j) {
+                    const int i = lane * per + j;
+                    v[j] = i < kBudgetBins - 1 ? bins[i] : (1ull << 40);
+                    run += v[j];
+                }
+                unsigned long long incl = run;  // inclusive scan over lanes
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const unsigned long long u = __shfl_up(incl, o);
+                    if (lane >= o) incl += u;
+                }
+                unsigned long long pre = incl - run;
+                int ok = 0;
+#pragma unroll
+                for (int j = 0; j < per; ++j) {
+                    pre += v[j];
+                    ok += pre <= (1ull << 32) ? 1 : 0;
+                }
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) ok += __shfl_xor(ok, o);
+                if (lane == 0) wcnt[0] = ok - 1;
+            }
+            __syncthreads();
+            drop_max = wcnt[0];
+        }
         int base = 0;
         for (int t0 = 0; t0 < nkb; t0 += kPredictThreads) {
             const int t = t0 + tid;
             bool keep = false;
             if (t < nkb) {
-                const float4 b = kbox[t];  // (xmin, xmax, ymin, ymax); empty tile = (+inf, -inf, ..)
-                const float dx = fmaxf(0.0f, fmaxf(b.x - qx1, qx0 - b.y));
-                const float dy = fmaxf(0.0f, fmaxf(b.z - qy1, qy0 - b.w));
-                const float d2 = fmaf(dy, dy, dx * dx);
-                keep = d2 <= skip_d2;
-                // largest possible contribution of tile t to a V entry of row block I1-1
-                if (keep && lgn_I) keep = fmaf(cexp, d2 * 1.001f, lgn_I[t]) > lg_tau_I;
+                const float d2 = box_d2(t);
+                if (lgn_I) {
+                    float rel;
+                    keep = bin_of(d2, t, rel) > drop_max;
+                } else {
+                    keep = d2 <= skip_d2;
+                }
                 if (!keep && mean_block) keep = d2 <= skip_d2_mean;
             }
             const unsigned long long bal = __ballot(keep);

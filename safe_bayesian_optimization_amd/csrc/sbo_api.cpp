@@ -310,15 +310,17 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                                          alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
     }
     // Error budget of the automatic K* tile cutoff (SBO_OPT_TILE_SKIP = -1),
-    // B = SBO_OPT_SKIP_BUDGET.  For a V entry: |dsigma^2| <= 2 sf2^(1/2)
-    // sqrt(N) max|dV_i| (|V|_2 <= sf2^(1/2)), so each V_i may move by
-    // tau_v = 2^-B sf2^(1/2) / (2 sqrt(N)).  Half of it goes to tiles whose
-    // every K* entry is below 2^-L (moves V_i by at most 2^-L |A_i|_1 <=
-    // 2^-L max_i |A_i|_1); the other half to tiles dropped by the tile-norm
-    // test: a row block I keeps tile t only if n_It 2^(c d^2) exceeds
-    // (tau_v/2) / 4(I+1), n_It = the tile's largest row sum of |A| -- far
-    // from row block I's own points A decays by orders of magnitude, so most
-    // (row block, query block) pairs that are far apart run no tile at all.
+    // B = SBO_OPT_SKIP_BUDGET: sigma^2 = sf2 - |V|^2 moves by at most
+    // 2 |V|_2 |dV|_2 + |dV|_2^2 with |V|_2 <= sf2^(1/2), so |dV(q)|_2 <=
+    // tau2 = 2^-B sf2^(1/2) / 2 (less 1 %) keeps it below 2^-B sf2.
+    //  - tile-norm test (one row block per workgroup): row block I may lose
+    //    |dV_I|_2 <= tau2 / sqrt(nI); a dropped tile t costs at most
+    //    nu_It K*max(t), nu_It = min(16 max row sum, 8 |A_It|_F) (the tile's
+    //    2-norm gain bound), and the kernel drops the smallest first.
+    //  - distance cutoff (row-block chunks, and the reported L): every K*
+    //    entry of a dropped tile is below 2^-L, so each V_i moves by at most
+    //    2^-L max_i |A_i|_1 and |dV|_2 by sqrt(N) times that; L keeps it
+    //    below tau2.
     // The mean (last row block) drops only tiles below 2^-L_mean, with
     // 2^-L_mean |sf2 alpha|_1 <= 2^-B sf2^(1/2).  Rows of earlier row blocks
     // are unchanged by an append: only the repacked row blocks are measured.
@@ -342,14 +344,14 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         for (float v : ha) al1 += std::fabs((double)v);
         ctx->alpha_l1 = al1 * sf2;
         const double tol = std::ldexp(1.0, -ctx->skip_budget), sf = std::sqrt(sf2);
-        const double tau_v = tol * sf / (2.0 * std::sqrt((double)n)) * 0.99;  // 1 % for the dV^2 term
+        const double tau2 = tol * sf / 2.0 * 0.99;  // 1 % for the dV^2 term
         auto cut = [](double need) {
             const double l2 = std::log2(std::max(need, 1.0));
             return std::isfinite(l2) ? std::min(160, std::max(16, (int)std::ceil(l2))) : 160;
         };
-        ctx->auto_skip_log2 = cut(ctx->max_row_l1 / (0.5 * tau_v));
+        ctx->auto_skip_log2 = cut(ctx->max_row_l1 * std::sqrt((double)n) / tau2);
         ctx->auto_skip_mean_log2 = cut(ctx->alpha_l1 / (tol * sf));
-        ctx->lg_tau_v = (float)std::log2(0.5 * tau_v);
+        ctx->lg_tau_v = (float)std::log2(tau2 / std::sqrt((double)nI));
     }
     SBO_HIP(ctx->kbox.reserve(sizeof(float4) * (size_t)(npad / sbo::kBK)));
     SBO_HIP(sbo::launch_tile_boxes(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, npad, ctx->kbox.as<float4>()));

@@ -98,8 +98,8 @@ struct sbo_ctx {
     int skip_log2 = -1;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-L (-1: auto)
     int auto_skip_log2 = 160;    // auto K* cutoff for V (half the budget), computed at fit (refresh_operand)
     int auto_skip_mean_log2 = 160;  // auto cutoff the last row block keeps for the mean
-    float lg_tau_v = -1000.0f;   // log2 of the V budget share of the tile-norm test (before / T_I)
-    sbo::DevBuf tile_lgn;        // per packed tile: log2 max_row sum_k |A[row][k]| (auto cutoff)
+    float lg_tau_v = -1000.0f;   // log2 of each row block's |dV_I|_2 budget (tile-norm test)
+    sbo::DevBuf tile_lgn;        // per packed tile: log2 of its 2-norm gain bound (auto cutoff)
     int skip_budget = 22;        // SBO_OPT_SKIP_BUDGET: the auto cutoff keeps the skip error below 2^-B
     double max_row_l1 = 0.0;     // max_i sum_j |A_ij|, A = sf2 L^-1
     double alpha_l1 = 0.0;       // sum_j |sf2 alpha_j|
@@ -159,13 +159,14 @@ hipError_t launch_widen(hipStream_t s, const float *src, int64_t ld_src, int64_t
                         double *dst, int64_t ld_dst);
 // Predictive sweep: part[I][q] = sum over rows of block I of (sf2 L^-1 k_q)^2,
 // mean[q] = m0 + sf2 alpha^T k_q.
-// Tile cutoff (SkipPlan): a workgroup (row block I, query block) drops k-tile
-// t when every K* entry is below 2^-L (the box distance), and -- with a
-// tile-norm table -- also when lgn[t] + log2 K*max <= lg_tau_v - log2(4(I+1)),
-// i.e. the tile's largest possible contribution to any V entry of the row
-// block is below its share of the budget; the last row block (which also
-// accumulates the mean) keeps every tile within 2^-L_mean.  L >= 150 drops
-// only exact zeros (bitwise identical to the dense sweep); L = 0: dense.
+// Tile cutoff (SkipPlan).  With a tile-norm table (automatic cutoff, one row
+// block per workgroup) a workgroup (row block I, query block) bounds tile t's
+// share of |dV_I(q)|_2 by 2^(lgn[t]) * K*max(box distance) and drops tiles
+// smallest bound first while the dropped bounds sum to at most 2^lg_tau_v
+// (binned, fixed point: order-independent); otherwise it drops tile t when
+// every K* entry is below 2^-L.  The last row block (which also accumulates
+// the mean) keeps every tile within 2^-L_mean.  L >= 150 drops only exact
+// zeros (bitwise identical to the dense sweep); L = 0: dense.
 // tiles_done (may be null): += number of (BM x BN x BK) tiles multiplied.
 struct SkipPlan {
     int L = 0;                  // 0: dense
@@ -177,8 +178,8 @@ hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, 
                           int64_t npad, const float *qx, const float *qy, int64_t m, int64_t ldp,
                           float ell, float m0, const SkipPlan &skip, float *part, float *mean,
                           unsigned long long *tiles_done, int variant, int row_chunk);
-// lgn[tile_start(I) + t] = log2 max_{rows r of I} sum_{k in t} |A[r][k]| (f64 sums) for
-// row blocks I >= I0 (-1000 for an all-zero tile).
+// lgn[tile_start(I) + t] = log2 min(16 max_r |A_It[r]|_1, 8 |A_It|_F) (f64 sums,
+// rounded up) for row blocks I >= I0 (-1000 for an all-zero tile).
 hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float *lgn);
 // d = (double)in - v;  out = (float)d
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);
