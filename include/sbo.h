@@ -227,10 +227,10 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * cross-tile accumulator (default); 1 = f64 cross-tile accumulator (same
  * accuracy at N = 16384, 5 % slower: tools/variant_accuracy.py). */
 #define SBO_OPT_KERNEL_VARIANT 5
-/* SBO_OPT_ROW_CHUNK: row blocks (256 rows each) one predictive workgroup
- * walks for its 128 queries; 0 = default (1: row-block-major grid, A tiles
- * shared in L2 by the concurrently running workgroups). */
-#define SBO_OPT_ROW_CHUNK 6
+/* SBO_OPT_SWEEP_GROUPS: workgroups of the persistent predictive sweep, each
+ * walking one tile-balanced range of the tick's plan; 0 = default (one per
+ * CU).  Results do not depend on it (bitwise). */
+#define SBO_OPT_SWEEP_GROUPS 6
 /* SBO_OPT_SKIP_BUDGET (B in [10, 60], default 22): the automatic K* cutoff
  * (SBO_OPT_TILE_SKIP = -1) keeps its worst-case error below 2^-B sf2 on any
  * variance and 2^-B sf2^(1/2) on any mean (2^-22 = 2.4e-7: under 3 % of the

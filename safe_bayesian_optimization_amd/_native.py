@@ -13,7 +13,7 @@ import os
 import subprocess
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "lib", "libsbo.so")
+LIB_PATH = os.environ.get("SBO_LIB") or os.path.join(_PKG, "lib", "libsbo.so")  # SBO_LIB: instrumented builds (tools/)
 
 SBO_DEVICE_PTRS = 0x1
 SBO_ASYNC = 0x2
@@ -37,7 +37,7 @@ SBO_OPT_SPATIAL_ORDER = 2
 SBO_OPT_TILE_SKIP = 3
 SBO_OPT_QUERY_ORDER = 4
 SBO_OPT_KERNEL_VARIANT = 5
-SBO_OPT_ROW_CHUNK = 6
+SBO_OPT_SWEEP_GROUPS = 6
 SBO_OPT_SKIP_BUDGET = 7
 
 

@@ -13,6 +13,9 @@
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit,
 // so the f64 acquisition arithmetic is the node's plain IEEE double sequence.
 #include <algorithm>
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
 
 #include "sbo_internal.hpp"
 
@@ -118,12 +121,18 @@ __global__ void widen_kernel(const float *__restrict__ src, int64_t lds, int64_t
     if (i < m) dst[i + j * ldd] = (!lower || i >= j) ? (double)src[i + j * lds] : 0.0;
 }
 
+// Per k-tile coordinates, step-major per lane group: k = 4p + g is stored at
+// g*16 + p (x, then y, then sf2*alpha), so lane group g reads the values of
+// consecutive k steps p, p+1 as one 8-byte pair.
+__device__ __forceinline__ int kcoord_slot(int o) { return (o & 3) * 16 + (o >> 2); }
+
 __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__restrict__ y,
                                    const float *__restrict__ alpha, int64_t n, int64_t npad,
                                    float sf2, float *__restrict__ kcoord) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= npad) return;
-    const int64_t t = k / kBK, o = k % kBK;
+    const int64_t t = k / kBK;
+    const int o = kcoord_slot((int)(k % kBK));
     float *c = kcoord + t * (3 * kBK);
     const bool in = k < n;
     c[o] = in ? x[k] : x[0];
@@ -212,14 +221,14 @@ __global__ void tile_box_kernel(const float *__restrict__ x, const float *__rest
 }
 
 // ---------------------------------------------------------- a3+a4 predict
-// Workgroup (qb, chunk): the BN = 128 queries [qb*BN, qb*BN+BN) against the
-// row blocks I of one chunk, each I = rows [I*BM, I*BM+BM) of A = sf2 L^-1
-// (BM = 256).  Eight waves, two per SIMD; wave w owns the 16 queries
-// qb*BN + 16w + (l&15) and ALL 256 rows of the current row block as sixteen
-// 16-row blocks: sixteen accumulators of v_mfma_f32_16x16x4_f32 (exact f32,
-// 64 FLOP/clk/SIMD).  The B operand K*[k][q] is generated per lane -- lane l
-// holds k = l>>4, q = l&15, exactly the MFMA B-fragment map -- so K* never
-// touches LDS or HBM.
+// Work item (I, qb): the BN = 128 queries [qb*BN, qb*BN+BN) against row
+// block I = rows [I*BM, I*BM+BM) of A = sf2 L^-1 (BM = 256), over the k-tiles
+// t < 4(I+1) the tick's plan keeps.  A workgroup has eight waves, two per
+// SIMD; wave w owns the 16 queries qb*BN + 16w + (l&15) and ALL 256 rows as
+// sixteen 16-row blocks: sixteen accumulators of v_mfma_f32_16x16x4_f32
+// (exact f32, 64 FLOP/clk/SIMD).  The B operand K*[k][q] is generated per
+// lane -- lane l holds k = l>>4, q = l&15, exactly the MFMA B-fragment map --
+// so K* never touches LDS or HBM.
 //
 // Why this shape: on gfx950 the VALU work of a wave does not overlap the
 // matrix pipe (measured, tools/mfma_probe.hip: four 32x32x2 MFMAs per K*
@@ -233,36 +242,62 @@ __global__ void tile_box_kernel(const float *__restrict__ x, const float *__rest
 // buffered, one barrier per stage).  tile_offset puts the four A operands of
 // row blocks 4jj..4jj+3 of one (k, row&15) side by side, so a k step is four
 // conflict-free ds_read_b128 per lane.  The mean rides along in the last row
-// block (every k visited) as an f64 FMA per k step.
+// block (every kept k visited) as an f64 FMA per k step.
 //
-// Tile skipping: a k-tile whose bounding box is farther from the
-// workgroup's query bounding box than the cutoff radius contributes K* <
-// 2^-L to every product (exactly +0.0 for L >= 150: c*d^2 < -150 underflows).
-// Each workgroup compacts, once, the ascending list of k-tiles its queries
-// need; row block I multiplies the prefix of that list below its diagonal
-// (t < 4(I+1)), so the surviving accumulation order is the dense order and
-// results are bitwise identical to the dense sweep at L >= 150.  The cutoff
-// L comes from an error budget (sbo_api.cpp).  One workgroup walks all row
-// blocks of its chunk as one flat stream of (row block, k-tile) items, so
-// the list is built once per chunk, the LDS-DMA pipeline runs across row
-// block boundaries, and row blocks with an empty prefix cost nothing.
+// Plan, then sweep.  plan_count_kernel decides, per work item, which k-tiles
+// run (error-budgeted, see below) and counts them; a scan turns the counts
+// into offsets; plan_write_kernel writes the kept tile indices (ascending)
+// and a descriptor per non-empty item, in row-block-major order, heaviest
+// row block first; plan_seg_kernel cuts that item list into one contiguous,
+// tile-balanced range per workgroup.  predict_kernel is persistent (one
+// workgroup per CU): it walks its range as one flat stream of (item, tile)
+// steps, so the LDS-DMA pipeline runs across item boundaries, and neither
+// the selection nor empty items nor workgroup launches cost sweep time
+// (measured on a launch-per-item kernel: selection 5.9 %, empty items 3 %,
+// launch gaps ~6 % of the C4 sweep).
+//
+// Tile selection: with the tile-norm table (automatic cutoff) each item
+// bounds tile t's share of |dV_I(q)|_2 by nu_It * K*max(box distance) and
+// drops tiles smallest bound first while the dropped bounds stay within the
+// row block's budget (binned, fixed point: order-independent); otherwise a
+// tile whose bounding box is farther from the query block's box than the
+// cutoff radius (every K* < 2^-L) is dropped.  The last row block also keeps
+// every tile within the mean's cutoff.  Kept tiles run in ascending t, the
+// dense order, so L >= 150 (only exact zeros dropped) is bitwise identical
+// to the dense sweep.
 //
 // Accuracy: a single f32 MFMA chain over all N training points accumulates
 // ~sqrt(N) roundings on large cancelling terms (2.2e-5 normwise variance
 // error at N = 8192, measured).  Each k-tile's chain therefore starts from
 // zero and is added into an outer accumulator; the K* evaluation error
 // (f32 coordinate differences and exp2), amplified by A, dominates what is
-// left (tools/variant_accuracy.py: 7e-6 at N = 16384 for either outer type).
+// left (tools/variant_accuracy.py: 5e-6 at N = 16384 for either outer type).
 constexpr int kStageFloats = kTileFloats + 3 * kBK;
-constexpr int kMaxList = 2048;   // k-tiles a workgroup can list (N <= 131072); beyond: dense
-constexpr int kMaxChunk = 128;   // row blocks per workgroup chunk
+#ifdef SBO_STAMPS
+// diagnostic build only: per-workgroup s_memtime stamps (entry, list built,
+// first stage in, sweep done), HW_ID/XCC_ID, row block and tile count
+constexpr int64_t kStampSlots = 1 << 20;
+__device__ unsigned long long sbo_stamps[kStampSlots * 6];
+}  // namespace
+extern "C" __attribute__((visibility("default"))) int sbo_debug_stamps(void *dst, int64_t slots) {
+    if (slots > kStampSlots) slots = kStampSlots;
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(sbo_stamps), (size_t)slots * 6 * 8, 0, hipMemcpyDeviceToHost);
+}
+namespace {
+#endif
 constexpr int kPredictWaves = kBN / 16;
 constexpr int kPredictThreads = 64 * kPredictWaves;
-constexpr int kSmemFloats = 2 * kStageFloats + kMaxList + 4 * kPredictWaves + kPredictWaves + kMaxChunk;
+constexpr int kDescWindow = 64;          // item descriptors (int4) per 1 KiB LDS window
+constexpr int kListWindow = 512;         // tile indices (u16) per 1 KiB LDS window
+constexpr int kSmemFloats = 2 * kStageFloats + 2 * 256 + 2 * 256;  // stages + 2 desc + 2 list windows
 constexpr int kBudgetFloor = 40;        // bounds below 2^-40 of the budget share bin 0
 constexpr int kBinsPerBit = 4;
 constexpr int kBudgetBins = kBudgetFloor * kBinsPerBit + 2;
-static_assert(kBudgetBins * 8 <= kStageFloats * 4, "budget bins alias stage 0");
+constexpr int kPlanThreads = 256;       // plan kernels: one query block, one row block per wave
+constexpr int kPlanWaves = kPlanThreads / 64;
+constexpr int kPlanD2 = 2048;           // k-tile distances cached in LDS (N <= 131072; beyond: recomputed)
+constexpr int kPlanKeyShift = 40;       // plan key: kept-tile count (low 40 bits) | non-empty (high bits)
+constexpr unsigned long long kPlanCountMask = (1ull << kPlanKeyShift) - 1ull;
 constexpr int kSteps = kBK / 4;          // 16x16x4 k steps per tile
 constexpr int kRowBlocks = kBM / 16;     // 16-row MFMA blocks per wave
 
@@ -274,58 +309,71 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // Software pipeline, pinned with scheduling fences (left alone, the compiler
 // minimises registers by issuing each A read right before its MFMA and then
 // waiting on it): step p first issues the LDS reads of the A operands of
-// step p+1 (four ds_read_b128 = the sixteen row blocks, tile_offset layout)
-// and of the coordinates of step p+2, then evaluates K* of step p+1 from
-// coordinates read one step earlier, beside the sixteen MFMAs of step p.  No
-// MFMA or exp waits on a read issued in its own step.
+// step p+1 (four ds_read_b128 = the sixteen row blocks, tile_offset layout);
+// every even step also reads the coordinate pairs of steps p+4, p+5 and
+// evaluates K* of steps p+2, p+3 as one packed pair (v_pk_add/mul/fma_f32,
+// then two v_exp_f32) beside the sixteen MFMAs of step p.  No MFMA or exp
+// waits on a read issued in its own step.  pc = this lane group's
+// coordinate row (kcoord_slot layout: step p of x at pc[p], y at
+// pc[kBK + p], sf2*alpha at pc[2*kBK + p]).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 kstar_pair(f32x2 x, f32x2 y, float xq, float yq, float cexp) {
+    const f32x2 dx = x - xq, dy = y - yq;
+    const f32x2 d2 = __builtin_elementwise_fma(dy, dy, dx * dx);
+    const f32x2 a = d2 * cexp;
+    f32x2 b;
+    b.x = fast_exp2(a.x);
+    b.y = fast_exp2(a.y);
+    return b;
+}
+
 template <bool MEAN>
 __device__ __forceinline__ void tile_steps(const float4 *__restrict__ pa, const float *__restrict__ pc, float xq,
                                            float yq, float cexp, f32x4 (&acc)[kRowBlocks], double &mu) {
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    const f32x2 *pc2 = reinterpret_cast<const f32x2 *>(pc);
     float4 a_cur[4];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) a_cur[jj] = pa[jj * 1024];
-    float b_cur;
-    {
-        const float dx = pc[0] - xq, dy = pc[kBK] - yq;
-        b_cur = fast_exp2(cexp * fmaf(dy, dy, dx * dx));
-    }
-    float x1 = pc[4], y1 = pc[kBK + 4];
+    f32x2 b_cur = kstar_pair(pc2[0], pc2[kBK / 2], xq, yq, cexp);  // steps 0, 1
+    f32x2 x1 = pc2[1], y1 = pc2[kBK / 2 + 1];                         // steps 2, 3
+    f32x2 b_nxt = b_cur;
 #pragma unroll
     for (int p = 0; p < kSteps; ++p) {
         float4 a_nxt[4];
-        float x2 = x1, y2 = y1;
+        f32x2 x2 = x1, y2 = y1;
         if (p + 1 < kSteps) {
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) a_nxt[jj] = pa[jj * 1024 + (p + 1) * 64];
         }
-        if (p + 2 < kSteps) {
-            x2 = pc[4 * (p + 2)];
-            y2 = pc[kBK + 4 * (p + 2)];
+        if ((p & 1) == 0 && p + 4 < kSteps) {
+            x2 = pc2[(p + 4) / 2];
+            y2 = pc2[kBK / 2 + (p + 4) / 2];
         }
-        const float alpha = MEAN ? pc[2 * kBK + 4 * p] : 0.0f;
+        const float alpha = MEAN ? pc[2 * kBK + p] : 0.0f;
         __builtin_amdgcn_sched_barrier(0);
-        float b_nxt = b_cur;
-        if (p + 1 < kSteps) {
-            const float dx = x1 - xq, dy = y1 - yq;
-            b_nxt = fast_exp2(cexp * fmaf(dy, dy, dx * dx));
-        }
-        if (MEAN) mu = fma((double)alpha, (double)b_cur, mu);
+        if ((p & 1) == 0 && p + 2 < kSteps) b_nxt = kstar_pair(x1, y1, xq, yq, cexp);
+        const float b = (p & 1) ? b_cur.y : b_cur.x;
+        if (MEAN) mu = fma((double)alpha, (double)b, mu);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-            acc[4 * jj + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].x, b_cur, p == 0 ? zero : acc[4 * jj + 0], 0, 0, 0);
-            acc[4 * jj + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].y, b_cur, p == 0 ? zero : acc[4 * jj + 1], 0, 0, 0);
-            acc[4 * jj + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].z, b_cur, p == 0 ? zero : acc[4 * jj + 2], 0, 0, 0);
-            acc[4 * jj + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].w, b_cur, p == 0 ? zero : acc[4 * jj + 3], 0, 0, 0);
+            acc[4 * jj + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].x, b, p == 0 ? zero : acc[4 * jj + 0], 0, 0, 0);
+            acc[4 * jj + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].y, b, p == 0 ? zero : acc[4 * jj + 1], 0, 0, 0);
+            acc[4 * jj + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].z, b, p == 0 ? zero : acc[4 * jj + 2], 0, 0, 0);
+            acc[4 * jj + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[jj].w, b, p == 0 ? zero : acc[4 * jj + 3], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (p + 1 < kSteps) {
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) a_cur[jj] = a_nxt[jj];
         }
-        x1 = x2;
-        y1 = y2;
-        b_cur = b_nxt;
+        if ((p & 1) == 0) {
+            x1 = x2;
+            y1 = y2;
+        } else {
+            b_cur = b_nxt;
+        }
     }
 }
 
@@ -340,186 +388,272 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
-// OT: outer (cross-tile) accumulator type.  Grid: nQ query blocks x nC row
-// block chunks of G row blocks.
+// ---- plan: which k-tiles each work item (I, qb) multiplies
+struct QBox {
+    float x0, x1, y0, y1;
+};
+
+__device__ __forceinline__ float tile_box_d2(const float4 b, const QBox &q) {
+    // b = (xmin, xmax, ymin, ymax); an empty tile (+inf, -inf, ..) is infinitely far
+    const float dx = fmaxf(0.0f, fmaxf(b.x - q.x1, q.x0 - b.y));
+    const float dy = fmaxf(0.0f, fmaxf(b.z - q.y1, q.y0 - b.w));
+    return fmaf(dy, dy, dx * dx);
+}
+
+// Budget bin of a tile whose bound is 2^(lgn_t) * K*max(d2), relative to the
+// row block's budget 2^lg_tau: bin 0 = below 2^-kBudgetFloor of it, bin
+// kBudgetBins-1 = over the whole budget on its own (never dropped).  w = the
+// bound in fixed point (2^32 = the budget), rounded up.
+__device__ __forceinline__ int budget_bin(float d2, float lgn_t, float cexp, float lg_tau, unsigned long long &w) {
+    const float rel = fmaf(cexp, d2 * 1.001f, lgn_t) - lg_tau + 0.01f;
+    const float f = (rel + (float)kBudgetFloor) * (float)kBinsPerBit + 1.0f;
+    const int bi = f < 0.0f ? 0 : (f >= (float)(kBudgetBins - 1) ? kBudgetBins - 1 : (int)f);
+    w = bi < kBudgetBins - 1 ? (unsigned long long)ceilf(exp2f(rel + 32.0f) * 1.0001f) + 1ull : 0ull;
+    return bi;
+}
+
+// Everything the two plan kernels share: the query block's box, the box
+// distance of every k-tile, and the per-item selection rule.
+struct PlanRule {
+    const float4 *kbox;
+    const float *lgn;   // per packed tile log2 gain bound (null: distance test)
+    float cexp, skip_d2, skip_d2_mean, lg_tau;
+    int nI;
+    QBox box;
+    const float *d2s;   // LDS cache of tile distances (t < kPlanD2)
+
+    __device__ __forceinline__ float d2(int t) const { return t < kPlanD2 ? d2s[t] : tile_box_d2(kbox[t], box); }
+
+    // Greedy budget threshold of row block I (wave-wide; bins is wave-private
+    // LDS): the largest prefix of bins, smallest bounds first, whose summed
+    // bounds (integer adds: order-independent) stay within the budget.
+    // Returns the last dropped bin (-1: none).
+    __device__ int threshold(int I, unsigned long long *bins, int lane) const {
+        if (!lgn) return -1;
+        const float *lgn_I = lgn + tile_start(I);
+        const int T = kTilesPerRowBlockStep * (I + 1);
+        for (int i = lane; i < kBudgetBins; i += 64) bins[i] = 0ull;
+        __builtin_amdgcn_wave_barrier();
+        for (int t = lane; t < T; t += 64) {
+            unsigned long long w;
+            const int bi = budget_bin(d2(t), lgn_I[t], cexp, lg_tau, w);
+            if (bi < kBudgetBins - 1) atomicAdd(bins + bi, w);
+        }
+        __builtin_amdgcn_wave_barrier();
+        constexpr int per = (kBudgetBins + 63) / 64;
+        unsigned long long v[per], run = 0;
+#pragma unroll
+        for (int j = 0; j < per; ++j) {
+            const int i = lane * per + j;
+            v[j] = i < kBudgetBins - 1 ? bins[i] : (1ull << 40);
+            run += v[j];
+        }
+        unsigned long long incl = run;  // inclusive scan over lanes
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long u = __shfl_up(incl, o);
+            if (lane >= o) incl += u;
+        }
+        unsigned long long pre = incl - run;
+        int ok = 0;
+#pragma unroll
+        for (int j = 0; j < per; ++j) {
+            pre += v[j];
+            ok += pre <= (1ull << 32) ? 1 : 0;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) ok += __shfl_xor(ok, o);
+        __builtin_amdgcn_wave_barrier();
+        return ok - 1;
+    }
+
+    __device__ __forceinline__ bool keep(int I, int t, int drop_max) const {
+        const float dd = d2(t);
+        bool k;
+        if (lgn) {
+            unsigned long long w;
+            k = budget_bin(dd, lgn[tile_start(I) + t], cexp, lg_tau, w) > drop_max;
+        } else {
+            k = skip_d2 <= 0.0f || dd <= skip_d2;  // skip_d2 <= 0: dense
+        }
+        if (!k && I == nI - 1) k = dd <= skip_d2_mean;  // the mean's own cutoff
+        return k;
+    }
+};
+
+// Query box of block qb (threads 0..127 hold its queries, 128..255 repeat
+// them) and the distance cache.
+__device__ QBox plan_setup(const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t qb,
+                           const float4 *__restrict__ kbox, int nkt, float *d2s, float *red) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t q = qb * kBN + (tid & (kBN - 1));
+    const int64_t qc = q < m ? q : m - 1;
+    const float xq = qx[qc], yq = qy[qc];
+    const float bx0 = wave_min(xq), bx1 = wave_max(xq), by0 = wave_min(yq), by1 = wave_max(yq);
+    if (lane == 0) {
+        red[wave * 4 + 0] = bx0; red[wave * 4 + 1] = bx1;
+        red[wave * 4 + 2] = by0; red[wave * 4 + 3] = by1;
+    }
+    __syncthreads();
+    QBox b = {red[0], red[1], red[2], red[3]};
+#pragma unroll
+    for (int w = 1; w < kPlanWaves; ++w) {
+        b.x0 = fminf(b.x0, red[w * 4 + 0]); b.x1 = fmaxf(b.x1, red[w * 4 + 1]);
+        b.y0 = fminf(b.y0, red[w * 4 + 2]); b.y1 = fmaxf(b.y1, red[w * 4 + 3]);
+    }
+    for (int t = tid; t < nkt && t < kPlanD2; t += kPlanThreads) d2s[t] = tile_box_d2(kbox[t], b);
+    __syncthreads();
+    return b;
+}
+
+// Item index of (I, qb): row-block major, heaviest (last) row block first.
+__device__ __forceinline__ int64_t plan_item(int I, int nI, int64_t nQ, int64_t qb) {
+    return (int64_t)(nI - 1 - I) * nQ + qb;
+}
+
+// Pass 1, one workgroup per query block, one row block per wave at a time:
+// the budget threshold and the kept-tile count of every item.  key packs
+// (count, non-empty) for the scan; empty items get their (exactly zero)
+// outputs here, so the sweep never visits them.
+__global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
+    const float4 *__restrict__ kbox, const float *__restrict__ lgn, int nI, int64_t nQ,
+    const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
+    float skip_d2_mean, float lg_tau, float m0, int64_t ldp, float *__restrict__ part, float *__restrict__ mean,
+    unsigned long long *__restrict__ key, unsigned char *__restrict__ thr) {
+    __shared__ float d2s[kPlanD2];
+    __shared__ float red[4 * kPlanWaves];
+    __shared__ unsigned long long bins[kPlanWaves][kBudgetBins];
+    const int64_t qb = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nkt = kTilesPerRowBlockStep * nI;
+    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s};
+    R.box = plan_setup(qx, qy, m, qb, kbox, nkt, d2s, red);
+    for (int I = wave; I < nI; I += kPlanWaves) {
+        const int T = kTilesPerRowBlockStep * (I + 1);
+        const int drop_max = R.threshold(I, bins[wave], lane);
+        int cnt = 0;
+        for (int t0 = 0; t0 < T; t0 += 64) {
+            const int t = t0 + lane;
+            cnt += __popcll(__ballot(t < T && R.keep(I, t, drop_max)));
+        }
+        const int64_t item = plan_item(I, nI, nQ, qb);
+        if (lane == 0) {
+            key[item] = (unsigned long long)cnt | ((cnt > 0 ? 1ull : 0ull) << kPlanKeyShift);
+            thr[item] = (unsigned char)(drop_max + 1);
+        }
+        if (cnt == 0)
+            for (int j = lane; j < kBN; j += 64) {
+                const int64_t q = qb * kBN + j;
+                if (q < m) {
+                    part[(int64_t)I * ldp + q] = 0.0f;
+                    if (I == nI - 1) mean[q] = m0;
+                }
+            }
+    }
+}
+
+// Pass 2 (after the inclusive scan of key): the kept tile indices of every
+// non-empty item, ascending, at its offset, and its descriptor
+// (I, qb, offset low 32 bits, count | offset high bits << 16).
+__global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
+    const float4 *__restrict__ kbox, const float *__restrict__ lgn, int nI, int64_t nQ,
+    const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
+    float skip_d2_mean, float lg_tau, const unsigned long long *__restrict__ key,
+    const unsigned long long *__restrict__ scan, const unsigned char *__restrict__ thr, int4 *__restrict__ desc,
+    unsigned short *__restrict__ tl) {
+    __shared__ float d2s[kPlanD2];
+    __shared__ float red[4 * kPlanWaves];
+    const int64_t qb = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nkt = kTilesPerRowBlockStep * nI;
+    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s};
+    R.box = plan_setup(qx, qy, m, qb, kbox, nkt, d2s, red);
+    for (int I = wave; I < nI; I += kPlanWaves) {
+        const int64_t item = plan_item(I, nI, nQ, qb);
+        const unsigned long long k = key[item];
+        const int cnt = (int)(k & kPlanCountMask);
+        if (cnt == 0) continue;
+        const unsigned long long ex = scan[item] - k;
+        const uint64_t off = ex & kPlanCountMask;
+        const int64_t ne = (int64_t)(ex >> kPlanKeyShift);
+        const int drop_max = (int)thr[item] - 1;
+        const int T = kTilesPerRowBlockStep * (I + 1);
+        uint64_t base = off;
+        for (int t0 = 0; t0 < T; t0 += 64) {
+            const int t = t0 + lane;
+            const bool kp = t < T && R.keep(I, t, drop_max);
+            const unsigned long long bal = __ballot(kp);
+            if (kp) tl[base + __popcll(bal & ((1ull << lane) - 1ull))] = (unsigned short)t;
+            base += __popcll(bal);
+        }
+        if (lane == 0) desc[ne] = make_int4(I, (int)qb, (int)(uint32_t)off, cnt | (int)((off >> 32) << 16));
+    }
+}
+
+// One thread per sweep workgroup: cut the non-empty item list into P
+// contiguous ranges of about equal tile count (seg[r] .. seg[r+1]).
+__global__ void plan_seg_kernel(const unsigned long long *__restrict__ scan, int64_t n_items,
+                                const int4 *__restrict__ desc, int P, int *__restrict__ seg,
+                                unsigned long long *__restrict__ tiles_done) {
+    const unsigned long long last = scan[n_items - 1];
+    const uint64_t total = last & kPlanCountMask;
+    const int64_t nne = (int64_t)(last >> kPlanKeyShift);
+    for (int w = threadIdx.x; w <= P; w += blockDim.x) {
+        if (w == P) {
+            seg[P] = (int)nne;
+            continue;
+        }
+        const uint64_t target = total * (uint64_t)w / (uint64_t)P;
+        int64_t lo = 0, hi = nne;  // first item whose offset >= target
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            const int4 d = desc[mid];
+            const uint64_t off = (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
+            if (off < target) lo = mid + 1; else hi = mid;
+        }
+        seg[w] = (int)lo;
+    }
+    if (threadIdx.x == 0 && tiles_done) atomicAdd(tiles_done, (unsigned long long)total);
+}
+
+// ---- the sweep (persistent: one workgroup per CU)
+// OT: outer (cross-tile) accumulator type.  Workgroup b walks the item range
+// r(b) of the plan; consecutive ranges go to one XCD (blocks are dealt to the
+// 8 XCDs round-robin), so an XCD's L2 sees neighbouring items.
 template <class OT, int LOADERS = kPredictWaves / 2>
 __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
-    const float *__restrict__ aug, const float *__restrict__ kcoord, const float4 *__restrict__ kbox, int nI, int nC,
-    int G, const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp, float cexp,
-    float skip_d2, float skip_d2_mean, const float *__restrict__ lgn, float lg_tau_v, float m0,
-    float *__restrict__ part, float *__restrict__ mean,
-    unsigned long long *__restrict__ tiles_done) {
+    const float *__restrict__ aug, const float *__restrict__ kcoord, const int4 *__restrict__ desc,
+    const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P, int n_items, int nI,
+    const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp, float cexp, float m0,
+    float *__restrict__ part, float *__restrict__ mean) {
     __shared__ __attribute__((aligned(16))) float smem[kSmemFloats];
-    int *tlist = reinterpret_cast<int *>(smem + 2 * kStageFloats);
-    float *wbox = smem + 2 * kStageFloats + kMaxList;               // [waves][4]
-    int *wcnt = reinterpret_cast<int *>(wbox + 4 * kPredictWaves);  // [waves]
-    int *rcnt = wcnt + kPredictWaves;                               // [G] list prefix per row block
-    // chunk-major, heaviest chunk first; consecutive workgroups take
-    // consecutive (Morton-adjacent) query blocks of one chunk.  Workgroups go
-    // to the 8 XCDs round-robin by index, so every XCD sees every chunk.
-    const int64_t nQ = (m + kBN - 1) / kBN;
-    const int64_t bid = blockIdx.x;
-    const int64_t qb = bid % nQ;
-    const int chunk = nC - 1 - (int)(bid / nQ);
-    const int I0 = chunk * G, I1 = min(I0 + G, nI);
+    const int bid = blockIdx.x;
+    const int rng = (P % 8 == 0) ? (bid % 8) * (P / 8) + bid / 8 : bid;
+    // (bounds are clamped so that a corrupt plan cannot address outside the buffers)
+    const int k0 = max(seg[rng], 0), k1 = min(seg[rng + 1], n_items);
+    if (k0 >= k1) return;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int g = lane >> 4;   // k within the step
     const int r = lane & 15;   // row within a 16-row block / query within the wave
-    const int nkb = I1 * kTilesPerRowBlockStep;
+#ifdef SBO_STAMPS
+    const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+#endif
 
-    const int64_t q = qb * kBN + wave * 16 + r;
-    const int64_t qc = q < m ? q : m - 1;
-    const float xq = qx[qc], yq = qy[qc];
-    const bool writer = lane < 16 && q < m;
+    // LDS: two stages, then two descriptor windows and two tile-list windows
+    // (1 KiB each), refilled one window ahead by LDS-DMA
+    const int4 *dwin = reinterpret_cast<const int4 *>(smem + 2 * kStageFloats);
+    const unsigned short *lwin = reinterpret_cast<const unsigned short *>(smem + 2 * kStageFloats + 512);
 
-    // ---- list the k-tiles this workgroup needs (ascending)
-    int cnt = nkb;
-    const int *list = nullptr;
-    if (skip_d2 > 0.0f && nkb <= kMaxList) {
-        const bool mean_block = (I1 == nI);  // the chunk holding the last row block also accumulates the mean
-        // budgeted test (one row block per workgroup only: a chunk shares one
-        // list, and the norms differ between its row blocks)
-        const float *lgn_I = (lgn && I1 - I0 == 1) ? lgn + tile_start(I0) : nullptr;
-        const float bx0 = wave_min(xq), bx1 = wave_max(xq), by0 = wave_min(yq), by1 = wave_max(yq);
-        if (lane == 0) {
-            wbox[wave * 4 + 0] = bx0; wbox[wave * 4 + 1] = bx1;
-            wbox[wave * 4 + 2] = by0; wbox[wave * 4 + 3] = by1;
-        }
-        unsigned long long *bins = reinterpret_cast<unsigned long long *>(smem);  // stage 0 is free until the sweep
-        if (lgn_I)
-            for (int i = tid; i < kBudgetBins; i += kPredictThreads) bins[i] = 0ull;
-        __syncthreads();
-        float qx0 = wbox[0], qx1 = wbox[1], qy0 = wbox[2], qy1 = wbox[3];
-#pragma unroll
-        for (int w = 1; w < kPredictWaves; ++w) {
-            qx0 = fminf(qx0, wbox[w * 4 + 0]); qx1 = fmaxf(qx1, wbox[w * 4 + 1]);
-            qy0 = fminf(qy0, wbox[w * 4 + 2]); qy1 = fmaxf(qy1, wbox[w * 4 + 3]);
-        }
-        auto box_d2 = [&](int t) {
-            const float4 b = kbox[t];  // (xmin, xmax, ymin, ymax); empty tile = (+inf, -inf, ..)
-            const float dx = fmaxf(0.0f, fmaxf(b.x - qx1, qx0 - b.y));
-            const float dy = fmaxf(0.0f, fmaxf(b.z - qy1, qy0 - b.w));
-            return fmaf(dy, dy, dx * dx);
-        };
-        // log2 of tile t's largest possible share of |dV_I|_2, relative to the
-        // row block's budget, and its budget bin (0: negligible, kBudgetBins-1:
-        // over budget on its own, never dropped)
-        auto bin_of = [&](float d2, int t, float &rel) {
-            rel = fmaf(cexp, d2 * 1.001f, lgn_I[t]) - lg_tau_v + 0.01f;
-            const float f = (rel + (float)kBudgetFloor) * (float)kBinsPerBit + 1.0f;
-            return f < 0.0f ? 0 : (f >= (float)(kBudgetBins - 1) ? kBudgetBins - 1 : (int)f);
-        };
-        int drop_max = -1;  // budget bins 0..drop_max are dropped
-        if (lgn_I) {
-            // greedy, smallest bins first: the largest prefix of bins whose
-            // summed bounds (fixed point 2^32 = the budget, each term rounded
-            // up, integer adds = order-independent) stay within the budget
-            for (int t = tid; t < nkb; t += kPredictThreads) {
-                float rel;
-                const int bi = bin_of(box_d2(t), t, rel);
-                if (bi < kBudgetBins - 1)
-                    atomicAdd(bins + bi, (unsigned long long)ceilf(exp2f(rel + 32.0f) * 1.0001f) + 1ull);
-            }
-            __syncthreads();
-            if (wave == 0) {
-                constexpr int per = (kBudgetBins + 63) / 64;
-                unsigned long long v[per], run = 0;
-#pragma unroll
-                for (int j = 0; j < per; ++j) {
-                    const int i = lane * per + j;
-                    v[j] = i < kBudgetBins - 1 ? bins[i] : (1ull << 40);
-                    run += v[j];
-                }
-                unsigned long long incl = run;  // inclusive scan over lanes
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const unsigned long long u = __shfl_up(incl, o);
-                    if (lane >= o) incl += u;
-                }
-                unsigned long long pre = incl - run;
-                int ok = 0;
-#pragma unroll
-                for (int j = 0; j < per; ++j) {
-                    pre += v[j];
-                    ok += pre <= (1ull << 32) ? 1 : 0;
-                }
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) ok += __shfl_xor(ok, o);
-                if (lane == 0) wcnt[0] = ok - 1;
-            }
-            __syncthreads();
-            drop_max = wcnt[0];
-        }
-        int base = 0;
-        for (int t0 = 0; t0 < nkb; t0 += kPredictThreads) {
-            const int t = t0 + tid;
-            bool keep = false;
-            if (t < nkb) {
-                const float d2 = box_d2(t);
-                if (lgn_I) {
-                    float rel;
-                    keep = bin_of(d2, t, rel) > drop_max;
-                } else {
-                    keep = d2 <= skip_d2;
-                }
-                if (!keep && mean_block) keep = d2 <= skip_d2_mean;
-            }
-            const unsigned long long bal = __ballot(keep);
-            const int before = __popcll(bal & ((1ull << lane) - 1ull));
-            __syncthreads();  // previous chunk's wcnt reads are done
-            if (lane == 0) wcnt[wave] = __popcll(bal);
-            __syncthreads();
-            int off = base, tot = 0;
-#pragma unroll
-            for (int w = 0; w < kPredictWaves; ++w) {
-                off += w < wave ? wcnt[w] : 0;
-                tot += wcnt[w];
-            }
-            if (keep) tlist[off + before] = t;
-            base += tot;
-        }
-        cnt = base;
-        list = tlist;
-        __syncthreads();
-    }
-    // ---- list prefix of each row block of the chunk: entries t < 4(I+1)
-    for (int i = tid; i < I1 - I0; i += kPredictThreads) {
-        const int lim = (I0 + i + 1) * kTilesPerRowBlockStep;
-        int n = lim < cnt ? lim : cnt;
-        if (list) {  // ascending list: lower bound of lim
-            int lo = 0, hi = cnt;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (list[mid] < lim) lo = mid + 1; else hi = mid;
-            }
-            n = lo;
-        }
-        rcnt[i] = n;
-    }
-    __syncthreads();
-    if (tid == 0 && tiles_done) {  // executed-work counter
-        unsigned long long tot = 0;
-        for (int i = 0; i < I1 - I0; ++i) tot += (unsigned long long)rcnt[i];
-        atomicAdd(tiles_done, tot);
-    }
-    // row blocks with an empty prefix contribute exactly zero
-    for (int I = I0; I < I1; ++I)
-        if (rcnt[I - I0] == 0 && writer) {
-            part[(int64_t)I * ldp + q] = 0.0f;
-            if (I == nI - 1) mean[q] = m0;
-        }
-
-    // ---- the sweep: a flat stream of (row block, k-tile) items
-    // LDS-DMA staging (global_load_lds_dwordx4): each wave instruction moves
-    // 1 KiB, lane-linear, no staging registers.  A stage = the 64 KiB [BK][BM]
-    // tile (16 instructions per loader wave) + 768 B of per-k coordinates.
-    // The DMA is issued from inline asm so that hipcc does not see an LDS
-    // write in flight: with a compiler-visible one pending it drains every
-    // ds_read wait to lgkmcnt(0) (waiting on reads issued one instruction
-    // earlier) instead of counting.  The stage is retired by the explicit
-    // vmcnt(0) + barrier at the end of each item.
+    // LDS-DMA (global_load_lds_dwordx4): each wave instruction moves 1 KiB,
+    // lane-linear, no staging registers.  A stage = the 64 KiB [BK][BM] tile
+    // (16 instructions per loader wave) + 768 B of per-k coordinates.  The
+    // DMA is issued from inline asm so that hipcc does not see an LDS write
+    // in flight: with a compiler-visible one pending it drains every ds_read
+    // wait to lgkmcnt(0) (waiting on reads issued one instruction earlier)
+    // instead of counting.  Every stage and window is retired by the
+    // explicit vmcnt(0) + barrier at the end of each step.
     typedef __attribute__((address_space(3))) char lds_char;
     constexpr int kTileBytes = kTileFloats * 4, kStageBytes = kStageFloats * 4, kCBytes = 3 * kBK * 4;
     // Only the last LOADERS waves (one per SIMD) issue the stage, 16 pieces
@@ -530,8 +664,12 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     const bool loader = lw >= 0;
     const char *gA = reinterpret_cast<const char *>(aug) + (loader ? lw : 0) * 1024 + lane * 16;
     const char *gC = reinterpret_cast<const char *>(kcoord) + lane * 16;
+    const char *gD = reinterpret_cast<const char *>(desc) + lane * 16;
+    const char *gL = reinterpret_cast<const char *>(tl) + lane * 16;
     const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
     const uint32_t lds_wave = lds_smem + (uint32_t)__builtin_amdgcn_readfirstlane(loader ? lw : 0) * 1024u;
+    const uint32_t lds_dwin = lds_smem + 2u * kStageBytes;
+    const uint32_t lds_lwin = lds_dwin + 2048u;
 #define SBO_DMA16(gsrc, ldst)                                                                           \
     do {                                                                                                \
         uint32_t keep_;                                                                                 \
@@ -552,35 +690,85 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
         if (lw == 0 && lane < kCBytes / 16)                                                             \
             SBO_DMA16(gC + (int64_t)(t_) * kCBytes, lds_smem + (uint32_t)((buf) * kStageBytes + kTileBytes)); \
     } while (0)
+    // descriptor window w (items [64w, 64w+64)) and tile-list window w
+    // (entries [512w, 512w+512)), each into LDS buffer w & 1
+#define SBO_DESC_WINDOW(w_)                                                                             \
+    do {                                                                                                \
+        if (lw == 1) SBO_DMA16(gD + (int64_t)(w_) * 1024, lds_dwin + (uint32_t)((w_) & 1) * 1024u);     \
+    } while (0)
+#define SBO_LIST_WINDOW(w_)                                                                             \
+    do {                                                                                                \
+        if (lw == 2) SBO_DMA16(gL + (int64_t)(w_) * 1024, lds_lwin + (uint32_t)((w_) & 1) * 1024u);     \
+    } while (0)
+    auto desc_at = [&](int k) {  // a descriptor from its (loaded) window; wave-uniform
+        const int4 d = dwin[((k / kDescWindow) & 1) * kDescWindow + k % kDescWindow];
+        const int I = min(max(__builtin_amdgcn_readfirstlane(d.x), 0), nI - 1);
+        return make_int4(I, __builtin_amdgcn_readfirstlane(d.y), __builtin_amdgcn_readfirstlane(d.z),
+                         __builtin_amdgcn_readfirstlane(d.w));
+    };
+    auto entry_off = [](const int4 &d) {
+        return (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
+    };
+    auto list_at = [&](uint64_t e, int I) {
+        const int t = __builtin_amdgcn_readfirstlane((int)lwin[((e / kListWindow) & 1) * kListWindow + e % kListWindow]);
+        return min(t, kTilesPerRowBlockStep * (I + 1) - 1);
+    };
 
-    int I = I0;
-    while (I < I1 && rcnt[I - I0] == 0) ++I;
-    if (I >= I1) return;
-    SBO_STAGE(I, list ? list[0] : 0, 0);
+    // ---- prologue: the first two windows of each kind, the first stage
+    SBO_DESC_WINDOW(k0 / kDescWindow);
+    SBO_DESC_WINDOW(k0 / kDescWindow + 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    int4 dc = desc_at(k0);
+    uint64_t e = entry_off(dc);
+    SBO_LIST_WINDOW(e / kListWindow);
+    SBO_LIST_WINDOW(e / kListWindow + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    SBO_STAGE(dc.x, list_at(e, dc.x), 0);
+    int64_t q = (int64_t)dc.y * kBN + wave * 16 + r;
+    float xq = qx[q < m ? q : m - 1], yq = qy[q < m ? q : m - 1];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#ifdef SBO_STAMPS
+    const unsigned long long st1 = __builtin_amdgcn_s_memtime();
+#endif
 
     OT outer[kRowBlocks][4];
 #pragma unroll
     for (int rb = 0; rb < kRowBlocks; ++rb)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) outer[rb][e] = (OT)0;
+        for (int c = 0; c < 4; ++c) outer[rb][c] = (OT)0;
     double mu = 0.0;
     f32x4 acc[kRowBlocks];
-    int j = 0, cur = 0;
+    int k = k0, j = 0, cur = 0;
     for (;;) {
-        const int n = rcnt[I - I0];
-        // next item: (I, j+1), or the first tile of the next non-empty row block
-        int In = I, jn = j + 1;
-        if (jn >= n) {
+        const int cnt = dc.w & 0xffff;
+        // the next step: (k, j+1), or the first tile of item k+1
+        int kn = k, jn = j + 1;
+        if (jn >= cnt) {
+            kn = k + 1;
             jn = 0;
-            do ++In; while (In < I1 && rcnt[In - I0] == 0);
         }
-        const bool more = In < I1;
-        if (more) SBO_STAGE(In, list ? list[jn] : jn, cur ^ 1);
+        const bool more = kn < k1;
+        int4 dn = dc;
+        float xqn = xq, yqn = yq;
+        if (more) {
+            if (kn != k) {
+                dn = desc_at(kn);
+                if (kn % kDescWindow == 0) SBO_DESC_WINDOW(kn / kDescWindow + 1);
+                const int64_t qn = (int64_t)dn.y * kBN + wave * 16 + r;
+                xqn = qx[qn < m ? qn : m - 1];
+                yqn = qy[qn < m ? qn : m - 1];
+            }
+            const uint64_t en = e + 1;
+            if (en % kListWindow == 0) SBO_LIST_WINDOW(en / kListWindow + 1);
+            SBO_STAGE(dn.x, list_at(en, dn.x), cur ^ 1);
+        }
         // per-lane bases; every k step is a constant offset from them
         const float4 *pa = reinterpret_cast<const float4 *>(smem + cur * kStageFloats) + g * 16 + r;
-        const float *pc = smem + cur * kStageFloats + kTileFloats + g;
+        const float *pc = smem + cur * kStageFloats + kTileFloats + g * (kBK / 4);
+        const int I = dc.x;
         if (I == nI - 1)
             tile_steps<true>(pa, pc, xq, yq, cexp, acc, mu);
         else
@@ -588,35 +776,60 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
 #pragma unroll
         for (int rb = 0; rb < kRowBlocks; ++rb)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) outer[rb][e] += (OT)acc[rb][e];
-        if (j == n - 1) {
-            // row block done: column sums of V^2 over its rows; lanes l, l+16,
+            for (int c = 0; c < 4; ++c) outer[rb][c] += (OT)acc[rb][c];
+        if (j == cnt - 1) {
+            // item done: column sums of V^2 over its rows; lanes l, l+16,
             // l+32, l+48 hold four row quarters of column l&15 of every block
             double s = 0.0;
 #pragma unroll
             for (int rb = 0; rb < kRowBlocks; ++rb)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    s = fma((double)outer[rb][e], (double)outer[rb][e], s);
-                    outer[rb][e] = (OT)0;
+                for (int c = 0; c < 4; ++c) {
+                    s = fma((double)outer[rb][c], (double)outer[rb][c], s);
+                    outer[rb][c] = (OT)0;
                 }
             s += __shfl_xor(s, 16);
             s += __shfl_xor(s, 32);
+            const bool writer = lane < 16 && q < m;
             if (writer) part[(int64_t)I * ldp + q] = (float)s;
             if (I == nI - 1) {
                 mu += __shfl_xor(mu, 16);
                 mu += __shfl_xor(mu, 32);
                 if (writer) mean[q] = (float)((double)m0 + mu);
+                mu = 0.0;
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (!more) break;
-        I = In;
+        if (kn != k) {
+            k = kn;
+            dc = dn;
+            xq = xqn;
+            yq = yqn;
+            q = (int64_t)dc.y * kBN + wave * 16 + r;
+        }
         j = jn;
+        ++e;
         cur ^= 1;
     }
+#ifdef SBO_STAMPS
+    if (tid == 0 && bid < kStampSlots) {
+        const unsigned long long st3 = __builtin_amdgcn_s_memtime();
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(hw), "=s"(xcc));
+        unsigned long long *slot = sbo_stamps + bid * 6;
+        slot[0] = st0;
+        slot[1] = st1;
+        slot[2] = st1;
+        slot[3] = st3;
+        slot[4] = ((unsigned long long)xcc << 32) | hw;
+        slot[5] = ((unsigned long long)(unsigned)(k1 - k0) << 32) | (unsigned)(e + 1 - entry_off(desc[k0]));
+    }
+#endif
 #undef SBO_STAGE
+#undef SBO_DESC_WINDOW
+#undef SBO_LIST_WINDOW
 #undef SBO_DMA16
 }
 
@@ -834,35 +1047,101 @@ hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int6
     return hipGetLastError();
 }
 
-hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox, int64_t npad,
-                          const float *qx, const float *qy, int64_t m, int64_t ldp, float ell, float m0,
-                          const SkipPlan &skip, float *part, float *mean, unsigned long long *tiles_done, int variant,
-                          int row_chunk) {
+namespace {
+struct PlanLayout {
+    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes, total;
+};
+
+PlanLayout plan_layout(int64_t nI, int64_t nQ, int P) {
+    const int64_t items = nI * nQ;
+    const int64_t cap = 2 * nI * (nI + 1) * nQ;  // every tile of every item (the dense sweep)
+    PlanLayout L{};
+    size_t o = 0;
+    auto take = [&](size_t b) {
+        const size_t at = o;
+        o = (o + b + 255) / 256 * 256;
+        return at;
+    };
+    L.key = take(8 * (size_t)items);
+    L.scan = take(8 * (size_t)items);
+    L.thr = take((size_t)items);
+    L.desc = take(16 * (size_t)(items + 2 * kDescWindow));
+    L.tl = take(2 * (size_t)(cap + 2 * kListWindow));
+    L.seg = take(4 * (size_t)(P + 1));
+    size_t tb = 0;
+    (void)rocprim::inclusive_scan(nullptr, tb, (const unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                                  (size_t)items, rocprim::plus<unsigned long long>());
+    L.temp = take(tb);
+    L.temp_bytes = tb;
+    L.total = o;
+    return L;
+}
+
+// k-tiles farther than this squared distance give c*d^2 < -L, i.e. every K*
+// entry < 2^-L (0.1% margin over the kernel's rounding); L >= 150 means every
+// such entry is exactly +0.0 in f32
+float cutoff_d2(int L, double ce) { return L > 0 ? (float)((double)L / -ce * 1.001) : -1.0f; }
+double exp2_coef(float ell) { return -1.0 / (2.0 * (double)ell * (double)ell * 0.69314718055994530942); }
+}  // namespace
+
+size_t predict_work_bytes(int64_t npad, int64_t m, int P) {
+    return plan_layout(npad / kBM, (m + kBN - 1) / kBN, P).total;
+}
+
+hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const float *qx, const float *qy, int64_t m,
+                       int64_t ldp, float ell, float m0, const SkipPlan &skip, float *part, float *mean,
+                       unsigned long long *tiles_done, int P, void *work, size_t work_bytes) {
     const int nI = (int)(npad / kBM);
     const int64_t nQ = (m + kBN - 1) / kBN;
-    const double ce = -1.0 / (2.0 * (double)ell * (double)ell * 0.69314718055994530942);
+    const int64_t items = (int64_t)nI * nQ;
+    if (m <= 0 || nI <= 0) return hipSuccess;
+    // key fields: items < 2^24, every kept-tile count < 2^40; tile index < 2^16
+    if (nQ > 0x7fffffff || items >= (1ll << (64 - kPlanKeyShift)) ||
+        2 * (int64_t)nI * (nI + 1) * nQ >= (1ll << kPlanKeyShift) || kTilesPerRowBlockStep * (int64_t)nI > 65535)
+        return hipErrorInvalidValue;
+    const PlanLayout L = plan_layout(nI, nQ, P);
+    if (work_bytes < L.total) return hipErrorInvalidValue;
+    char *w = static_cast<char *>(work);
+    auto *key = reinterpret_cast<unsigned long long *>(w + L.key);
+    auto *scan = reinterpret_cast<unsigned long long *>(w + L.scan);
+    auto *thr = reinterpret_cast<unsigned char *>(w + L.thr);
+    auto *desc = reinterpret_cast<int4 *>(w + L.desc);
+    auto *tl = reinterpret_cast<unsigned short *>(w + L.tl);
+    auto *seg = reinterpret_cast<int *>(w + L.seg);
+    const double ce = exp2_coef(ell);
     const float cexp = (float)ce;
-    // k-tiles farther than this squared distance give c*d^2 < -L, i.e.
-    // every K* entry < 2^-L (0.1% margin over the kernel's rounding);
-    // L >= 150 means every such entry is exactly +0.0 in f32
-    const float skip_d2 = skip.L > 0 ? (float)((double)skip.L / -ce * 1.001) : -1.0f;
-    const float skip_d2_mean = skip.L > 0 && skip.L_mean > skip.L ? (float)((double)skip.L_mean / -ce * 1.001) : skip_d2;
-    // Row blocks per workgroup (chunk).  Default 1: the grid is row-block
-    // major, so the workgroups running at any moment all read row block I's
-    // A tiles and share them in L2 -- 18 GB of HBM fetch per C4 sweep,
-    // against 577 GB when each workgroup walks every row block for its
-    // queries (same time: the sweep is MFMA-bound either way; measured with
-    // rocprofv3 FETCH_SIZE).
-    const int G = row_chunk > 0 ? std::min(row_chunk, nI) : 1;
-    const int nC = (nI + G - 1) / G;
-    if (G > kMaxChunk) return hipErrorInvalidValue;
-    const int64_t blocks = nQ * nC;
-    if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-#define SBO_PREDICT_ARGS aug, kcoord, kbox, nI, nC, G, qx, qy, m, ldp, cexp, skip_d2, skip_d2_mean, skip.lgn, \
-        skip.lg_tau_v, m0, part, mean, tiles_done
+    const float skip_d2 = cutoff_d2(skip.L, ce);
+    const float skip_d2_mean = skip.L > 0 && skip.L_mean > skip.L ? cutoff_d2(skip.L_mean, ce) : skip_d2;
+    const float *lgn = skip.L > 0 ? skip.lgn : nullptr;
+    hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, lgn, nI, nQ, qx, qy,
+                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t tb = L.temp_bytes;
+    e = rocprim::inclusive_scan(w + L.temp, tb, key, scan, (size_t)items, rocprim::plus<unsigned long long>(), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, lgn, nI, nQ, qx, qy,
+                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, key, scan, thr, desc, tl);
+    hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done);
+    return hipGetLastError();
+}
+
+hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, const float *qx,
+                          const float *qy, int64_t m, int64_t ldp, float ell, float m0, float *part, float *mean,
+                          int variant, int P, const void *work) {
+    const int nI = (int)(npad / kBM);
+    const int64_t nQ = (m + kBN - 1) / kBN;
+    if (m <= 0 || nI <= 0) return hipSuccess;
+    const PlanLayout L = plan_layout(nI, nQ, P);
+    const char *w = static_cast<const char *>(work);
+    const auto *desc = reinterpret_cast<const int4 *>(w + L.desc);
+    const auto *tl = reinterpret_cast<const unsigned short *>(w + L.tl);
+    const auto *seg = reinterpret_cast<const int *>(w + L.seg);
+    const float cexp = (float)exp2_coef(ell);
+#define SBO_PREDICT_ARGS aug, kcoord, desc, tl, seg, P, (int)(nI * nQ), nI, qx, qy, m, ldp, cexp, m0, part, mean
     switch (variant) {
-        case 1: hipLaunchKernelGGL((predict_kernel<double>), dim3((unsigned)blocks), dim3(kPredictThreads), 0, s, SBO_PREDICT_ARGS); break;
-        default: hipLaunchKernelGGL((predict_kernel<float>), dim3((unsigned)blocks), dim3(kPredictThreads), 0, s, SBO_PREDICT_ARGS); break;
+        case 1: hipLaunchKernelGGL((predict_kernel<double>), dim3((unsigned)P), dim3(kPredictThreads), 0, s, SBO_PREDICT_ARGS); break;
+        default: hipLaunchKernelGGL((predict_kernel<float>), dim3((unsigned)P), dim3(kPredictThreads), 0, s, SBO_PREDICT_ARGS); break;
     }
 #undef SBO_PREDICT_ARGS
     return hipGetLastError();

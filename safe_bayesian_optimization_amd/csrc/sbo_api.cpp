@@ -413,14 +413,18 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         qx = sx;
         qy = sy;
     }
+    const int P = ctx->sweep_groups > 0 ? ctx->sweep_groups : std::max(1, ctx->num_cu);
+    SBO_HIP(ctx->plan_work.reserve(sbo::predict_work_bytes(ctx->npad, m, P)));
+    SBO_HIP(sbo::launch_plan(ctx->stream, ctx->kbox.as<float4>(), ctx->npad, qx, qy, m, ldp,
+                             (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan, ctx->part.as<float>(),
+                             ctx->mean.as<float>(), ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr, P,
+                             ctx->plan_work.as<void>(), ctx->plan_work.capacity()));
     {
         Bracket br(ctx, ctx->ev_predict);
-        SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(),
-                                    ctx->kbox.as<float4>(), ctx->npad, qx, qy, m, ldp,
-                                    (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan,
-                                    ctx->part.as<float>(), ctx->mean.as<float>(),
-                                    ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr,
-                                    ctx->kernel_variant, ctx->row_chunk));
+        SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(), ctx->npad, qx, qy,
+                                    m, ldp, (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean,
+                                    ctx->part.as<float>(), ctx->mean.as<float>(), ctx->kernel_variant, P,
+                                    ctx->plan_work.as<void>()));
     }
     const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
     SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<float>(), ctx->mean.as<float>(), (int)nI, ldp, m, sf2,
@@ -459,7 +463,8 @@ SBO_API sbo_status sbo_create(int device, sbo_ctx **out) {
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess ||
         rocblas_create_handle(&ctx->blas) != rocblas_status_success ||
         hipHostMalloc(reinterpret_cast<void **>(&ctx->host_key), sizeof(sbo_key)) != hipSuccess ||
-        ctx->info.reserve(256) != hipSuccess) {
+        ctx->info.reserve(256) != hipSuccess ||
+        hipDeviceGetAttribute(&ctx->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
         sbo_destroy(ctx);
         return SBO_E_DEVICE;
     }
@@ -833,9 +838,9 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             SBO_CHECK(value >= 10 && value <= 60, SBO_E_INVAL, "SBO_OPT_SKIP_BUDGET must be in [10, 60]");
             ctx->skip_budget = (int)value;
             return SBO_OK;
-        case SBO_OPT_ROW_CHUNK:
-            SBO_CHECK(value >= 0 && value <= 128, SBO_E_INVAL, "SBO_OPT_ROW_CHUNK must be in [0, 128]");
-            ctx->row_chunk = (int)value;
+        case SBO_OPT_SWEEP_GROUPS:
+            SBO_CHECK(value >= 0 && value <= 65536, SBO_E_INVAL, "SBO_OPT_SWEEP_GROUPS must be in [0, 65536]");
+            ctx->sweep_groups = (int)value;
             return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
             SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be 0 or 1");

@@ -107,7 +107,9 @@ struct sbo_ctx {
     float bbox[4] = {0.f, 0.f, 0.f, 0.f};  // training bounding box (x0, x1, y0, y1)
     bool query_order = true;     // SBO_OPT_QUERY_ORDER: sweep queries in Morton order
     int kernel_variant = 0;      // SBO_OPT_KERNEL_VARIANT: predictive kernel build (A/B)
-    int row_chunk = 0;           // SBO_OPT_ROW_CHUNK: row blocks per predictive workgroup (0: auto)
+    int sweep_groups = 0;        // SBO_OPT_SWEEP_GROUPS: persistent sweep workgroups (0: one per CU)
+    int num_cu = 0;              // compute units of the device
+    sbo::DevBuf plan_work;       // the tick's tile plan (launch_plan)
     sbo::DevBuf fwork, fowner, fimg, fpix, fout;  // device frontier (sbo_frontier / sbo_subgoal)
     sbo::DevBuf qwork;           // query ordering workspace
     sbo::DevBuf kbox;            // per k-tile bounding boxes (float4)
@@ -174,10 +176,18 @@ struct SkipPlan {
     const float *lgn = nullptr; // per packed tile log2 norms (null: distance test only)
     float lg_tau_v = 0.0f;
 };
-hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, const float4 *kbox,
-                          int64_t npad, const float *qx, const float *qy, int64_t m, int64_t ldp,
-                          float ell, float m0, const SkipPlan &skip, float *part, float *mean,
-                          unsigned long long *tiles_done, int variant, int row_chunk);
+// The tick's plan (which k-tiles each (row block, query block) item runs,
+// non-empty items in row-block-major order, one balanced item range per
+// sweep workgroup) in `work` (predict_work_bytes); empty items' outputs are
+// written here.  P = sweep workgroups (one per CU).
+size_t predict_work_bytes(int64_t npad, int64_t m, int P);
+hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const float *qx, const float *qy, int64_t m,
+                       int64_t ldp, float ell, float m0, const SkipPlan &skip, float *part, float *mean,
+                       unsigned long long *tiles_done, int P, void *work, size_t work_bytes);
+// The sweep over the plan in `work` (persistent, P workgroups).
+hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, const float *qx,
+                          const float *qy, int64_t m, int64_t ldp, float ell, float m0, float *part, float *mean,
+                          int variant, int P, const void *work);
 // lgn[tile_start(I) + t] = log2 min(16 max_r |A_It[r]|_1, 8 |A_It|_F) (f64 sums,
 // rounded up) for row blocks I >= I0 (-1000 for an all-zero tile).
 hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float *lgn);

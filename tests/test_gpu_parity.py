@@ -378,33 +378,36 @@ def test_tile_skip_exact_and_bounded(dev, mapper):
     assert res[0][2] == res[64][2]
 
 
-def test_row_chunk_and_outer_variant(mapper):
-    """Workgroup decomposition does not change the arithmetic: every row
-    block's accumulation order is the same whether a workgroup walks 1, 3 or
-    all row blocks (bitwise equal, empty prefixes and a ragged last chunk
-    included).  The f64 cross-tile accumulator (variant 1) agrees with the
-    f32 default to the contract tolerance."""
+def test_sweep_partition_and_outer_variant(mapper):
+    """The persistent sweep's partition of the plan does not change the
+    arithmetic: 1, 3, 7 or 1000 workgroups (more than there are non-empty
+    items: some walk empty ranges) give bitwise the same posterior as one per
+    CU, for the budgeted, a fixed and the dense cutoff.  The f64 cross-tile
+    accumulator (variant 1) agrees with the f32 default to the contract
+    tolerance."""
     wl = synthetic(5000, 90, 70, seed=23)   # npad 5120 = 20 row blocks
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
     gm.fit(wl.x, wl.y, wl.obs)
-    res = {}
-    # a fixed distance cutoff: the tile-norm test of the auto cutoff is per row
-    # block, so chunks of several row blocks keep a (harmless) superset there
-    gm.set_option(N.SBO_OPT_TILE_SKIP, 40)
-    for chunk in (0, 1, 3, 20):
-        gm.set_option(N.SBO_OPT_ROW_CHUNK, chunk)
-        res[chunk] = gm.predict(wl.qx, wl.qy)
-    gm.set_option(N.SBO_OPT_ROW_CHUNK, 0)
+    base = None
+    for skip in (-1, 40, 0):
+        gm.set_option(N.SBO_OPT_TILE_SKIP, skip)
+        res = {}
+        for groups in (0, 1, 3, 7, 1000):
+            gm.set_option(N.SBO_OPT_SWEEP_GROUPS, groups)
+            res[groups] = gm.predict(wl.qx, wl.qy)
+        for groups in (1, 3, 7, 1000):
+            assert np.array_equal(res[groups][0], res[0][0]) and np.array_equal(res[groups][1], res[0][1]), (skip, groups)
+        if skip == -1:
+            base = res[0]
+    gm.set_option(N.SBO_OPT_SWEEP_GROUPS, 0)
     gm.set_option(N.SBO_OPT_TILE_SKIP, -1)
-    for chunk in (1, 3, 20):
-        assert np.array_equal(res[chunk][0], res[0][0]) and np.array_equal(res[chunk][1], res[0][1])
     gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 1)
     mu64, sd64 = gm.predict(wl.qx, wl.qy)
     gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 0)
-    assert nrel(mu64, res[0][0].astype(np.float64)) < 1e-6   # the mean is f64-accumulated in both
-    assert nrel(sd64.astype(np.float64) ** 2, res[0][1].astype(np.float64) ** 2) < 1e-5
+    assert nrel(mu64, base[0].astype(np.float64)) < 1e-6   # the mean is f64-accumulated in both
+    assert nrel(sd64.astype(np.float64) ** 2, base[1].astype(np.float64) ** 2) < 1e-5
     with pytest.raises(N.SboError):
-        gm.set_option(N.SBO_OPT_ROW_CHUNK, 129)
+        gm.set_option(N.SBO_OPT_SWEEP_GROUPS, -1)
     with pytest.raises(N.SboError):
         gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 2)
 
