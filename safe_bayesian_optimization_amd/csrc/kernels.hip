@@ -278,10 +278,18 @@ constexpr int kStageFloats = kTileFloats + 3 * kBK;
 // first stage in, sweep done), HW_ID/XCC_ID, row block and tile count
 constexpr int64_t kStampSlots = 1 << 20;
 __device__ unsigned long long sbo_stamps[kStampSlots * 6];
+// per (workgroup < 64, wave): cycles summed over the sweep steps in four
+// segments -- barrier exit -> stage issued, -> tile MFMAs + outer sum done,
+// -> epilogue + vmcnt(0) done, -> next barrier exit -- and the step count
+__device__ unsigned long long sbo_wstamps[64 * 8 * 5];
 }  // namespace
 extern "C" __attribute__((visibility("default"))) int sbo_debug_stamps(void *dst, int64_t slots) {
     if (slots > kStampSlots) slots = kStampSlots;
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(sbo_stamps), (size_t)slots * 6 * 8, 0, hipMemcpyDeviceToHost);
+}
+extern "C" __attribute__((visibility("default"))) int sbo_debug_wave_stamps(void *dst) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(sbo_wstamps), sizeof(unsigned long long) * 64 * 8 * 5, 0,
+                                    hipMemcpyDeviceToHost);
 }
 namespace {
 #endif
@@ -742,6 +750,11 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     double mu = 0.0;
     f32x4 acc[kRowBlocks];
     int k = k0, j = 0, cur = 0;
+#ifdef SBO_STAMPS
+#define SBO_T(v) do { __builtin_amdgcn_sched_barrier(0); asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) :: "memory"); __builtin_amdgcn_sched_barrier(0); } while (0)
+    unsigned long long wseg[4] = {0, 0, 0, 0}, ta, tb, tc, td;
+    SBO_T(ta);
+#endif
     for (;;) {
         const int cnt = dc.w & 0xffff;
         // the next step: (k, j+1), or the first tile of item k+1
@@ -769,6 +782,10 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
         const float4 *pa = reinterpret_cast<const float4 *>(smem + cur * kStageFloats) + g * 16 + r;
         const float *pc = smem + cur * kStageFloats + kTileFloats + g * (kBK / 4);
         const int I = dc.x;
+#ifdef SBO_STAMPS
+        SBO_T(tb);
+        wseg[0] += tb - ta;
+#endif
         if (I == nI - 1)
             tile_steps<true>(pa, pc, xq, yq, cexp, acc, mu);
         else
@@ -777,6 +794,10 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
         for (int rb = 0; rb < kRowBlocks; ++rb)
 #pragma unroll
             for (int c = 0; c < 4; ++c) outer[rb][c] += (OT)acc[rb][c];
+#ifdef SBO_STAMPS
+        SBO_T(tc);
+        wseg[1] += tc - tb;
+#endif
         if (j == cnt - 1) {
             // item done: column sums of V^2 over its rows; lanes l, l+16,
             // l+32, l+48 hold four row quarters of column l&15 of every block
@@ -800,7 +821,15 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef SBO_STAMPS
+        SBO_T(td);
+        wseg[2] += td - tc;
+#endif
         __syncthreads();
+#ifdef SBO_STAMPS
+        SBO_T(ta);
+        wseg[3] += ta - td;
+#endif
         if (!more) break;
         if (kn != k) {
             k = kn;
@@ -814,6 +843,12 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
         cur ^= 1;
     }
 #ifdef SBO_STAMPS
+    if (lane == 0 && bid < 64) {
+        unsigned long long *ws = sbo_wstamps + (bid * 8 + wave) * 5;
+        for (int i = 0; i < 4; ++i) ws[i] = wseg[i];
+        ws[4] = e + 1 - entry_off(desc[k0]);
+    }
+#undef SBO_T
     if (tid == 0 && bid < kStampSlots) {
         const unsigned long long st3 = __builtin_amdgcn_s_memtime();
         unsigned hw, xcc;

@@ -1,9 +1,8 @@
-"""Per-workgroup phase timing of the predictive kernel from the diagnostic
-build (-DSBO_STAMPS, libsbo_stamps.so: s_memtime at entry, after the tile
-list, after the first stage, after the sweep, plus HW_ID/XCC_ID, row block
-and tile count per workgroup, written to a device array -- no printf).
-Runs one C4 tick and prints where the workgroup time goes, and the idle gap
-between consecutive workgroups on the same CU (dispatch cost).
+"""Per-workgroup timing of the persistent predictive sweep from the
+diagnostic build (-DSBO_STAMPS, libsbo_stamps.so: s_memtime at entry, after
+the prologue and at the end, HW_ID/XCC_ID, items and tiles per workgroup,
+written to a device array -- no printf).  Runs two ticks and prints the
+per-tile sweep cost and the tail imbalance across workgroups.
 
   SBO_LIB=$PWD/safe_bayesian_optimization_amd/lib/libsbo_stamps.so python tools/stamp_summary.py --config C4"""
 import argparse
@@ -40,44 +39,44 @@ def main():
     for _ in range(2):
         gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs)
     torch.cuda.synchronize()
-    nq = (m + 127) // 128
-    nI = -(-n // 256)
-    wgs = min(nq * nI, 1 << 20)
+    wgs = 4096
     buf = np.zeros(wgs * 6, np.uint64)
     rc = N.lib().sbo_debug_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_int64(wgs))
     assert rc == 0, rc
     s = buf.reshape(wgs, 6).astype(np.int64)
-    st0, st1, st2, st3 = s[:, 0], s[:, 1], s[:, 2], s[:, 3]
-    hw, meta = s[:, 4], s[:, 5]
-    tiles = meta & 0xFFFFFFFF
-    I = meta >> 32
-    busy = tiles > 0
-    lst, first, sweep = st1 - st0, st2 - st1, st3 - st2
-    cu = ((hw >> 32) << 16) | (((hw >> 8) & 0xF) << 8) | (((hw >> 13) & 0x1) << 4) | ((hw >> 12) & 0x1)
-    # cu key: xcc, cu_id (bits 11:8), sh_id (12), se_id (15:13)
-    cu = ((hw >> 32) << 12) | (((hw >> 13) & 0x7) << 6) | (((hw >> 12) & 0x1) << 5) | ((hw >> 8) & 0xF)
-    span = st3.max() - st0.min()
-    print(f"{wgs} workgroups, {np.mean(~busy) * 100:.1f}% empty, {tiles.sum()} tiles, {len(np.unique(cu))} CUs seen")
-    print(f"kernel span {span:.3e} cycles; busy-WG mean tiles {tiles[busy].mean():.2f}")
-    tot = (st3 - st0).sum()
-    print(f"share of WG-resident cycles: list {lst.sum() / tot * 100:.1f}%  first stage {first[busy].sum() / tot * 100:.1f}%  "
-          f"sweep {sweep[busy].sum() / tot * 100:.1f}%  (empty WGs {(st3 - st0)[~busy].sum() / tot * 100:.1f}%)")
-    print(f"sweep cycles per tile: {sweep[busy].sum() / tiles[busy].sum():.0f} (median per WG "
-          f"{np.median(sweep[busy] / tiles[busy]):.0f});  list median busy {np.median(lst[busy]):.0f} empty "
-          f"{np.median(lst[~busy]):.0f};  first stage median {np.median(first[busy]):.0f}")
-    # per-CU timelines: idle gap between one WG's end and the next WG's start
-    order = np.lexsort((st0, cu))
-    c, b, e = cu[order], st0[order], st3[order]
-    same = c[1:] == c[:-1]
-    gaps = (b[1:] - e[:-1])[same]
-    per_cu_busy = np.zeros(0)
-    print(f"gap between consecutive WGs on a CU: median {np.median(gaps):.0f}, mean {gaps.mean():.0f} cycles; "
-          f"total gaps / total span x CUs = {gaps.sum() / (span * len(np.unique(cu))) * 100:.1f}%")
-    for lo, hi in ((0, 8), (8, 32), (32, nI - 1), (nI - 1, nI)):
-        sel = busy & (I >= lo) & (I < hi)
-        if sel.any():
-            print(f"  I in [{lo},{hi}): {sel.sum()} busy WGs, mean tiles {tiles[sel].mean():.1f}, sweep/tile "
-                  f"{sweep[sel].sum() / tiles[sel].sum():.0f}, first {np.median(first[sel]):.0f}, list {np.median(lst[sel]):.0f}")
+    s = s[s[:, 3] > 0]
+    st0, st1, st3 = s[:, 0], s[:, 1], s[:, 3]
+    items = s[:, 5] >> 32
+    tiles = s[:, 5] & 0xFFFFFFFF
+    dur = st3 - st0
+    pro = st1 - st0
+    print(f"{len(s)} persistent workgroups; tiles per WG mean {tiles.mean():.0f} (min {tiles.min()}, max {tiles.max()}), "
+          f"items per WG mean {items.mean():.0f}")
+    print(f"WG duration (cycles): mean {dur.mean():.4g}  min {dur.min():.4g}  max {dur.max():.4g}  "
+          f"-> tail imbalance max/mean {dur.max() / dur.mean():.4f}")
+    print(f"prologue median {np.median(pro):.0f} cycles; sweep cycles per tile {((dur - pro).sum() / tiles.sum()):.0f} "
+          f"(ideal MFMA 16384: {16384 / ((dur - pro).sum() / tiles.sum()) * 100:.1f} %)")
+    xcc = s[:, 4] >> 32
+    for x in np.unique(xcc):
+        sel = xcc == x
+        print(f"  XCC {x}: {sel.sum()} WGs, duration mean {dur[sel].mean():.4g} max {dur[sel].max():.4g}, "
+              f"cycles/tile {((dur - pro)[sel].sum() / tiles[sel].sum()):.0f}")
+    bid = np.nonzero(buf.reshape(wgs, 6)[:, 3] > 0)[0]
+    rng = (bid % 8) * (len(bid) // 8) + bid // 8
+    o = np.argsort(rng)
+    d = (dur / tiles)[o]
+    print("  cycles/tile by range (16 groups, range order): " + " ".join(f"{v:.0f}" for v in d.reshape(16, -1).mean(1)))
+    wb = np.zeros(64 * 8 * 5, np.uint64)
+    if N.lib().sbo_debug_wave_stamps(ctypes.c_void_p(wb.ctypes.data)) == 0:
+        w = wb.reshape(64, 8, 5).astype(np.float64)
+        w = w[w[:, 0, 4] > 0]
+        steps = w[:, :, 4:5]
+        per = (w[:, :, :4] / steps).mean(0)   # [wave][segment] cycles per step
+        print("  per step, by wave (cycles): stage-issue | tile MFMA+outer | epilogue+vmcnt | barrier wait")
+        for wv in range(8):
+            print(f"    wave {wv}: " + " | ".join(f"{v:7.0f}" for v in per[wv]) + f"   total {per[wv].sum():.0f}")
+    print(f"cycles per item beyond its tiles' share: "
+          f"{((dur - pro).sum() - tiles.sum() * np.median((dur - pro) / tiles)) / items.sum():.0f}")
 
 
 if __name__ == "__main__":
