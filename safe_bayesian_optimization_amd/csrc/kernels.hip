@@ -1161,6 +1161,17 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     return hipGetLastError();
 }
 
+void plan_views(int64_t npad, int64_t m, int P, const void *work, const int4 **desc, const unsigned short **tl,
+                const int **seg) {
+    const PlanLayout L = plan_layout(npad / kBM, (m + kBN - 1) / kBN, P);
+    const char *w = static_cast<const char *>(work);
+    *desc = reinterpret_cast<const int4 *>(w + L.desc);
+    *tl = reinterpret_cast<const unsigned short *>(w + L.tl);
+    *seg = reinterpret_cast<const int *>(w + L.seg);
+}
+
+float exp2_coef_f(float ell) { return (float)exp2_coef(ell); }
+
 hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, const float *qx,
                           const float *qy, int64_t m, int64_t ldp, float ell, float m0, float *part, float *mean,
                           int variant, int P, const void *work) {

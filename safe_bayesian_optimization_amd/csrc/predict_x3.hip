@@ -1,0 +1,588 @@
+// predict_x3.hip -- the predictive sweep (a3+a4) on bf16 MFMA with split
+// operands: f32-accurate V = A K*^T at 6/16 of the f32 MFMA cycles.
+//
+// Every f32 operand value v is split into three bf16 pieces, v = v0 + v1 + v2
+// (round to nearest at each step: |v1| <= 2^-8 |v|, |v2| <= 2^-16 |v|, the
+// remainder below 2^-24 |v|), and a product a*k is taken as the six terms
+//     a2 k0 + a1 k1 + a0 k2 + a1 k0 + a0 k1 + a0 k0
+// (smallest first; the dropped a1 k2, a2 k1, a2 k2 are below 2^-23 |a k|,
+// the order of an f32 rounding).  Each term is one v_mfma_f32_16x16x32_bf16
+// (exact bf16 products, f32 accumulation): 6 x 16 cycles per 16x16x32
+// block against 8 x 32 cycles of v_mfma_f32_16x16x4_f32, and unlike the f32
+// MFMA, a bf16 MFMA leaves the SIMD's vector issue free for 8 of its 16
+// cycles, so the K* chain and its split run in the matrix pipe's shadow.
+//
+// A = sf2 L^-1 is split once per fit/append/import (pack_x3_kernel, from the
+// f32 packed operand); K* is split in registers as it is generated.
+//
+// Work items, the tick plan and the persistent walk are those of
+// predict_kernel (kernels.hip): workgroup = 256 rows x 128 queries, eight
+// waves, wave w owns queries 16w..16w+15 and all 256 rows as sixteen 16-row
+// MFMA blocks; each 64-k tile is two half-steps of 32 k (an LDS stage of
+// 3 planes x 256 rows x 32 k bf16 = 48 KiB), its MFMA chain starts from zero
+// and is added into an f32 outer sum once the tile is done.
+//
+// Staging: three LDS slots, stage i+2 issued at the top of step i by LDS-DMA
+// (global_load_lds_dwordx4 from inline asm), retired by a counted vmcnt at
+// the end of step i+1; the slot also carries the half-tile's coordinates,
+// sf2 alpha and the item's 128 query coordinates, which the first loader
+// wave issues BEFORE its A pieces, so that the end-of-step wait that leaves
+// the A pieces of stage i+2 in flight has retired them -- the K* of step
+// i+1 is computed during step i, beside its MFMAs.
+#include <cstdint>
+#include <type_traits>
+
+#include "sbo_internal.hpp"
+
+namespace sbo {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kXH = 32;                  // k per half-step
+constexpr int kXPlane = kBM * kXH * 2;   // one bf16 plane of a half-tile: 16 KiB
+constexpr int kXA = 3 * kXPlane;         // the A stage: 48 KiB
+constexpr int kXC = 4 * kXH * 4;         // x[32], y[32], sf2 alpha[32], pad: 512 B
+constexpr int kXQ = 2 * kBN * 4;         // the item's qx[128], qy[128]: 1 KiB
+constexpr int kXSlot = kXA + kXC + kXQ;  // 50,688 B
+constexpr int kXSlots = 3;
+constexpr int kXWin = kXSlots * kXSlot;  // descriptor and tile-list windows follow the slots
+constexpr int kXSmem = kXWin + 4096;
+constexpr int kDescWin = 64, kListWin = 512;
+
+__device__ __forceinline__ float fast_exp2(float v) { return __builtin_amdgcn_exp2f(v); }
+__device__ __forceinline__ float lo_f32(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_f32(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// two f32 -> one dword of two bf16 (element 0 low), round to nearest even
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    const f32x2 v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+
+// v = v0 + v1 + v2 for a pair of values (element 0 in the low halves)
+__device__ __forceinline__ void split3(float a, float b, uint32_t &w0, uint32_t &w1, uint32_t &w2) {
+    w0 = pk_bf16(a, b);
+    const float ra = a - lo_f32(w0), rb = b - hi_f32(w0);
+    w1 = pk_bf16(ra, rb);
+    w2 = pk_bf16(ra - lo_f32(w1), rb - hi_f32(w1));
+}
+
+__device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+__device__ __forceinline__ f32x4 mfma(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+}
+
+typedef __attribute__((address_space(3))) char lds_char;
+
+__device__ __forceinline__ u32x4 lds_b128(const lds_char *p) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(p);
+}
+__device__ __forceinline__ float lds_f(const lds_char *p) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) float *>(p);
+}
+
+// K* pieces of a step for the wave's NC 16-query column blocks
+// (lane (g, r): k = 8g + j of the half-tile, query 16 (NC w + c) + r)
+template <int NC>
+struct KPieces {
+    u32x4 h[NC], m[NC], l[NC];
+};
+
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2v lds_f2(const lds_char *p) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) f32x2v *>(p);
+}
+
+__device__ __forceinline__ float kstar1(float xk, float yk, float xq, float yq, float cexp) {
+    const float dx = xk - xq, dy = yk - yq;
+    return fast_exp2(fmaf(dy, dy, dx * dx) * cexp);
+}
+
+// Pin a value's computation to this point of the instruction stream (the
+// IR-level sinking passes ignore sched_barrier and would otherwise bunch the
+// next step's K* work after the last MFMA), in an arch VGPR.
+#define SBO_PIN(v) asm volatile("" : "+v"(v))
+#ifdef SBO_X3_PIN_OUTER
+#define SBO_PIN_O(v) SBO_PIN(v)
+#else
+#define SBO_PIN_O(v) do { } while (0)
+#endif
+
+// One half-step of one wave: 16 row blocks x NC column blocks x 6 MFMAs on
+// this slot's A planes (each A fragment feeds every column block) and this
+// step's K* pieces kb, with the next step's K* pieces and its mean terms
+// (scaled by msc: 1 for the last row block, else 0) built beside them: pair i of every column
+// block in row blocks 4i .. 4i+3 (read the pair's coordinates, evaluate,
+// split and add the mean terms).
+//   FRESH: first half of a tile (the chains start from zero); otherwise the
+//   finished chains of each row block are added into `outer` two blocks
+//   later (off the MFMA's result latency).
+template <int NC, bool FRESH, int DIAG>
+__device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn, const float (&xq)[NC],
+                                        const float (&yq)[NC], int g, float cexp, float msc, const KPieces<NC> &kb,
+                                        f32x4 (&acc)[NC][16], f32x4 (&outer)[NC][16], KPieces<NC> &nx,
+                                        double (&mu)[NC]) {
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    u32x4 a0 = lds_b128(pa), a1 = lds_b128(pa + kXPlane), a2 = lds_b128(pa + 2 * kXPlane);
+    // coordinates of pair 0; pair i+1's are read while pair i is built
+    f32x2v xk = lds_f2(pcn + g * 32), yk = lds_f2(pcn + 128 + g * 32), ak = lds_f2(pcn + 256 + g * 32);
+    f32x2v e[NC];
+#pragma unroll
+    for (int rb = 0; rb < 16; ++rb) {
+        u32x4 b0, b1, b2;
+        if (rb + 1 < 16) {
+            b0 = lds_b128(pa + (rb + 1) * 1024);
+            b1 = lds_b128(pa + kXPlane + (rb + 1) * 1024);
+            b2 = lds_b128(pa + 2 * kXPlane + (rb + 1) * 1024);
+        }
+        // ---- the next step's K*, pair i over row blocks 4i .. 4i+3:
+        // evaluate (two slots), split, mean terms + the next pair's coordinates
+        const int i = rb >> 2, ph = rb & 3;
+        if (DIAG & 1) {
+        } else if (ph <= 1) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                float ev = kstar1(ph == 0 ? xk.x : xk.y, ph == 0 ? yk.x : yk.y, xq[c], yq[c], cexp);
+                SBO_PIN(ev);
+                if (ph == 0) e[c].x = ev; else e[c].y = ev;
+            }
+        } else if (ph == 2) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                uint32_t w0, w1, w2;
+                split3(e[c].x, e[c].y, w0, w1, w2);
+                SBO_PIN(w0);
+                SBO_PIN(w1);
+                SBO_PIN(w2);
+                nx.h[c][i] = w0;
+                nx.m[c][i] = w1;
+                nx.l[c][i] = w2;
+            }
+        } else {
+            const f32x2v as = ak * msc;  // msc = 0: not the mean's row block
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                mu[c] = fma((double)as.x, (double)e[c].x, mu[c]);
+                mu[c] = fma((double)as.y, (double)e[c].y, mu[c]);
+                SBO_PIN(mu[c]);
+            }
+            if (i < 3) {
+                xk = lds_f2(pcn + g * 32 + (i + 1) * 8);
+                yk = lds_f2(pcn + 128 + g * 32 + (i + 1) * 8);
+                ak = lds_f2(pcn + 256 + g * 32 + (i + 1) * 8);
+            }
+        }
+        if (!FRESH && !(DIAG & 4) && rb > 1) {  // those chains finished a block ago
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                outer[c][rb - 2] += acc[c][rb - 2];
+                SBO_PIN_O(outer[c][rb - 2]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            f32x4 v = FRESH ? zero : acc[c][rb];
+            v = mfma(a2, kb.h[c], v);
+            v = mfma(a1, kb.m[c], v);
+            v = mfma(a0, kb.l[c], v);
+            v = mfma(a1, kb.h[c], v);
+            v = mfma(a0, kb.m[c], v);
+            v = mfma(a0, kb.h[c], v);
+            acc[c][rb] = v;
+        }
+        // interleave: each MFMA followed by two VALU and one LDS read, so the
+        // vector work issues in the matrix pipe's shadow (a bf16 MFMA holds
+        // the SIMD's issue for 8 of its 16 cycles)
+#pragma unroll
+        for (int j = 0; j < 6 * NC; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (rb + 1 < 16) {
+            a0 = b0;
+            a1 = b1;
+            a2 = b2;
+        }
+    }
+    if (!FRESH && !(DIAG & 4)) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            outer[c][14] += acc[c][14];
+            outer[c][15] += acc[c][15];
+            SBO_PIN_O(outer[c][14]);
+            SBO_PIN_O(outer[c][15]);
+        }
+    }
+}
+
+// K* pieces of one step directly (the prologue's first step)
+template <int NC>
+__device__ __forceinline__ void x3_kstar(const lds_char *pc, const float (&xq)[NC], const float (&yq)[NC], int g,
+                                         float cexp, bool mean, KPieces<NC> &kb, double (&mu)[NC]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f32x2v xk = lds_f2(pc + g * 32 + i * 8), yk = lds_f2(pc + 128 + g * 32 + i * 8);
+        const f32x2v ak = lds_f2(pc + 256 + g * 32 + i * 8);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const float e0 = kstar1(xk.x, yk.x, xq[c], yq[c], cexp), e1 = kstar1(xk.y, yk.y, xq[c], yq[c], cexp);
+            uint32_t w0, w1, w2;
+            split3(e0, e1, w0, w1, w2);
+            kb.h[c][i] = w0;
+            kb.m[c][i] = w1;
+            kb.l[c][i] = w2;
+            if (mean) {
+                mu[c] = fma((double)ak.x, (double)e0, mu[c]);
+                mu[c] = fma((double)ak.y, (double)e1, mu[c]);
+            }
+        }
+    }
+}
+
+// per staged step: row block, query block, and flags
+struct XStep {
+    int I, qb, flags;  // bit 0: second half, bit 1: first step of its item, bit 2: last step, bit 3: valid
+};
+constexpr int kFirst = 2, kLast = 4, kValid = 8;
+
+// The persistent sweep.  NC = 1: eight waves (two per SIMD), wave w owns
+// queries 16w .. 16w+15; NC = 2: four waves (one per SIMD), wave w owns
+// queries 32w .. 32w+31.  Every wave loads an equal share of each stage.
+// DIAG (timing diagnostics only, results wrong): 1 no next-step K*, 2 no A
+// pieces staged, 4 no outer sums.
+template <int NC, int DIAG>
+__global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
+    const char *__restrict__ ax3, const float *__restrict__ kc3, const int4 *__restrict__ desc,
+    const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P, int n_items, int nI,
+    const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp, float cexp, float m0,
+    float *__restrict__ part, float *__restrict__ mean) {
+    __shared__ __attribute__((aligned(16))) char smem[kXSmem];
+    constexpr int kLoaders = 8 / NC;                  // waves
+    constexpr int kPieces = (kXA / 1024) / kLoaders;  // A pieces per wave per stage (6 or 12)
+    static_assert(kPieces == 6 || kPieces == 12, "the end-of-step wait below counts 6 or 12 pieces");
+    const int bid = blockIdx.x;
+    const int rng = (P % 8 == 0) ? (bid % 8) * (P / 8) + bid / 8 : bid;
+    const int k0 = max(seg[rng], 0), k1 = min(seg[rng + 1], n_items);
+    if (k0 >= k1) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int lw = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave = loader index
+    const int g = lane >> 4, r = lane & 15;
+
+    const lds_char *lds = (const lds_char *)smem;
+    const int4 *dwin = reinterpret_cast<const int4 *>(smem + kXWin);
+    const unsigned short *lwin = reinterpret_cast<const unsigned short *>(smem + kXWin + 2048);
+    // LDS-DMA with an SGPR base (global_load_lds_dwordx4 v_off, s_base): the
+    // only per-lane operand is the byte offset lane*16
+    const uint32_t voff = (uint32_t)lane * 16u;
+    const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
+    const uint32_t lds_wave = lds_smem + (uint32_t)lw * 1024u;
+    const uint32_t lds_dwin = lds_smem + (uint32_t)kXWin;
+    const uint32_t lds_lwin = lds_dwin + 2048u;
+#define SBO_DMA16(sbase, ldst)                                                                          \
+    do {                                                                                                \
+        uint32_t keep_;                                                                                 \
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t" \
+                     "s_mov_b32 m0, %0"                                                                 \
+                     : "=&s"(keep_)                                                                     \
+                     : "v"(voff), "s"((const void *)(sbase)), "s"(ldst)                                 \
+                     : "memory");                                                                       \
+    } while (0)
+    // one half-tile stage into LDS slot `sl`: wave 0 brings the item's
+    // queries (lanes 0-31 qx, 32-63 qy) and the half-tile's coordinates
+    // first, then every wave its A pieces (the youngest kPieces of its
+    // vector-memory operations)
+#define SBO_X3_STAGE(Tg_, t_, h_, qb_, sl_)                                                             \
+    do {                                                                                                \
+        const uint32_t d_ = lds_smem + (uint32_t)(sl_) * kXSlot;                                        \
+        if (lw == 0) {                                                                                  \
+            if (lane < 32) SBO_DMA16(qx + (int64_t)(qb_) * kBN, d_ + kXA + kXC);                        \
+            else SBO_DMA16(qy + (int64_t)(qb_) * kBN - 128, d_ + kXA + kXC);                            \
+            if (lane < 32) SBO_DMA16(kc3 + (int64_t)(t_) * (2 * kXC / 4) + (h_) * (kXC / 4), d_ + kXA);  \
+        }                                                                                               \
+        const char *s_ = ax3 + ((Tg_) * 2 + (h_)) * (int64_t)kXA + lw * 1024;                          \
+        const uint32_t w_ = lds_wave + (uint32_t)(sl_) * kXSlot;                                        \
+        if (!(DIAG & 2))                                                                                \
+            _Pragma("unroll") for (int j = 0; j < kPieces; ++j)                                         \
+                SBO_DMA16(s_ + j * kLoaders * 1024, w_ + (uint32_t)(j * kLoaders * 1024));              \
+    } while (0)
+#define SBO_DESC_WINDOW(w_)                                                                             \
+    do {                                                                                                \
+        if (lw == 1) SBO_DMA16(reinterpret_cast<const char *>(desc) + (int64_t)(w_) * 1024, lds_dwin + (uint32_t)((w_) & 1) * 1024u);     \
+    } while (0)
+#define SBO_LIST_WINDOW(w_)                                                                             \
+    do {                                                                                                \
+        if (lw == 2) SBO_DMA16(reinterpret_cast<const char *>(tl) + (int64_t)(w_) * 1024, lds_lwin + (uint32_t)((w_) & 1) * 1024u);     \
+    } while (0)
+    auto desc_at = [&](int k) {
+        const int4 d = dwin[((k / kDescWin) & 1) * kDescWin + k % kDescWin];
+        const int I = min(max(__builtin_amdgcn_readfirstlane(d.x), 0), nI - 1);
+        return make_int4(I, __builtin_amdgcn_readfirstlane(d.y), __builtin_amdgcn_readfirstlane(d.z),
+                         __builtin_amdgcn_readfirstlane(d.w));
+    };
+    auto entry_off = [](const int4 &d) { return (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32); };
+    auto list_at = [&](uint64_t e, int I) {
+        const int t = __builtin_amdgcn_readfirstlane((int)lwin[((e / kListWin) & 1) * kListWin + e % kListWin]);
+        return min(t, kTilesPerRowBlockStep * (I + 1) - 1);
+    };
+
+    // ---- lookahead cursor: the step being staged
+    SBO_DESC_WINDOW(k0 / kDescWin);
+    SBO_DESC_WINDOW(k0 / kDescWin + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int la_k = k0, la_j = 0, la_h = 0;
+    int4 la_d = desc_at(k0);
+    uint64_t la_e = entry_off(la_d);
+    SBO_LIST_WINDOW(la_e / kListWin);
+    SBO_LIST_WINDOW(la_e / kListWin + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    auto stage = [&](int sl) {
+        const int cnt = la_d.w & 0xffff;
+        XStep s;
+        s.I = la_d.x;
+        s.qb = la_d.y;
+        s.flags = la_h | (la_j == 0 && la_h == 0 ? kFirst : 0) | (la_j == cnt - 1 && la_h == 1 ? kLast : 0) | kValid;
+        const int t = list_at(la_e, la_d.x);
+        SBO_X3_STAGE(tile_start(la_d.x) + t, t, la_h, la_d.y, sl);
+        la_h ^= 1;
+        if (la_h == 0) {
+            ++la_j;
+            ++la_e;
+            if (la_j >= cnt) {
+                ++la_k;
+                la_j = 0;
+                if (la_k < k1) {
+                    la_d = desc_at(la_k);
+                    if (la_k % kDescWin == 0) SBO_DESC_WINDOW(la_k / kDescWin + 1);
+                }
+            }
+            if (la_e % kListWin == 0) SBO_LIST_WINDOW(la_e / kListWin + 1);
+        }
+        return s;
+    };
+
+    XStep s0 = stage(0), s1 = {0, 0, 0}, s2 = {0, 0, 0};
+    if (la_k < k1) s1 = stage(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const int qo = lw * 16 * NC + r;  // the lane's queries in the block: qo + 16 c
+    f32x4 acc[NC][16], outer[NC][16];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int rb = 0; rb < 16; ++rb) {
+            acc[c][rb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            outer[c][rb] = acc[c][rb];
+        }
+    double mu[NC];
+    KPieces<NC> kb, nx;
+    {
+        const lds_char *pq = lds + kXA + kXC;
+        float xq[NC], yq[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            mu[c] = 0.0;
+            xq[c] = lds_f(pq + (qo + 16 * c) * 4);
+            yq[c] = lds_f(pq + (kBN + qo + 16 * c) * 4);
+        }
+        x3_kstar<NC>(lds + kXA, xq, yq, g, cexp, s0.I == nI - 1, kb, mu);
+    }
+    // deferred outputs of the item finished in the previous step (stored at
+    // the top of the next step, before its stage DMA, so that the vmcnt count
+    // at the end of every step is the A pieces of one stage)
+    bool pend = false, pend_mean = false;
+    float pend_s[NC], pend_mu[NC];
+    int64_t pend_q = 0;
+    int pend_I = 0;
+    auto flush = [&]() {
+        if (pend && lane < 16) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int64_t q = pend_q + 16 * c;
+                if (q < m) {
+                    part[(int64_t)pend_I * ldp + q] = pend_s[c];
+                    if (pend_mean) mean[q] = pend_mu[c];
+                }
+            }
+        }
+        pend = false;
+    };
+    int cur = 0;
+    bool more = true;
+    // one half-step; items are whole tiles, so the steps alternate FRESH
+    // (first half: chains from zero) and second halves (which may end an item)
+    auto half_step = [&](auto fresh_tag) {
+        constexpr bool FRESH = decltype(fresh_tag)::value;
+        if (FRESH) flush();
+        const bool issue = la_k < k1;
+        const int nslot = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
+        s2 = issue ? stage(nslot) : XStep{0, 0, 0};
+        const int cslot = cur == 2 ? 0 : cur + 1;  // (cur + 1) % 3: the next step's coordinates
+        const lds_char *pa = lds + cur * kXSlot + lane * 16;
+        const lds_char *pcn = lds + cslot * kXSlot + kXA;
+        const lds_char *pqn = pcn + kXC;
+        const bool nvalid = (s1.flags & kValid) != 0;
+        const float msc = nvalid && s1.I == nI - 1 ? 1.0f : 0.0f;
+        if (!FRESH) {
+            // this step may end its item: the item's mean terms are all in
+            // (its K* were built one step ahead); close it before the next
+            // item's terms start
+            if ((s0.flags & kLast) && s0.I == nI - 1) {
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    double u = mu[c];
+                    u += __shfl_xor(u, 16);
+                    u += __shfl_xor(u, 32);
+                    pend_mu[c] = (float)((double)m0 + u);
+                }
+            }
+            if (nvalid && (s1.flags & kFirst))
+#pragma unroll
+                for (int c = 0; c < NC; ++c) mu[c] = 0.0;
+        }
+        float xq[NC], yq[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            xq[c] = lds_f(pqn + (qo + 16 * c) * 4);
+            yq[c] = lds_f(pqn + (kBN + qo + 16 * c) * 4);
+        }
+        x3_half<NC, FRESH, DIAG>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu);
+        if (!FRESH && (s0.flags & kLast)) {
+            // item done: column sums of V^2 over its rows (lanes l, l+16, l+32,
+            // l+48 hold four row quarters of column l&15 of every block)
+            pend = true;
+            pend_I = s0.I;
+            pend_q = (int64_t)s0.qb * kBN + qo;
+            pend_mean = s0.I == nI - 1;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                double sv = 0.0;
+#pragma unroll
+                for (int rb = 0; rb < 16; ++rb)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        sv = fma((double)outer[c][rb][e], (double)outer[c][rb][e], sv);
+                        outer[c][rb][e] = 0.0f;
+                    }
+                sv += __shfl_xor(sv, 16);
+                sv += __shfl_xor(sv, 32);
+                pend_s[c] = (float)sv;
+            }
+        }
+        // retire stage i+1: its queries and coordinates (wave 0) precede its
+        // A pieces and were retired one step earlier; leave stage i+2's A in flight
+        if (issue) {
+            if constexpr (kPieces == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        more = nvalid;
+        s0 = s1;
+        s1 = s2;
+        kb = nx;
+        cur = cslot;
+    };
+    do {
+        half_step(std::integral_constant<bool, true>{});
+        half_step(std::integral_constant<bool, false>{});
+    } while (more);
+    flush();
+#undef SBO_X3_STAGE
+#undef SBO_DESC_WINDOW
+#undef SBO_LIST_WINDOW
+#undef SBO_DMA16
+}
+
+// Split the f32 packed operand (tiles T0 .. T1-1, tile_offset layout) into
+// the three bf16 planes of the x3 layout: tile T, half h, plane p, row block
+// rb, lane l = 16 g + r holds A[16 rb + r][32 h + 8 g + j], j = 0..7, at
+// byte T*2*kXA + h*kXA + p*kXPlane + rb*1024 + l*16 + 2j.
+__global__ __launch_bounds__(256) void pack_x3_kernel(const float *__restrict__ aug, int64_t T0, int64_t nt,
+                                                      char *__restrict__ ax3) {
+    const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (id >= nt * 2048) return;
+    const int lane = (int)(id & 63), rb = (int)((id >> 6) & 15), h = (int)((id >> 10) & 1);
+    const int64_t T = T0 + (id >> 11);
+    const int r = lane & 15, g = lane >> 4, row = rb * 16 + r;
+    const float *src = aug + T * kTileFloats;
+    u32x4 w0, w1, w2;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int k = kXH * h + 8 * g + 2 * d;
+        uint32_t a, b, c;
+        split3(src[tile_offset(k, row)], src[tile_offset(k + 1, row)], a, b, c);
+        w0[d] = a;
+        w1[d] = b;
+        w2[d] = c;
+    }
+    char *dst = ax3 + T * (2 * kXA) + h * kXA + rb * 1024 + lane * 16;
+    *reinterpret_cast<u32x4 *>(dst) = w0;
+    *reinterpret_cast<u32x4 *>(dst + kXPlane) = w1;
+    *reinterpret_cast<u32x4 *>(dst + 2 * kXPlane) = w2;
+}
+
+// Per k-tile coordinates in natural order per half: kc3[t*256 + h*128 + c*32 + i]
+// = (x, y, sf2 alpha, 0)[c] of k = 64t + 32h + i, from the kcoord layout
+// (k = 4p + g of a tile at g*16 + p).
+__global__ void pack_kc3_kernel(const float *__restrict__ kcoord, int64_t nkt, float *__restrict__ kc3) {
+    const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (id >= nkt * 256) return;
+    const int64_t t = id >> 8;
+    const int o = (int)(id & 255), h = o >> 7, c = (o >> 5) & 3, i = o & 31;
+    const int kk = kXH * h + i;
+    kc3[id] = c < 3 ? kcoord[t * (3 * kBK) + c * kBK + (kk & 3) * 16 + (kk >> 2)] : 0.0f;
+}
+
+}  // namespace
+
+size_t x3_operand_bytes(int64_t npad) { return (size_t)total_tiles(npad / kBM) * 2 * kXA; }
+size_t x3_coord_bytes(int64_t npad) { return (size_t)(npad / kBK) * 256 * sizeof(float); }
+
+hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, int64_t I0, char *ax3,
+                          float *kc3) {
+    const int64_t nI = npad / kBM;
+    const int64_t T0 = tile_start(I0), T1 = tile_start(nI);
+    if (T1 > T0) {
+        const int64_t th = (T1 - T0) * 2048;
+        hipLaunchKernelGGL(pack_x3_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, aug, T0, T1 - T0, ax3);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    const int64_t nkt = npad / kBK;
+    hipLaunchKernelGGL(pack_kc3_kernel, dim3((unsigned)((nkt * 256 + 255) / 256)), dim3(256), 0, s, kcoord, nkt, kc3);
+    return hipGetLastError();
+}
+
+hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, const int4 *desc,
+                             const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
+                             const float *qy, int64_t m, int64_t ldp, float cexp, float m0, float *part, float *mean,
+                             int variant) {
+#define SBO_X3_LAUNCH(NC, D) \
+    hipLaunchKernelGGL((predict_x3_kernel<NC, D>), dim3((unsigned)P), dim3(64 * 8 / NC), 0, s, ax3, kc3, desc, tl, \
+                       seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean)
+    switch (variant) {
+        case 3: SBO_X3_LAUNCH(1, 0); break;
+        case 4: SBO_X3_LAUNCH(2, 1); break;
+        case 5: SBO_X3_LAUNCH(2, 2); break;
+        case 6: SBO_X3_LAUNCH(1, 1); break;
+        case 7: SBO_X3_LAUNCH(1, 2); break;
+        default: SBO_X3_LAUNCH(2, 0); break;
+    }
+#undef SBO_X3_LAUNCH
+    return hipGetLastError();
+}
+
+}  // namespace sbo

@@ -53,13 +53,13 @@ size_t query_order_bytes(int64_t m) {
     size_t temp = 0;
     (void)rocprim::radix_sort_pairs(nullptr, temp, (uint32_t *)nullptr, (uint32_t *)nullptr, (int32_t *)nullptr,
                               (int32_t *)nullptr, (size_t)m, 0, 32, nullptr);
-    const size_t a = (size_t)round_up(m, 64);
+    const size_t a = (size_t)round_up(m, kBN);  // gathered coordinates padded to whole query blocks
     return 4 * a * 4 + 2 * a * 4 + round_up((int64_t)temp, 256);
 }
 
 hipError_t launch_query_order(hipStream_t s, const float *qx, const float *qy, int64_t m, const float bbox[4],
                               void *work, size_t work_bytes, int32_t **perm_out, float **sqx, float **sqy) {
-    const size_t a = (size_t)round_up(m, 64);
+    const size_t a = (size_t)round_up(m, kBN);  // gathered coordinates padded to whole query blocks
     char *p = static_cast<char *>(work);
     uint32_t *code_in = reinterpret_cast<uint32_t *>(p);
     uint32_t *code_out = code_in + a;

@@ -360,6 +360,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     if (hinfo != 0) ctx->linv_n = 0;
     SBO_CHECK(hinfo == 0, SBO_E_NOT_SPD, "trtri: singular factor (info=" + std::to_string(hinfo) + ")");
     ctx->npad = npad;
+    ctx->x3_I0 = std::min(ctx->x3_I0, I0);  // the split operand is derived lazily (run_tick)
     ctx->fitted = true;
     return SBO_OK;
 }
@@ -419,7 +420,39 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
                              (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan, ctx->part.as<float>(),
                              ctx->mean.as<float>(), ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr, P,
                              ctx->plan_work.as<void>(), ctx->plan_work.capacity()));
-    {
+    if (ctx->kernel_variant >= 2) {
+        // split-operand sweep: derive the bf16 planes of any repacked row
+        // block, and give the kernel whole 128-query blocks to read
+        const int64_t nIc = ctx->npad / sbo::kBM;
+        if (ctx->x3_I0 < nIc) {
+            const int64_t I0 = std::max<int64_t>(ctx->x3_I0, 0);
+            SBO_HIP(grow_keep(ctx, ctx->ax3, sbo::x3_operand_bytes(ctx->npad),
+                              sbo::x3_operand_bytes(I0 * sbo::kBM)));
+            SBO_HIP(ctx->kc3.reserve(sbo::x3_coord_bytes(ctx->npad)));
+            SBO_HIP(sbo::launch_pack_x3(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(), ctx->npad, I0,
+                                        ctx->ax3.as<char>(), ctx->kc3.as<float>()));
+            ctx->x3_I0 = INT64_MAX;
+        }
+        if (!perm) {
+            const int64_t mp = sbo::round_up(m, sbo::kBN);
+            SBO_HIP(ctx->qpad.reserve(sizeof(float) * 2 * (size_t)mp));
+            float *px = ctx->qpad.as<float>(), *py = px + mp;
+            SBO_HIP(hipMemcpyAsync(px, qx, sizeof(float) * (size_t)m, hipMemcpyDeviceToDevice, ctx->stream));
+            SBO_HIP(hipMemcpyAsync(py, qy, sizeof(float) * (size_t)m, hipMemcpyDeviceToDevice, ctx->stream));
+            qx = px;
+            qy = py;
+        }
+        const int4 *desc = nullptr;
+        const unsigned short *tl = nullptr;
+        const int *seg = nullptr;
+        sbo::plan_views(ctx->npad, m, P, ctx->plan_work.as<void>(), &desc, &tl, &seg);
+        Bracket br(ctx, ctx->ev_predict);
+        SBO_HIP(sbo::launch_predict_x3(ctx->stream, ctx->ax3.as<char>(), ctx->kc3.as<float>(), desc, tl, seg, P,
+                                       (int)(nIc * ((m + sbo::kBN - 1) / sbo::kBN)), (int)nIc, qx, qy, m, ldp,
+                                       sbo::exp2_coef_f((float)ctx->hyper.length_scale),
+                                       (float)ctx->hyper.prior_mean, ctx->part.as<float>(), ctx->mean.as<float>(),
+                                       ctx->kernel_variant));
+    } else {
         Bracket br(ctx, ctx->ev_predict);
         SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(), ctx->npad, qx, qy,
                                     m, ldp, (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean,
@@ -843,7 +876,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->sweep_groups = (int)value;
             return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
-            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be 0 or 1");
+            SBO_CHECK(value >= 0 && value <= 7, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 7]");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
         case SBO_OPT_TILE_SKIP:
@@ -1106,6 +1139,7 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
     ctx->auto_skip_mean_log2 = h.auto_skip_mean_log2;
     ctx->lg_tau_v = h.lg_tau_v;
     ctx->spatial_order = h.spatial_order;
+    ctx->x3_I0 = 0;
     ctx->fitted = true;
     return SBO_OK;
 }

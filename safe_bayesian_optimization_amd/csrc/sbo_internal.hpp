@@ -116,6 +116,9 @@ struct sbo_ctx {
     sbo::DevBuf alpha;           // K^-1 (y - m0), length cap
     sbo::DevBuf aug;             // packed sf2 * L^-1 tiles
     sbo::DevBuf kcoord;          // per k-tile: x[BK], y[BK], sf2*alpha[BK]
+    sbo::DevBuf ax3, kc3;        // split (bf16 x3) operand and its coordinates (kernel variants 2, 3)
+    int64_t x3_I0 = 0;           // first row block whose split operand is stale (>= nI: current)
+    sbo::DevBuf qpad;            // queries padded to whole blocks (split sweep without query ordering)
     sbo::DevBuf info;            // rocSOLVER info
     sbo::DevBuf scratch;         // append workspace
     int64_t npad = 0;            // rows/cols of the packed operand (multiple of BM)
@@ -188,6 +191,25 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
 hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, const float *qx,
                           const float *qy, int64_t m, int64_t ldp, float ell, float m0, float *part, float *mean,
                           int variant, int P, const void *work);
+// exp2 coefficient of the RBF kernel: k = exp2(cexp d^2), cexp = -1/(2 l^2 ln 2)
+float exp2_coef_f(float ell);
+// The plan's descriptors, tile lists and per-workgroup ranges inside `work`.
+void plan_views(int64_t npad, int64_t m, int P, const void *work, const int4 **desc, const unsigned short **tl,
+                const int **seg);
+// Split-operand (bf16 x3) predictive sweep, predict_x3.hip: the packed
+// operand split into three bf16 planes per half-tile and the per-k-tile
+// coordinates in natural order, for row blocks >= I0 (coordinates: all).
+size_t x3_operand_bytes(int64_t npad);
+size_t x3_coord_bytes(int64_t npad);
+hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, int64_t I0, char *ax3,
+                          float *kc3);
+// The sweep over the plan with the split operand; qx/qy must be readable in
+// whole 128-query blocks (padded to round_up(m, kBN)).  variant: 2 (4-7:
+// timing diagnostics with parts of the work left out).
+hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, const int4 *desc,
+                             const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
+                             const float *qy, int64_t m, int64_t ldp, float cexp, float m0, float *part, float *mean,
+                             int variant);
 // lgn[tile_start(I) + t] = log2 min(16 max_r |A_It[r]|_1, 8 |A_It|_F) (f64 sums,
 // rounded up) for row blocks I >= I0 (-1000 for an all-zero tile).
 hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float *lgn);
