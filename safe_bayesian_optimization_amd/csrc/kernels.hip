@@ -624,6 +624,68 @@ __global__ void plan_seg_kernel(const unsigned long long *__restrict__ scan, int
     if (threadIdx.x == 0 && tiles_done) atomicAdd(tiles_done, (unsigned long long)total);
 }
 
+// XCD-interleaved item order (P a multiple of 8).  The sweep's workgroup b
+// runs on XCD b % 8, and an XCD's 32 CUs share one L2: with contiguous
+// per-workgroup ranges they work on 32 far-apart items at once and share no
+// A tile (the staged bytes all come from beyond L2).  Instead each XCD takes
+// one tile-balanced contiguous chunk [a, b) of the item list (plan_seg with
+// 8 ranges, xseg), and its G = P/8 workgroups take the chunk's items
+// round-robin -- slot c runs items a + c, a + c + G, ... -- so at any time
+// they sweep G neighbouring items (same row block, Morton-adjacent query
+// blocks, mostly the same k-tiles).  The descriptors and tile lists are
+// permuted so that every workgroup's items stay contiguous (the sweep walks
+// one contiguous range either way).
+__device__ __forceinline__ int64_t xcd_position(int64_t k, const int *__restrict__ xseg, int G) {
+    int x = 0;
+#pragma unroll
+    for (int i = 1; i < 8; ++i) x += k >= xseg[i] ? 1 : 0;
+    const int64_t a = xseg[x], n = xseg[x + 1] - a, q = n / G, rm = n % G, c = (k - a) % G, j = (k - a) / G;
+    return a + c * q + (c < rm ? c : rm) + j;
+}
+
+__global__ void plan_perm_kernel(const unsigned long long *__restrict__ scan, int64_t n_items,
+                                 const int4 *__restrict__ desc, const int *__restrict__ xseg, int G,
+                                 int *__restrict__ pos_of, unsigned long long *__restrict__ cnt2) {
+    const int64_t nne = (int64_t)(scan[n_items - 1] >> kPlanKeyShift);
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nne) return;
+    const int64_t p = xcd_position(k, xseg, G);
+    pos_of[k] = (int)p;
+    cnt2[p] = (unsigned long long)(desc[k].w & 0xffff);
+}
+
+// one wave per item: its tile list to the new offset, its descriptor to its new position
+__global__ __launch_bounds__(256) void plan_move_kernel(const unsigned long long *__restrict__ scan, int64_t n_items,
+                                                        const int4 *__restrict__ desc,
+                                                        const unsigned short *__restrict__ tl,
+                                                        const int *__restrict__ pos_of,
+                                                        const unsigned long long *__restrict__ off2,
+                                                        int4 *__restrict__ desc2, unsigned short *__restrict__ tl2) {
+    const int64_t nne = (int64_t)(scan[n_items - 1] >> kPlanKeyShift);
+    const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (k >= nne) return;
+    const int4 d = desc[k];
+    const int cnt = d.w & 0xffff;
+    const uint64_t off = (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
+    const int p = pos_of[k];
+    const uint64_t o2 = off2[p];
+    for (int i = lane; i < cnt; i += 64) tl2[o2 + i] = tl[off + i];
+    if (lane == 0) desc2[p] = make_int4(d.x, d.y, (int)(uint32_t)o2, cnt | (int)((o2 >> 32) << 16));
+}
+
+__global__ void plan_seg2_kernel(const int *__restrict__ xseg, int G, int P, int *__restrict__ seg2) {
+    for (int r = threadIdx.x; r <= P; r += blockDim.x) {
+        if (r == P) {
+            seg2[P] = xseg[8];
+            continue;
+        }
+        const int x = r / G, c = r % G;
+        const int a = xseg[x], n = xseg[x + 1] - a, q = n / G, rm = n % G;
+        seg2[r] = a + c * q + (c < rm ? c : rm);
+    }
+}
+
 // ---- the sweep (persistent: one workgroup per CU)
 // OT: outer (cross-tile) accumulator type.  Workgroup b walks the item range
 // r(b) of the plan; consecutive ranges go to one XCD (blocks are dealt to the
@@ -1084,8 +1146,14 @@ hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int6
 
 namespace {
 struct PlanLayout {
-    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes, total;
+    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes;
+    // XCD-interleaved order (P % 8 == 0): the sweep reads desc2 / tl2 / seg2
+    bool xcd;
+    size_t xseg, pos_of, cnt2, off2, desc2, tl2, seg2, temp2, temp2_bytes;
+    size_t total;
 };
+
+bool xcd_interleave(int P) { return P >= 8 && P % 8 == 0; }
 
 PlanLayout plan_layout(int64_t nI, int64_t nQ, int P) {
     const int64_t items = nI * nQ;
@@ -1108,6 +1176,21 @@ PlanLayout plan_layout(int64_t nI, int64_t nQ, int P) {
                                   (size_t)items, rocprim::plus<unsigned long long>());
     L.temp = take(tb);
     L.temp_bytes = tb;
+    L.xcd = xcd_interleave(P);
+    if (L.xcd) {
+        L.xseg = take(4 * 9);
+        L.pos_of = take(4 * (size_t)items);
+        L.cnt2 = take(8 * (size_t)items);
+        L.off2 = take(8 * (size_t)items);
+        L.desc2 = take(16 * (size_t)(items + 2 * kDescWindow));
+        L.tl2 = take(2 * (size_t)(cap + 2 * kListWindow));
+        L.seg2 = take(4 * (size_t)(P + 1));
+        size_t t2 = 0;
+        (void)rocprim::exclusive_scan(nullptr, t2, (const unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                                      0ull, (size_t)items, rocprim::plus<unsigned long long>());
+        L.temp2 = take(t2);
+        L.temp2_bytes = t2;
+    }
     L.total = o;
     return L;
 }
@@ -1157,7 +1240,33 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, lgn, nI, nQ, qx, qy,
                        m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, key, scan, thr, desc, tl);
-    hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done);
+    if (!L.xcd) {
+        hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done);
+        return hipGetLastError();
+    }
+    auto *xseg = reinterpret_cast<int *>(w + L.xseg);
+    auto *pos_of = reinterpret_cast<int *>(w + L.pos_of);
+    auto *cnt2 = reinterpret_cast<unsigned long long *>(w + L.cnt2);
+    auto *off2 = reinterpret_cast<unsigned long long *>(w + L.off2);
+    auto *desc2 = reinterpret_cast<int4 *>(w + L.desc2);
+    auto *tl2 = reinterpret_cast<unsigned short *>(w + L.tl2);
+    auto *seg2 = reinterpret_cast<int *>(w + L.seg2);
+    const int G = P / 8;
+    // (positions past the last non-empty item keep count 0 for the scan)
+    e = hipMemsetAsync(cnt2, 0, 8 * (size_t)items, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, 8, xseg, tiles_done);
+    hipLaunchKernelGGL(plan_perm_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, scan, items, desc,
+                       xseg, G, pos_of, cnt2);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t t2 = L.temp2_bytes;
+    e = rocprim::exclusive_scan(w + L.temp2, t2, cnt2, off2, 0ull, (size_t)items,
+                                rocprim::plus<unsigned long long>(), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(plan_move_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, scan, items, desc, tl,
+                       pos_of, off2, desc2, tl2);
+    hipLaunchKernelGGL(plan_seg2_kernel, dim3(1), dim3(256), 0, s, xseg, G, P, seg2);
     return hipGetLastError();
 }
 
@@ -1165,9 +1274,9 @@ void plan_views(int64_t npad, int64_t m, int P, const void *work, const int4 **d
                 const int **seg) {
     const PlanLayout L = plan_layout(npad / kBM, (m + kBN - 1) / kBN, P);
     const char *w = static_cast<const char *>(work);
-    *desc = reinterpret_cast<const int4 *>(w + L.desc);
-    *tl = reinterpret_cast<const unsigned short *>(w + L.tl);
-    *seg = reinterpret_cast<const int *>(w + L.seg);
+    *desc = reinterpret_cast<const int4 *>(w + (L.xcd ? L.desc2 : L.desc));
+    *tl = reinterpret_cast<const unsigned short *>(w + (L.xcd ? L.tl2 : L.tl));
+    *seg = reinterpret_cast<const int *>(w + (L.xcd ? L.seg2 : L.seg));
 }
 
 float exp2_coef_f(float ell) { return (float)exp2_coef(ell); }
@@ -1178,11 +1287,10 @@ hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, 
     const int nI = (int)(npad / kBM);
     const int64_t nQ = (m + kBN - 1) / kBN;
     if (m <= 0 || nI <= 0) return hipSuccess;
-    const PlanLayout L = plan_layout(nI, nQ, P);
-    const char *w = static_cast<const char *>(work);
-    const auto *desc = reinterpret_cast<const int4 *>(w + L.desc);
-    const auto *tl = reinterpret_cast<const unsigned short *>(w + L.tl);
-    const auto *seg = reinterpret_cast<const int *>(w + L.seg);
+    const int4 *desc = nullptr;
+    const unsigned short *tl = nullptr;
+    const int *seg = nullptr;
+    plan_views(npad, m, P, work, &desc, &tl, &seg);
     const float cexp = (float)exp2_coef(ell);
 #define SBO_PREDICT_ARGS aug, kcoord, desc, tl, seg, P, (int)(nI * nQ), nI, qx, qy, m, ldp, cexp, m0, part, mean
     switch (variant) {

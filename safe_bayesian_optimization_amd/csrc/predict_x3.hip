@@ -257,7 +257,7 @@ constexpr int kFirst = 2, kLast = 4, kValid = 8;
 // queries 16w .. 16w+15; NC = 2: four waves (one per SIMD), wave w owns
 // queries 32w .. 32w+31.  Every wave loads an equal share of each stage.
 // DIAG (timing diagnostics only, results wrong): 1 no next-step K*, 2 no A
-// pieces staged, 4 no outer sums.
+// pieces staged, 4 no outer sums, 8 every A stage from the first tile (L2-resident).
 template <int NC, int DIAG>
 __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
     const char *__restrict__ ax3, const float *__restrict__ kc3, const int4 *__restrict__ desc,
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
             else SBO_DMA16(qy + (int64_t)(qb_) * kBN - 128, d_ + kXA + kXC);                            \
             if (lane < 32) SBO_DMA16(kc3 + (int64_t)(t_) * (2 * kXC / 4) + (h_) * (kXC / 4), d_ + kXA);  \
         }                                                                                               \
-        const char *s_ = ax3 + ((Tg_) * 2 + (h_)) * (int64_t)kXA + lw * 1024;                          \
+        const char *s_ = ax3 + ((DIAG & 8) ? 0 : ((Tg_) * 2 + (h_)) * (int64_t)kXA) + lw * 1024;       \
         const uint32_t w_ = lds_wave + (uint32_t)(sl_) * kXSlot;                                        \
         if (!(DIAG & 2))                                                                                \
             _Pragma("unroll") for (int j = 0; j < kPieces; ++j)                                         \
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
         }
         // retire stage i+1: its queries and coordinates (wave 0) precede its
         // A pieces and were retired one step earlier; leave stage i+2's A in flight
-        if (issue) {
+        if (issue && !(DIAG & 2)) {
             if constexpr (kPieces == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         } else {
@@ -579,6 +579,7 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 5: SBO_X3_LAUNCH(2, 2); break;
         case 6: SBO_X3_LAUNCH(1, 1); break;
         case 7: SBO_X3_LAUNCH(1, 2); break;
+        case 8: SBO_X3_LAUNCH(1, 8); break;
         default: SBO_X3_LAUNCH(2, 0); break;
     }
 #undef SBO_X3_LAUNCH

@@ -409,7 +409,47 @@ def test_sweep_partition_and_outer_variant(mapper):
     with pytest.raises(N.SboError):
         gm.set_option(N.SBO_OPT_SWEEP_GROUPS, -1)
     with pytest.raises(N.SboError):
-        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 2)
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 9)
+
+
+@pytest.mark.parametrize("variant", [2, 3])
+def test_split_operand_sweep(mapper, variant):
+    """The split-operand (bf16 x3) sweep: bitwise the same for every
+    partition of the plan (1, 3, 7, 8, 1000 workgroups, and one per CU with
+    the XCD-interleaved item order), for the budgeted, a fixed and the dense
+    cutoff; within the contract of the f32 sweep and of the fp64 oracle given
+    the device factor; the mean is the f32 sweep's (f64-accumulated in both)."""
+    wl = synthetic(5000, 90, 70, seed=23)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    for skip in (-1, 40, 0):
+        gm.set_option(N.SBO_OPT_TILE_SKIP, skip)
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 0)
+        gm.set_option(N.SBO_OPT_SWEEP_GROUPS, 0)
+        mu32, sd32 = gm.predict(wl.qx, wl.qy)
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, variant)
+        res = {}
+        for groups in (0, 1, 3, 7, 8, 1000):
+            gm.set_option(N.SBO_OPT_SWEEP_GROUPS, groups)
+            res[groups] = gm.predict(wl.qx, wl.qy)
+        for groups in (1, 3, 7, 8, 1000):
+            assert np.array_equal(res[groups][0], res[0][0]) and np.array_equal(res[groups][1], res[0][1]), (skip, groups)
+        mu, sd = res[0]
+        assert nrel(mu, mu32.astype(np.float64)) < 1e-6
+        assert nrel(sd.astype(np.float64) ** 2, sd32.astype(np.float64) ** 2) < 1e-5
+    gm.set_option(N.SBO_OPT_SWEEP_GROUPS, 0)
+    gm.set_option(N.SBO_OPT_TILE_SKIP, -1)
+    # vs the fp64 oracle given the device factor
+    L, alpha = gm.factor()
+    o = gm.order()
+    sel = np.arange(0, wl.qx.size, 7)
+    omu, ovar = O.predict(O.colmajor_from_lower(L.astype(np.float64)), alpha.astype(np.float64),
+                          wl.x.astype(np.float32)[o], wl.y.astype(np.float32)[o], wl.qx.astype(np.float32)[sel],
+                          wl.qy.astype(np.float32)[sel], wl.hyper.length_scale, wl.hyper.sf2, wl.hyper.prior_mean)
+    mu, sd = gm.predict(wl.qx, wl.qy)
+    assert nrel(mu[sel].astype(np.float64), omu) < 1e-5
+    assert nrel(sd[sel].astype(np.float64) ** 2, ovar) < 1e-5
+    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 0)
 
 
 def test_spatial_order_does_not_change_the_posterior(mapper):

@@ -13,7 +13,7 @@ def main(d, cus=256):
     per = {}
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "predict_kernel" not in r["Kernel_Name"]:
+            if "predict_kernel" not in r["Kernel_Name"] and "predict_x3_kernel" not in r["Kernel_Name"]:
                 continue
             e = per.setdefault(r["Dispatch_Id"], {"ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
             e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -26,8 +26,8 @@ def main(d, cus=256):
             if "SQ_VALU_MFMA_BUSY_CYCLES" in e:
                 busy = e["SQ_VALU_MFMA_BUSY_CYCLES"] / (e["GRBM_GUI_ACTIVE"] / 8 * cus * 4)
                 line += f"  matrix pipe busy {busy * 100:.1f}%"
-        for c in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
-            if c in e and "SQ_WAVE_CYCLES" in e and c != "SQ_WAVE_CYCLES":
+        for c in sorted(e):
+            if c.startswith("SQ_") and c not in ("SQ_WAVE_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES") and "SQ_WAVE_CYCLES" in e:
                 line += f"  {c} {e[c] / e['SQ_WAVE_CYCLES'] * 100:.1f}%"
         print(line)
 

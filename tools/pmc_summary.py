@@ -17,8 +17,9 @@ def per_kernel(path, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            k = "predict_kernel" if "predict_kernel" in r["Kernel_Name"] else (
-                "rbf_fill_kernel" if "rbf_fill" in r["Kernel_Name"] else None)
+            kn = r["Kernel_Name"]
+            k = "predict_kernel" if ("predict_kernel" in kn or "predict_x3_kernel" in kn) else (
+                "rbf_fill_kernel" if "rbf_fill" in kn else None)
             if k:
                 vals.setdefault(k, {}).setdefault(r["Dispatch_Id"], 0.0)
                 vals[k][r["Dispatch_Id"]] += float(r["Counter_Value"])
@@ -31,7 +32,7 @@ def main(out, cfg, dst):
     dur = {}
     for f in glob.glob(out + "/trace/**/*kernel_stats.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "predict_kernel" in r["Name"]:
+            if "predict_kernel" in r["Name"] or "predict_x3_kernel" in r["Name"]:
                 dur["predict_kernel"] = float(r["AverageNs"]) * 1e-6
     res = {"config": cfg, "units": "bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)"}
     for k in fetch:
