@@ -168,8 +168,9 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
             const f32x2v as = ak * msc;  // msc = 0: not the mean's row block
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
-                mu[c] = fma((double)as.x, (double)e[c].x, mu[c]);
-                mu[c] = fma((double)as.y, (double)e[c].y, mu[c]);
+                // the pair's terms in f32 (one rounding of a two-term sum, the
+                // order of K*'s own), accumulated in f64
+                mu[c] += (double)fmaf(as.x, e[c].x, as.y * e[c].y);
                 SBO_PIN(mu[c]);
             }
             if (i < 3) {
@@ -239,10 +240,7 @@ __device__ __forceinline__ void x3_kstar(const lds_char *pc, const float (&xq)[N
             kb.h[c][i] = w0;
             kb.m[c][i] = w1;
             kb.l[c][i] = w2;
-            if (mean) {
-                mu[c] = fma((double)ak.x, (double)e0, mu[c]);
-                mu[c] = fma((double)ak.y, (double)e1, mu[c]);
-            }
+            if (mean) mu[c] += (double)fmaf(ak.x, e0, ak.y * e1);  // as in x3_half
         }
     }
 }
@@ -287,14 +285,9 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
     const uint32_t lds_dwin = lds_smem + (uint32_t)kXWin;
     const uint32_t lds_lwin = lds_dwin + 2048u;
 #define SBO_DMA16(sbase, ldst)                                                                          \
-    do {                                                                                                \
-        uint32_t keep_;                                                                                 \
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t" \
-                     "s_mov_b32 m0, %0"                                                                 \
-                     : "=&s"(keep_)                                                                     \
-                     : "v"(voff), "s"((const void *)(sbase)), "s"(ldst)                                 \
-                     : "memory");                                                                       \
-    } while (0)
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"((const void *)(sbase)),     \
+                 "{m0}"(ldst)                                                                           \
+                 : "memory")
     // one half-tile stage into LDS slot `sl`: wave 0 brings the item's
     // queries (lanes 0-31 qx, 32-63 qy) and the half-tile's coordinates
     // first, then every wave its A pieces (the youngest kPieces of its

@@ -418,7 +418,7 @@ def test_split_operand_sweep(mapper, variant):
     partition of the plan (1, 3, 7, 8, 1000 workgroups, and one per CU with
     the XCD-interleaved item order), for the budgeted, a fixed and the dense
     cutoff; within the contract of the f32 sweep and of the fp64 oracle given
-    the device factor; the mean is the f32 sweep's (f64-accumulated in both)."""
+    the device factor."""
     wl = synthetic(5000, 90, 70, seed=23)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
     gm.fit(wl.x, wl.y, wl.obs)
@@ -435,7 +435,7 @@ def test_split_operand_sweep(mapper, variant):
         for groups in (1, 3, 7, 8, 1000):
             assert np.array_equal(res[groups][0], res[0][0]) and np.array_equal(res[groups][1], res[0][1]), (skip, groups)
         mu, sd = res[0]
-        assert nrel(mu, mu32.astype(np.float64)) < 1e-6
+        assert nrel(mu, mu32.astype(np.float64)) < 5e-6   # pair sums in f32, accumulated in f64
         assert nrel(sd.astype(np.float64) ** 2, sd32.astype(np.float64) ** 2) < 1e-5
     gm.set_option(N.SBO_OPT_SWEEP_GROUPS, 0)
     gm.set_option(N.SBO_OPT_TILE_SKIP, -1)

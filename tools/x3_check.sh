@@ -1,7 +1,6 @@
 #!/bin/bash
 mkdir -p gpurun_out/x3
 O=gpurun_out/x3
-step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -6 $O/$name.log; [ $rc -eq 0 ] || exit $rc; }
+step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -10 $O/$name.log; [ $rc -eq 0 ] || exit $rc; }
 step gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step ab_c4 300 python tools/ab_variants.py --config C4 --variants 0 2 3 --rounds 2
-step pmc 600 bash tools/collect_pmc.sh C4 x3 --opt SBO_OPT_KERNEL_VARIANT=3
+step ab_c4 300 python tools/ab_variants.py --config C4 --variants 0 2 3 --rounds 3
