@@ -34,6 +34,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA peak (spec, 2.4 GHz)
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (spec; not the 2:1-sparsity figure)
+SPLIT_VARIANTS = (2, 3)         # split-operand (bf16 x3) sweeps: six bf16 MFMA products per f32 product
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = "GP posterior+acq grid-points/sec at N train pts; 1/2/4/8 GPU"
 DATA = "synthetic (SplitMix64 smooth field + N(0,sn2) noise in BASELINE config shapes; terrain.csv is a missing blob)"
@@ -52,6 +54,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-outputs", action="store_true", help="skip writing mu/sd/lo/hi/S (argmax only)")
+    p.add_argument("--variant", type=int, default=3,
+                   help="predictive kernel (SBO_OPT_KERNEL_VARIANT): 3 split-operand bf16 sweep (default), 0 f32 MFMA")
     return p.parse_args()
 
 
@@ -138,6 +142,7 @@ def run_sweep(a, dev, world, rank):
 
     stream = torch.cuda.current_stream(dev)
     gm = TerrainMapper(dev.index, wl.hyper)
+    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, a.variant)
     gm.ctx.set_stream(stream)
     lib = N.lib()
     prof = Prof(lib, gm.ctx.handle)
@@ -265,19 +270,16 @@ def run_sweep(a, dev, world, rank):
     return {
         "metric": METRIC, "value": value, "unit": "grid-points/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": a.scaling,
-        "vs_baseline": None, "dtype": "f32", "data": DATA,
+        "vs_baseline": None, "dtype": dtype_of(a.variant), "data": DATA,
         "config": {"workload": a.config, "n_train": n, "grid": [gw, gh], "M": m_total, "M_per_rank": m,
                    "beta": wl.beta, "f_min": round(wl.f_min, 6),
                    "hyper": [wl.hyper.length_scale, wl.hyper.sigma_f, wl.hyper.noise_level],
                    "kstar_cutoff_log2": cutoff, "parallelism": f"m-shard{world}" if world > 1 else "single",
                    "outputs_written": not a.no_outputs},
-        "roofline": {"kernel": "predict_kernel (V = sf2 L^-1 K*^T, f32 MFMA 16x16x4)", "bound": "mfma",
-                     "achieved": achieved, "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_F32_MFMA_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
-                     "avg_launch_ms": pred_ms, "max_rank_launch_ms": pred_ms_max,
-                     "algorithmic_flops_per_launch": exec_flops_launch,
-                     "dense_flops_per_launch": dense_flops_launch,
-                     "dense_equivalent_tflops": dense_flops_launch / (pred_ms * 1e-3) / 1e12},
+        "roofline": dict(predict_roofline(a.variant, exec_flops_launch, pred_ms), traffic=traffic,
+                         traffic_source=traffic_src, avg_launch_ms=pred_ms, max_rank_launch_ms=pred_ms_max,
+                         dense_flops_per_launch=dense_flops_launch,
+                         dense_equivalent_tflops=dense_flops_launch / (pred_ms * 1e-3) / 1e12),
         "fill_roofline": {"kernel": "rbf_fill_kernel", "bound": "hbm", "achieved": fill_gbs, "peak": PEAK_HBM_GBS,
                           "unit": "GB/s", "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None,
                           "avg_launch_ms": fill_ms, "algorithmic_bytes": fill_bytes},
@@ -286,6 +288,31 @@ def run_sweep(a, dev, world, rank):
         "subgoal": subgoal,
         "cpu_baseline": cpu,
     }
+
+
+def dtype_of(variant):
+    return "f32 (bf16x3-split MFMA, f32 accumulation)" if variant in SPLIT_VARIANTS else "f32"
+
+
+def predict_roofline(variant, flops_f32, ms):
+    """Roofline of the predictive kernel.  flops_f32 = the algorithmic work of
+    one launch, 2*BM*BN*BK per multiplied k-tile (device counter).  The
+    split-operand sweep issues six bf16 MFMA products per f32 product, so its
+    matrix-pipe work is 6 x flops_f32 against the dense bf16 peak; the f32
+    MFMA sweep's is flops_f32 against the dense f32 peak."""
+    f32_tf = flops_f32 / (ms * 1e-3) / 1e12
+    if variant in SPLIT_VARIANTS:
+        mf = 6.0 * flops_f32
+        ach = mf / (ms * 1e-3) / 1e12
+        return {"kernel": "predict_x3_kernel (V = sf2 L^-1 K*^T: bf16x3-split operands, six "
+                          "v_mfma_f32_16x16x32_bf16 per f32 product, f32 accumulation)",
+                "bound": "mfma", "achieved": ach, "peak": PEAK_BF16_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / PEAK_BF16_MFMA_TFLOPS, "mfma_flops_per_launch": mf,
+                "algorithmic_flops_per_launch": flops_f32, "f32_equivalent_tflops": f32_tf,
+                "f32_equivalent_over_f32_peak": f32_tf / PEAK_F32_MFMA_TFLOPS}
+    return {"kernel": "predict_kernel (V = sf2 L^-1 K*^T, f32 MFMA 16x16x4)", "bound": "mfma", "achieved": f32_tf,
+            "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": f32_tf / PEAK_F32_MFMA_TFLOPS,
+            "algorithmic_flops_per_launch": flops_f32}
 
 
 def run_streaming(a, dev, world, rank):
@@ -302,6 +329,7 @@ def run_streaming(a, dev, world, rank):
     chunks = np.linspace(n0, n_end, iters + 1).round().astype(int)
     stream = torch.cuda.current_stream(dev)
     gm = TerrainMapper(dev.index, wl.hyper)
+    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, a.variant)
     gm.ctx.set_stream(stream)
     prof = Prof(N.lib(), gm.ctx.handle)
     f32 = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
@@ -346,17 +374,15 @@ def run_streaming(a, dev, world, rank):
     prof.reset(False)
     steps = reps * iters
     pred_ms = pr["predict_ms"] / max(pr["predict_launches"], 1)
-    achieved = pr["predict_flops"] / max(pr["predict_launches"], 1) / (pred_ms * 1e-3) / 1e12
+    flops = pr["predict_flops"] / max(pr["predict_launches"], 1)
     (s, i), = key_tensor_to_pairs(last)
     return {
         "metric": METRIC, "value": m * steps / elapsed, "unit": "grid-points/s", "n_gpus": 1, "steps": steps,
         "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": DATA,
+        "vs_baseline": None, "dtype": dtype_of(a.variant), "data": DATA,
         "config": {"workload": "C5", "n_train": [n0, n_end], "iterations": iters, "grid": [g, g], "M": m,
                    "parallelism": "single", "step": "sbo_append (block Cholesky) + sbo_tick (includes one fit per loop)"},
-        "roofline": {"kernel": "predict_kernel", "bound": "mfma", "achieved": achieved,
-                     "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_F32_MFMA_TFLOPS,
-                     "traffic": None, "avg_launch_ms": pred_ms},
+        "roofline": dict(predict_roofline(a.variant, flops, pred_ms), traffic=None, avg_launch_ms=pred_ms),
         "append_ms_avg": t_app * 1e3 / steps, "tick_ms_avg": t_tick * 1e3 / steps,
         "argmax": {"index": i, "score": s}, "cpu_baseline": None,
     }

@@ -223,9 +223,14 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * workgroup's 128 queries are spatially compact and skip more k-tiles;
  * outputs and argmax indices stay in the caller's order. */
 #define SBO_OPT_QUERY_ORDER 4
-/* SBO_OPT_KERNEL_VARIANT (A/B builds of the predictive kernel): 0 = f32
- * cross-tile accumulator (default); 1 = f64 cross-tile accumulator (same
- * accuracy at N = 16384, 5 % slower: tools/variant_accuracy.py). */
+/* SBO_OPT_KERNEL_VARIANT, the predictive sweep: 3 (default) = split
+ * operands on bf16 MFMA -- sf2 L^-1 and K* as three bf16 pieces each, six
+ * v_mfma_f32_16x16x32_bf16 products per f32 product, f32 accumulation,
+ * eight waves per CU (f32-accurate: variance error vs a host f64 sweep
+ * 5.07e-6 at N = 16384 against 5.00e-6 for variant 0; 1.7x faster);
+ * 2 = the same with four waves of 32 queries; 0 = f32 MFMA (16x16x4) with
+ * an f32 cross-tile accumulator; 1 = variant 0 with an f64 one.  4-8:
+ * timing diagnostics with parts of the work left out (wrong results). */
 #define SBO_OPT_KERNEL_VARIANT 5
 /* SBO_OPT_SWEEP_GROUPS: workgroups of the persistent predictive sweep, each
  * walking one tile-balanced range of the tick's plan; 0 = default (one per

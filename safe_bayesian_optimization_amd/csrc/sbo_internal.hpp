@@ -106,7 +106,7 @@ struct sbo_ctx {
     std::vector<int64_t> order;  // internal row -> caller's training index
     float bbox[4] = {0.f, 0.f, 0.f, 0.f};  // training bounding box (x0, x1, y0, y1)
     bool query_order = true;     // SBO_OPT_QUERY_ORDER: sweep queries in Morton order
-    int kernel_variant = 0;      // SBO_OPT_KERNEL_VARIANT: predictive kernel build (A/B)
+    int kernel_variant = 3;      // SBO_OPT_KERNEL_VARIANT: predictive kernel (3: split-operand bf16 sweep)
     int sweep_groups = 0;        // SBO_OPT_SWEEP_GROUPS: persistent sweep workgroups (0: one per CU)
     int num_cu = 0;              // compute units of the device
     sbo::DevBuf plan_work;       // the tick's tile plan (launch_plan)

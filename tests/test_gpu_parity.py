@@ -387,6 +387,7 @@ def test_sweep_partition_and_outer_variant(mapper):
     tolerance."""
     wl = synthetic(5000, 90, 70, seed=23)   # npad 5120 = 20 row blocks
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 0)
     gm.fit(wl.x, wl.y, wl.obs)
     base = None
     for skip in (-1, 40, 0):
@@ -403,7 +404,7 @@ def test_sweep_partition_and_outer_variant(mapper):
     gm.set_option(N.SBO_OPT_TILE_SKIP, -1)
     gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 1)
     mu64, sd64 = gm.predict(wl.qx, wl.qy)
-    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 0)
+    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 3)
     assert nrel(mu64, base[0].astype(np.float64)) < 1e-6   # the mean is f64-accumulated in both
     assert nrel(sd64.astype(np.float64) ** 2, base[1].astype(np.float64) ** 2) < 1e-5
     with pytest.raises(N.SboError):
@@ -449,7 +450,7 @@ def test_split_operand_sweep(mapper, variant):
     mu, sd = gm.predict(wl.qx, wl.qy)
     assert nrel(mu[sel].astype(np.float64), omu) < 1e-5
     assert nrel(sd[sel].astype(np.float64) ** 2, ovar) < 1e-5
-    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 0)
+    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 3)
 
 
 def test_spatial_order_does_not_change_the_posterior(mapper):
