@@ -229,8 +229,10 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * eight waves per CU (f32-accurate: variance error vs a host f64 sweep
  * 5.07e-6 at N = 16384 against 5.00e-6 for variant 0; 1.7x faster);
  * 2 = the same with four waves of 32 queries; 0 = f32 MFMA (16x16x4) with
- * an f32 cross-tile accumulator; 1 = variant 0 with an f64 one.  4-8:
- * timing diagnostics with parts of the work left out (wrong results). */
+ * an f32 cross-tile accumulator; 1 = variant 0 with an f64 one; 9, 10 =
+ * variant 3 with the A stage issued in one burst per step, resp. A
+ * fragments read one row block ahead.  4-8: timing diagnostics with parts
+ * of the work left out (wrong results). */
 #define SBO_OPT_KERNEL_VARIANT 5
 /* SBO_OPT_SWEEP_GROUPS: workgroups of the persistent predictive sweep, each
  * walking one tile-balanced range of the tick's plan; 0 = default (one per

@@ -87,6 +87,12 @@ __device__ __forceinline__ float lds_f(const lds_char *p) {
     return *reinterpret_cast<const __attribute__((address_space(3))) float *>(p);
 }
 
+// One LDS-DMA piece: 64 lanes x 16 B from sbase + voff to LDS at M0 = ldst
+// (+ lane x 16).  s_nop: the M0 write -> LDS-DMA hazard.
+__device__ __forceinline__ void dma16(uint32_t voff, const void *sbase, uint32_t ldst) {
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(ldst) : "memory");
+}
+
 // K* pieces of a step for the wave's NC 16-query column blocks
 // (lane (g, r): k = 8g + j of the half-tile, query 16 (NC w + c) + r)
 template <int NC>
@@ -123,23 +129,36 @@ __device__ __forceinline__ float kstar1(float xk, float yk, float xq, float yq, 
 //   FRESH: first half of a tile (the chains start from zero); otherwise the
 //   finished chains of each row block are added into `outer` two blocks
 //   later (off the MFMA's result latency).
-template <int NC, bool FRESH, int DIAG>
+template <int NC, bool FRESH, int DIAG, int PIECES>
 __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn, const float (&xq)[NC],
                                         const float (&yq)[NC], int g, float cexp, float msc, const KPieces<NC> &kb,
                                         f32x4 (&acc)[NC][16], f32x4 (&outer)[NC][16], KPieces<NC> &nx,
-                                        double (&mu)[NC]) {
+                                        double (&mu)[NC], uint32_t voff, const char *asrc, uint32_t adst) {
+    // SPREAD (DIAG & 16): this wave's A pieces of stage i+2 are issued one
+    // per row block between the MFMAs instead of in a burst at the top
+    constexpr bool SPREAD = (DIAG & 16) != 0;
+    constexpr int kStride = (8 / NC) * 1024;
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    // A fragments: row block rb in use, rb+1 landed or landing, rb+2 issued
+    // during rb (DIAG & 32: one block ahead only)
+    constexpr int AHEAD = (DIAG & 32) ? 1 : 2;
     u32x4 a0 = lds_b128(pa), a1 = lds_b128(pa + kXPlane), a2 = lds_b128(pa + 2 * kXPlane);
+    u32x4 n0 = a0, n1 = a1, n2 = a2;
+    if (AHEAD == 2) {
+        n0 = lds_b128(pa + 1024);
+        n1 = lds_b128(pa + kXPlane + 1024);
+        n2 = lds_b128(pa + 2 * kXPlane + 1024);
+    }
     // coordinates of pair 0; pair i+1's are read while pair i is built
     f32x2v xk = lds_f2(pcn + g * 32), yk = lds_f2(pcn + 128 + g * 32), ak = lds_f2(pcn + 256 + g * 32);
     f32x2v e[NC];
 #pragma unroll
     for (int rb = 0; rb < 16; ++rb) {
         u32x4 b0, b1, b2;
-        if (rb + 1 < 16) {
-            b0 = lds_b128(pa + (rb + 1) * 1024);
-            b1 = lds_b128(pa + kXPlane + (rb + 1) * 1024);
-            b2 = lds_b128(pa + 2 * kXPlane + (rb + 1) * 1024);
+        if (rb + AHEAD < 16) {
+            b0 = lds_b128(pa + (rb + AHEAD) * 1024);
+            b1 = lds_b128(pa + kXPlane + (rb + AHEAD) * 1024);
+            b2 = lds_b128(pa + 2 * kXPlane + (rb + AHEAD) * 1024);
         }
         // ---- the next step's K*, pair i over row blocks 4i .. 4i+3:
         // evaluate (two slots), split, mean terms + the next pair's coordinates
@@ -179,6 +198,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                 ak = lds_f2(pcn + 256 + g * 32 + (i + 1) * 8);
             }
         }
+        if (SPREAD && rb >= 1 && rb <= PIECES) dma16(voff, asrc + (rb - 1) * kStride, adst + (rb - 1) * kStride);
         if (!FRESH && !(DIAG & 4) && rb > 1) {  // those chains finished a block ago
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
@@ -207,7 +227,16 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (rb + 1 < 16) {
+        if (AHEAD == 2) {
+            a0 = n0;
+            a1 = n1;
+            a2 = n2;
+            if (rb + 2 < 16) {
+                n0 = b0;
+                n1 = b1;
+                n2 = b2;
+            }
+        } else if (rb + 1 < 16) {
             a0 = b0;
             a1 = b1;
             a2 = b2;
@@ -255,7 +284,9 @@ constexpr int kFirst = 2, kLast = 4, kValid = 8;
 // queries 16w .. 16w+15; NC = 2: four waves (one per SIMD), wave w owns
 // queries 32w .. 32w+31.  Every wave loads an equal share of each stage.
 // DIAG (timing diagnostics only, results wrong): 1 no next-step K*, 2 no A
-// pieces staged, 4 no outer sums, 8 every A stage from the first tile (L2-resident).
+// pieces staged, 4 no outer sums, 8 every A stage from the first tile (L2-resident);
+// 16 (not a diagnostic): A pieces spread over the row blocks; 32: A fragments
+// read one row block ahead instead of two.
 template <int NC, int DIAG>
 __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
     const char *__restrict__ ax3, const float *__restrict__ kc3, const int4 *__restrict__ desc,
@@ -292,7 +323,7 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
     // queries (lanes 0-31 qx, 32-63 qy) and the half-tile's coordinates
     // first, then every wave its A pieces (the youngest kPieces of its
     // vector-memory operations)
-#define SBO_X3_STAGE(Tg_, t_, h_, qb_, sl_)                                                             \
+#define SBO_X3_STAGE(Tg_, t_, h_, qb_, sl_, burst_)                                                     \
     do {                                                                                                \
         const uint32_t d_ = lds_smem + (uint32_t)(sl_) * kXSlot;                                        \
         if (lw == 0) {                                                                                  \
@@ -302,7 +333,9 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
         }                                                                                               \
         const char *s_ = ax3 + ((DIAG & 8) ? 0 : ((Tg_) * 2 + (h_)) * (int64_t)kXA) + lw * 1024;       \
         const uint32_t w_ = lds_wave + (uint32_t)(sl_) * kXSlot;                                        \
-        if (!(DIAG & 2))                                                                                \
+        a_src = s_;                                                                                     \
+        a_dst = w_;                                                                                     \
+        if (!(DIAG & 2) && ((burst_) || !(DIAG & 16)))                                                  \
             _Pragma("unroll") for (int j = 0; j < kPieces; ++j)                                         \
                 SBO_DMA16(s_ + j * kLoaders * 1024, w_ + (uint32_t)(j * kLoaders * 1024));              \
     } while (0)
@@ -339,14 +372,16 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    auto stage = [&](int sl) {
+    const char *a_src = ax3;  // this wave's A pieces of the last staged step (spread mode)
+    uint32_t a_dst = 0;
+    auto stage = [&](int sl, bool burst) {
         const int cnt = la_d.w & 0xffff;
         XStep s;
         s.I = la_d.x;
         s.qb = la_d.y;
         s.flags = la_h | (la_j == 0 && la_h == 0 ? kFirst : 0) | (la_j == cnt - 1 && la_h == 1 ? kLast : 0) | kValid;
         const int t = list_at(la_e, la_d.x);
-        SBO_X3_STAGE(tile_start(la_d.x) + t, t, la_h, la_d.y, sl);
+        SBO_X3_STAGE(tile_start(la_d.x) + t, t, la_h, la_d.y, sl, burst);
         la_h ^= 1;
         if (la_h == 0) {
             ++la_j;
@@ -364,8 +399,8 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
         return s;
     };
 
-    XStep s0 = stage(0), s1 = {0, 0, 0}, s2 = {0, 0, 0};
-    if (la_k < k1) s1 = stage(1);
+    XStep s0 = stage(0, true), s1 = {0, 0, 0}, s2 = {0, 0, 0};
+    if (la_k < k1) s1 = stage(1, true);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
@@ -420,7 +455,8 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
         if (FRESH) flush();
         const bool issue = la_k < k1;
         const int nslot = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
-        s2 = issue ? stage(nslot) : XStep{0, 0, 0};
+        s2 = issue ? stage(nslot, false) : XStep{0, 0, 0};
+        if (!issue) a_dst = lds_wave + (uint32_t)nslot * kXSlot;  // spread mode: a harmless re-stage into the free slot
         const int cslot = cur == 2 ? 0 : cur + 1;  // (cur + 1) % 3: the next step's coordinates
         const lds_char *pa = lds + cur * kXSlot + lane * 16;
         const lds_char *pcn = lds + cslot * kXSlot + kXA;
@@ -450,7 +486,7 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
             xq[c] = lds_f(pqn + (qo + 16 * c) * 4);
             yq[c] = lds_f(pqn + (kBN + qo + 16 * c) * 4);
         }
-        x3_half<NC, FRESH, DIAG>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu);
+        x3_half<NC, FRESH, DIAG, kPieces>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src, a_dst);
         if (!FRESH && (s0.flags & kLast)) {
             // item done: column sums of V^2 over its rows (lanes l, l+16, l+32,
             // l+48 hold four row quarters of column l&15 of every block)
@@ -475,7 +511,7 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
         }
         // retire stage i+1: its queries and coordinates (wave 0) precede its
         // A pieces and were retired one step earlier; leave stage i+2's A in flight
-        if (issue && !(DIAG & 2)) {
+        if ((issue || (DIAG & 16)) && !(DIAG & 2)) {
             if constexpr (kPieces == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         } else {
@@ -492,6 +528,7 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
         half_step(std::integral_constant<bool, true>{});
         half_step(std::integral_constant<bool, false>{});
     } while (more);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
     flush();
 #undef SBO_X3_STAGE
 #undef SBO_DESC_WINDOW
@@ -567,13 +604,15 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
     hipLaunchKernelGGL((predict_x3_kernel<NC, D>), dim3((unsigned)P), dim3(64 * 8 / NC), 0, s, ax3, kc3, desc, tl, \
                        seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean)
     switch (variant) {
-        case 3: SBO_X3_LAUNCH(1, 0); break;
-        case 4: SBO_X3_LAUNCH(2, 1); break;
-        case 5: SBO_X3_LAUNCH(2, 2); break;
-        case 6: SBO_X3_LAUNCH(1, 1); break;
-        case 7: SBO_X3_LAUNCH(1, 2); break;
-        case 8: SBO_X3_LAUNCH(1, 8); break;
-        default: SBO_X3_LAUNCH(2, 0); break;
+        case 2: SBO_X3_LAUNCH(2, 16); break;   // four waves of 32 queries
+        case 4: SBO_X3_LAUNCH(2, 17); break;   // diagnostics: no next-step K*
+        case 5: SBO_X3_LAUNCH(2, 18); break;   //   no A pieces
+        case 6: SBO_X3_LAUNCH(1, 17); break;   //   no next-step K*
+        case 7: SBO_X3_LAUNCH(1, 18); break;   //   no A pieces
+        case 8: SBO_X3_LAUNCH(1, 24); break;   //   every stage from the first tile
+        case 9: SBO_X3_LAUNCH(1, 0); break;    // A pieces in a burst at the top of the step
+        case 10: SBO_X3_LAUNCH(1, 48); break;  // A fragments one row block ahead
+        default: SBO_X3_LAUNCH(1, 16); break;  // 3: eight waves of 16 queries, A pieces spread
     }
 #undef SBO_X3_LAUNCH
     return hipGetLastError();
