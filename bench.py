@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--grid", type=int, default=None, help="override grid side")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    p.add_argument("--sharding", default="cost", choices=["cost", "equal"],
+                   help="strong scaling: cost-balanced contiguous row blocks (default) or equal point counts")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-outputs", action="store_true", help="skip writing mu/sd/lo/hi/S (argmax only)")
@@ -122,7 +124,7 @@ def run_sweep(a, dev, world, rank):
 
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
     from safe_bayesian_optimization_amd import _native as N
-    from safe_bayesian_optimization_amd.dist import allreduce_key, shard_range
+    from safe_bayesian_optimization_amd.dist import allreduce_key, cost_balanced_range, shard_range
     from safe_bayesian_optimization_amd.gp import _to_hyper
     from safe_bayesian_optimization_amd.terrain import CONFIGS
 
@@ -132,13 +134,7 @@ def run_sweep(a, dev, world, rank):
         gw = gh = a.grid
     wl = synthetic(n, gw, gh, seed=0, name=a.config)
     m_total = wl.qx.size
-    if a.scaling == "weak":
-        lo, hi = 0, m_total
-        m_all = m_total * world
-    else:
-        lo, hi = shard_range(m_total, rank, world)
-        m_all = m_total
-    m = hi - lo
+    m_all = m_total * world if a.scaling == "weak" else m_total
 
     stream = torch.cuda.current_stream(dev)
     gm = TerrainMapper(dev.index, wl.hyper)
@@ -149,11 +145,6 @@ def run_sweep(a, dev, world, rank):
 
     f32 = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
     X, Y, OBS = f32(wl.x), f32(wl.y), f32(wl.obs)
-    qx, qy = f32(wl.qx[lo:hi]), f32(wl.qy[lo:hi])
-    outs = {} if a.no_outputs else dict(
-        mu=torch.empty(m, dtype=torch.float32, device=dev), sd=torch.empty(m, dtype=torch.float32, device=dev),
-        lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
-        safe=torch.empty(m, dtype=torch.uint8, device=dev))
     key = torch.empty(2, dtype=torch.int64, device=dev)
 
     # ---- fit (replicated on every rank), timed separately: the first fit in
@@ -197,6 +188,22 @@ def run_sweep(a, dev, world, rank):
         fit_bcast = {"ms": (time.perf_counter() - t0) * 1e3, "state_bytes": int(size.item()),
                      "how": "rank 0 sbo_fit + sbo_export_state, broadcast, sbo_import_state"}
         del blob
+    # ---- this rank's contiguous block of grid rows (strong scaling): cut so
+    # that every rank sweeps about the same number of k-tiles (rank 0 plans
+    # all M queries once, sbo_query_cost, and broadcasts the cuts), or equal
+    # point counts with --sharding equal
+    if a.scaling == "weak":
+        lo, hi = 0, m_total
+    elif world > 1 and a.sharding == "cost":
+        lo, hi = cost_balanced_range(gm, f32(wl.qx), f32(wl.qy), rank, world)
+    else:
+        lo, hi = shard_range(m_total, rank, world)
+    m = hi - lo
+    qx, qy = f32(wl.qx[lo:hi]), f32(wl.qy[lo:hi])
+    outs = {} if a.no_outputs else dict(
+        mu=torch.empty(m, dtype=torch.float32, device=dev), sd=torch.empty(m, dtype=torch.float32, device=dev),
+        lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
+        safe=torch.empty(m, dtype=torch.uint8, device=dev))
     cutoff, row_l1, alpha_l1 = gm.skip_info()
 
     # ---- RBF fill (a1) alone, warm (the fill inside fit also paid the code-object load)
@@ -275,6 +282,7 @@ def run_sweep(a, dev, world, rank):
                    "beta": wl.beta, "f_min": round(wl.f_min, 6),
                    "hyper": [wl.hyper.length_scale, wl.hyper.sigma_f, wl.hyper.noise_level],
                    "kstar_cutoff_log2": cutoff, "parallelism": f"m-shard{world}" if world > 1 else "single",
+                   "sharding": (a.sharding if world > 1 and a.scaling == "strong" else None),
                    "outputs_written": not a.no_outputs},
         "roofline": dict(predict_roofline(a.variant, exec_flops_launch, pred_ms), traffic=traffic,
                          traffic_source=traffic_src, avg_launch_ms=pred_ms, max_rank_launch_ms=pred_ms_max,

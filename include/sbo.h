@@ -128,6 +128,15 @@ SBO_API sbo_status sbo_tick(sbo_ctx *ctx, const float *qx, const float *qy, int6
                             float *mu, float *sd, double *lo, double *hi, uint8_t *safe,
                             sbo_key *out, uint32_t flags);
 
+/* Sweep work of each query under the current fit: builds the tick's tile
+ * plan for these queries (no sweep) and writes cost[i] = the k-tiles its
+ * 128-query block multiplies, summed over row blocks, / the block's size,
+ * in the caller's order.  For cost-balanced M-sharding across ranks (every
+ * rank computes the same costs from the same inputs: the plan is
+ * deterministic); no reference counterpart. */
+SBO_API sbo_status sbo_query_cost(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, float *cost,
+                                  uint32_t flags);
+
 /* Combine two shard keys (the cross-rank reduction of sbo_tick / sbo_argmax). */
 SBO_API sbo_key sbo_key_combine(sbo_key a, sbo_key b);
 

@@ -30,7 +30,7 @@ EXPORTS = (
     "sbo_key_combine", "sbo_find_safety_contour_indices", "sbo_next_subgoal", "sbo_find_contours_external",
     "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
     "sbo_get_order", "sbo_profile_work", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
-    "sbo_state_bytes", "sbo_export_state", "sbo_import_state",
+    "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
 )
 SBO_OPT_INVERSE_BITS = 1
 SBO_OPT_SPATIAL_ORDER = 2
@@ -107,6 +107,8 @@ def lib():
     L.sbo_argmax.restype = st
     L.sbo_tick.argtypes = [vp, vp, vp, i64, dbl, dbl, i32, i64, vp, vp, vp, vp, vp, vp, u32]
     L.sbo_tick.restype = st
+    L.sbo_query_cost.argtypes = [vp, vp, vp, i64, vp, u32]
+    L.sbo_query_cost.restype = st
     L.sbo_key_combine.argtypes = [sbo_key, sbo_key]
     L.sbo_key_combine.restype = sbo_key
     L.sbo_find_safety_contour_indices.argtypes = [vp, vp, vp, i64, i32, i32, vp, i64, ctypes.POINTER(i64)]

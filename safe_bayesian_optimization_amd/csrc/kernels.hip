@@ -686,6 +686,27 @@ __global__ void plan_seg2_kernel(const int *__restrict__ xseg, int G, int P, int
     }
 }
 
+// Sweep work per query from a plan (load balancing across ranks): the kept
+// tiles of its 128-query block summed over row blocks, shared by the block's
+// queries; written in the caller's order (perm: sweep position -> caller).
+__global__ void plan_block_cost_kernel(const unsigned long long *__restrict__ key, int nI, int64_t nQ,
+                                       float *__restrict__ bcost) {
+    const int64_t qb = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (qb >= nQ) return;
+    unsigned long long c = 0;
+    for (int I = 0; I < nI; ++I) c += key[plan_item(I, nI, nQ, qb)] & kPlanCountMask;
+    bcost[qb] = (float)c;
+}
+
+__global__ void plan_query_cost_kernel(const float *__restrict__ bcost, int64_t m, const int32_t *__restrict__ perm,
+                                       float *__restrict__ cost) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int64_t qb = i / kBN;
+    const int64_t nb = (m - qb * kBN) < kBN ? (m - qb * kBN) : kBN;
+    cost[perm ? (int64_t)perm[i] : i] = bcost[qb] / (float)nb;
+}
+
 // ---- the sweep (persistent: one workgroup per CU)
 // OT: outer (cross-tile) accumulator type.  Workgroup b walks the item range
 // r(b) of the plan; consecutive ranges go to one XCD (blocks are dealt to the
@@ -1280,6 +1301,20 @@ void plan_views(int64_t npad, int64_t m, int P, const void *work, const int4 **d
 }
 
 float exp2_coef_f(float ell) { return (float)exp2_coef(ell); }
+
+hipError_t launch_plan_cost(hipStream_t s, int64_t npad, int64_t m, int P, const void *work, const int32_t *perm,
+                            float *bcost, float *cost) {
+    const int nI = (int)(npad / kBM);
+    const int64_t nQ = (m + kBN - 1) / kBN;
+    if (m <= 0 || nI <= 0) return hipSuccess;
+    const PlanLayout L = plan_layout(nI, nQ, P);
+    const auto *key = reinterpret_cast<const unsigned long long *>(static_cast<const char *>(work) + L.key);
+    hipLaunchKernelGGL(plan_block_cost_kernel, dim3((unsigned)((nQ + 255) / 256)), dim3(256), 0, s, key, nI, nQ,
+                       bcost);
+    hipLaunchKernelGGL(plan_query_cost_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, bcost, m, perm,
+                       cost);
+    return hipGetLastError();
+}
 
 hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, const float *qx,
                           const float *qy, int64_t m, int64_t ldp, float ell, float m0, float *part, float *mean,

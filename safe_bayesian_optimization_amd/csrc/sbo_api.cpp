@@ -385,7 +385,7 @@ sbo_status factor_and_refresh(sbo_ctx *ctx) {
 // Predictive sweep + acquisition over m queries already on the device.
 sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, double beta, double f_min,
                     int score_kind, int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
-                    uint8_t *safe, sbo_key *key_dev) {
+                    uint8_t *safe, sbo_key *key_dev, float *cost = nullptr) {
     const int64_t nI = ctx->npad / sbo::kBM;
     const int64_t ldp = sbo::round_up(m, 64);
     SBO_HIP(ctx->part.reserve(sizeof(float) * (size_t)nI * (size_t)ldp));
@@ -418,8 +418,15 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     SBO_HIP(ctx->plan_work.reserve(sbo::predict_work_bytes(ctx->npad, m, P)));
     SBO_HIP(sbo::launch_plan(ctx->stream, ctx->kbox.as<float4>(), ctx->npad, qx, qy, m, ldp,
                              (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan, ctx->part.as<float>(),
-                             ctx->mean.as<float>(), ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr, P,
+                             ctx->mean.as<float>(),
+                             ctx->prof && !cost ? ctx->counters.as<unsigned long long>() : nullptr, P,
                              ctx->plan_work.as<void>(), ctx->plan_work.capacity()));
+    if (cost) {  // sbo_query_cost: the plan's work per query, no sweep
+        SBO_HIP(ctx->qcost.reserve(sizeof(float) * (size_t)((m + sbo::kBN - 1) / sbo::kBN)));
+        SBO_HIP(sbo::launch_plan_cost(ctx->stream, ctx->npad, m, P, ctx->plan_work.as<void>(), perm,
+                                      ctx->qcost.as<float>(), cost));
+        return SBO_OK;
+    }
     if (ctx->kernel_variant >= 2) {
         // split-operand sweep: derive the bf16 planes of any repacked row
         // block, and give the kernel whole 128-query blocks to read
@@ -645,6 +652,33 @@ SBO_API sbo_status sbo_predict(sbo_ctx *ctx, const float *qx, const float *qy, i
                                uint32_t flags) {
     return sbo_tick(ctx, qx, qy, m, 0.0, 0.0, SBO_SCORE_WIDTH, 0, mu, sd, nullptr, nullptr, nullptr, nullptr,
                     flags);
+}
+
+SBO_API sbo_status sbo_query_cost(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, float *cost,
+                                  uint32_t flags) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(ctx->fitted, SBO_E_STATE, "sbo_query_cost: call sbo_fit first");
+    SBO_CHECK(qx && qy && cost, SBO_E_INVAL, "sbo_query_cost: null pointer");
+    SBO_CHECK(m > 0, SBO_E_EMPTY, "sbo_query_cost: m must be > 0");
+    SBO_HIP(hipSetDevice(ctx->device));
+    if (dev(flags)) {
+        if (sbo_status st = run_tick(ctx, qx, qy, m, 0.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, nullptr, nullptr,
+                                     nullptr, nullptr, nullptr, cost))
+            return st;
+        return finish(ctx, flags);
+    }
+    const size_t need = Carve::need(m, 4) * 3;
+    SBO_HIP(ctx->hq.reserve(need));
+    Carve c(ctx->hq.as<void>());
+    float *dqx = c.take<float>(m), *dqy = c.take<float>(m), *dc = c.take<float>(m);
+    SBO_HIP(hipMemcpyAsync(dqx, qx, sizeof(float) * m, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(dqy, qy, sizeof(float) * m, hipMemcpyHostToDevice, ctx->stream));
+    if (sbo_status st = run_tick(ctx, dqx, dqy, m, 0.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, nullptr, nullptr, nullptr,
+                                 nullptr, nullptr, dc))
+        return st;
+    SBO_HIP(hipMemcpyAsync(cost, dc, sizeof(float) * m, hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    return SBO_OK;
 }
 
 SBO_API sbo_status sbo_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, double beta, double f_min,

@@ -119,6 +119,7 @@ struct sbo_ctx {
     sbo::DevBuf ax3, kc3;        // split (bf16 x3) operand and its coordinates (kernel variants 2, 3)
     int64_t x3_I0 = 0;           // first row block whose split operand is stale (>= nI: current)
     sbo::DevBuf qpad;            // queries padded to whole blocks (split sweep without query ordering)
+    sbo::DevBuf qcost;           // sbo_query_cost scratch
     sbo::DevBuf info;            // rocSOLVER info
     sbo::DevBuf scratch;         // append workspace
     int64_t npad = 0;            // rows/cols of the packed operand (multiple of BM)
@@ -193,6 +194,11 @@ hipError_t launch_predict(hipStream_t s, const float *aug, const float *kcoord, 
                           int variant, int P, const void *work);
 // exp2 coefficient of the RBF kernel: k = exp2(cexp d^2), cexp = -1/(2 l^2 ln 2)
 float exp2_coef_f(float ell);
+// Per-query sweep work of the plan in `work` (kept k-tiles of the query's
+// block summed over row blocks / block size), in the caller's order.
+// bcost: (m + kBN - 1) / kBN floats of scratch.
+hipError_t launch_plan_cost(hipStream_t s, int64_t npad, int64_t m, int P, const void *work, const int32_t *perm,
+                            float *bcost, float *cost);
 // The plan's descriptors, tile lists and per-workgroup ranges inside `work`.
 void plan_views(int64_t npad, int64_t m, int P, const void *work, const int4 **desc, const unsigned short **tl,
                 const int **seg);

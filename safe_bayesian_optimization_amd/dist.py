@@ -24,6 +24,85 @@ def shard_range(m: int, rank: int, world: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < rem else 0)
 
 
+def query_work_estimate(qx, qy, x, y, length_scale: float, radius: float = 6.0) -> np.ndarray:
+    """Relative sweep work of each query: the number of training points within
+    ``radius`` length scales (box neighbourhood on an l-sized histogram).  The
+    sweep's kept k-tiles per query block follow the training points whose K*
+    can matter, so strips near the domain's edges cost less than central ones
+    (measured up to 1.9x apart for 8 equal strips at C4, tools/shard_emulate.py)."""
+    qx = np.asarray(qx, np.float64)
+    qy = np.asarray(qy, np.float64)
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    x0 = min(qx.min(), x.min())
+    y0 = min(qy.min(), y.min())
+    h = float(length_scale)
+    nx = int((max(qx.max(), x.max()) - x0) / h) + 1
+    ny = int((max(qy.max(), y.max()) - y0) / h) + 1
+    hist = np.zeros((ny, nx), np.float64)
+    np.add.at(hist, (np.minimum(((y - y0) / h).astype(np.int64), ny - 1),
+                     np.minimum(((x - x0) / h).astype(np.int64), nx - 1)), 1.0)
+    r = int(np.ceil(radius))
+    c = np.pad(hist, r).cumsum(0).cumsum(1)            # summed-area table of the padded histogram
+    c = np.pad(c, ((1, 0), (1, 0)))
+    k = 2 * r + 1
+    box = c[k:, k:] - c[:-k, k:] - c[k:, :-k] + c[:-k, :-k]   # (ny, nx): points within r bins
+    iy = np.minimum(((qy - y0) / h).astype(np.int64), ny - 1)
+    ix = np.minimum(((qx - x0) / h).astype(np.int64), nx - 1)
+    return box[iy, ix] + 1.0
+
+
+def balanced_cuts(weights, world: int, align: int = 128) -> list[int]:
+    """Cut points 0 = c_0 <= c_1 <= ... <= c_world = m of contiguous blocks that
+    carry about equal total weight (interior cuts on multiples of ``align``)."""
+    w = np.asarray(weights, np.float64)
+    m = w.size
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    cuts = [0]
+    for r in range(1, world):
+        c = int(np.searchsorted(cum, cum[-1] * r / world))
+        c = min(max(c - c % align, cuts[-1]), m)
+        cuts.append(c)
+    cuts.append(m)
+    return cuts
+
+
+def balanced_shard_range(weights, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous block [lo, hi) of rank ``rank`` under balanced_cuts."""
+    cuts = balanced_cuts(weights, world)
+    return cuts[rank], cuts[rank + 1]
+
+
+def cost_balanced_range(gm, qx, qy, rank: int, world: int, group=None) -> tuple[int, int]:
+    """Rank's contiguous block of the M queries such that every rank sweeps
+    about the same number of k-tiles: rank 0 builds the tick plan of all M
+    queries (sbo_query_cost, ~1 ms at C4, no sweep), cuts it, and broadcasts
+    the cut points, so the ranks agree even if their fits differ in the last
+    bit.  Equal-size strips of the C4 grid differ by up to 2x in work (the
+    K* cutoff keeps fewer tiles near the domain's edges and the factor's fill
+    follows the Hilbert order of the training points); cost-balanced strips
+    take the emulated 8-rank split from 6.0x to 7.0x of one rank
+    (tools/shard_emulate.py)."""
+    import torch
+    import torch.distributed as dist
+    m = int(qx.numel())
+    cuts = torch.zeros(world + 1, dtype=torch.int64, device=qx.device)
+    if rank == 0:
+        cost = gm.query_cost(qx, qy)
+        cost = cost.cpu().numpy() if hasattr(cost, "cpu") else np.asarray(cost)
+        cuts.copy_(torch.as_tensor(balanced_cuts(cost, world), dtype=torch.int64))
+    if world > 1:
+        if dist.get_backend(group) == "gloo" and cuts.is_cuda:
+            h = cuts.cpu()
+            dist.broadcast(h, 0, group=group)
+            cuts.copy_(h)
+        else:
+            dist.broadcast(cuts, 0, group=group)
+    c = [int(v) for v in cuts.cpu()]
+    assert c[0] == 0 and c[-1] == m and all(a <= b for a, b in zip(c, c[1:])), c
+    return c[rank], c[rank + 1]
+
+
 def combine_keys(keys) -> tuple[float, int]:
     """Reduce (score, idx) pairs: highest score, lowest index on ties; idx -1 = none."""
     best_s, best_i = 0.0, -1

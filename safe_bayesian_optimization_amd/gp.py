@@ -196,6 +196,21 @@ class TerrainMapper:
                                           ctypes.byref(key), fl))
         return key
 
+    def query_cost(self, qx, qy):
+        """Sweep work of each query under the current fit (sbo_query_cost):
+        the k-tiles its 128-query block multiplies, per query.  Deterministic,
+        so every rank computes the same cost-balanced shard cut
+        (dist.balanced_shard_range)."""
+        (qx, qy), fl = _prep([qx, qy], np.float32, "float32")
+        m = int(qx.numel() if _is_dev(qx) else qx.size)
+        if fl & N.SBO_DEVICE_PTRS:
+            import torch
+            cost = torch.empty(m, dtype=torch.float32, device=qx.device)
+        else:
+            cost = np.empty(m, np.float32)
+        self.ctx.check(self._lib.sbo_query_cost(self.ctx.handle, _ptr(qx), _ptr(qy), m, _ptr(cost), fl))
+        return cost
+
     # --------------------------------------------------------- test access
     def order(self) -> np.ndarray:
         """Caller's training index of each internal row (the factor's order)."""

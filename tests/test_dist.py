@@ -10,7 +10,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import oracle as O
-from safe_bayesian_optimization_amd.dist import allreduce_key, combine_keys, shard_range
+from safe_bayesian_optimization_amd.dist import (allreduce_key, balanced_cuts, combine_keys, cost_balanced_range,
+                                                shard_range)
 
 
 def test_shard_range_partitions():
@@ -73,4 +74,65 @@ def test_gloo_world2_key_allgather():
         p.join(timeout=60)
     want = O.argmax(score, mask)
     for _, (s, i) in res:
+        assert i == want[0] and s == want[1]
+
+
+def test_balanced_cuts_partition_and_balance():
+    rng = np.random.default_rng(3)
+    for m in [1, 100, 5000, 100003]:
+        w = rng.gamma(2.0, 1.0, m) * np.linspace(1.0, 4.0, m)   # work rising along the strip order
+        for world in [1, 2, 3, 8]:
+            c = balanced_cuts(w, world)
+            assert c[0] == 0 and c[-1] == m and all(a <= b for a, b in zip(c, c[1:]))
+            assert all(x % 128 == 0 for x in c[1:-1])
+            if m >= 128 * world * 8:
+                share = [w[a:b].sum() for a, b in zip(c, c[1:])]
+                # each block within one aligned row block of the ideal share
+                assert max(share) - w.sum() / world <= 128 * w.max() + 1e-9
+
+
+class _FakeMapper:
+    def __init__(self, cost):
+        self.cost = cost
+
+    def query_cost(self, qx, qy):
+        return self.cost
+
+
+def _cost_worker(rank, world, port, cost, score, mask, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = cost.size
+    qx = torch.zeros(m)
+    # only rank 0's mapper knows the costs: the cut must come from the broadcast
+    gm = _FakeMapper(cost if rank == 0 else np.ones(m, np.float32))
+    a, b = cost_balanced_range(gm, qx, qx, rank, world)
+    i, v = O.argmax(score[a:b], mask[a:b])
+    gi = a + i if i >= 0 else -1
+    key = torch.tensor([struct.unpack("<q", struct.pack("<d", v))[0], gi], dtype=torch.int64)
+    q.put((rank, (a, b), allreduce_key(key)))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_cost_balanced_shards():
+    rng = np.random.default_rng(11)
+    m = 20000
+    cost = np.linspace(1.0, 9.0, m).astype(np.float32)       # the second half costs more
+    score = np.round(rng.uniform(0, 5, m), 1)
+    mask = (rng.uniform(size=m) < 0.5).astype(np.uint8)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cost_worker, args=(r, 2, port, cost, score, mask, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    (_, s0, k0), (_, s1, k1) = res
+    assert s0[0] == 0 and s0[1] == s1[0] and s1[1] == m
+    assert s0[1] == balanced_cuts(cost, 2)[1] and s0[1] > m // 2   # the cheap half is the longer one
+    want = O.argmax(score, mask)
+    for s, i in (k0, k1):
         assert i == want[0] and s == want[1]

@@ -608,3 +608,25 @@ def test_state_export_import(dev, mapper):
     b.fit(wl.x, wl.y, wl.obs)      # a refit restores the full state
     b.append(wl.x[:5] + 0.01, wl.y[:5], wl.obs[:5])
     b.close()
+
+
+def test_query_cost_is_the_plan(mapper):
+    """sbo_query_cost: per-query share of its block's kept k-tiles -- summed
+    over the queries it is the tick's multiplied-tile count (the device work
+    counter), it is deterministic, and it does not disturb the next tick."""
+    wl = synthetic(3000, 80, 60, seed=31)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    mu0, sd0 = gm.predict(wl.qx, wl.qy)
+    cost = gm.query_cost(wl.qx, wl.qy)
+    assert cost.shape == wl.qx.shape and np.all(cost >= 0)
+    assert np.array_equal(cost, gm.query_cost(wl.qx, wl.qy))
+    lib = N.lib()
+    lib.sbo_profile(gm.ctx.handle, 1)
+    mu1, sd1 = gm.predict(wl.qx, wl.qy)
+    w = ctypes.c_double()
+    lib.sbo_profile_work(gm.ctx.handle, ctypes.byref(w))
+    lib.sbo_profile(gm.ctx.handle, 0)
+    tiles = w.value / (2.0 * 256 * 128 * 64)
+    assert tiles > 0 and abs(float(cost.astype(np.float64).sum()) - tiles) <= 1e-4 * tiles
+    assert np.array_equal(mu0, mu1) and np.array_equal(sd0, sd1)
