@@ -184,13 +184,14 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                 nx.l[c][i] = w2;
             }
         } else {
-            const f32x2v as = ak * msc;  // msc = 0: not the mean's row block
+            if (msc != 0.0f) {  // the next step is the mean's row block (uniform branch)
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                // the pair's terms in f32 (one rounding of a two-term sum, the
-                // order of K*'s own), accumulated in f64
-                mu[c] += (double)fmaf(as.x, e[c].x, as.y * e[c].y);
-                SBO_PIN(mu[c]);
+                for (int c = 0; c < NC; ++c) {
+                    // the pair's terms in f32 (one rounding of a two-term sum,
+                    // the order of K*'s own), accumulated in f64
+                    mu[c] += (double)fmaf(ak.x, e[c].x, ak.y * e[c].y);
+                    SBO_PIN(mu[c]);
+                }
             }
             if (i < 3) {
                 xk = lds_f2(pcn + g * 32 + (i + 1) * 8);
