@@ -200,7 +200,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
             }
         }
         if (SPREAD && rb >= 1 && rb <= PIECES) dma16(voff, asrc + (rb - 1) * kStride, adst + (rb - 1) * kStride);
-        if (!FRESH && !(DIAG & 4) && rb > 1) {  // those chains finished a block ago
+        if (!FRESH && !(DIAG & 68) && rb > 1) {  // those chains finished a block ago
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 outer[c][rb - 2] += acc[c][rb - 2];
@@ -209,7 +209,8 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
         }
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            f32x4 v = FRESH ? zero : acc[c][rb];
+            // (DIAG & 64: one chain over the whole item, no outer sums -- timing only)
+            f32x4 v = (FRESH && !(DIAG & 64)) ? zero : acc[c][rb];
             v = mfma(a2, kb.h[c], v);
             v = mfma(a1, kb.m[c], v);
             v = mfma(a0, kb.l[c], v);
@@ -243,7 +244,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
             a2 = b2;
         }
     }
-    if (!FRESH && !(DIAG & 4)) {
+    if (!FRESH && !(DIAG & 68)) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             outer[c][14] += acc[c][14];
@@ -491,6 +492,14 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
         if (!FRESH && (s0.flags & kLast)) {
             // item done: column sums of V^2 over its rows (lanes l, l+16, l+32,
             // l+48 hold four row quarters of column l&15 of every block)
+            if (DIAG & 64)
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+#pragma unroll
+                    for (int rb = 0; rb < 16; ++rb) {
+                        outer[c][rb] = acc[c][rb];
+                        acc[c][rb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                    }
             pend = true;
             pend_I = s0.I;
             pend_q = (int64_t)s0.qb * kBN + qo;
@@ -613,6 +622,8 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 8: SBO_X3_LAUNCH(1, 24); break;   //   every stage from the first tile
         case 9: SBO_X3_LAUNCH(1, 0); break;    // A pieces in a burst at the top of the step
         case 10: SBO_X3_LAUNCH(1, 48); break;  // A fragments one row block ahead
+        case 11: SBO_X3_LAUNCH(1, 80); break;  // diagnostics: one chain per item, no outer sums
+        case 12: SBO_X3_LAUNCH(1, 81); break;  //   and no next-step K*
         default: SBO_X3_LAUNCH(1, 16); break;  // 3: eight waves of 16 queries, A pieces spread
     }
 #undef SBO_X3_LAUNCH
