@@ -276,6 +276,120 @@ __device__ __forceinline__ void x3_kstar(const lds_char *pc, const float (&xq)[N
     }
 }
 
+// ---- the wide shape (variant 13): v_mfma_f32_32x32x16_bf16, four waves of
+// 32 queries.  A 32x32x16 MFMA holds the SIMD's issue for 8 of its 32 cycles
+// (the 16x16x32 form: 8 of 16), so the same matrix work leaves twice the
+// issue slots to the K* VALU.  Lane l holds A[32 rb + (l&31)][16 s + 8(l>>5)
+// + j] (A planes laid out [rb (8)][s (2)][lane][8 bf16] per half-tile, see
+// pack_x3_kernel), B = K*[k = 16 s + 8(l>>5) + j][query l&31], and the 32x32
+// accumulator col = l&31, rows (r&3) + 8(r>>2) + 4(l>>5).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+}
+
+// One half-step of one wave (wide shape): 16 sub-steps u = (rb, s), six
+// MFMAs each; the next step's K* pair p = u/2 (values j = 2(p&3), +1 of
+// sub-step p>>2) is evaluated at even u and split (+ mean terms, + the next
+// pair's coordinates) at odd u; the finished chains of row block rb-1 are
+// added into `outer` over sub-steps 2rb, 2rb+1.
+template <bool FRESH, int DIAG>
+__device__ __forceinline__ void x3w_half(const lds_char *pa, const lds_char *pcn, float xq, float yq, int h,
+                                         float cexp, float msc, const KPieces<2> &kb, f32x16 (&acc)[8],
+                                         f32x16 (&outer)[8], KPieces<2> &nx, double &mu, uint32_t voff,
+                                         const char *asrc, uint32_t adst) {
+    constexpr int kStride = 4 * 1024;  // four loader waves
+    const f32x16 zero = {};
+    u32x4 a0 = lds_b128(pa), a1 = lds_b128(pa + kXPlane), a2 = lds_b128(pa + 2 * kXPlane);
+    f32x2v xk = lds_f2(pcn + h * 32), yk = lds_f2(pcn + 128 + h * 32), ak = lds_f2(pcn + 256 + h * 32);
+    f32x2v e = {0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int rb = u >> 1, s = u & 1;
+        u32x4 b0, b1, b2;
+        if (u + 1 < 16) {
+            b0 = lds_b128(pa + (u + 1) * 1024);
+            b1 = lds_b128(pa + kXPlane + (u + 1) * 1024);
+            b2 = lds_b128(pa + 2 * kXPlane + (u + 1) * 1024);
+        }
+        if (u >= 1 && u <= 12) dma16(voff, asrc + (u - 1) * kStride, adst + (u - 1) * kStride);
+        const int p = u >> 1, sp = p >> 2, dp = p & 3;
+        if (DIAG & 1) {
+        } else if (s == 0) {
+            e.x = kstar1(xk.x, yk.x, xq, yq, cexp);
+            e.y = kstar1(xk.y, yk.y, xq, yq, cexp);
+            SBO_PIN(e.x);
+            SBO_PIN(e.y);
+        } else {
+            uint32_t w0, w1, w2;
+            split3(e.x, e.y, w0, w1, w2);
+            SBO_PIN(w0);
+            SBO_PIN(w1);
+            SBO_PIN(w2);
+            nx.h[sp][dp] = w0;
+            nx.m[sp][dp] = w1;
+            nx.l[sp][dp] = w2;
+            if (msc != 0.0f) {  // the next step is the mean's row block (uniform branch)
+                mu += (double)fmaf(ak.x, e.x, ak.y * e.y);
+                SBO_PIN(mu);
+            }
+            if (p < 7) {  // pair p+1: sub-step (p+1)>>2, values 2((p+1)&3), +1
+                const int o = ((p + 1) >> 2) * 64 + h * 32 + ((p + 1) & 3) * 8;
+                xk = lds_f2(pcn + o);
+                yk = lds_f2(pcn + 128 + o);
+                ak = lds_f2(pcn + 256 + o);
+            }
+        }
+        if (!FRESH && rb > 0) {  // row block rb-1 finished a sub-step ago: half of it per sub-step
+#pragma unroll
+            for (int e2 = 0; e2 < 8; ++e2) {
+                outer[rb - 1][8 * s + e2] += acc[rb - 1][8 * s + e2];
+            }
+        }
+        f32x16 v = (FRESH && s == 0) ? zero : acc[rb];
+        v = mfma32(a2, kb.h[s], v);
+        v = mfma32(a1, kb.m[s], v);
+        v = mfma32(a0, kb.l[s], v);
+        v = mfma32(a1, kb.h[s], v);
+        v = mfma32(a0, kb.m[s], v);
+        v = mfma32(a0, kb.h[s], v);
+        acc[rb] = v;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // VALU
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (u + 1 < 16) {
+            a0 = b0;
+            a1 = b1;
+            a2 = b2;
+        }
+    }
+    if (!FRESH) outer[7] += acc[7];
+}
+
+// K* pieces of one step directly (wide shape, the prologue's first step)
+__device__ __forceinline__ void x3w_kstar(const lds_char *pc, float xq, float yq, int h, float cexp, bool mean,
+                                          KPieces<2> &kb, double &mu) {
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+        for (int dp = 0; dp < 4; ++dp) {
+            const int o = sp * 64 + h * 32 + dp * 8;
+            const f32x2v xk = lds_f2(pc + o), yk = lds_f2(pc + 128 + o), ak = lds_f2(pc + 256 + o);
+            const float e0 = kstar1(xk.x, yk.x, xq, yq, cexp), e1 = kstar1(xk.y, yk.y, xq, yq, cexp);
+            uint32_t w0, w1, w2;
+            split3(e0, e1, w0, w1, w2);
+            kb.h[sp][dp] = w0;
+            kb.m[sp][dp] = w1;
+            kb.l[sp][dp] = w2;
+            if (mean) mu += (double)fmaf(ak.x, e0, ak.y * e1);
+        }
+}
+
 // per staged step: row block, query block, and flags
 struct XStep {
     int I, qb, flags;  // bit 0: second half, bit 1: first step of its item, bit 2: last step, bit 3: valid
@@ -290,13 +404,17 @@ constexpr int kFirst = 2, kLast = 4, kValid = 8;
 // 16 (not a diagnostic): A pieces spread over the row blocks; 32: A fragments
 // read one row block ahead instead of two.
 template <int NC, int DIAG>
-__global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
+__global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     const char *__restrict__ ax3, const float *__restrict__ kc3, const int4 *__restrict__ desc,
     const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P, int n_items, int nI,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp, float cexp, float m0,
     float *__restrict__ part, float *__restrict__ mean) {
     __shared__ __attribute__((aligned(16))) char smem[kXSmem];
-    constexpr int kLoaders = 8 / NC;                  // waves
+    // NC = 1, 2: 16x16x32 MFMA, NC 16-query column blocks per wave; NC = 3:
+    // the wide shape (32x32x16, 32 queries per wave)
+    constexpr bool WIDE = NC == 3;
+    constexpr int NQ = NC == 2 ? 2 : 1;                // queries per lane
+    constexpr int kLoaders = NC == 1 ? 8 : 4;         // waves
     constexpr int kPieces = (kXA / 1024) / kLoaders;  // A pieces per wave per stage (6 or 12)
     static_assert(kPieces == 6 || kPieces == 12, "the end-of-step wait below counts 6 or 12 pieces");
     const int bid = blockIdx.x;
@@ -406,39 +524,45 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    const int qo = lw * 16 * NC + r;  // the lane's queries in the block: qo + 16 c
-    f32x4 acc[NC][16], outer[NC][16];
+    // the lane's queries in the block: qo + 16 c (c < NQ)
+    const int qo = WIDE ? lw * 32 + (lane & 31) : lw * 16 * NC + r;
+    constexpr int kCB = NC == 2 ? 2 : 1, kRB = WIDE ? 8 : 16;
+    typedef std::conditional_t<WIDE, f32x16, f32x4> AccT;
+    AccT acc[kCB][kRB], outer[kCB][kRB];
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
+    for (int c = 0; c < kCB; ++c)
 #pragma unroll
-        for (int rb = 0; rb < 16; ++rb) {
-            acc[c][rb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int rb = 0; rb < kRB; ++rb) {
+            acc[c][rb] = AccT{};
             outer[c][rb] = acc[c][rb];
         }
-    double mu[NC];
-    KPieces<NC> kb, nx;
+    double mu[NQ];
+    KPieces<WIDE ? 2 : NC> kb, nx;
     {
         const lds_char *pq = lds + kXA + kXC;
-        float xq[NC], yq[NC];
+        float xq[NQ], yq[NQ];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
+        for (int c = 0; c < NQ; ++c) {
             mu[c] = 0.0;
             xq[c] = lds_f(pq + (qo + 16 * c) * 4);
             yq[c] = lds_f(pq + (kBN + qo + 16 * c) * 4);
         }
-        x3_kstar<NC>(lds + kXA, xq, yq, g, cexp, s0.I == nI - 1, kb, mu);
+        if constexpr (WIDE)
+            x3w_kstar(lds + kXA, xq[0], yq[0], lane >> 5, cexp, s0.I == nI - 1, kb, mu[0]);
+        else
+            x3_kstar<NC>(lds + kXA, xq, yq, g, cexp, s0.I == nI - 1, kb, mu);
     }
     // deferred outputs of the item finished in the previous step (stored at
     // the top of the next step, before its stage DMA, so that the vmcnt count
     // at the end of every step is the A pieces of one stage)
     bool pend = false, pend_mean = false;
-    float pend_s[NC], pend_mu[NC];
+    float pend_s[NQ], pend_mu[NQ];
     int64_t pend_q = 0;
     int pend_I = 0;
     auto flush = [&]() {
-        if (pend && lane < 16) {
+        if (pend && lane < (WIDE ? 32 : 16)) {
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
+            for (int c = 0; c < NQ; ++c) {
                 const int64_t q = pend_q + 16 * c;
                 if (q < m) {
                     part[(int64_t)pend_I * ldp + q] = pend_s[c];
@@ -471,50 +595,56 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
             // item's terms start
             if ((s0.flags & kLast) && s0.I == nI - 1) {
 #pragma unroll
-                for (int c = 0; c < NC; ++c) {
+                for (int c = 0; c < NQ; ++c) {
                     double u = mu[c];
-                    u += __shfl_xor(u, 16);
+                    if (!WIDE) u += __shfl_xor(u, 16);
                     u += __shfl_xor(u, 32);
                     pend_mu[c] = (float)((double)m0 + u);
                 }
             }
             if (nvalid && (s1.flags & kFirst))
 #pragma unroll
-                for (int c = 0; c < NC; ++c) mu[c] = 0.0;
+                for (int c = 0; c < NQ; ++c) mu[c] = 0.0;
         }
-        float xq[NC], yq[NC];
+        float xq[NQ], yq[NQ];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
+        for (int c = 0; c < NQ; ++c) {
             xq[c] = lds_f(pqn + (qo + 16 * c) * 4);
             yq[c] = lds_f(pqn + (kBN + qo + 16 * c) * 4);
         }
-        x3_half<NC, FRESH, DIAG, kPieces>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src, a_dst);
+        if constexpr (WIDE)
+            x3w_half<FRESH, DIAG>(pa, pcn, xq[0], yq[0], lane >> 5, cexp, msc, kb, acc[0], outer[0], nx, mu[0],
+                                  voff, a_src, a_dst);
+        else
+            x3_half<NC, FRESH, DIAG, kPieces>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
+                                              a_dst);
         if (!FRESH && (s0.flags & kLast)) {
             // item done: column sums of V^2 over its rows (lanes l, l+16, l+32,
             // l+48 hold four row quarters of column l&15 of every block)
             if (DIAG & 64)
 #pragma unroll
-                for (int c = 0; c < NC; ++c)
+                for (int c = 0; c < kCB; ++c)
 #pragma unroll
-                    for (int rb = 0; rb < 16; ++rb) {
+                    for (int rb = 0; rb < kRB; ++rb) {
                         outer[c][rb] = acc[c][rb];
-                        acc[c][rb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                        acc[c][rb] = AccT{};
                     }
             pend = true;
             pend_I = s0.I;
             pend_q = (int64_t)s0.qb * kBN + qo;
             pend_mean = s0.I == nI - 1;
+            constexpr int kE = WIDE ? 16 : 4;
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
+            for (int c = 0; c < kCB; ++c) {
                 double sv = 0.0;
 #pragma unroll
-                for (int rb = 0; rb < 16; ++rb)
+                for (int rb = 0; rb < kRB; ++rb)
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
+                    for (int e = 0; e < kE; ++e) {
                         sv = fma((double)outer[c][rb][e], (double)outer[c][rb][e], sv);
                         outer[c][rb][e] = 0.0f;
                     }
-                sv += __shfl_xor(sv, 16);
+                if (!WIDE) sv += __shfl_xor(sv, 16);
                 sv += __shfl_xor(sv, 32);
                 pend_s[c] = (float)sv;
             }
@@ -550,18 +680,21 @@ __global__ __launch_bounds__(64 * 8 / NC, 1) void predict_x3_kernel(
 // the three bf16 planes of the x3 layout: tile T, half h, plane p, row block
 // rb, lane l = 16 g + r holds A[16 rb + r][32 h + 8 g + j], j = 0..7, at
 // byte T*2*kXA + h*kXA + p*kXPlane + rb*1024 + l*16 + 2j.
+// wide = 1: the 32x32x16 layout of the wide shape, lane l of 1 KiB run
+// u = 2 rb + s holds A[32 rb + (l&31)][32 h + 16 s + 8(l>>5) + j].
 __global__ __launch_bounds__(256) void pack_x3_kernel(const float *__restrict__ aug, int64_t T0, int64_t nt,
-                                                      char *__restrict__ ax3) {
+                                                      int wide, char *__restrict__ ax3) {
     const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (id >= nt * 2048) return;
     const int lane = (int)(id & 63), rb = (int)((id >> 6) & 15), h = (int)((id >> 10) & 1);
     const int64_t T = T0 + (id >> 11);
-    const int r = lane & 15, g = lane >> 4, row = rb * 16 + r;
+    const int row = wide ? (rb >> 1) * 32 + (lane & 31) : rb * 16 + (lane & 15);
+    const int k0 = wide ? kXH * h + 16 * (rb & 1) + 8 * (lane >> 5) : kXH * h + 8 * (lane >> 4);
     const float *src = aug + T * kTileFloats;
     u32x4 w0, w1, w2;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const int k = kXH * h + 8 * g + 2 * d;
+        const int k = k0 + 2 * d;
         uint32_t a, b, c;
         split3(src[tile_offset(k, row)], src[tile_offset(k + 1, row)], a, b, c);
         w0[d] = a;
@@ -591,13 +724,14 @@ __global__ void pack_kc3_kernel(const float *__restrict__ kcoord, int64_t nkt, f
 size_t x3_operand_bytes(int64_t npad) { return (size_t)total_tiles(npad / kBM) * 2 * kXA; }
 size_t x3_coord_bytes(int64_t npad) { return (size_t)(npad / kBK) * 256 * sizeof(float); }
 
-hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, int64_t I0, char *ax3,
-                          float *kc3) {
+hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, int64_t I0, int wide,
+                          char *ax3, float *kc3) {
     const int64_t nI = npad / kBM;
     const int64_t T0 = tile_start(I0), T1 = tile_start(nI);
     if (T1 > T0) {
         const int64_t th = (T1 - T0) * 2048;
-        hipLaunchKernelGGL(pack_x3_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, aug, T0, T1 - T0, ax3);
+        hipLaunchKernelGGL(pack_x3_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, aug, T0, T1 - T0, wide,
+                           ax3);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -611,7 +745,7 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
                              const float *qy, int64_t m, int64_t ldp, float cexp, float m0, float *part, float *mean,
                              int variant) {
 #define SBO_X3_LAUNCH(NC, D) \
-    hipLaunchKernelGGL((predict_x3_kernel<NC, D>), dim3((unsigned)P), dim3(64 * 8 / NC), 0, s, ax3, kc3, desc, tl, \
+    hipLaunchKernelGGL((predict_x3_kernel<NC, D>), dim3((unsigned)P), dim3(NC == 1 ? 512 : 256), 0, s, ax3, kc3, desc, tl, \
                        seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean)
     switch (variant) {
         case 2: SBO_X3_LAUNCH(2, 16); break;   // four waves of 32 queries
@@ -624,6 +758,8 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 10: SBO_X3_LAUNCH(1, 48); break;  // A fragments one row block ahead
         case 11: SBO_X3_LAUNCH(1, 80); break;  // diagnostics: one chain per item, no outer sums
         case 12: SBO_X3_LAUNCH(1, 81); break;  //   and no next-step K*
+        case 13: SBO_X3_LAUNCH(3, 16); break;  // wide shape: 32x32x16 MFMA, four waves of 32 queries
+        case 14: SBO_X3_LAUNCH(3, 17); break;  //   diagnostics: no next-step K*
         default: SBO_X3_LAUNCH(1, 16); break;  // 3: eight waves of 16 queries, A pieces spread
     }
 #undef SBO_X3_LAUNCH

@@ -431,14 +431,17 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         // split-operand sweep: derive the bf16 planes of any repacked row
         // block, and give the kernel whole 128-query blocks to read
         const int64_t nIc = ctx->npad / sbo::kBM;
+        const int layout = sbo::x3_layout(ctx->kernel_variant);
+        if (layout != ctx->x3_layout) ctx->x3_I0 = 0;  // another layout: derive all of it
         if (ctx->x3_I0 < nIc) {
             const int64_t I0 = std::max<int64_t>(ctx->x3_I0, 0);
             SBO_HIP(grow_keep(ctx, ctx->ax3, sbo::x3_operand_bytes(ctx->npad),
                               sbo::x3_operand_bytes(I0 * sbo::kBM)));
             SBO_HIP(ctx->kc3.reserve(sbo::x3_coord_bytes(ctx->npad)));
             SBO_HIP(sbo::launch_pack_x3(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(), ctx->npad, I0,
-                                        ctx->ax3.as<char>(), ctx->kc3.as<float>()));
+                                        layout, ctx->ax3.as<char>(), ctx->kc3.as<float>()));
             ctx->x3_I0 = INT64_MAX;
+            ctx->x3_layout = layout;
         }
         if (!perm) {
             const int64_t mp = sbo::round_up(m, sbo::kBN);
@@ -910,7 +913,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->sweep_groups = (int)value;
             return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
-            SBO_CHECK(value >= 0 && value <= 12, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 12]");
+            SBO_CHECK(value >= 0 && value <= 14, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 14]");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
         case SBO_OPT_TILE_SKIP:

@@ -118,6 +118,7 @@ struct sbo_ctx {
     sbo::DevBuf kcoord;          // per k-tile: x[BK], y[BK], sf2*alpha[BK]
     sbo::DevBuf ax3, kc3;        // split (bf16 x3) operand and its coordinates (kernel variants 2, 3)
     int64_t x3_I0 = 0;           // first row block whose split operand is stale (>= nI: current)
+    int x3_layout = -1;          // layout of the derived split operand (sbo::x3_layout)
     sbo::DevBuf qpad;            // queries padded to whole blocks (split sweep without query ordering)
     sbo::DevBuf qcost;           // sbo_query_cost scratch
     sbo::DevBuf info;            // rocSOLVER info
@@ -207,8 +208,10 @@ void plan_views(int64_t npad, int64_t m, int P, const void *work, const int4 **d
 // coordinates in natural order, for row blocks >= I0 (coordinates: all).
 size_t x3_operand_bytes(int64_t npad);
 size_t x3_coord_bytes(int64_t npad);
-hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, int64_t I0, char *ax3,
-                          float *kc3);
+hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, int64_t I0, int wide,
+                          char *ax3, float *kc3);
+// the split operand's layout a kernel variant reads (1: the wide 32x32x16 shape)
+inline int x3_layout(int variant) { return (variant == 13 || variant == 14) ? 1 : 0; }
 // The sweep over the plan with the split operand; qx/qy must be readable in
 // whole 128-query blocks (padded to round_up(m, kBN)).  variant: 2 (4-7:
 // timing diagnostics with parts of the work left out).

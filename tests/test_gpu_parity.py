@@ -410,10 +410,10 @@ def test_sweep_partition_and_outer_variant(mapper):
     with pytest.raises(N.SboError):
         gm.set_option(N.SBO_OPT_SWEEP_GROUPS, -1)
     with pytest.raises(N.SboError):
-        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 13)
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 15)
 
 
-@pytest.mark.parametrize("variant", [2, 3, 9])
+@pytest.mark.parametrize("variant", [2, 3, 9, 13])
 def test_split_operand_sweep(mapper, variant):
     """The split-operand (bf16 x3) sweep: bitwise the same for every
     partition of the plan (1, 3, 7, 8, 1000 workgroups, and one per CU with
