@@ -133,11 +133,12 @@ template <int NC, bool FRESH, int DIAG, int PIECES>
 __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn, const float (&xq)[NC],
                                         const float (&yq)[NC], int g, float cexp, float msc, const KPieces<NC> &kb,
                                         f32x4 (&acc)[NC][16], f32x4 (&outer)[NC][16], KPieces<NC> &nx,
-                                        double (&mu)[NC], uint32_t voff, const char *asrc, uint32_t adst) {
+                                        double (&mu)[NC], uint32_t voff, const char *asrc, uint32_t adst,
+                                        bool loader) {
     // SPREAD (DIAG & 16): this wave's A pieces of stage i+2 are issued one
     // per row block between the MFMAs instead of in a burst at the top
     constexpr bool SPREAD = (DIAG & 16) != 0;
-    constexpr int kStride = (8 / NC) * 1024;
+    constexpr int kStride = (PIECES == 6 ? 8 : 4) * 1024;  // loader waves x 1 KiB
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
     // A fragments: row block rb in use, rb+1 landed or landing, rb+2 issued
     // during rb (DIAG & 32: one block ahead only)
@@ -199,7 +200,8 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                 ak = lds_f2(pcn + 256 + g * 32 + (i + 1) * 8);
             }
         }
-        if (SPREAD && rb >= 1 && rb <= PIECES) dma16(voff, asrc + (rb - 1) * kStride, adst + (rb - 1) * kStride);
+        if (SPREAD && rb >= 1 && rb <= PIECES && loader)
+            dma16(voff, asrc + (rb - 1) * kStride, adst + (rb - 1) * kStride);
         if (!FRESH && !(DIAG & 68) && rb > 1) {  // those chains finished a block ago
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
@@ -222,11 +224,20 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
         // interleave: each MFMA followed by two VALU and one LDS read, so the
         // vector work issues in the matrix pipe's shadow (a bf16 MFMA holds
         // the SIMD's issue for 8 of its 16 cycles)
+        if constexpr (DIAG & 128) {  // A/B: more VALU per MFMA gap
 #pragma unroll
-        for (int j = 0; j < 6 * NC; ++j) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            for (int j = 0; j < 6 * NC; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            }
+        } else if constexpr (!(DIAG & 256)) {  // (256: the compiler's own order)
+#pragma unroll
+            for (int j = 0; j < 6 * NC; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
         if (AHEAD == 2) {
@@ -414,8 +425,10 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     // the wide shape (32x32x16, 32 queries per wave)
     constexpr bool WIDE = NC == 3;
     constexpr int NQ = NC == 2 ? 2 : 1;                // queries per lane
-    constexpr int kLoaders = NC == 1 ? 8 : 4;         // waves
-    constexpr int kPieces = (kXA / 1024) / kLoaders;  // A pieces per wave per stage (6 or 12)
+    // A-stage loaders: every wave, or (DIAG & 1024, NC = 1) only waves 4-7
+    constexpr bool HALF_LOAD = NC == 1 && (DIAG & 1024);
+    constexpr int kLoaders = (NC == 1 && !HALF_LOAD) ? 8 : 4;
+    constexpr int kPieces = (kXA / 1024) / kLoaders;  // A pieces per loader wave per stage (6 or 12)
     static_assert(kPieces == 6 || kPieces == 12, "the end-of-step wait below counts 6 or 12 pieces");
     const int bid = blockIdx.x;
     const int rng = (P % 8 == 0) ? (bid % 8) * (P / 8) + bid / 8 : bid;
@@ -432,7 +445,9 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     // only per-lane operand is the byte offset lane*16
     const uint32_t voff = (uint32_t)lane * 16u;
     const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
-    const uint32_t lds_wave = lds_smem + (uint32_t)lw * 1024u;
+    const int ldr = HALF_LOAD ? lw - 4 : lw;  // loader index (< 0: no A pieces)
+    const bool is_loader = ldr >= 0;
+    const uint32_t lds_wave = lds_smem + (uint32_t)(is_loader ? ldr : 0) * 1024u;
     const uint32_t lds_dwin = lds_smem + (uint32_t)kXWin;
     const uint32_t lds_lwin = lds_dwin + 2048u;
 #define SBO_DMA16(sbase, ldst)                                                                          \
@@ -451,11 +466,11 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
             else SBO_DMA16(qy + (int64_t)(qb_) * kBN - 128, d_ + kXA + kXC);                            \
             if (lane < 32) SBO_DMA16(kc3 + (int64_t)(t_) * (2 * kXC / 4) + (h_) * (kXC / 4), d_ + kXA);  \
         }                                                                                               \
-        const char *s_ = ax3 + ((DIAG & 8) ? 0 : ((Tg_) * 2 + (h_)) * (int64_t)kXA) + lw * 1024;       \
+        const char *s_ = ax3 + ((DIAG & 8) ? 0 : ((Tg_) * 2 + (h_)) * (int64_t)kXA) + (is_loader ? ldr : 0) * 1024; \
         const uint32_t w_ = lds_wave + (uint32_t)(sl_) * kXSlot;                                        \
         a_src = s_;                                                                                     \
         a_dst = w_;                                                                                     \
-        if (!(DIAG & 2) && ((burst_) || !(DIAG & 16)))                                                  \
+        if (!(DIAG & 2) && is_loader && ((burst_) || !(DIAG & 16)))                                     \
             _Pragma("unroll") for (int j = 0; j < kPieces; ++j)                                         \
                 SBO_DMA16(s_ + j * kLoaders * 1024, w_ + (uint32_t)(j * kLoaders * 1024));              \
     } while (0)
@@ -617,7 +632,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
                                   voff, a_src, a_dst);
         else
             x3_half<NC, FRESH, DIAG, kPieces>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
-                                              a_dst);
+                                              a_dst, is_loader);
         if (!FRESH && (s0.flags & kLast)) {
             // item done: column sums of V^2 over its rows (lanes l, l+16, l+32,
             // l+48 hold four row quarters of column l&15 of every block)
@@ -651,13 +666,16 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         }
         // retire stage i+1: its queries and coordinates (wave 0) precede its
         // A pieces and were retired one step earlier; leave stage i+2's A in flight
-        if ((issue || (DIAG & 16)) && !(DIAG & 2)) {
+        if ((issue || (DIAG & 16)) && !(DIAG & 2) && is_loader) {
             if constexpr (kPieces == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (DIAG & 512)  // timing only: no step barrier (races on the slots)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         more = nvalid;
         s0 = s1;
         s1 = s2;
@@ -760,6 +778,11 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 12: SBO_X3_LAUNCH(1, 81); break;  //   and no next-step K*
         case 13: SBO_X3_LAUNCH(3, 16); break;  // wide shape: 32x32x16 MFMA, four waves of 32 queries
         case 14: SBO_X3_LAUNCH(3, 17); break;  //   diagnostics: no next-step K*
+        case 15: SBO_X3_LAUNCH(1, 144); break;  // schedule A/B: four VALU per MFMA gap
+        case 16: SBO_X3_LAUNCH(1, 272); break;  //   the compiler's own interleave
+        case 17: SBO_X3_LAUNCH(1, 528); break;  // diagnostics: no step barrier (wrong results)
+        case 18: SBO_X3_LAUNCH(1, 529); break;  //   and no next-step K*
+        case 19: SBO_X3_LAUNCH(1, 1040); break;  // A stage loaded by waves 4-7 only (12 pieces each)
         default: SBO_X3_LAUNCH(1, 16); break;  // 3: eight waves of 16 queries, A pieces spread
     }
 #undef SBO_X3_LAUNCH

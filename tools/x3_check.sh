@@ -2,6 +2,5 @@
 mkdir -p gpurun_out/x3
 O=gpurun_out/x3
 export TMPDIR=/tmp
-step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -3 $O/$name.log | cut -c1-400; [ $rc -eq 0 ] || exit $rc; }
-step gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --steps 3 --no-cpu
+step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -6 $O/$name.log | cut -c1-400; [ $rc -eq 0 ] || exit $rc; }
+step ab_c4 300 python tools/ab_variants.py --config C4 --variants 3 19 --rounds 3
