@@ -159,12 +159,14 @@ __global__ __launch_bounds__(kBM) void row_l1_kernel(const float *__restrict__ a
     atomicAdd(row_l1 + I * kBM + r, s);
 }
 
-// Per packed tile: log2 of a bound on the tile's 2-norm gain, nu with
-// |A_It k|_2 <= nu max|k| for every 64-vector k:  nu = min(16 max_r |A_r|_1,
-// 8 |A_It|_F)  (|.|_2 <= sqrt(256) |.|_inf, resp. |A k|_2 <= |A|_F |k|_2 and
-// |k|_2 <= 8 max|k|).  One workgroup per tile, thread r = row r, f64 sums.
+// Per packed tile, two gain bounds for |A_It k|_2 (log2, rounded up):
+// .x = log2(16 max_r |A_r|_1)  (|A k|_2 <= sqrt(256) |A k|_inf <= 16 max_r |A_r|_1 max|k|)
+// .y = log2(|A_It|_F)           (|A k|_2 <= |A|_F |k|_2)
+// the plan pairs .x with the largest K* of the tile and .y with a bound on
+// |k|_2 from the tile's points.  One workgroup per tile, thread r = row r,
+// f64 sums.
 __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
-                                                        float *__restrict__ lgn) {
+                                                        float2 *__restrict__ lgn) {
     __shared__ double red[2][kBM / 64];
     const int64_t tile = t0 + blockIdx.x;
     const float *t = aug + tile * kTileFloats;
@@ -190,8 +192,8 @@ __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict_
             s = fmax(s, red[0][w]);
             q += red[1][w];
         }
-        const double nu = fmin(16.0 * s, 8.0 * sqrt(q));
-        lgn[tile] = nu > 0.0 ? (float)log2(nu) + 1e-5f : -1000.0f;  // rounded up
+        lgn[tile] = make_float2(s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f,
+                                q > 0.0 ? (float)(0.5 * log2(q)) + 1e-5f : -1000.0f);
     }
 }
 
@@ -408,12 +410,15 @@ __device__ __forceinline__ float tile_box_d2(const float4 b, const QBox &q) {
     return fmaf(dy, dy, dx * dx);
 }
 
-// Budget bin of a tile whose bound is 2^(lgn_t) * K*max(d2), relative to the
-// row block's budget 2^lg_tau: bin 0 = below 2^-kBudgetFloor of it, bin
-// kBudgetBins-1 = over the whole budget on its own (never dropped).  w = the
-// bound in fixed point (2^32 = the budget), rounded up.
-__device__ __forceinline__ int budget_bin(float d2, float lgn_t, float cexp, float lg_tau, unsigned long long &w) {
-    const float rel = fmaf(cexp, d2 * 1.001f, lgn_t) - lg_tau + 0.01f;
+// Budget bin of a tile whose bound on |dV|_2 is
+//     min(2^lgn.x K*max(d2), 2^lgn.y |k|_2 bound (2^kn)),
+// relative to the row block's budget 2^lg_tau: bin 0 = below 2^-kBudgetFloor
+// of it, bin kBudgetBins-1 = over the whole budget on its own (never
+// dropped).  w = the bound in fixed point (2^32 = the budget), rounded up.
+__device__ __forceinline__ int budget_bin(float d2, float kn, float2 lgn_t, float cexp, float lg_tau,
+                                          unsigned long long &w) {
+    const float b = fminf(fmaf(cexp, d2 * 0.999f, lgn_t.x), lgn_t.y + kn);
+    const float rel = b - lg_tau + 0.01f;
     const float f = (rel + (float)kBudgetFloor) * (float)kBinsPerBit + 1.0f;
     const int bi = f < 0.0f ? 0 : (f >= (float)(kBudgetBins - 1) ? kBudgetBins - 1 : (int)f);
     w = bi < kBudgetBins - 1 ? (unsigned long long)ceilf(exp2f(rel + 32.0f) * 1.0001f) + 1ull : 0ull;
@@ -424,13 +429,16 @@ __device__ __forceinline__ int budget_bin(float d2, float lgn_t, float cexp, flo
 // distance of every k-tile, and the per-item selection rule.
 struct PlanRule {
     const float4 *kbox;
-    const float *lgn;   // per packed tile log2 gain bound (null: distance test)
+    const float2 *lgn;  // per packed tile log2 gain bounds (null: distance test)
     float cexp, skip_d2, skip_d2_mean, lg_tau;
     int nI;
     QBox box;
     const float *d2s;   // LDS cache of tile distances (t < kPlanD2)
+    const float *kns;   // LDS cache of the tiles' log2 |k|_2 bounds (t < kPlanD2)
 
     __device__ __forceinline__ float d2(int t) const { return t < kPlanD2 ? d2s[t] : tile_box_d2(kbox[t], box); }
+    // beyond the cache: |k|_2 <= 8 K*max
+    __device__ __forceinline__ float kn(int t) const { return t < kPlanD2 ? kns[t] : 3.0f + cexp * d2(t) * 0.999f; }
 
     // Greedy budget threshold of row block I (wave-wide; bins is wave-private
     // LDS): the largest prefix of bins, smallest bounds first, whose summed
@@ -438,13 +446,13 @@ struct PlanRule {
     // Returns the last dropped bin (-1: none).
     __device__ int threshold(int I, unsigned long long *bins, int lane) const {
         if (!lgn) return -1;
-        const float *lgn_I = lgn + tile_start(I);
+        const float2 *lgn_I = lgn + tile_start(I);
         const int T = kTilesPerRowBlockStep * (I + 1);
         for (int i = lane; i < kBudgetBins; i += 64) bins[i] = 0ull;
         __builtin_amdgcn_wave_barrier();
         for (int t = lane; t < T; t += 64) {
             unsigned long long w;
-            const int bi = budget_bin(d2(t), lgn_I[t], cexp, lg_tau, w);
+            const int bi = budget_bin(d2(t), kn(t), lgn_I[t], cexp, lg_tau, w);
             if (bi < kBudgetBins - 1) atomicAdd(bins + bi, w);
         }
         __builtin_amdgcn_wave_barrier();
@@ -480,7 +488,7 @@ struct PlanRule {
         bool k;
         if (lgn) {
             unsigned long long w;
-            k = budget_bin(dd, lgn[tile_start(I) + t], cexp, lg_tau, w) > drop_max;
+            k = budget_bin(dd, kn(t), lgn[tile_start(I) + t], cexp, lg_tau, w) > drop_max;
         } else {
             k = skip_d2 <= 0.0f || dd <= skip_d2;  // skip_d2 <= 0: dense
         }
@@ -491,8 +499,25 @@ struct PlanRule {
 
 // Query box of block qb (threads 0..127 hold its queries, 128..255 repeat
 // them) and the distance cache.
+// Bound on log2 |k_t(q)|_2 for every query q of the box: the tile's points p
+// (kcoord; padding points count too, which only raises the bound) give
+// K*(p, q) <= 2^(cexp dist(p, box)^2), so |k|_2^2 <= sum_p 2^(2 cexp dist^2)
+// (summed scaled by 2^120 against underflow; 0.999 / 1.002 margins over the
+// kernel's f32 rounding); if even that underflows, the box bound 8 K*max.
+__device__ __forceinline__ float tile_knorm(const float *__restrict__ kc, const QBox &b, float cexp, float d2box) {
+    float sum = 0.0f;
+    for (int i = 0; i < kBK; ++i) {
+        const float px = kc[i], py = kc[kBK + i];
+        const float dx = fmaxf(0.0f, fmaxf(b.x0 - px, px - b.x1));
+        const float dy = fmaxf(0.0f, fmaxf(b.y0 - py, py - b.y1));
+        sum += __builtin_amdgcn_exp2f(fmaf(2.0f * cexp, fmaf(dy, dy, dx * dx) * 0.999f, 120.0f));
+    }
+    return sum > 0.0f ? 0.5f * (__log2f(sum * 1.002f) - 120.0f) + 0.001f : 3.0f + cexp * d2box * 0.999f;
+}
+
 __device__ QBox plan_setup(const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t qb,
-                           const float4 *__restrict__ kbox, int nkt, float *d2s, float *red) {
+                           const float4 *__restrict__ kbox, const float *__restrict__ kcoord, float cexp, int nkt,
+                           float *d2s, float *kns, float *red) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t q = qb * kBN + (tid & (kBN - 1));
     const int64_t qc = q < m ? q : m - 1;
@@ -509,7 +534,13 @@ __device__ QBox plan_setup(const float *__restrict__ qx, const float *__restrict
         b.x0 = fminf(b.x0, red[w * 4 + 0]); b.x1 = fmaxf(b.x1, red[w * 4 + 1]);
         b.y0 = fminf(b.y0, red[w * 4 + 2]); b.y1 = fmaxf(b.y1, red[w * 4 + 3]);
     }
-    for (int t = tid; t < nkt && t < kPlanD2; t += kPlanThreads) d2s[t] = tile_box_d2(kbox[t], b);
+    for (int t = tid; t < nkt && t < kPlanD2; t += kPlanThreads) {
+        const float d = tile_box_d2(kbox[t], b);
+        d2s[t] = d;
+        // only tiles whose box bound can reach the budget floors need the point sum
+        kns[t] = (kcoord && cexp * d > -400.0f) ? tile_knorm(kcoord + (int64_t)t * (3 * kBK), b, cexp, d)
+                                                : 3.0f + cexp * d * 0.999f;
+    }
     __syncthreads();
     return b;
 }
@@ -524,18 +555,19 @@ __device__ __forceinline__ int64_t plan_item(int I, int nI, int64_t nQ, int64_t 
 // (count, non-empty) for the scan; empty items get their (exactly zero)
 // outputs here, so the sweep never visits them.
 __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
-    const float4 *__restrict__ kbox, const float *__restrict__ lgn, int nI, int64_t nQ,
+    const float4 *__restrict__ kbox, const float *__restrict__ kcoord, const float2 *__restrict__ lgn, int nI,
+    int64_t nQ,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, float m0, int64_t ldp, float *__restrict__ part, float *__restrict__ mean,
     unsigned long long *__restrict__ key, unsigned char *__restrict__ thr) {
-    __shared__ float d2s[kPlanD2];
+    __shared__ float d2s[kPlanD2], kns[kPlanD2];
     __shared__ float red[4 * kPlanWaves];
     __shared__ unsigned long long bins[kPlanWaves][kBudgetBins];
     const int64_t qb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nkt = kTilesPerRowBlockStep * nI;
-    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s};
-    R.box = plan_setup(qx, qy, m, qb, kbox, nkt, d2s, red);
+    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns};
+    R.box = plan_setup(qx, qy, m, qb, kbox, lgn ? kcoord : nullptr, cexp, nkt, d2s, kns, red);
     for (int I = wave; I < nI; I += kPlanWaves) {
         const int T = kTilesPerRowBlockStep * (I + 1);
         const int drop_max = R.threshold(I, bins[wave], lane);
@@ -564,18 +596,19 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
 // non-empty item, ascending, at its offset, and its descriptor
 // (I, qb, offset low 32 bits, count | offset high bits << 16).
 __global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
-    const float4 *__restrict__ kbox, const float *__restrict__ lgn, int nI, int64_t nQ,
+    const float4 *__restrict__ kbox, const float *__restrict__ kcoord, const float2 *__restrict__ lgn, int nI,
+    int64_t nQ,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, const unsigned long long *__restrict__ key,
     const unsigned long long *__restrict__ scan, const unsigned char *__restrict__ thr, int4 *__restrict__ desc,
     unsigned short *__restrict__ tl) {
-    __shared__ float d2s[kPlanD2];
+    __shared__ float d2s[kPlanD2], kns[kPlanD2];
     __shared__ float red[4 * kPlanWaves];
     const int64_t qb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nkt = kTilesPerRowBlockStep * nI;
-    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s};
-    R.box = plan_setup(qx, qy, m, qb, kbox, nkt, d2s, red);
+    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns};
+    R.box = plan_setup(qx, qy, m, qb, kbox, lgn ? kcoord : nullptr, cexp, nkt, d2s, kns, red);
     for (int I = wave; I < nI; I += kPlanWaves) {
         const int64_t item = plan_item(I, nI, nQ, qb);
         const unsigned long long k = key[item];
@@ -1141,7 +1174,7 @@ hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t 
     return hipGetLastError();
 }
 
-hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float *lgn) {
+hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float2 *lgn) {
     const int64_t nI = npad / kBM;
     const int64_t t0 = tile_start(I0), t1 = tile_start(nI);
     if (t1 <= t0) return hipSuccess;
@@ -1251,15 +1284,17 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     const float cexp = (float)ce;
     const float skip_d2 = cutoff_d2(skip.L, ce);
     const float skip_d2_mean = skip.L > 0 && skip.L_mean > skip.L ? cutoff_d2(skip.L_mean, ce) : skip_d2;
-    const float *lgn = skip.L > 0 ? skip.lgn : nullptr;
-    hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, lgn, nI, nQ, qx, qy,
+    const float2 *lgn = skip.L > 0 ? skip.lgn : nullptr;
+    hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn, nI,
+                       nQ, qx, qy,
                        m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t tb = L.temp_bytes;
     e = rocprim::inclusive_scan(w + L.temp, tb, key, scan, (size_t)items, rocprim::plus<unsigned long long>(), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, lgn, nI, nQ, qx, qy,
+    hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn, nI,
+                       nQ, qx, qy,
                        m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, key, scan, thr, desc, tl);
     if (!L.xcd) {
         hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done);
