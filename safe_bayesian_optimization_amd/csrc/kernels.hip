@@ -161,39 +161,93 @@ __global__ __launch_bounds__(kBM) void row_l1_kernel(const float *__restrict__ a
 
 // Per packed tile, two gain bounds for |A_It k|_2 (log2, rounded up):
 // .x = log2(16 max_r |A_r|_1)  (|A k|_2 <= sqrt(256) |A k|_inf <= 16 max_r |A_r|_1 max|k|)
-// .y = log2(|A_It|_F)           (|A k|_2 <= |A|_F |k|_2)
+// .y = log2 of a bound on the spectral norm ||A_It||_2  (|A k|_2 <= ||A||_2 |k|_2):
+//      with the 64x64 Gram matrix G = A^T A (PSD, f64), ||A||_2^2 = lambda_max(G)
+//      <= ||G^8||_inf^(1/8) (any induced norm bounds the spectral radius),
+//      also <= |A|_F^2 = trace G; the smaller of the two.
 // the plan pairs .x with the largest K* of the tile and .y with a bound on
-// |k|_2 from the tile's points.  One workgroup per tile, thread r = row r,
-// f64 sums.
+// |k|_2 from the tile's points.  One workgroup per tile, f64 arithmetic.
 __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
                                                         float2 *__restrict__ lgn) {
+    __shared__ float at[kBM * kBK];            // the tile, [row][k]  (64 KiB)
+    __shared__ double gm[kBK * kBK];           // G, then its powers (32 KiB)
+    __shared__ double hm[kBK * kBK];           // squaring scratch  (32 KiB)
     __shared__ double red[2][kBM / 64];
     const int64_t tile = t0 + blockIdx.x;
     const float *t = aug + tile * kTileFloats;
-    const int r = threadIdx.x;
-    double s = 0.0, q = 0.0;
+    const int tid = threadIdx.x;
+    double s = 0.0;
     for (int k = 0; k < kBK; ++k) {
-        const double a = (double)t[tile_offset(k, r)];
-        s += fabs(a);
-        q = fma(a, a, q);
+        const float a = t[tile_offset(k, tid)];
+        at[tid * kBK + k] = a;
+        s += fabs((double)a);
     }
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        s = fmax(s, __shfl_xor(s, o));
-        q += __shfl_xor(q, o);
-    }
-    if ((r & 63) == 0) {
-        red[0][r >> 6] = s;
-        red[1][r >> 6] = q;
+    for (int o = 32; o >= 1; o >>= 1) s = fmax(s, __shfl_xor(s, o));
+    if ((tid & 63) == 0) red[0][tid >> 6] = s;
+    __syncthreads();
+    // G[i][j], thread: i = tid / 4, j = 16 (tid % 4) + 0..15
+    const int gi = tid >> 2, gj = (tid & 3) * 16;
+    {
+        double acc[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) acc[c] = 0.0;
+        for (int r = 0; r < kBM; ++r) {
+            const double ai = (double)at[r * kBK + gi];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) acc[c] = fma(ai, (double)at[r * kBK + gj + c], acc[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 16; ++c) gm[gi * kBK + gj + c] = acc[c];
     }
     __syncthreads();
-    if (r == 0) {
-        for (int w = 1; w < kBM / 64; ++w) {
-            s = fmax(s, red[0][w]);
-            q += red[1][w];
+    const double fro2 = [&] {  // trace G = |A|_F^2 (every thread reads it)
+        double tr = 0.0;
+        for (int i = 0; i < kBK; ++i) tr += gm[i * kBK + i];
+        return tr;
+    }();
+    // three squarings, G <- (G/c)^2 with c = the largest entry (exact power-of-two
+    // rescale), tracking log2 of the scale: G^8 = 2^e8 * gm
+    double e8 = 0.0;
+    for (int it = 0; it < 3; ++it) {
+        double mx = 0.0;
+        for (int i = tid; i < kBK * kBK; i += kBM) mx = fmax(mx, fabs(gm[i]));
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+        if ((tid & 63) == 0) red[1][tid >> 6] = mx;
+        __syncthreads();
+        mx = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+        __syncthreads();
+        if (!(mx > 0.0)) break;
+        const int ex = ilogb(mx);
+        double acc[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) acc[c] = 0.0;
+        for (int k = 0; k < kBK; ++k) {
+            const double g1 = ldexp(gm[gi * kBK + k], -ex);
+#pragma unroll
+            for (int c = 0; c < 16; ++c) acc[c] = fma(g1, ldexp(gm[k * kBK + gj + c], -ex), acc[c]);
         }
+#pragma unroll
+        for (int c = 0; c < 16; ++c) hm[gi * kBK + gj + c] = acc[c];
+        e8 = 2.0 * (e8 + (double)ex);  // (2^e G')^2 = 2^(2e) G'^2
+        __syncthreads();
+        for (int i = tid; i < kBK * kBK; i += kBM) gm[i] = hm[i];
+        __syncthreads();
+    }
+    // ||G^8||_inf: largest absolute row sum
+    double rs = 0.0;
+    if (tid < kBK)
+        for (int j = 0; j < kBK; ++j) rs += fabs(gm[tid * kBK + j]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) rs = fmax(rs, __shfl_xor(rs, o));
+    if (tid == 0) {
+        s = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+        // log2 ||A||_2 <= (log2 ||G^8||_inf) / 16, with a margin for the f64 rounding
+        const double lg_spec = rs > 0.0 ? (log2(rs) + e8) / 16.0 + 1e-4 : -1000.0;
+        const double lg_fro = fro2 > 0.0 ? 0.5 * log2(fro2) : -1000.0;
         lgn[tile] = make_float2(s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f,
-                                q > 0.0 ? (float)(0.5 * log2(q)) + 1e-5f : -1000.0f);
+                                (float)fmin(lg_spec, lg_fro) + 1e-5f);
     }
 }
 
