@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA peak (spec, 2.4 GHz)
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (spec; not the 2:1-sparsity figure)
-SPLIT_VARIANTS = (2, 3)         # split-operand (bf16 x3) sweeps: six bf16 MFMA products per f32 product
+SPLIT_VARIANTS = (2, 3, 22, 23)  # split-operand (bf16 x3) sweeps: up to six bf16 MFMA products per f32 product
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = "GP posterior+acq grid-points/sec at N train pts; 1/2/4/8 GPU"
 DATA = "synthetic (SplitMix64 smooth field + N(0,sn2) noise in BASELINE config shapes; terrain.csv is a missing blob)"
@@ -73,10 +73,12 @@ class Prof:
     def read(self):
         pm, pl, fm, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_int64()
         self.lib.sbo_profile_read(self.h, ctypes.byref(pm), ctypes.byref(pl), ctypes.byref(fm), ctypes.byref(fl))
-        w = ctypes.c_double()
+        w, mf = ctypes.c_double(), ctypes.c_double()
+        lv = (ctypes.c_int64 * 3)()
         self.lib.sbo_profile_work(self.h, ctypes.byref(w))
+        self.lib.sbo_profile_mfma(self.h, ctypes.byref(mf), lv)
         return dict(predict_ms=pm.value, predict_launches=pl.value, fill_ms=fm.value, fill_launches=fl.value,
-                    predict_flops=w.value)
+                    predict_flops=w.value, mfma_flops=mf.value, tiles_by_level=list(lv))
 
 
 def main():
@@ -242,6 +244,8 @@ def run_sweep(a, dev, world, rank):
     prof.reset(False)
     pred_ms = pr["predict_ms"] / max(pr["predict_launches"], 1)
     exec_flops_launch = pr["predict_flops"] / max(pr["predict_launches"], 1)
+    mfma_flops_launch = pr["mfma_flops"] / max(pr["predict_launches"], 1)
+    levels_launch = [x / max(pr["predict_launches"], 1) for x in pr["tiles_by_level"]]
     elapsed, pred_ms_max = _max_over_ranks([elapsed, pred_ms], dev, world, a.backend)
     if rank != 0:
         return None
@@ -284,7 +288,8 @@ def run_sweep(a, dev, world, rank):
                    "kstar_cutoff_log2": cutoff, "parallelism": f"m-shard{world}" if world > 1 else "single",
                    "sharding": (a.sharding if world > 1 and a.scaling == "strong" else None),
                    "outputs_written": not a.no_outputs},
-        "roofline": dict(predict_roofline(a.variant, exec_flops_launch, pred_ms), traffic=traffic,
+        "roofline": dict(predict_roofline(a.variant, exec_flops_launch, pred_ms, mfma_flops_launch, levels_launch),
+                         traffic=traffic,
                          traffic_source=traffic_src, avg_launch_ms=pred_ms, max_rank_launch_ms=pred_ms_max,
                          dense_flops_per_launch=dense_flops_launch,
                          dense_equivalent_tflops=dense_flops_launch / (pred_ms * 1e-3) / 1e12),
@@ -302,22 +307,22 @@ def dtype_of(variant):
     return "f32 (bf16x3-split MFMA, f32 accumulation)" if variant in SPLIT_VARIANTS else "f32"
 
 
-def predict_roofline(variant, flops_f32, ms):
+def predict_roofline(variant, flops_f32, ms, mfma_flops, levels):
     """Roofline of the predictive kernel.  flops_f32 = the algorithmic work of
-    one launch, 2*BM*BN*BK per multiplied k-tile (device counter).  The
-    split-operand sweep issues six bf16 MFMA products per f32 product, so its
-    matrix-pipe work is 6 x flops_f32 against the dense bf16 peak; the f32
-    MFMA sweep's is flops_f32 against the dense f32 peak."""
+    one launch, 2*BM*BN*BK per multiplied k-tile (device counter); mfma_flops
+    = the matrix-core work it issued (device counter: 2*BM*BN*BK per bf16
+    MFMA product -- six per tile at full precision, three / one at the plan's
+    reduced precision levels; one per tile for the f32 sweep), priced against
+    the dense bf16 (split sweeps) or f32 peak."""
     f32_tf = flops_f32 / (ms * 1e-3) / 1e12
+    ach = mfma_flops / (ms * 1e-3) / 1e12
     if variant in SPLIT_VARIANTS:
-        mf = 6.0 * flops_f32
-        ach = mf / (ms * 1e-3) / 1e12
-        return {"kernel": "predict_x3_kernel (V = sf2 L^-1 K*^T: bf16x3-split operands, six "
+        return {"kernel": "predict_x3_kernel (V = sf2 L^-1 K*^T: bf16x3-split operands, up to six "
                           "v_mfma_f32_16x16x32_bf16 per f32 product, f32 accumulation)",
                 "bound": "mfma", "achieved": ach, "peak": PEAK_BF16_MFMA_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / PEAK_BF16_MFMA_TFLOPS, "mfma_flops_per_launch": mf,
-                "algorithmic_flops_per_launch": flops_f32, "f32_equivalent_tflops": f32_tf,
-                "f32_equivalent_over_f32_peak": f32_tf / PEAK_F32_MFMA_TFLOPS}
+                "frac": ach / PEAK_BF16_MFMA_TFLOPS, "mfma_flops_per_launch": mfma_flops,
+                "algorithmic_flops_per_launch": flops_f32, "tiles_by_level_per_launch": levels,
+                "f32_equivalent_tflops": f32_tf, "f32_equivalent_over_f32_peak": f32_tf / PEAK_F32_MFMA_TFLOPS}
     return {"kernel": "predict_kernel (V = sf2 L^-1 K*^T, f32 MFMA 16x16x4)", "bound": "mfma", "achieved": f32_tf,
             "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": f32_tf / PEAK_F32_MFMA_TFLOPS,
             "algorithmic_flops_per_launch": flops_f32}
@@ -383,6 +388,8 @@ def run_streaming(a, dev, world, rank):
     steps = reps * iters
     pred_ms = pr["predict_ms"] / max(pr["predict_launches"], 1)
     flops = pr["predict_flops"] / max(pr["predict_launches"], 1)
+    mflops = pr["mfma_flops"] / max(pr["predict_launches"], 1)
+    levels = [x / max(pr["predict_launches"], 1) for x in pr["tiles_by_level"]]
     (s, i), = key_tensor_to_pairs(last)
     return {
         "metric": METRIC, "value": m * steps / elapsed, "unit": "grid-points/s", "n_gpus": 1, "steps": steps,
@@ -390,7 +397,8 @@ def run_streaming(a, dev, world, rank):
         "vs_baseline": None, "dtype": dtype_of(a.variant), "data": DATA,
         "config": {"workload": "C5", "n_train": [n0, n_end], "iterations": iters, "grid": [g, g], "M": m,
                    "parallelism": "single", "step": "sbo_append (block Cholesky) + sbo_tick (includes one fit per loop)"},
-        "roofline": dict(predict_roofline(a.variant, flops, pred_ms), traffic=None, avg_launch_ms=pred_ms),
+        "roofline": dict(predict_roofline(a.variant, flops, pred_ms, mflops, levels), traffic=None,
+                         avg_launch_ms=pred_ms),
         "append_ms_avg": t_app * 1e3 / steps, "tick_ms_avg": t_tick * 1e3 / steps,
         "argmax": {"index": i, "score": s}, "cpu_baseline": None,
     }

@@ -233,15 +233,19 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * outputs and argmax indices stay in the caller's order. */
 #define SBO_OPT_QUERY_ORDER 4
 /* SBO_OPT_KERNEL_VARIANT, the predictive sweep: 3 (default) = split
- * operands on bf16 MFMA -- sf2 L^-1 and K* as three bf16 pieces each, six
- * v_mfma_f32_16x16x32_bf16 products per f32 product, f32 accumulation,
- * eight waves per CU (f32-accurate: variance error vs a host f64 sweep
- * 5.07e-6 at N = 16384 against 5.00e-6 for variant 0; 1.7x faster);
- * 2 = the same with four waves of 32 queries; 0 = f32 MFMA (16x16x4) with
- * an f32 cross-tile accumulator; 1 = variant 0 with an f64 one; 9, 10 =
- * variant 3 with the A stage issued in one burst per step, resp. A
- * fragments read one row block ahead.  4-8: timing diagnostics with parts
- * of the work left out (wrong results). */
+ * operands on bf16 MFMA -- sf2 L^-1 and K* as three bf16 pieces each, up to
+ * six v_mfma_f32_16x16x32_bf16 products per f32 product, f32 accumulation,
+ * eight waves per CU; with the automatic cutoff the tile plan runs tiles
+ * whose share of the variance is small at three or one product(s), charged
+ * to the same error budget as the skipped tiles (SBO_OPT_SKIP_BUDGET);
+ * 22 = variant 3 with every kept tile at six products (f32-accurate:
+ * variance error vs a host f64 sweep 5.07e-6 at N = 16384 against 5.00e-6
+ * for variant 0); 2 = variant 22 with four waves of 32 queries; 0 = f32
+ * MFMA (16x16x4) with an f32 cross-tile accumulator; 1 = variant 0 with an
+ * f64 one; 9, 10 = variant 22 with the A stage issued in one burst per
+ * step, resp. A fragments read one row block ahead; 13 = the 32x32x16
+ * shape.  4-8, 11, 12, 14-21: timing diagnostics (some with parts of the
+ * work left out: wrong results). */
 #define SBO_OPT_KERNEL_VARIANT 5
 /* SBO_OPT_SWEEP_GROUPS: workgroups of the persistent predictive sweep, each
  * walking one tile-balanced range of the tick's plan; 0 = default (one per
@@ -277,6 +281,13 @@ SBO_API sbo_status sbo_profile_read(sbo_ctx *ctx, double *predict_ms, int64_t *p
 /* MFMA flops the predictive sweep actually executed since sbo_profile(ctx, 1)
  * (2*BM*BN*BK per multiplied tile; skipped exactly-zero tiles excluded). */
 SBO_API sbo_status sbo_profile_work(sbo_ctx *ctx, double *predict_flops);
+/* Matrix-core flops the predictive sweep issued since sbo_profile(ctx, 1):
+ * 2*BM*BN*BK per MFMA product per multiplied tile -- six products per tile
+ * for the split sweeps at full precision, three / one at the reduced
+ * precision levels (variant 3), one for the f32 sweeps (variants 0, 1);
+ * tiles_by_level (may be NULL): the multiplied tiles at six, three, one
+ * product(s). */
+SBO_API sbo_status sbo_profile_mfma(sbo_ctx *ctx, double *mfma_flops, int64_t *tiles_by_level /* [3] or NULL */);
 
 #ifdef __cplusplus
 }

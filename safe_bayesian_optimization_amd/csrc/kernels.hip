@@ -159,16 +159,19 @@ __global__ __launch_bounds__(kBM) void row_l1_kernel(const float *__restrict__ a
     atomicAdd(row_l1 + I * kBM + r, s);
 }
 
-// Per packed tile, two gain bounds for |A_It k|_2 (log2, rounded up):
+// Per packed tile, gain bounds (log2, rounded up):
 // .x = log2(16 max_r |A_r|_1)  (|A k|_2 <= sqrt(256) |A k|_inf <= 16 max_r |A_r|_1 max|k|)
 // .y = log2 of a bound on the spectral norm ||A_It||_2  (|A k|_2 <= ||A||_2 |k|_2):
 //      with the 64x64 Gram matrix G = A^T A (PSD, f64), ||A||_2^2 = lambda_max(G)
 //      <= ||G^8||_inf^(1/8) (any induced norm bounds the spectral radius),
-//      also <= |A|_F^2 = trace G; the smaller of the two.
+//      also <= |A|_F^2 = trace G; the smaller of the two;
+// .z = log2(|A_It|_F), which also bounds || |A_It| ||_2 (the entrywise
+//      absolute values: the bound on the split products a tile's lower
+//      precision levels leave out).
 // the plan pairs .x with the largest K* of the tile and .y with a bound on
 // |k|_2 from the tile's points.  One workgroup per tile, f64 arithmetic.
 __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
-                                                        float2 *__restrict__ lgn) {
+                                                        float4 *__restrict__ lgn) {
     __shared__ float at[kBM * kBK];            // the tile, [row][k]  (64 KiB)
     __shared__ double gm[kBK * kBK];           // G, then its powers (32 KiB)
     __shared__ double hm[kBK * kBK];           // squaring scratch  (32 KiB)
@@ -246,8 +249,8 @@ __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict_
         // log2 ||A||_2 <= (log2 ||G^8||_inf) / 16, with a margin for the f64 rounding
         const double lg_spec = rs > 0.0 ? (log2(rs) + e8) / 16.0 + 1e-4 : -1000.0;
         const double lg_fro = fro2 > 0.0 ? 0.5 * log2(fro2) : -1000.0;
-        lgn[tile] = make_float2(s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f,
-                                (float)fmin(lg_spec, lg_fro) + 1e-5f);
+        lgn[tile] = make_float4(s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f,
+                                (float)fmin(lg_spec, lg_fro) + 1e-5f, (float)lg_fro + 1e-5f, 0.0f);
     }
 }
 
@@ -464,50 +467,97 @@ __device__ __forceinline__ float tile_box_d2(const float4 b, const QBox &q) {
     return fmaf(dy, dy, dx * dx);
 }
 
-// Budget bin of a tile whose bound on |dV|_2 is
-//     min(2^lgn.x K*max(d2), 2^lgn.y |k|_2 bound (2^kn)),
-// relative to the row block's budget 2^lg_tau: bin 0 = below 2^-kBudgetFloor
-// of it, bin kBudgetBins-1 = over the whole budget on its own (never
-// dropped).  w = the bound in fixed point (2^32 = the budget), rounded up.
-__device__ __forceinline__ int budget_bin(float d2, float kn, float2 lgn_t, float cexp, float lg_tau,
-                                          unsigned long long &w) {
-    const float b = fminf(fmaf(cexp, d2 * 0.999f, lgn_t.x), lgn_t.y + kn);
-    const float rel = b - lg_tau + 0.01f;
-    const float f = (rel + (float)kBudgetFloor) * (float)kBinsPerBit + 1.0f;
+// A kept tile runs at one of three precision levels: all six split
+// products (code 0), the three largest a1 k0 + a0 k1 + a0 k0 (code 1: the
+// dropped terms are below 3.1 2^-16 |a| |k| per product), or a0 k0 alone
+// (code 2: below 2.03 2^-8 + 3.1 2^-16).  Lowering a tile's level, or
+// dropping it, costs part of the row block's error budget: with
+// b_abs = min(2^x K*max, 2^z |k|_2) bounding | |A_It| |k_t| |_2 and
+// b = min(2^x K*max, 2^y |k|_2) bounding |A_It k_t|_2, the three increments
+//     code 0 -> 1:  c3 = 3.1 2^-16 b_abs
+//     code 1 -> 2:  c1 - c3,  c1 = (2.03 2^-8 + 3.1 2^-16) b_abs
+//     code 2 -> drop: b - c1
+// sum to the tile's drop bound and are spent greedily over all tiles of the
+// row block, cheapest first by error per sweep time saved (the increments
+// are ranked by log2(error) + kLvlKey[j], kLvlKey from the measured per-tile
+// time of the three levels and of the drop; a tile's keys never go down, so
+// its spent increments are a prefix).
+// For each increment: its bin relative to the budget 2^lg_tau (bin 0 = below
+// 2^-kBudgetFloor of it, bin kBudgetBins-1 = over the whole budget, never
+// spent) and its weight in fixed point (2^32 = the budget), rounded up.
+constexpr float kLg3 = -14.36f;  // log2(3.1 2^-16), rounded up
+constexpr float kLg1 = -6.96f;   // log2(2.03 2^-8 + 3.1 2^-16), rounded up
+
+// log2(drop saving / level saving): per-tile sweep time at C4 of six, three,
+// one product(s): 18.6, 12.9, 9.9 ns (variants 22, 20, 21)
+constexpr float kLvlKey0 = 0.80f;  // six -> three products saves 5.7 ns
+constexpr float kLvlKey1 = 1.72f;  // three -> one saves 3.0 ns (the drop: 9.9 ns)
+
+__device__ __forceinline__ int inc_bin(float l, unsigned long long &w, float key = 0.0f) {  // l = log2(inc / budget)
+    const float f = (l + key + (float)kBudgetFloor) * (float)kBinsPerBit + 1.0f;
     const int bi = f < 0.0f ? 0 : (f >= (float)(kBudgetBins - 1) ? kBudgetBins - 1 : (int)f);
-    w = bi < kBudgetBins - 1 ? (unsigned long long)ceilf(exp2f(rel + 32.0f) * 1.0001f) + 1ull : 0ull;
+    w = bi < kBudgetBins - 1 ? (unsigned long long)ceilf(exp2f(l + 32.0f) * 1.0001f) + 1ull : 0ull;
     return bi;
+}
+
+__device__ __forceinline__ void tile_increments(float d2, float kn, float4 lgn_t, float cexp, float lg_tau,
+                                                int (&bi)[3], unsigned long long (&w)[3]) {
+    const float kmax = cexp * d2 * 0.999f;
+    const float b = fminf(lgn_t.x + kmax, lgn_t.y + kn) - lg_tau + 0.01f;
+    const float babs = fminf(lgn_t.x + kmax, lgn_t.z + kn) - lg_tau + 0.01f;
+    const float r3 = babs + kLg3, r1 = babs + kLg1;
+    bi[0] = inc_bin(r3, w[0], kLvlKey0);
+    bi[1] = inc_bin(r1 + __log2f(1.0f - exp2f(r3 - r1)), w[1], kLvlKey1);
+    const float dl = r1 - b;  // <= -3.96: |A|_F <= 8 ||A||_2
+    bi[2] = dl < -0.01f ? inc_bin(b + __log2f(1.0f - exp2f(dl)), w[2]) : inc_bin(b, w[2]);
+    // monotone: the three bins never go down (so a tile's spent increments are a prefix)
+    bi[1] = max(bi[1], bi[0]);
+    bi[2] = max(bi[2], bi[1]);
 }
 
 // Everything the two plan kernels share: the query block's box, the box
 // distance of every k-tile, and the per-item selection rule.
 struct PlanRule {
     const float4 *kbox;
-    const float2 *lgn;  // per packed tile log2 gain bounds (null: distance test)
+    const float4 *lgn;  // per packed tile log2 gain bounds (null: distance test)
     float cexp, skip_d2, skip_d2_mean, lg_tau;
     int nI;
     QBox box;
     const float *d2s;   // LDS cache of tile distances (t < kPlanD2)
     const float *kns;   // LDS cache of the tiles' log2 |k|_2 bounds (t < kPlanD2)
+    int levels;         // precision levels allowed (0: every kept tile at full precision)
 
     __device__ __forceinline__ float d2(int t) const { return t < kPlanD2 ? d2s[t] : tile_box_d2(kbox[t], box); }
     // beyond the cache: |k|_2 <= 8 K*max
     __device__ __forceinline__ float kn(int t) const { return t < kPlanD2 ? kns[t] : 3.0f + cexp * d2(t) * 0.999f; }
 
+    __device__ __forceinline__ void incs(int I, int t, int (&bi)[3], unsigned long long (&w)[3]) const {
+        tile_increments(d2(t), kn(t), lgn[tile_start(I) + t], cexp, lg_tau, bi, w);
+        if (!levels) {  // only the whole drop: the first two increments free, the third the whole drop bound
+            bi[0] = bi[1] = 0;
+            w[0] = w[1] = 0ull;
+            const float kmax = cexp * d2(t) * 0.999f;
+            const float4 l = lgn[tile_start(I) + t];
+            bi[2] = inc_bin(fminf(l.x + kmax, l.y + kn(t)) - lg_tau + 0.01f, w[2]);
+        }
+    }
+
     // Greedy budget threshold of row block I (wave-wide; bins is wave-private
-    // LDS): the largest prefix of bins, smallest bounds first, whose summed
-    // bounds (integer adds: order-independent) stay within the budget.
-    // Returns the last dropped bin (-1: none).
+    // LDS): the largest prefix of bins, smallest increments first, whose
+    // summed weights (integer adds: order-independent) stay within the
+    // budget.  Returns the last spent bin (-1: none).
     __device__ int threshold(int I, unsigned long long *bins, int lane) const {
         if (!lgn) return -1;
-        const float2 *lgn_I = lgn + tile_start(I);
         const int T = kTilesPerRowBlockStep * (I + 1);
         for (int i = lane; i < kBudgetBins; i += 64) bins[i] = 0ull;
         __builtin_amdgcn_wave_barrier();
         for (int t = lane; t < T; t += 64) {
-            unsigned long long w;
-            const int bi = budget_bin(d2(t), kn(t), lgn_I[t], cexp, lg_tau, w);
-            if (bi < kBudgetBins - 1) atomicAdd(bins + bi, w);
+            int bi[3];
+            unsigned long long w[3];
+            incs(I, t, bi, w);
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                if (bi[j] < kBudgetBins - 1) atomicAdd(bins + bi[j], w[j]);
         }
         __builtin_amdgcn_wave_barrier();
         constexpr int per = (kBudgetBins + 63) / 64;
@@ -537,17 +587,24 @@ struct PlanRule {
         return ok - 1;
     }
 
-    __device__ __forceinline__ bool keep(int I, int t, int drop_max) const {
+    // The tile's level code (0 full, 1 three products, 2 one product) or -1
+    // (dropped) under the row block's threshold.
+    __device__ __forceinline__ int level(int I, int t, int drop_max) const {
         const float dd = d2(t);
-        bool k;
+        int code;
         if (lgn) {
-            unsigned long long w;
-            k = budget_bin(dd, kn(t), lgn[tile_start(I) + t], cexp, lg_tau, w) > drop_max;
+            int bi[3];
+            unsigned long long w[3];
+            incs(I, t, bi, w);
+            const int spent = (bi[0] <= drop_max) + (bi[1] <= drop_max) + (bi[2] <= drop_max);
+            code = spent == 3 ? -1 : (levels ? spent : 0);
         } else {
-            k = skip_d2 <= 0.0f || dd <= skip_d2;  // skip_d2 <= 0: dense
+            code = (skip_d2 <= 0.0f || dd <= skip_d2) ? 0 : -1;  // skip_d2 <= 0: dense
         }
-        if (!k && I == nI - 1) k = dd <= skip_d2_mean;  // the mean's own cutoff
-        return k;
+        // the mean's own cutoff (last row block): keep at the cheapest level
+        // (its V error is below the drop bound already spent)
+        if (code < 0 && I == nI - 1 && dd <= skip_d2_mean) code = lgn && levels ? 2 : 0;
+        return code;
     }
 };
 
@@ -609,7 +666,8 @@ __device__ __forceinline__ int64_t plan_item(int I, int nI, int64_t nQ, int64_t 
 // (count, non-empty) for the scan; empty items get their (exactly zero)
 // outputs here, so the sweep never visits them.
 __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
-    const float4 *__restrict__ kbox, const float *__restrict__ kcoord, const float2 *__restrict__ lgn, int nI,
+    const float4 *__restrict__ kbox, const float *__restrict__ kcoord, const float4 *__restrict__ lgn, int levels,
+    int nI,
     int64_t nQ,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, float m0, int64_t ldp, float *__restrict__ part, float *__restrict__ mean,
@@ -620,7 +678,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     const int64_t qb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nkt = kTilesPerRowBlockStep * nI;
-    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns};
+    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns, levels};
     R.box = plan_setup(qx, qy, m, qb, kbox, lgn ? kcoord : nullptr, cexp, nkt, d2s, kns, red);
     for (int I = wave; I < nI; I += kPlanWaves) {
         const int T = kTilesPerRowBlockStep * (I + 1);
@@ -628,7 +686,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
         int cnt = 0;
         for (int t0 = 0; t0 < T; t0 += 64) {
             const int t = t0 + lane;
-            cnt += __popcll(__ballot(t < T && R.keep(I, t, drop_max)));
+            cnt += __popcll(__ballot(t < T && R.level(I, t, drop_max) >= 0));
         }
         const int64_t item = plan_item(I, nI, nQ, qb);
         if (lane == 0) {
@@ -650,19 +708,22 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
 // non-empty item, ascending, at its offset, and its descriptor
 // (I, qb, offset low 32 bits, count | offset high bits << 16).
 __global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
-    const float4 *__restrict__ kbox, const float *__restrict__ kcoord, const float2 *__restrict__ lgn, int nI,
+    const float4 *__restrict__ kbox, const float *__restrict__ kcoord, const float4 *__restrict__ lgn, int levels,
+    int nI,
     int64_t nQ,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, const unsigned long long *__restrict__ key,
     const unsigned long long *__restrict__ scan, const unsigned char *__restrict__ thr, int4 *__restrict__ desc,
-    unsigned short *__restrict__ tl) {
+    unsigned short *__restrict__ tl, int prod_full, unsigned long long *__restrict__ products) {
+    // products (may be null): [0] += MFMA products, [1], [2] += tiles at level 1, 2
     __shared__ float d2s[kPlanD2], kns[kPlanD2];
     __shared__ float red[4 * kPlanWaves];
     const int64_t qb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nkt = kTilesPerRowBlockStep * nI;
-    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns};
+    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns, levels};
     R.box = plan_setup(qx, qy, m, qb, kbox, lgn ? kcoord : nullptr, cexp, nkt, d2s, kns, red);
+    unsigned long long prod = 0, nl1 = 0, nl2 = 0;
     for (int I = wave; I < nI; I += kPlanWaves) {
         const int64_t item = plan_item(I, nI, nQ, qb);
         const unsigned long long k = key[item];
@@ -676,12 +737,31 @@ __global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
         uint64_t base = off;
         for (int t0 = 0; t0 < T; t0 += 64) {
             const int t = t0 + lane;
-            const bool kp = t < T && R.keep(I, t, drop_max);
+            const int code = t < T ? R.level(I, t, drop_max) : -1;
+            const bool kp = code >= 0;
             const unsigned long long bal = __ballot(kp);
-            if (kp) tl[base + __popcll(bal & ((1ull << lane) - 1ull))] = (unsigned short)t;
+            if (kp) {
+                tl[base + __popcll(bal & ((1ull << lane) - 1ull))] = (unsigned short)(t | (code << kLevelShift));
+                prod += code == 0 ? prod_full : (code == 1 ? 3 : 1);
+                nl1 += code == 1 ? 1 : 0;
+                nl2 += code == 2 ? 1 : 0;
+            }
             base += __popcll(bal);
         }
         if (lane == 0) desc[ne] = make_int4(I, (int)qb, (int)(uint32_t)off, cnt | (int)((off >> 32) << 16));
+    }
+    if (products) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            prod += __shfl_xor(prod, o);
+            nl1 += __shfl_xor(nl1, o);
+            nl2 += __shfl_xor(nl2, o);
+        }
+        if (lane == 0 && prod) {
+            atomicAdd(products, prod);
+            atomicAdd(products + 1, nl1);
+            atomicAdd(products + 2, nl2);
+        }
     }
 }
 
@@ -888,7 +968,9 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
         return (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
     };
     auto list_at = [&](uint64_t e, int I) {
-        const int t = __builtin_amdgcn_readfirstlane((int)lwin[((e / kListWindow) & 1) * kListWindow + e % kListWindow]);
+        // (every level at full f32 precision here: the level code is ignored)
+        const int t = __builtin_amdgcn_readfirstlane((int)lwin[((e / kListWindow) & 1) * kListWindow + e % kListWindow]) &
+                      ((1 << kLevelShift) - 1);
         return min(t, kTilesPerRowBlockStep * (I + 1) - 1);
     };
 
@@ -1228,7 +1310,7 @@ hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t 
     return hipGetLastError();
 }
 
-hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float2 *lgn) {
+hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float4 *lgn) {
     const int64_t nI = npad / kBM;
     const int64_t t0 = tile_start(I0), t1 = tile_start(nI);
     if (t1 <= t0) return hipSuccess;
@@ -1321,9 +1403,9 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     const int64_t nQ = (m + kBN - 1) / kBN;
     const int64_t items = (int64_t)nI * nQ;
     if (m <= 0 || nI <= 0) return hipSuccess;
-    // key fields: items < 2^24, every kept-tile count < 2^40; tile index < 2^16
+    // key fields: items < 2^24, every kept-tile count < 2^40; tile index < 2^14 (level code above)
     if (nQ > 0x7fffffff || items >= (1ll << (64 - kPlanKeyShift)) ||
-        2 * (int64_t)nI * (nI + 1) * nQ >= (1ll << kPlanKeyShift) || kTilesPerRowBlockStep * (int64_t)nI > 65535)
+        2 * (int64_t)nI * (nI + 1) * nQ >= (1ll << kPlanKeyShift) || kTilesPerRowBlockStep * (int64_t)nI > (1 << kLevelShift) - 1)
         return hipErrorInvalidValue;
     const PlanLayout L = plan_layout(nI, nQ, P);
     if (work_bytes < L.total) return hipErrorInvalidValue;
@@ -1338,8 +1420,10 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     const float cexp = (float)ce;
     const float skip_d2 = cutoff_d2(skip.L, ce);
     const float skip_d2_mean = skip.L > 0 && skip.L_mean > skip.L ? cutoff_d2(skip.L_mean, ce) : skip_d2;
-    const float2 *lgn = skip.L > 0 ? skip.lgn : nullptr;
-    hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn, nI,
+    const float4 *lgn = skip.L > 0 ? skip.lgn : nullptr;
+    const int levels = lgn && skip.levels ? 1 : 0;
+    hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn,
+                       levels, nI,
                        nQ, qx, qy,
                        m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr);
     hipError_t e = hipGetLastError();
@@ -1347,9 +1431,10 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     size_t tb = L.temp_bytes;
     e = rocprim::inclusive_scan(w + L.temp, tb, key, scan, (size_t)items, rocprim::plus<unsigned long long>(), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn, nI,
-                       nQ, qx, qy,
-                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, key, scan, thr, desc, tl);
+    hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn,
+                       levels, nI, nQ, qx, qy,
+                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, key, scan, thr, desc, tl, skip.prod_full,
+                       tiles_done ? tiles_done + 1 : nullptr);
     if (!L.xcd) {
         hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done);
         return hipGetLastError();

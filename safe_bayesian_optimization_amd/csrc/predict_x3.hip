@@ -129,7 +129,10 @@ __device__ __forceinline__ float kstar1(float xk, float yk, float xq, float yq, 
 //   FRESH: first half of a tile (the chains start from zero); otherwise the
 //   finished chains of each row block are added into `outer` two blocks
 //   later (off the MFMA's result latency).
-template <int NC, bool FRESH, int DIAG, int PIECES>
+//   LV: the tile's precision level (the plan's code): 0 all six products,
+//   1 the three largest (a1 kh + a0 km + a0 kh), 2 a0 kh alone; the A planes
+//   a level leaves out are not read from LDS.
+template <int NC, bool FRESH, int DIAG, int PIECES, int LV = 0>
 __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn, const float (&xq)[NC],
                                         const float (&yq)[NC], int g, float cexp, float msc, const KPieces<NC> &kb,
                                         f32x4 (&acc)[NC][16], f32x4 (&outer)[NC][16], KPieces<NC> &nx,
@@ -143,23 +146,29 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
     // A fragments: row block rb in use, rb+1 landed or landing, rb+2 issued
     // during rb (DIAG & 32: one block ahead only)
     constexpr int AHEAD = (DIAG & 32) ? 1 : 2;
-    u32x4 a0 = lds_b128(pa), a1 = lds_b128(pa + kXPlane), a2 = lds_b128(pa + 2 * kXPlane);
+    // (DIAG 2048 / 4096: every tile at level 1 / 2, timing diagnostics)
+    constexpr int EL = (DIAG & 4096) ? 2 : ((DIAG & 2048) ? 1 : LV);
+    constexpr bool P1 = EL <= 1, P2 = EL == 0;  // planes a1, a2 in use
+    constexpr int NPROD = EL == 0 ? 6 : (EL == 1 ? 3 : 1);
+    u32x4 a0 = lds_b128(pa), a1 = {}, a2 = {};
+    if (P1) a1 = lds_b128(pa + kXPlane);
+    if (P2) a2 = lds_b128(pa + 2 * kXPlane);
     u32x4 n0 = a0, n1 = a1, n2 = a2;
     if (AHEAD == 2) {
         n0 = lds_b128(pa + 1024);
-        n1 = lds_b128(pa + kXPlane + 1024);
-        n2 = lds_b128(pa + 2 * kXPlane + 1024);
+        if (P1) n1 = lds_b128(pa + kXPlane + 1024);
+        if (P2) n2 = lds_b128(pa + 2 * kXPlane + 1024);
     }
     // coordinates of pair 0; pair i+1's are read while pair i is built
     f32x2v xk = lds_f2(pcn + g * 32), yk = lds_f2(pcn + 128 + g * 32), ak = lds_f2(pcn + 256 + g * 32);
     f32x2v e[NC];
 #pragma unroll
     for (int rb = 0; rb < 16; ++rb) {
-        u32x4 b0, b1, b2;
+        u32x4 b0 = {}, b1 = {}, b2 = {};
         if (rb + AHEAD < 16) {
             b0 = lds_b128(pa + (rb + AHEAD) * 1024);
-            b1 = lds_b128(pa + kXPlane + (rb + AHEAD) * 1024);
-            b2 = lds_b128(pa + 2 * kXPlane + (rb + AHEAD) * 1024);
+            if (P1) b1 = lds_b128(pa + kXPlane + (rb + AHEAD) * 1024);
+            if (P2) b2 = lds_b128(pa + 2 * kXPlane + (rb + AHEAD) * 1024);
         }
         // ---- the next step's K*, pair i over row blocks 4i .. 4i+3:
         // evaluate (two slots), split, mean terms + the next pair's coordinates
@@ -213,11 +222,15 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
         for (int c = 0; c < NC; ++c) {
             // (DIAG & 64: one chain over the whole item, no outer sums -- timing only)
             f32x4 v = (FRESH && !(DIAG & 64)) ? zero : acc[c][rb];
-            v = mfma(a2, kb.h[c], v);
-            v = mfma(a1, kb.m[c], v);
-            v = mfma(a0, kb.l[c], v);
-            v = mfma(a1, kb.h[c], v);
-            v = mfma(a0, kb.m[c], v);
+            if constexpr (P2) {
+                v = mfma(a2, kb.h[c], v);
+                v = mfma(a1, kb.m[c], v);
+                v = mfma(a0, kb.l[c], v);
+            }
+            if constexpr (P1) {
+                v = mfma(a1, kb.h[c], v);
+                v = mfma(a0, kb.m[c], v);
+            }
             v = mfma(a0, kb.h[c], v);
             acc[c][rb] = v;
         }
@@ -226,14 +239,14 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
         // the SIMD's issue for 8 of its 16 cycles)
         if constexpr (DIAG & 128) {  // A/B: more VALU per MFMA gap
 #pragma unroll
-            for (int j = 0; j < 6 * NC; ++j) {
+            for (int j = 0; j < NPROD * NC; ++j) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
                 __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
             }
         } else if constexpr (!(DIAG & 256)) {  // (256: the compiler's own order)
 #pragma unroll
-            for (int j = 0; j < 6 * NC; ++j) {
+            for (int j = 0; j < NPROD * NC; ++j) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
                 __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
@@ -404,6 +417,7 @@ __device__ __forceinline__ void x3w_kstar(const lds_char *pc, float xq, float yq
 // per staged step: row block, query block, and flags
 struct XStep {
     int I, qb, flags;  // bit 0: second half, bit 1: first step of its item, bit 2: last step, bit 3: valid
+    int lv;            // the tile's precision level
 };
 constexpr int kFirst = 2, kLast = 4, kValid = 8;
 
@@ -413,7 +427,8 @@ constexpr int kFirst = 2, kLast = 4, kValid = 8;
 // DIAG (timing diagnostics only, results wrong): 1 no next-step K*, 2 no A
 // pieces staged, 4 no outer sums, 8 every A stage from the first tile (L2-resident);
 // 16 (not a diagnostic): A pieces spread over the row blocks; 32: A fragments
-// read one row block ahead instead of two.
+// read one row block ahead instead of two; 8192 (not a diagnostic): every
+// tile at the precision level its plan entry names (code << kLevelShift).
 template <int NC, int DIAG>
 __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     const char *__restrict__ ax3, const float *__restrict__ kc3, const int4 *__restrict__ desc,
@@ -427,6 +442,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     constexpr int NQ = NC == 2 ? 2 : 1;                // queries per lane
     // A-stage loaders: every wave, or (DIAG & 1024, NC = 1) only waves 4-7
     constexpr bool HALF_LOAD = NC == 1 && (DIAG & 1024);
+    constexpr bool LEVELS = !WIDE && (DIAG & 8192);
     constexpr int kLoaders = (NC == 1 && !HALF_LOAD) ? 8 : 4;
     constexpr int kPieces = (kXA / 1024) / kLoaders;  // A pieces per loader wave per stage (6 or 12)
     static_assert(kPieces == 6 || kPieces == 12, "the end-of-step wait below counts 6 or 12 pieces");
@@ -489,9 +505,8 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
                          __builtin_amdgcn_readfirstlane(d.w));
     };
     auto entry_off = [](const int4 &d) { return (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32); };
-    auto list_at = [&](uint64_t e, int I) {
-        const int t = __builtin_amdgcn_readfirstlane((int)lwin[((e / kListWin) & 1) * kListWin + e % kListWin]);
-        return min(t, kTilesPerRowBlockStep * (I + 1) - 1);
+    auto list_at = [&](uint64_t e) {  // (tile index, level code) of list entry e
+        return __builtin_amdgcn_readfirstlane((int)lwin[((e / kListWin) & 1) * kListWin + e % kListWin]);
     };
 
     // ---- lookahead cursor: the step being staged
@@ -515,7 +530,9 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         s.I = la_d.x;
         s.qb = la_d.y;
         s.flags = la_h | (la_j == 0 && la_h == 0 ? kFirst : 0) | (la_j == cnt - 1 && la_h == 1 ? kLast : 0) | kValid;
-        const int t = list_at(la_e, la_d.x);
+        const int te = list_at(la_e);
+        const int t = min(te & ((1 << kLevelShift) - 1), kTilesPerRowBlockStep * (la_d.x + 1) - 1);
+        s.lv = LEVELS ? min(te >> kLevelShift, 2) : 0;
         SBO_X3_STAGE(tile_start(la_d.x) + t, t, la_h, la_d.y, sl, burst);
         la_h ^= 1;
         if (la_h == 0) {
@@ -534,7 +551,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         return s;
     };
 
-    XStep s0 = stage(0, true), s1 = {0, 0, 0}, s2 = {0, 0, 0};
+    XStep s0 = stage(0, true), s1 = {0, 0, 0, 0}, s2 = {0, 0, 0, 0};
     if (la_k < k1) s1 = stage(1, true);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -596,7 +613,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         if (FRESH) flush();
         const bool issue = la_k < k1;
         const int nslot = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
-        s2 = issue ? stage(nslot, false) : XStep{0, 0, 0};
+        s2 = issue ? stage(nslot, false) : XStep{0, 0, 0, 0};
         if (!issue) a_dst = lds_wave + (uint32_t)nslot * kXSlot;  // spread mode: a harmless re-stage into the free slot
         const int cslot = cur == 2 ? 0 : cur + 1;  // (cur + 1) % 3: the next step's coordinates
         const lds_char *pa = lds + cur * kXSlot + lane * 16;
@@ -630,6 +647,12 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         if constexpr (WIDE)
             x3w_half<FRESH, DIAG>(pa, pcn, xq[0], yq[0], lane >> 5, cexp, msc, kb, acc[0], outer[0], nx, mu[0],
                                   voff, a_src, a_dst);
+        else if (LEVELS && s0.lv == 2)
+            x3_half<NC, FRESH, DIAG, kPieces, 2>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
+                                                 a_dst, is_loader);
+        else if (LEVELS && s0.lv == 1)
+            x3_half<NC, FRESH, DIAG, kPieces, 1>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
+                                                 a_dst, is_loader);
         else
             x3_half<NC, FRESH, DIAG, kPieces>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
                                               a_dst, is_loader);
@@ -783,7 +806,11 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 17: SBO_X3_LAUNCH(1, 528); break;  // diagnostics: no step barrier (wrong results)
         case 18: SBO_X3_LAUNCH(1, 529); break;  //   and no next-step K*
         case 19: SBO_X3_LAUNCH(1, 1040); break;  // A stage loaded by waves 4-7 only (12 pieces each)
-        default: SBO_X3_LAUNCH(1, 16); break;  // 3: eight waves of 16 queries, A pieces spread
+        case 20: SBO_X3_LAUNCH(1, 2064); break;  // diagnostics: 3 of the 6 split products
+        case 21: SBO_X3_LAUNCH(1, 4112); break;  //   1 of the 6
+        case 22: SBO_X3_LAUNCH(1, 16); break;    // variant 3 with every tile at full precision
+        case 23: SBO_X3_LAUNCH(1, 8208); break;  // variant 3 with A fragments two row blocks ahead
+        default: SBO_X3_LAUNCH(1, 8240); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A one block ahead
     }
 #undef SBO_X3_LAUNCH
     return hipGetLastError();

@@ -327,9 +327,9 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     {
         SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)npad));
         SBO_HIP(sbo::launch_row_l1(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->scratch.as<double>()));
-        SBO_HIP(grow_keep(ctx, ctx->tile_lgn, sizeof(float2) * (size_t)sbo::total_tiles(nI),
-                          sizeof(float2) * old_tiles));
-        SBO_HIP(sbo::launch_tile_norms(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->tile_lgn.as<float2>()));
+        SBO_HIP(grow_keep(ctx, ctx->tile_lgn, sizeof(float4) * (size_t)sbo::total_tiles(nI),
+                          sizeof(float4) * old_tiles));
+        SBO_HIP(sbo::launch_tile_norms(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->tile_lgn.as<float4>()));
         const int64_t r0 = I0 * sbo::kBM;
         std::vector<double> rl1((size_t)(npad - r0));
         std::vector<float> ha((size_t)n);
@@ -399,12 +399,14 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     if (ctx->skip_log2 < 0) {
         plan.L = ctx->auto_skip_log2;
         plan.L_mean = ctx->auto_skip_mean_log2;
-        plan.lgn = ctx->tile_lgn.as<float2>();
+        plan.lgn = ctx->tile_lgn.as<float4>();
+        plan.levels = sbo::x3_levels(ctx->kernel_variant) ? 1 : 0;
         plan.kcoord = ctx->kcoord.as<float>();
         plan.lg_tau_v = ctx->lg_tau_v;
     } else {
         plan.L = ctx->skip_log2;
     }
+    plan.prod_full = ctx->kernel_variant >= 2 ? 6 : 1;
     if (ctx->query_order && plan.L > 0 && m > sbo::kBN) {
         const size_t wb = sbo::query_order_bytes(m);
         SBO_HIP(ctx->qwork.reserve(wb));
@@ -872,6 +874,22 @@ SBO_API sbo_status sbo_profile_work(sbo_ctx *ctx, double *predict_flops) {
     return SBO_OK;
 }
 
+SBO_API sbo_status sbo_profile_mfma(sbo_ctx *ctx, double *mfma_flops, int64_t *tiles_by_level) {
+    if (!ctx || !mfma_flops) return SBO_E_INVAL;
+    unsigned long long t[4] = {0, 0, 0, 0};
+    if (ctx->counters.capacity()) {
+        SBO_HIP(hipMemcpyAsync(t, ctx->counters.as<void>(), sizeof(t), hipMemcpyDeviceToHost, ctx->stream));
+        SBO_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    *mfma_flops = 2.0 * sbo::kBM * sbo::kBN * sbo::kBK * (double)t[1];
+    if (tiles_by_level) {
+        tiles_by_level[1] = (int64_t)t[2];
+        tiles_by_level[2] = (int64_t)t[3];
+        tiles_by_level[0] = (int64_t)t[0] - (int64_t)(t[2] + t[3]);
+    }
+    return SBO_OK;
+}
+
 SBO_API sbo_status sbo_profile_read(sbo_ctx *ctx, double *predict_ms, int64_t *predict_launches, double *fill_ms,
                                     int64_t *fill_launches) {
     if (!ctx) return SBO_E_INVAL;
@@ -914,7 +932,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->sweep_groups = (int)value;
             return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
-            SBO_CHECK(value >= 0 && value <= 19, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 19]");
+            SBO_CHECK(value >= 0 && value <= 23, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 23]");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
         case SBO_OPT_TILE_SKIP:
@@ -1065,7 +1083,7 @@ SBO_API sbo_status sbo_subgoal(sbo_ctx *ctx, const double *Dx, const double *Dy,
 // ------------------------------------------------- fitted state, 8(e)
 namespace {
 
-constexpr uint64_t kStateMagic = 0x3353544154534253ull;  // "SBSTATS3" (two tile norms)
+constexpr uint64_t kStateMagic = 0x3453544154534253ull;  // "SBSTATS4" (three tile norms, 16 B per tile)
 
 struct StateHeader {
     uint64_t magic;
@@ -1100,7 +1118,7 @@ StateHeader state_layout(const sbo_ctx *ctx) {
     h.off_kcoord = sbo::round_up(h.off_aug + 4 * sbo::total_tiles(ctx->npad / sbo::kBM) * sbo::kTileFloats, 256);
     h.off_kbox = sbo::round_up(h.off_kcoord + 4 * nt * 3 * sbo::kBK, 256);
     h.off_lgn = sbo::round_up(h.off_kbox + 16 * nt, 256);
-    h.total = sbo::round_up(h.off_lgn + 8 * sbo::total_tiles(ctx->npad / sbo::kBM), 256);
+    h.total = sbo::round_up(h.off_lgn + 16 * sbo::total_tiles(ctx->npad / sbo::kBM), 256);
     return h;
 }
 
@@ -1133,7 +1151,7 @@ SBO_API sbo_status sbo_export_state(sbo_ctx *ctx, void *dev_buf, int64_t cap) {
     SBO_HIP(hipMemcpyAsync(b + h.off_kbox, ctx->kbox.as<void>(), 16 * (size_t)nt, hipMemcpyDeviceToDevice,
                            ctx->stream));
     SBO_HIP(hipMemcpyAsync(b + h.off_lgn, ctx->tile_lgn.as<void>(),
-                           8 * (size_t)sbo::total_tiles(ctx->npad / sbo::kBM), hipMemcpyDeviceToDevice, ctx->stream));
+                           16 * (size_t)sbo::total_tiles(ctx->npad / sbo::kBM), hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));  // the header and order live on this host stack
     return SBO_OK;
 }
@@ -1156,7 +1174,7 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
     SBO_HIP(ctx->aug.reserve(aug_bytes));
     SBO_HIP(ctx->kcoord.reserve(4 * (size_t)nt * 3 * sbo::kBK));
     SBO_HIP(ctx->kbox.reserve(16 * (size_t)nt));
-    SBO_HIP(ctx->tile_lgn.reserve(8 * (size_t)sbo::total_tiles(h.npad / sbo::kBM)));
+    SBO_HIP(ctx->tile_lgn.reserve(16 * (size_t)sbo::total_tiles(h.npad / sbo::kBM)));
     ctx->order.resize((size_t)h.n);
     SBO_HIP(hipMemcpyAsync(ctx->order.data(), b + h.off_order, 8 * (size_t)h.n, hipMemcpyDeviceToHost, ctx->stream));
     SBO_HIP(hipMemcpyAsync(ctx->aug.as<void>(), b + h.off_aug, aug_bytes, hipMemcpyDeviceToDevice, ctx->stream));
@@ -1164,7 +1182,7 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
                            hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipMemcpyAsync(ctx->kbox.as<void>(), b + h.off_kbox, 16 * (size_t)nt, hipMemcpyDeviceToDevice,
                            ctx->stream));
-    SBO_HIP(hipMemcpyAsync(ctx->tile_lgn.as<void>(), b + h.off_lgn, 8 * (size_t)sbo::total_tiles(h.npad / sbo::kBM),
+    SBO_HIP(hipMemcpyAsync(ctx->tile_lgn.as<void>(), b + h.off_lgn, 16 * (size_t)sbo::total_tiles(h.npad / sbo::kBM),
                            hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
     ctx->n = h.n;

@@ -174,13 +174,17 @@ hipError_t launch_widen(hipStream_t s, const float *src, int64_t ld_src, int64_t
 // every K* entry is below 2^-L.  The last row block (which also accumulates
 // the mean) keeps every tile within 2^-L_mean.  L >= 150 drops only exact
 // zeros (bitwise identical to the dense sweep); L = 0: dense.
-// tiles_done (may be null): += number of (BM x BN x BK) tiles multiplied.
+// tiles_done (may be null): [0] += number of (BM x BN x BK) tiles multiplied,
+// [1] += MFMA products issued on them (prod_full per full tile, 3 / 1 per
+// tile at the reduced levels).
 struct SkipPlan {
     int L = 0;                  // 0: dense
     int L_mean = 0;             // last row block; <= L means "same as L"
-    const float2 *lgn = nullptr;   // per packed tile log2 gain bounds (null: distance test only)
+    const float4 *lgn = nullptr;   // per packed tile log2 gain bounds (null: distance test only)
     const float *kcoord = nullptr; // per k-tile coordinates (the |k|_2 bound of the tile-norm test)
     float lg_tau_v = 0.0f;
+    int levels = 0;     // with lgn: tiles may run at the reduced precision levels (split sweep)
+    int prod_full = 1;  // MFMA products per full-precision tile (6: split sweep), for the counter
 };
 // The tick's plan (which k-tiles each (row block, query block) item runs,
 // non-empty items in row-block-major order, one balanced item range per
@@ -212,6 +216,10 @@ size_t x3_coord_bytes(int64_t npad);
 hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, int64_t I0, int wide,
                           char *ax3, float *kc3);
 // the split operand's layout a kernel variant reads (1: the wide 32x32x16 shape)
+// tile-list entry of the plan: k-tile index | precision level code << kLevelShift
+constexpr int kLevelShift = 14;
+// the split sweeps that honour the plan's precision levels
+inline bool x3_levels(int variant) { return variant == 3 || variant == 23; }
 inline int x3_layout(int variant) { return (variant == 13 || variant == 14) ? 1 : 0; }
 // The sweep over the plan with the split operand; qx/qy must be readable in
 // whole 128-query blocks (padded to round_up(m, kBN)).  variant: 2 (4-7:
@@ -222,7 +230,7 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
                              int variant);
 // lgn[tile_start(I) + t] = (log2 16 max_r |A_It[r]|_1, log2 |A_It|_F) (f64
 // sums, rounded up) for row blocks I >= I0 (-1000 for an all-zero tile).
-hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float2 *lgn);
+hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float4 *lgn);
 // d = (double)in - v;  out = (float)d
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out);

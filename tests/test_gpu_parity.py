@@ -410,7 +410,7 @@ def test_sweep_partition_and_outer_variant(mapper):
     with pytest.raises(N.SboError):
         gm.set_option(N.SBO_OPT_SWEEP_GROUPS, -1)
     with pytest.raises(N.SboError):
-        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 20)
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 24)
 
 
 @pytest.mark.parametrize("variant", [2, 3, 9, 13])
@@ -630,3 +630,43 @@ def test_query_cost_is_the_plan(mapper):
     tiles = w.value / (2.0 * 256 * 128 * 64)
     assert tiles > 0 and abs(float(cost.astype(np.float64).sum()) - tiles) <= 1e-4 * tiles
     assert np.array_equal(mu0, mu1) and np.array_equal(sd0, sd1)
+
+
+def test_precision_levels(mapper):
+    """Variant 3 runs the plan's far tiles at three / one bf16 product(s)
+    instead of six, charged to the same error budget as the skipped tiles:
+    the issued-product counter is 6 l0 + 3 l1 + l2 of the per-level tile
+    counts, both levels occur on a spread-out workload, and the result stays
+    within the budget (2^-22 sf2 on sigma^2) of the all-six-products sweep
+    (variant 22) -- itself within the budget of the dense sweep."""
+    wl = synthetic(8192, 200, 160, seed=21)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    lib = N.lib()
+    m = wl.qx.size
+    res = {}
+    for v in (22, 3):
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, v)
+        lib.sbo_profile(gm.ctx.handle, 1)
+        out = dict(mu=np.empty(m, np.float32), sd=np.empty(m, np.float32))
+        k = gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
+        w, mf = ctypes.c_double(), ctypes.c_double()
+        lv = (ctypes.c_int64 * 3)()
+        lib.sbo_profile_work(gm.ctx.handle, ctypes.byref(w))
+        lib.sbo_profile_mfma(gm.ctx.handle, ctypes.byref(mf), lv)
+        lib.sbo_profile(gm.ctx.handle, 0)
+        unit = 2.0 * 256 * 128 * 64
+        tiles, prods = w.value / unit, mf.value / unit
+        assert sum(lv) == round(tiles) and prods == 6 * lv[0] + 3 * lv[1] + lv[2], (v, list(lv), tiles, prods)
+        res[v] = (out["mu"], out["sd"], k.idx, list(lv))
+    gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 3)
+    assert res[22][3][1] == 0 and res[22][3][2] == 0
+    l0, l1, l2 = res[3][3]
+    print(f"tiles at six / three / one product(s): {l0} {l1} {l2} (variant 22: {res[22][3][0]})")
+    assert l1 > 0 and l2 > 0
+    ulp = np.finfo(np.float32).eps
+    dvar = np.abs(res[3][1].astype(np.float64) ** 2 - res[22][1].astype(np.float64) ** 2).max()
+    dmu = np.abs(res[3][0].astype(np.float64) - res[22][0]).max()
+    assert dvar <= 2 * 2.0 ** -22 + 4 * ulp
+    assert dmu <= 2 * 2.0 ** -22 + 2 * ulp * np.abs(res[22][0]).max()
+    assert res[3][2] == res[22][2]

@@ -46,17 +46,21 @@ def main():
             gm.tick(qx, qy, wl.beta, wl.f_min, outputs=dict(mu=mu, sd=sd))
             pm, pl, fm, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_int64()
             lib.sbo_profile_read(gm.ctx.handle, ctypes.byref(pm), ctypes.byref(pl), ctypes.byref(fm), ctypes.byref(fl))
-            w = ctypes.c_double()
+            w, mf = ctypes.c_double(), ctypes.c_double()
             lib.sbo_profile_work(gm.ctx.handle, ctypes.byref(w))
+            lv = (ctypes.c_int64 * 3)()
+            lib.sbo_profile_mfma(gm.ctx.handle, ctypes.byref(mf), lv)
             if r > 0:
-                times[v].append((pm.value, w.value / (pm.value * 1e-3) / 1e12))
+                times[v].append((pm.value, w.value / (pm.value * 1e-3) / 1e12, w.value, mf.value, list(lv)))
             outs[v] = (mu.cpu().numpy(), sd.cpu().numpy())
     for v in a.variants:
         ms = np.median([x[0] for x in times[v]])
         tf = np.median([x[1] for x in times[v]])
         dmu = np.abs(outs[v][0] - outs[a.variants[0]][0]).max()
         dsd = np.abs(outs[v][1] - outs[a.variants[0]][1]).max()
-        print(f"variant {v}: {ms:.2f} ms  {tf:.1f} TF exec  | max|dmu| {dmu:.2e} max|dsd| {dsd:.2e}", flush=True)
+        fl, mf = times[v][-1][2], times[v][-1][3]
+        print(f"variant {v}: {ms:.2f} ms  {tf:.1f} TF exec  tiles {fl / (2 * 256 * 128 * 64):.4g}  MFMA products/tile "
+              f"{mf / max(fl, 1.0):.3f} levels {times[v][-1][4]}  | max|dmu| {dmu:.2e} max|dsd| {dsd:.2e}", flush=True)
 
 
 if __name__ == "__main__":

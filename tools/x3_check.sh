@@ -2,8 +2,6 @@
 mkdir -p gpurun_out/x3
 O=gpurun_out/x3
 export TMPDIR=/tmp
-step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -6 $O/$name.log | cut -c1-400; [ $rc -eq 0 ] || exit $rc; }
-step gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step acc 300 python tools/variant_accuracy.py --n 8192 16384 --variants 3 0
-step ab_c4 300 python tools/ab_variants.py --config C4 --variants 3 0 --rounds 2
-step ab_c3 300 python tools/ab_variants.py --config C3 --variants 3 --rounds 2
+step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -4 $O/$name.log | cut -c1-1500; [ $rc -eq 0 ] || exit $rc; }
+step tests 600 python -u -m pytest -x -q -s --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "precision_levels or query_cost or tile_skip"
+step bench_c4 300 python bench.py --no-cpu
