@@ -488,11 +488,6 @@ __device__ __forceinline__ float tile_box_d2(const float4 b, const QBox &q) {
 constexpr float kLg3 = -14.36f;  // log2(3.1 2^-16), rounded up
 constexpr float kLg1 = -6.96f;   // log2(2.03 2^-8 + 3.1 2^-16), rounded up
 
-// log2(drop saving / level saving): per-tile sweep time at C4 of six, three,
-// one product(s): 18.6, 12.9, 9.9 ns (variants 22, 20, 21)
-constexpr float kLvlKey0 = 0.80f;  // six -> three products saves 5.7 ns
-constexpr float kLvlKey1 = 1.72f;  // three -> one saves 3.0 ns (the drop: 9.9 ns)
-
 __device__ __forceinline__ int inc_bin(float l, unsigned long long &w, float key = 0.0f) {  // l = log2(inc / budget)
     const float f = (l + key + (float)kBudgetFloor) * (float)kBinsPerBit + 1.0f;
     const int bi = f < 0.0f ? 0 : (f >= (float)(kBudgetBins - 1) ? kBudgetBins - 1 : (int)f);
@@ -501,13 +496,13 @@ __device__ __forceinline__ int inc_bin(float l, unsigned long long &w, float key
 }
 
 __device__ __forceinline__ void tile_increments(float d2, float kn, float4 lgn_t, float cexp, float lg_tau,
-                                                int (&bi)[3], unsigned long long (&w)[3]) {
+                                                float2 key, int (&bi)[3], unsigned long long (&w)[3]) {
     const float kmax = cexp * d2 * 0.999f;
     const float b = fminf(lgn_t.x + kmax, lgn_t.y + kn) - lg_tau + 0.01f;
     const float babs = fminf(lgn_t.x + kmax, lgn_t.z + kn) - lg_tau + 0.01f;
     const float r3 = babs + kLg3, r1 = babs + kLg1;
-    bi[0] = inc_bin(r3, w[0], kLvlKey0);
-    bi[1] = inc_bin(r1 + __log2f(1.0f - exp2f(r3 - r1)), w[1], kLvlKey1);
+    bi[0] = inc_bin(r3, w[0], key.x);
+    bi[1] = inc_bin(r1 + __log2f(1.0f - exp2f(r3 - r1)), w[1], key.y);
     const float dl = r1 - b;  // <= -3.96: |A|_F <= 8 ||A||_2
     bi[2] = dl < -0.01f ? inc_bin(b + __log2f(1.0f - exp2f(dl)), w[2]) : inc_bin(b, w[2]);
     // monotone: the three bins never go down (so a tile's spent increments are a prefix)
@@ -525,15 +520,17 @@ struct PlanRule {
     QBox box;
     const float *d2s;   // LDS cache of tile distances (t < kPlanD2)
     const float *kns;   // LDS cache of the tiles' log2 |k|_2 bounds (t < kPlanD2)
-    int levels;         // precision levels allowed (0: every kept tile at full precision)
+    int levels;         // 0: every kept tile at full precision; 1: budgeted levels; 2 + l: timing
+                        // diagnostic, the drop-only plan with every kept tile at level l
+    float2 key;         // rank keys of the two level increments (SkipPlan::lvl_key)
 
     __device__ __forceinline__ float d2(int t) const { return t < kPlanD2 ? d2s[t] : tile_box_d2(kbox[t], box); }
     // beyond the cache: |k|_2 <= 8 K*max
     __device__ __forceinline__ float kn(int t) const { return t < kPlanD2 ? kns[t] : 3.0f + cexp * d2(t) * 0.999f; }
 
     __device__ __forceinline__ void incs(int I, int t, int (&bi)[3], unsigned long long (&w)[3]) const {
-        tile_increments(d2(t), kn(t), lgn[tile_start(I) + t], cexp, lg_tau, bi, w);
-        if (!levels) {  // only the whole drop: the first two increments free, the third the whole drop bound
+        tile_increments(d2(t), kn(t), lgn[tile_start(I) + t], cexp, lg_tau, key, bi, w);
+        if (levels != 1) {  // only the whole drop: the first two increments free, the third the whole drop bound
             bi[0] = bi[1] = 0;
             w[0] = w[1] = 0ull;
             const float kmax = cexp * d2(t) * 0.999f;
@@ -597,7 +594,7 @@ struct PlanRule {
             unsigned long long w[3];
             incs(I, t, bi, w);
             const int spent = (bi[0] <= drop_max) + (bi[1] <= drop_max) + (bi[2] <= drop_max);
-            code = spent == 3 ? -1 : (levels ? spent : 0);
+            code = spent == 3 ? -1 : (levels == 1 ? spent : (levels > 1 ? levels - 2 : 0));
         } else {
             code = (skip_d2 <= 0.0f || dd <= skip_d2) ? 0 : -1;  // skip_d2 <= 0: dense
         }
@@ -667,7 +664,7 @@ __device__ __forceinline__ int64_t plan_item(int I, int nI, int64_t nQ, int64_t 
 // outputs here, so the sweep never visits them.
 __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     const float4 *__restrict__ kbox, const float *__restrict__ kcoord, const float4 *__restrict__ lgn, int levels,
-    int nI,
+    float2 lvl_key, int nI,
     int64_t nQ,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, float m0, int64_t ldp, float *__restrict__ part, float *__restrict__ mean,
@@ -678,7 +675,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     const int64_t qb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nkt = kTilesPerRowBlockStep * nI;
-    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns, levels};
+    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns, levels, lvl_key};
     R.box = plan_setup(qx, qy, m, qb, kbox, lgn ? kcoord : nullptr, cexp, nkt, d2s, kns, red);
     for (int I = wave; I < nI; I += kPlanWaves) {
         const int T = kTilesPerRowBlockStep * (I + 1);
@@ -709,7 +706,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
 // (I, qb, offset low 32 bits, count | offset high bits << 16).
 __global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
     const float4 *__restrict__ kbox, const float *__restrict__ kcoord, const float4 *__restrict__ lgn, int levels,
-    int nI,
+    float2 lvl_key, int nI,
     int64_t nQ,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, const unsigned long long *__restrict__ key,
@@ -721,7 +718,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
     const int64_t qb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nkt = kTilesPerRowBlockStep * nI;
-    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns, levels};
+    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns, levels, lvl_key};
     R.box = plan_setup(qx, qy, m, qb, kbox, lgn ? kcoord : nullptr, cexp, nkt, d2s, kns, red);
     unsigned long long prod = 0, nl1 = 0, nl2 = 0;
     for (int I = wave; I < nI; I += kPlanWaves) {
@@ -1421,9 +1418,9 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     const float skip_d2 = cutoff_d2(skip.L, ce);
     const float skip_d2_mean = skip.L > 0 && skip.L_mean > skip.L ? cutoff_d2(skip.L_mean, ce) : skip_d2;
     const float4 *lgn = skip.L > 0 ? skip.lgn : nullptr;
-    const int levels = lgn && skip.levels ? 1 : 0;
+    const int levels = lgn ? skip.levels : 0;
     hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn,
-                       levels, nI,
+                       levels, make_float2(skip.lvl_key[0], skip.lvl_key[1]), nI,
                        nQ, qx, qy,
                        m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr);
     hipError_t e = hipGetLastError();
@@ -1432,7 +1429,7 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     e = rocprim::inclusive_scan(w + L.temp, tb, key, scan, (size_t)items, rocprim::plus<unsigned long long>(), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn,
-                       levels, nI, nQ, qx, qy,
+                       levels, make_float2(skip.lvl_key[0], skip.lvl_key[1]), nI, nQ, qx, qy,
                        m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, key, scan, thr, desc, tl, skip.prod_full,
                        tiles_done ? tiles_done + 1 : nullptr);
     if (!L.xcd) {

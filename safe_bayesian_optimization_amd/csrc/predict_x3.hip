@@ -92,6 +92,17 @@ __device__ __forceinline__ float lds_f(const lds_char *p) {
 __device__ __forceinline__ void dma16(uint32_t voff, const void *sbase, uint32_t ldst) {
     asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(ldst) : "memory");
 }
+// the same under a wave-uniform EXEC mask (0: no lane moves data, but the
+// instruction still issues and counts in vmcnt, so the step's wait count
+// stays static) -- no control flow in the scheduled MFMA region
+__device__ __forceinline__ void dma16_masked(uint32_t voff, const void *sbase, uint32_t ldst, uint64_t mask) {
+    uint64_t sv;
+    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                 "s_mov_b64 exec, %0"
+                 : "=&s"(sv)
+                 : "v"(voff), "s"(sbase), "{m0}"(ldst), "s"(mask)
+                 : "memory", "scc");
+}
 
 // K* pieces of a step for the wave's NC 16-query column blocks
 // (lane (g, r): k = 8g + j of the half-tile, query 16 (NC w + c) + r)
@@ -137,7 +148,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                                         const float (&yq)[NC], int g, float cexp, float msc, const KPieces<NC> &kb,
                                         f32x4 (&acc)[NC][16], f32x4 (&outer)[NC][16], KPieces<NC> &nx,
                                         double (&mu)[NC], uint32_t voff, const char *asrc, uint32_t adst,
-                                        bool loader) {
+                                        bool loader, int npieces) {
     // SPREAD (DIAG & 16): this wave's A pieces of stage i+2 are issued one
     // per row block between the MFMAs instead of in a burst at the top
     constexpr bool SPREAD = (DIAG & 16) != 0;
@@ -150,6 +161,8 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
     constexpr int EL = (DIAG & 4096) ? 2 : ((DIAG & 2048) ? 1 : LV);
     constexpr bool P1 = EL <= 1, P2 = EL == 0;  // planes a1, a2 in use
     constexpr int NPROD = EL == 0 ? 6 : (EL == 1 ? 3 : 1);
+    constexpr int LAG = (DIAG & 32768) ? 2 : (EL == 0 ? 2 : (EL == 1 ? 4 : 8));
+    const int npu = __builtin_amdgcn_readfirstlane(npieces);
     u32x4 a0 = lds_b128(pa), a1 = {}, a2 = {};
     if (P1) a1 = lds_b128(pa + kXPlane);
     if (P2) a2 = lds_b128(pa + 2 * kXPlane);
@@ -209,13 +222,26 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                 ak = lds_f2(pcn + 256 + g * 32 + (i + 1) * 8);
             }
         }
-        if (SPREAD && rb >= 1 && rb <= PIECES && loader)
-            dma16(voff, asrc + (rb - 1) * kStride, adst + (rb - 1) * kStride);
-        if (!FRESH && !(DIAG & 68) && rb > 1) {  // those chains finished a block ago
+        if (SPREAD && rb >= 1 && rb <= PIECES && loader) {
+            // (DIAG & 8192: only the pieces of the planes the staged tile's level reads)
+            if constexpr (DIAG & 16384) {
+                // issued after the row block instead (below)
+            } else if constexpr (DIAG & 8192) {
+                const uint32_t mh = (uint32_t)__builtin_amdgcn_readfirstlane(rb <= npieces ? -1 : 0);
+                dma16_masked(voff, asrc + (rb - 1) * kStride, adst + (rb - 1) * kStride,
+                             ((uint64_t)mh << 32) | mh);
+            }
+            else
+                dma16(voff, asrc + (rb - 1) * kStride, adst + (rb - 1) * kStride);
+        }
+        // the finished chains of block rb - LAG (LAG row blocks = 2 (six
+        // products), 4 (three) or 8 (one) x NPROD MFMAs ago: off the MFMA
+        // result latency)
+        if (!FRESH && !(DIAG & 68) && rb >= LAG) {
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
-                outer[c][rb - 2] += acc[c][rb - 2];
-                SBO_PIN_O(outer[c][rb - 2]);
+                outer[c][rb - LAG] += acc[c][rb - LAG];
+                SBO_PIN_O(outer[c][rb - LAG]);
             }
         }
 #pragma unroll
@@ -253,6 +279,13 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
             }
         }
         __builtin_amdgcn_sched_barrier(0);
+        // DIAG & 16384: piece rb of stage i+2 after row block rb, and only the
+        // planes its level reads (a uniform branch at the scheduling-region
+        // boundary; the step's vmcnt wait counts npieces)
+        if constexpr (SPREAD && (DIAG & 16384)) {
+            if (rb < PIECES && loader && (rb < PIECES / 3 || rb < npu))
+                dma16(voff, asrc + rb * kStride, adst + rb * kStride);
+        }
         if (AHEAD == 2) {
             a0 = n0;
             a1 = n1;
@@ -270,12 +303,12 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
     }
     if (!FRESH && !(DIAG & 68)) {
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            outer[c][14] += acc[c][14];
-            outer[c][15] += acc[c][15];
-            SBO_PIN_O(outer[c][14]);
-            SBO_PIN_O(outer[c][15]);
-        }
+        for (int rb = 16 - LAG; rb < 16; ++rb)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                outer[c][rb] += acc[c][rb];
+                SBO_PIN_O(outer[c][rb]);
+            }
     }
 }
 
@@ -614,6 +647,8 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         const bool issue = la_k < k1;
         const int nslot = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
         s2 = issue ? stage(nslot, false) : XStep{0, 0, 0, 0};
+        // A pieces the staged tile's level needs (plane p = pieces p*kPieces/3 ..)
+        const int np2 = LEVELS ? (kPieces / 3) * (3 - s2.lv) : kPieces;
         if (!issue) a_dst = lds_wave + (uint32_t)nslot * kXSlot;  // spread mode: a harmless re-stage into the free slot
         const int cslot = cur == 2 ? 0 : cur + 1;  // (cur + 1) % 3: the next step's coordinates
         const lds_char *pa = lds + cur * kXSlot + lane * 16;
@@ -649,17 +684,17 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
                                   voff, a_src, a_dst);
         else if (LEVELS && s0.lv == 2)
             x3_half<NC, FRESH, DIAG, kPieces, 2>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
-                                                 a_dst, is_loader);
+                                                 a_dst, is_loader, np2);
         else if (LEVELS && s0.lv == 1)
             x3_half<NC, FRESH, DIAG, kPieces, 1>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
-                                                 a_dst, is_loader);
+                                                 a_dst, is_loader, np2);
         else
             x3_half<NC, FRESH, DIAG, kPieces>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
-                                              a_dst, is_loader);
+                                              a_dst, is_loader, np2);
         if (!FRESH && (s0.flags & kLast)) {
             // item done: column sums of V^2 over its rows (lanes l, l+16, l+32,
             // l+48 hold four row quarters of column l&15 of every block)
-            if (DIAG & 64)
+            if (DIAG & 64) {
 #pragma unroll
                 for (int c = 0; c < kCB; ++c)
 #pragma unroll
@@ -667,6 +702,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
                         outer[c][rb] = acc[c][rb];
                         acc[c][rb] = AccT{};
                     }
+            }
             pend = true;
             pend_I = s0.I;
             pend_q = (int64_t)s0.qb * kBN + qo;
@@ -690,8 +726,15 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         // retire stage i+1: its queries and coordinates (wave 0) precede its
         // A pieces and were retired one step earlier; leave stage i+2's A in flight
         if ((issue || (DIAG & 16)) && !(DIAG & 2) && is_loader) {
-            if constexpr (kPieces == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            if constexpr (kPieces == 12) {
+                asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            } else if constexpr (LEVELS && (DIAG & 16384)) {  // stage i+2 issued np2 pieces
+                if (np2 == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                else if (np2 == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            }
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -810,6 +853,14 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 21: SBO_X3_LAUNCH(1, 4112); break;  //   1 of the 6
         case 22: SBO_X3_LAUNCH(1, 16); break;    // variant 3 with every tile at full precision
         case 23: SBO_X3_LAUNCH(1, 8208); break;  // variant 3 with A fragments two row blocks ahead
+        case 24: SBO_X3_LAUNCH(1, 24624); break;  // variant 3 issuing only the A pieces a level reads
+        case 25: SBO_X3_LAUNCH(1, 4113); break;   // diagnostics: 1 product, no next-step K*
+        case 26: SBO_X3_LAUNCH(1, 4114); break;   //   1 product, no A pieces
+        case 27: SBO_X3_LAUNCH(1, 4115); break;   //   1 product, neither
+        case 28: SBO_X3_LAUNCH(1, 4116); break;   //   1 product, no outer sums
+        case 29: SBO_X3_LAUNCH(1, 4119); break;   //   1 product, none of the three
+        case 30: SBO_X3_LAUNCH(1, 41008); break;  // variant 3 with the outer sums two blocks behind at every level
+        case 31: SBO_X3_LAUNCH(1, 36880); break;  // diagnostics: 1 product, outer sums two blocks behind
         default: SBO_X3_LAUNCH(1, 8240); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A one block ahead
     }
 #undef SBO_X3_LAUNCH

@@ -407,6 +407,8 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         plan.L = ctx->skip_log2;
     }
     plan.prod_full = ctx->kernel_variant >= 2 ? 6 : 1;
+    if (const char *e = getenv("SBO_LVL_KEYS")) sscanf(e, "%f,%f", &plan.lvl_key[0], &plan.lvl_key[1]);  // tuning
+    if (const char *e = getenv("SBO_LVL_FORCE"); e && plan.levels) plan.levels = 2 + atoi(e);  // timing diagnostic
     if (ctx->query_order && plan.L > 0 && m > sbo::kBN) {
         const size_t wb = sbo::query_order_bytes(m);
         SBO_HIP(ctx->qwork.reserve(wb));
@@ -932,7 +934,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->sweep_groups = (int)value;
             return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
-            SBO_CHECK(value >= 0 && value <= 23, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 23]");
+            SBO_CHECK(value >= 0 && value <= 31, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 31]");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
         case SBO_OPT_TILE_SKIP:

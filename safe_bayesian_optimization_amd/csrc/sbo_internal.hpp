@@ -185,6 +185,10 @@ struct SkipPlan {
     float lg_tau_v = 0.0f;
     int levels = 0;     // with lgn: tiles may run at the reduced precision levels (split sweep)
     int prod_full = 1;  // MFMA products per full-precision tile (6: split sweep), for the counter
+    // rank of a tile's two level increments against drops: log2(time a drop
+    // saves / time the level step saves), per-tile sweep time at C4 of six,
+    // three, one product(s) 18.6, 12.9, 9.9 ns (variants 22, 20, 21)
+    float lvl_key[2] = {0.80f, 1.72f};
 };
 // The tick's plan (which k-tiles each (row block, query block) item runs,
 // non-empty items in row-block-major order, one balanced item range per
@@ -219,7 +223,7 @@ hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, 
 // tile-list entry of the plan: k-tile index | precision level code << kLevelShift
 constexpr int kLevelShift = 14;
 // the split sweeps that honour the plan's precision levels
-inline bool x3_levels(int variant) { return variant == 3 || variant == 23; }
+inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30; }
 inline int x3_layout(int variant) { return (variant == 13 || variant == 14) ? 1 : 0; }
 // The sweep over the plan with the split operand; qx/qy must be readable in
 // whole 128-query blocks (padded to round_up(m, kBN)).  variant: 2 (4-7:
