@@ -130,8 +130,9 @@ SBO_API sbo_status sbo_tick(sbo_ctx *ctx, const float *qx, const float *qy, int6
 
 /* Sweep work of each query under the current fit: builds the tick's tile
  * plan for these queries (no sweep) and writes cost[i] = the k-tiles its
- * 128-query block multiplies, summed over row blocks, / the block's size,
- * in the caller's order.  For cost-balanced M-sharding across ranks (every
+ * 128-query block multiplies, summed over row blocks and weighted by their
+ * precision level's sweep time (1, 42/64, 33/64 for six, three, one
+ * product(s)), / the block's size, in the caller's order.  For cost-balanced M-sharding across ranks (every
  * rank computes the same costs from the same inputs: the plan is
  * deterministic); no reference counterpart. */
 SBO_API sbo_status sbo_query_cost(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, float *cost,

@@ -365,6 +365,10 @@ constexpr int kPlanWaves = kPlanThreads / 64;
 constexpr int kPlanD2 = 2048;           // k-tile distances cached in LDS (N <= 131072; beyond: recomputed)
 constexpr int kPlanKeyShift = 40;       // plan key: kept-tile count (low 40 bits) | non-empty (high bits)
 constexpr unsigned long long kPlanCountMask = (1ull << kPlanKeyShift) - 1ull;
+// Sweep time of a kept tile by precision level, in 1/64 of a full tile
+// (forced-level C4 sweeps: 20.6, 13.5, 10.6 ns per tile): the weight the
+// workgroup ranges and sbo_query_cost balance
+constexpr unsigned kLevelWeight0 = 64, kLevelWeight1 = 42, kLevelWeight2 = 33;
 constexpr int kSteps = kBK / 4;          // 16x16x4 k steps per tile
 constexpr int kRowBlocks = kBM / 16;     // 16-row MFMA blocks per wave
 
@@ -668,7 +672,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     int64_t nQ,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, float m0, int64_t ldp, float *__restrict__ part, float *__restrict__ mean,
-    unsigned long long *__restrict__ key, unsigned char *__restrict__ thr) {
+    unsigned long long *__restrict__ key, unsigned char *__restrict__ thr, unsigned long long *__restrict__ wkey) {
     __shared__ float d2s[kPlanD2], kns[kPlanD2];
     __shared__ float red[4 * kPlanWaves];
     __shared__ unsigned long long bins[kPlanWaves][kBudgetBins];
@@ -681,14 +685,20 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
         const int T = kTilesPerRowBlockStep * (I + 1);
         const int drop_max = R.threshold(I, bins[wave], lane);
         int cnt = 0;
+        unsigned wsum = 0;
         for (int t0 = 0; t0 < T; t0 += 64) {
             const int t = t0 + lane;
-            cnt += __popcll(__ballot(t < T && R.level(I, t, drop_max) >= 0));
+            const int code = t < T ? R.level(I, t, drop_max) : -1;
+            const int n0 = __popcll(__ballot(code == 0)), n1 = __popcll(__ballot(code == 1)),
+                      n2 = __popcll(__ballot(code == 2));
+            cnt += n0 + n1 + n2;
+            wsum += kLevelWeight0 * n0 + kLevelWeight1 * n1 + kLevelWeight2 * n2;
         }
         const int64_t item = plan_item(I, nI, nQ, qb);
         if (lane == 0) {
             key[item] = (unsigned long long)cnt | ((cnt > 0 ? 1ull : 0ull) << kPlanKeyShift);
             thr[item] = (unsigned char)(drop_max + 1);
+            wkey[item] = wsum;
         }
         if (cnt == 0)
             for (int j = lane; j < kBN; j += 64) {
@@ -763,24 +773,28 @@ __global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
 }
 
 // One thread per sweep workgroup: cut the non-empty item list into P
-// contiguous ranges of about equal tile count (seg[r] .. seg[r+1]).
+// contiguous ranges of about equal sweep time -- the level-weighted tile
+// count (wkey, inclusive scan wscan) -- (seg[r] .. seg[r+1]).
 __global__ void plan_seg_kernel(const unsigned long long *__restrict__ scan, int64_t n_items,
                                 const int4 *__restrict__ desc, int P, int *__restrict__ seg,
-                                unsigned long long *__restrict__ tiles_done) {
+                                unsigned long long *__restrict__ tiles_done, const unsigned long long *__restrict__ wkey,
+                                const unsigned long long *__restrict__ wscan, int nI, int64_t nQ) {
     const unsigned long long last = scan[n_items - 1];
     const uint64_t total = last & kPlanCountMask;
+    const uint64_t wtotal = wscan[n_items - 1];
     const int64_t nne = (int64_t)(last >> kPlanKeyShift);
     for (int w = threadIdx.x; w <= P; w += blockDim.x) {
         if (w == P) {
             seg[P] = (int)nne;
             continue;
         }
-        const uint64_t target = total * (uint64_t)w / (uint64_t)P;
-        int64_t lo = 0, hi = nne;  // first item whose offset >= target
+        const uint64_t target = wtotal * (uint64_t)w / (uint64_t)P;
+        int64_t lo = 0, hi = nne;  // first item whose weighted offset >= target
         while (lo < hi) {
             const int64_t mid = (lo + hi) >> 1;
             const int4 d = desc[mid];
-            const uint64_t off = (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
+            const int64_t it = plan_item(d.x, nI, nQ, d.y);
+            const uint64_t off = wscan[it] - wkey[it];
             if (off < target) lo = mid + 1; else hi = mid;
         }
         seg[w] = (int)lo;
@@ -853,13 +867,13 @@ __global__ void plan_seg2_kernel(const int *__restrict__ xseg, int G, int P, int
 // Sweep work per query from a plan (load balancing across ranks): the kept
 // tiles of its 128-query block summed over row blocks, shared by the block's
 // queries; written in the caller's order (perm: sweep position -> caller).
-__global__ void plan_block_cost_kernel(const unsigned long long *__restrict__ key, int nI, int64_t nQ,
+__global__ void plan_block_cost_kernel(const unsigned long long *__restrict__ wkey, int nI, int64_t nQ,
                                        float *__restrict__ bcost) {
     const int64_t qb = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (qb >= nQ) return;
     unsigned long long c = 0;
-    for (int I = 0; I < nI; ++I) c += key[plan_item(I, nI, nQ, qb)] & kPlanCountMask;
-    bcost[qb] = (float)c;
+    for (int I = 0; I < nI; ++I) c += wkey[plan_item(I, nI, nQ, qb)];
+    bcost[qb] = (float)((double)c / (double)kLevelWeight0);  // in full-precision tiles
 }
 
 __global__ void plan_query_cost_kernel(const float *__restrict__ bcost, int64_t m, const int32_t *__restrict__ perm,
@@ -1333,7 +1347,7 @@ hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int6
 
 namespace {
 struct PlanLayout {
-    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes;
+    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes, wkey, wscan;
     // XCD-interleaved order (P % 8 == 0): the sweep reads desc2 / tl2 / seg2
     bool xcd;
     size_t xseg, pos_of, cnt2, off2, desc2, tl2, seg2, temp2, temp2_bytes;
@@ -1355,6 +1369,8 @@ PlanLayout plan_layout(int64_t nI, int64_t nQ, int P) {
     L.key = take(8 * (size_t)items);
     L.scan = take(8 * (size_t)items);
     L.thr = take((size_t)items);
+    L.wkey = take(8 * (size_t)items);
+    L.wscan = take(8 * (size_t)items);
     L.desc = take(16 * (size_t)(items + 2 * kDescWindow));
     L.tl = take(2 * (size_t)(cap + 2 * kListWindow));
     L.seg = take(4 * (size_t)(P + 1));
@@ -1413,6 +1429,8 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     auto *desc = reinterpret_cast<int4 *>(w + L.desc);
     auto *tl = reinterpret_cast<unsigned short *>(w + L.tl);
     auto *seg = reinterpret_cast<int *>(w + L.seg);
+    auto *wkey = reinterpret_cast<unsigned long long *>(w + L.wkey);
+    auto *wscan = reinterpret_cast<unsigned long long *>(w + L.wscan);
     const double ce = exp2_coef(ell);
     const float cexp = (float)ce;
     const float skip_d2 = cutoff_d2(skip.L, ce);
@@ -1422,18 +1440,22 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn,
                        levels, make_float2(skip.lvl_key[0], skip.lvl_key[1]), nI,
                        nQ, qx, qy,
-                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr);
+                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr, wkey);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t tb = L.temp_bytes;
     e = rocprim::inclusive_scan(w + L.temp, tb, key, scan, (size_t)items, rocprim::plus<unsigned long long>(), s);
+    if (e != hipSuccess) return e;
+    tb = L.temp_bytes;
+    e = rocprim::inclusive_scan(w + L.temp, tb, wkey, wscan, (size_t)items, rocprim::plus<unsigned long long>(), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn,
                        levels, make_float2(skip.lvl_key[0], skip.lvl_key[1]), nI, nQ, qx, qy,
                        m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, key, scan, thr, desc, tl, skip.prod_full,
                        tiles_done ? tiles_done + 1 : nullptr);
     if (!L.xcd) {
-        hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done);
+        hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done, wkey,
+                           wscan, nI, nQ);
         return hipGetLastError();
     }
     auto *xseg = reinterpret_cast<int *>(w + L.xseg);
@@ -1447,7 +1469,8 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     // (positions past the last non-empty item keep count 0 for the scan)
     e = hipMemsetAsync(cnt2, 0, 8 * (size_t)items, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, 8, xseg, tiles_done);
+    hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, 8, xseg, tiles_done, wkey, wscan,
+                       nI, nQ);
     hipLaunchKernelGGL(plan_perm_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, scan, items, desc,
                        xseg, G, pos_of, cnt2);
     e = hipGetLastError();
@@ -1479,8 +1502,8 @@ hipError_t launch_plan_cost(hipStream_t s, int64_t npad, int64_t m, int P, const
     const int64_t nQ = (m + kBN - 1) / kBN;
     if (m <= 0 || nI <= 0) return hipSuccess;
     const PlanLayout L = plan_layout(nI, nQ, P);
-    const auto *key = reinterpret_cast<const unsigned long long *>(static_cast<const char *>(work) + L.key);
-    hipLaunchKernelGGL(plan_block_cost_kernel, dim3((unsigned)((nQ + 255) / 256)), dim3(256), 0, s, key, nI, nQ,
+    const auto *wkey = reinterpret_cast<const unsigned long long *>(static_cast<const char *>(work) + L.wkey);
+    hipLaunchKernelGGL(plan_block_cost_kernel, dim3((unsigned)((nQ + 255) / 256)), dim3(256), 0, s, wkey, nI, nQ,
                        bcost);
     hipLaunchKernelGGL(plan_query_cost_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, bcost, m, perm,
                        cost);

@@ -407,8 +407,8 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         plan.L = ctx->skip_log2;
     }
     plan.prod_full = ctx->kernel_variant >= 2 ? 6 : 1;
-    if (const char *e = getenv("SBO_LVL_KEYS")) sscanf(e, "%f,%f", &plan.lvl_key[0], &plan.lvl_key[1]);  // tuning
-    if (const char *e = getenv("SBO_LVL_FORCE"); e && plan.levels) plan.levels = 2 + atoi(e);  // timing diagnostic
+    // timing diagnostic: the drop-only plan with every kept tile at level SBO_LVL_FORCE
+    if (const char *e = getenv("SBO_LVL_FORCE"); e && plan.levels) plan.levels = 2 + std::clamp(atoi(e), 0, 2);
     if (ctx->query_order && plan.L > 0 && m > sbo::kBN) {
         const size_t wb = sbo::query_order_bytes(m);
         SBO_HIP(ctx->qwork.reserve(wb));

@@ -624,11 +624,16 @@ def test_query_cost_is_the_plan(mapper):
     lib = N.lib()
     lib.sbo_profile(gm.ctx.handle, 1)
     mu1, sd1 = gm.predict(wl.qx, wl.qy)
-    w = ctypes.c_double()
+    w, mf = ctypes.c_double(), ctypes.c_double()
+    lv = (ctypes.c_int64 * 3)()
     lib.sbo_profile_work(gm.ctx.handle, ctypes.byref(w))
+    lib.sbo_profile_mfma(gm.ctx.handle, ctypes.byref(mf), lv)
     lib.sbo_profile(gm.ctx.handle, 0)
     tiles = w.value / (2.0 * 256 * 128 * 64)
-    assert tiles > 0 and abs(float(cost.astype(np.float64).sum()) - tiles) <= 1e-4 * tiles
+    assert tiles > 0 and sum(lv) == round(tiles)
+    # tiles weighted by their precision level's sweep time (64 / 42 / 33 of 64)
+    weighted = (64 * lv[0] + 42 * lv[1] + 33 * lv[2]) / 64.0
+    assert abs(float(cost.astype(np.float64).sum()) - weighted) <= 1e-4 * weighted
     assert np.array_equal(mu0, mu1) and np.array_equal(sd0, sd1)
 
 

@@ -20,5 +20,6 @@ step bench_c5 600 python bench.py --config C5
 step prof_c4 600 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run --output-format csv -- python bench.py --no-cpu --steps 3
 step clock_c4 900 bash tools/pmc_clock.sh c4 --config C4 --ticks 2
 [ -x tools/mfma_probe.bin ] || hipcc -O3 --offload-arch=gfx950 tools/mfma_probe.hip -o tools/mfma_probe.bin
+step shards 300 python tools/shard_emulate.py --config C4 --balance 0
 step mfma_probe 300 ./tools/mfma_probe.bin
 echo done
