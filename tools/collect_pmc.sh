@@ -12,3 +12,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-forma
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python tools/run_predict.py --config $CFG --ticks 2 "$@"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python tools/run_predict.py --config $CFG --ticks 2 "$@"
 python tools/pmc_summary.py $OUT $CFG profiles/${TAG}_pmc_${CFG}.json
+cp profiles/${TAG}_pmc_${CFG}.json $OUT/summary.json
