@@ -163,26 +163,32 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
     constexpr int NPROD = EL == 0 ? 6 : (EL == 1 ? 3 : 1);
     constexpr int LAG = (DIAG & 32768) ? 2 : (EL == 0 ? 2 : (EL == 1 ? 4 : 8));
     const int npu = __builtin_amdgcn_readfirstlane(npieces);
-    u32x4 a0 = lds_b128(pa), a1 = {}, a2 = {};
-    if (P1) a1 = lds_b128(pa + kXPlane);
-    if (P2) a2 = lds_b128(pa + 2 * kXPlane);
-    u32x4 n0 = a0, n1 = a1, n2 = a2;
-    if (AHEAD == 2) {
-        n0 = lds_b128(pa + 1024);
-        if (P1) n1 = lds_b128(pa + kXPlane + 1024);
-        if (P2) n2 = lds_b128(pa + 2 * kXPlane + 1024);
+    // A fragments of row block r are read AH blocks ahead of their use: the
+    // fewer MFMAs a block has, the more blocks ahead (DIAG & 65536: 4 at one
+    // product, 2 at three), so the LDS latency stays covered
+    constexpr int AH = (DIAG & 131072) ? (EL == 2 ? 8 : (EL == 1 ? 3 : AHEAD))
+                       : (DIAG & 65536) ? (EL == 2 ? 4 : (EL == 1 ? 2 : AHEAD)) : AHEAD;
+    u32x4 f0[16], f1[16], f2[16];
+#pragma unroll
+    for (int r = 0; r < AH; ++r) {
+        f0[r] = lds_b128(pa + r * 1024);
+        if constexpr (P1) f1[r] = lds_b128(pa + kXPlane + r * 1024);
+        if constexpr (P2) f2[r] = lds_b128(pa + 2 * kXPlane + r * 1024);
     }
     // coordinates of pair 0; pair i+1's are read while pair i is built
     f32x2v xk = lds_f2(pcn + g * 32), yk = lds_f2(pcn + 128 + g * 32), ak = lds_f2(pcn + 256 + g * 32);
     f32x2v e[NC];
 #pragma unroll
     for (int rb = 0; rb < 16; ++rb) {
-        u32x4 b0 = {}, b1 = {}, b2 = {};
-        if (rb + AHEAD < 16) {
-            b0 = lds_b128(pa + (rb + AHEAD) * 1024);
-            if (P1) b1 = lds_b128(pa + kXPlane + (rb + AHEAD) * 1024);
-            if (P2) b2 = lds_b128(pa + 2 * kXPlane + (rb + AHEAD) * 1024);
+        if (rb + AH < 16) {
+            f0[rb + AH] = lds_b128(pa + (rb + AH) * 1024);
+            if constexpr (P1) f1[rb + AH] = lds_b128(pa + kXPlane + (rb + AH) * 1024);
+            if constexpr (P2) f2[rb + AH] = lds_b128(pa + 2 * kXPlane + (rb + AH) * 1024);
         }
+        const u32x4 a0 = f0[rb];
+        u32x4 a1 = {}, a2 = {};
+        if constexpr (P1) a1 = f1[rb];
+        if constexpr (P2) a2 = f2[rb];
         // ---- the next step's K*, pair i over row blocks 4i .. 4i+3:
         // evaluate (two slots), split, mean terms + the next pair's coordinates
         const int i = rb >> 2, ph = rb & 3;
@@ -285,20 +291,6 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
         if constexpr (SPREAD && (DIAG & 16384)) {
             if (rb < PIECES && loader && (rb < PIECES / 3 || rb < npu))
                 dma16(voff, asrc + rb * kStride, adst + rb * kStride);
-        }
-        if (AHEAD == 2) {
-            a0 = n0;
-            a1 = n1;
-            a2 = n2;
-            if (rb + 2 < 16) {
-                n0 = b0;
-                n1 = b1;
-                n2 = b2;
-            }
-        } else if (rb + 1 < 16) {
-            a0 = b0;
-            a1 = b1;
-            a2 = b2;
         }
     }
     if (!FRESH && !(DIAG & 68)) {
@@ -861,7 +853,9 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 29: SBO_X3_LAUNCH(1, 4119); break;   //   1 product, none of the three
         case 30: SBO_X3_LAUNCH(1, 41008); break;  // variant 3 with the outer sums two blocks behind at every level
         case 31: SBO_X3_LAUNCH(1, 36880); break;  // diagnostics: 1 product, outer sums two blocks behind
-        default: SBO_X3_LAUNCH(1, 8240); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A one block ahead
+        case 32: SBO_X3_LAUNCH(1, 8240); break;   // variant 3 with A fragments one block ahead at every level
+        case 33: SBO_X3_LAUNCH(1, 139312); break;  // variant 3 with A fragments 8 / 3 blocks ahead at one / three products
+        default: SBO_X3_LAUNCH(1, 73776); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead
     }
 #undef SBO_X3_LAUNCH
     return hipGetLastError();

@@ -223,7 +223,7 @@ hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, 
 // tile-list entry of the plan: k-tile index | precision level code << kLevelShift
 constexpr int kLevelShift = 14;
 // the split sweeps that honour the plan's precision levels
-inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30; }
+inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33; }
 inline int x3_layout(int variant) { return (variant == 13 || variant == 14) ? 1 : 0; }
 // The sweep over the plan with the split operand; qx/qy must be readable in
 // whole 128-query blocks (padded to round_up(m, kBN)).  variant: 2 (4-7:
