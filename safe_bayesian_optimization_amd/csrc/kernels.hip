@@ -532,6 +532,16 @@ struct PlanRule {
     // beyond the cache: |k|_2 <= 8 K*max
     __device__ __forceinline__ float kn(int t) const { return t < kPlanD2 ? kns[t] : 3.0f + cexp * d2(t) * 0.999f; }
 
+    // A tile whose largest possible increment (the drop bound by K*max, plus
+    // the larger level rank key) is below bin 0's upper edge: all three of
+    // its increments go to bin 0 with weight <= 2 each (exp2(l + 32) < 2^-8
+    // rounds up to at most 1, plus 1), so the plan books 6 for it without
+    // evaluating the bounds -- most candidate tiles of a row block.
+    __device__ __forceinline__ bool far_tile(int I, int t, float dd) const {
+        const float kf = fmaxf(0.0f, fmaxf(key.x + kLg3, key.y + kLg1));
+        return lgn[tile_start(I) + t].x + cexp * dd * 0.999f - lg_tau + 0.01f + kf < -(float)kBudgetFloor;
+    }
+
     __device__ __forceinline__ void incs(int I, int t, int (&bi)[3], unsigned long long (&w)[3]) const {
         tile_increments(d2(t), kn(t), lgn[tile_start(I) + t], cexp, lg_tau, key, bi, w);
         if (levels != 1) {  // only the whole drop: the first two increments free, the third the whole drop bound
@@ -552,7 +562,12 @@ struct PlanRule {
         const int T = kTilesPerRowBlockStep * (I + 1);
         for (int i = lane; i < kBudgetBins; i += 64) bins[i] = 0ull;
         __builtin_amdgcn_wave_barrier();
+        unsigned long long nfar = 0;
         for (int t = lane; t < T; t += 64) {
+            if (far_tile(I, t, d2(t))) {
+                ++nfar;
+                continue;
+            }
             int bi[3];
             unsigned long long w[3];
             incs(I, t, bi, w);
@@ -560,6 +575,7 @@ struct PlanRule {
             for (int j = 0; j < 3; ++j)
                 if (bi[j] < kBudgetBins - 1) atomicAdd(bins + bi[j], w[j]);
         }
+        if (nfar) atomicAdd(bins, 6ull * nfar);
         __builtin_amdgcn_wave_barrier();
         constexpr int per = (kBudgetBins + 63) / 64;
         unsigned long long v[per], run = 0;
@@ -594,10 +610,15 @@ struct PlanRule {
         const float dd = d2(t);
         int code;
         if (lgn) {
-            int bi[3];
-            unsigned long long w[3];
-            incs(I, t, bi, w);
-            const int spent = (bi[0] <= drop_max) + (bi[1] <= drop_max) + (bi[2] <= drop_max);
+            int spent;
+            if (far_tile(I, t, dd)) {
+                spent = drop_max >= 0 ? 3 : 0;
+            } else {
+                int bi[3];
+                unsigned long long w[3];
+                incs(I, t, bi, w);
+                spent = (bi[0] <= drop_max) + (bi[1] <= drop_max) + (bi[2] <= drop_max);
+            }
             code = spent == 3 ? -1 : (levels == 1 ? spent : (levels > 1 ? levels - 2 : 0));
         } else {
             code = (skip_d2 <= 0.0f || dd <= skip_d2) ? 0 : -1;  // skip_d2 <= 0: dense

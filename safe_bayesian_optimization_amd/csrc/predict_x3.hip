@@ -855,6 +855,11 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 31: SBO_X3_LAUNCH(1, 36880); break;  // diagnostics: 1 product, outer sums two blocks behind
         case 32: SBO_X3_LAUNCH(1, 8240); break;   // variant 3 with A fragments one block ahead at every level
         case 33: SBO_X3_LAUNCH(1, 139312); break;  // variant 3 with A fragments 8 / 3 blocks ahead at one / three products
+        case 34: SBO_X3_LAUNCH(1, 69648); break;  // diagnostics (A 4 ahead): 1 product
+        case 35: SBO_X3_LAUNCH(1, 70160); break;  //   1 product, no step barrier (wrong results)
+        case 36: SBO_X3_LAUNCH(1, 69651); break;  //   1 product, no next-step K*, no A pieces
+        case 37: SBO_X3_LAUNCH(1, 70163); break;  //   and no barrier
+        case 38: SBO_X3_LAUNCH(1, 69655); break;  //   no K*, no A pieces, no outer sums
         default: SBO_X3_LAUNCH(1, 73776); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead
     }
 #undef SBO_X3_LAUNCH

@@ -934,7 +934,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->sweep_groups = (int)value;
             return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
-            SBO_CHECK(value >= 0 && value <= 33, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 33]");
+            SBO_CHECK(value >= 0 && value <= 38, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 38]");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
         case SBO_OPT_TILE_SKIP:
