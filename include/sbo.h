@@ -288,6 +288,12 @@ SBO_API sbo_status sbo_profile_work(sbo_ctx *ctx, double *predict_flops);
  * precision levels (variant 3), one for the f32 sweeps (variants 0, 1);
  * tiles_by_level (may be NULL): the multiplied tiles at six, three, one
  * product(s). */
+/* Diagnostic: with SBO_OPT_KERNEL_VARIANT 39 (the default sweep with phase
+ * stamps, s_memtime; never timed as the product) the summed cycles of every
+ * sweep wave since the last call, cycles[0..11]: step top, half-step body,
+ * item end, vmcnt wait, barrier, whole half-steps, body at six / three / one
+ * product(s), half-steps at six / three / one product(s); then reset. */
+SBO_API sbo_status sbo_debug_x3_stamps(sbo_ctx *ctx, double *cycles, int n);
 SBO_API sbo_status sbo_profile_mfma(sbo_ctx *ctx, double *mfma_flops, int64_t *tiles_by_level /* [3] or NULL */);
 
 #ifdef __cplusplus

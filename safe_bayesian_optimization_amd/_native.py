@@ -29,7 +29,7 @@ EXPORTS = (
     "sbo_fit", "sbo_append", "sbo_num_train", "sbo_predict", "sbo_compute_sets", "sbo_argmax", "sbo_tick",
     "sbo_key_combine", "sbo_find_safety_contour_indices", "sbo_next_subgoal", "sbo_find_contours_external",
     "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
-    "sbo_get_order", "sbo_profile_work", "sbo_profile_mfma", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
+    "sbo_get_order", "sbo_profile_work", "sbo_profile_mfma", "sbo_debug_x3_stamps", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
     "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
 )
 SBO_OPT_INVERSE_BITS = 1
@@ -148,6 +148,8 @@ def lib():
     L.sbo_profile_work.restype = st
     L.sbo_profile_mfma.argtypes = [vp, ctypes.POINTER(dbl), ctypes.POINTER(i64)]
     L.sbo_profile_mfma.restype = st
+    L.sbo_debug_x3_stamps.argtypes = [vp, ctypes.POINTER(dbl), ctypes.c_int]
+    L.sbo_debug_x3_stamps.restype = st
     _lib = L
     return L
 

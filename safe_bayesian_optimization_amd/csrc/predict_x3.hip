@@ -30,7 +30,9 @@
 // the A pieces of stage i+2 in flight has retired them -- the K* of step
 // i+1 is computed during step i, beside its MFMAs.
 #include <cstdint>
+#include <algorithm>
 #include <type_traits>
+#include <vector>
 
 #include "sbo_internal.hpp"
 
@@ -439,6 +441,14 @@ __device__ __forceinline__ void x3w_kstar(const lds_char *pc, float xq, float yq
         }
 }
 
+// Phase stamps of the diagnostic build (DIAG & 262144), per workgroup and
+// wave: cycles in [0] step top (flush, stage), [1] the half-step body,
+// [2] item end, [3] vmcnt wait, [4] barrier, [5] whole half-steps, [6..8] the
+// body by level, [9..11] half-steps by level.  Read by sbo_debug_x3_stamps.
+constexpr int kStampFields = 16;
+constexpr int kStampSlots = 1024 * 8;
+__device__ unsigned long long g_x3_stamps[kStampSlots * kStampFields];
+
 // per staged step: row block, query block, and flags
 struct XStep {
     int I, qb, flags;  // bit 0: second half, bit 1: first step of its item, bit 2: last step, bit 3: valid
@@ -631,10 +641,20 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     };
     int cur = 0;
     bool more = true;
+    constexpr bool STAMP = (DIAG & 262144) != 0;
+    unsigned long long stc[12] = {};
+#define SBO_STAMP(t_)                                                                          \
+    do {                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+    } while (0)
     // one half-step; items are whole tiles, so the steps alternate FRESH
     // (first half: chains from zero) and second halves (which may end an item)
     auto half_step = [&](auto fresh_tag) {
         constexpr bool FRESH = decltype(fresh_tag)::value;
+        unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;
+        if constexpr (STAMP) SBO_STAMP(t0);
         if (FRESH) flush();
         const bool issue = la_k < k1;
         const int nslot = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
@@ -671,6 +691,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
             xq[c] = lds_f(pqn + (qo + 16 * c) * 4);
             yq[c] = lds_f(pqn + (kBN + qo + 16 * c) * 4);
         }
+        if constexpr (STAMP) SBO_STAMP(t1);
         if constexpr (WIDE)
             x3w_half<FRESH, DIAG>(pa, pcn, xq[0], yq[0], lane >> 5, cexp, msc, kb, acc[0], outer[0], nx, mu[0],
                                   voff, a_src, a_dst);
@@ -683,6 +704,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         else
             x3_half<NC, FRESH, DIAG, kPieces>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
                                               a_dst, is_loader, np2);
+        if constexpr (STAMP) SBO_STAMP(t2);
         if (!FRESH && (s0.flags & kLast)) {
             // item done: column sums of V^2 over its rows (lanes l, l+16, l+32,
             // l+48 hold four row quarters of column l&15 of every block)
@@ -715,6 +737,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
                 pend_s[c] = (float)sv;
             }
         }
+        if constexpr (STAMP) SBO_STAMP(t3);
         // retire stage i+1: its queries and coordinates (wave 0) precede its
         // A pieces and were retired one step earlier; leave stage i+2's A in flight
         if ((issue || (DIAG & 16)) && !(DIAG & 2) && is_loader) {
@@ -730,10 +753,23 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        if constexpr (STAMP) SBO_STAMP(t4);
         if constexpr (DIAG & 512)  // timing only: no step barrier (races on the slots)
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         else
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (STAMP) {
+            SBO_STAMP(t5);
+            const int lvs = LEVELS ? s0.lv : 0;
+            stc[0] += t1 - t0;
+            stc[1] += t2 - t1;
+            stc[2] += t3 - t2;
+            stc[3] += t4 - t3;
+            stc[4] += t5 - t4;
+            stc[5] += t5 - t0;
+            stc[6 + lvs] += t2 - t1;
+            stc[9 + lvs] += 1;
+        }
         more = nvalid;
         s0 = s1;
         s1 = s2;
@@ -746,6 +782,13 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     } while (more);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
     flush();
+    if constexpr (STAMP) {
+        const int slot = bid * 8 + lw;
+        if (lane == 0 && slot < kStampSlots)
+#pragma unroll
+            for (int j = 0; j < 12; ++j) g_x3_stamps[(size_t)slot * kStampFields + j] = stc[j];
+    }
+#undef SBO_STAMP
 #undef SBO_X3_STAGE
 #undef SBO_DESC_WINDOW
 #undef SBO_LIST_WINDOW
@@ -816,6 +859,17 @@ hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, 
     return hipGetLastError();
 }
 
+hipError_t read_x3_stamps(double *out, int n) {
+    std::vector<unsigned long long> h((size_t)kStampSlots * kStampFields);
+    hipError_t e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_x3_stamps), h.size() * sizeof(unsigned long long));
+    if (e != hipSuccess) return e;
+    for (int j = 0; j < n; ++j) out[j] = 0.0;
+    for (size_t sl = 0; sl < (size_t)kStampSlots; ++sl)
+        for (int j = 0; j < n && j < kStampFields; ++j) out[j] += (double)h[sl * kStampFields + j];
+    std::fill(h.begin(), h.end(), 0ull);  // reset for the next read
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_x3_stamps), h.data(), h.size() * sizeof(unsigned long long));
+}
+
 hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, const int4 *desc,
                              const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
                              const float *qy, int64_t m, int64_t ldp, float cexp, float m0, float *part, float *mean,
@@ -860,6 +914,7 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 36: SBO_X3_LAUNCH(1, 69651); break;  //   1 product, no next-step K*, no A pieces
         case 37: SBO_X3_LAUNCH(1, 70163); break;  //   and no barrier
         case 38: SBO_X3_LAUNCH(1, 69655); break;  //   no K*, no A pieces, no outer sums
+        case 39: SBO_X3_LAUNCH(1, 335920); break;  // variant 3 with phase stamps (sbo_debug_x3_stamps)
         default: SBO_X3_LAUNCH(1, 73776); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead
     }
 #undef SBO_X3_LAUNCH

@@ -876,6 +876,14 @@ SBO_API sbo_status sbo_profile_work(sbo_ctx *ctx, double *predict_flops) {
     return SBO_OK;
 }
 
+SBO_API sbo_status sbo_debug_x3_stamps(sbo_ctx *ctx, double *cycles, int n) {
+    if (!ctx || !cycles || n <= 0) return SBO_E_INVAL;
+    SBO_HIP(hipSetDevice(ctx->device));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    SBO_HIP(sbo::read_x3_stamps(cycles, n));
+    return SBO_OK;
+}
+
 SBO_API sbo_status sbo_profile_mfma(sbo_ctx *ctx, double *mfma_flops, int64_t *tiles_by_level) {
     if (!ctx || !mfma_flops) return SBO_E_INVAL;
     unsigned long long t[4] = {0, 0, 0, 0};
@@ -934,7 +942,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->sweep_groups = (int)value;
             return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
-            SBO_CHECK(value >= 0 && value <= 38, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 38]");
+            SBO_CHECK(value >= 0 && value <= 39, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 39]");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
         case SBO_OPT_TILE_SKIP:

@@ -223,11 +223,14 @@ hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, 
 // tile-list entry of the plan: k-tile index | precision level code << kLevelShift
 constexpr int kLevelShift = 14;
 // the split sweeps that honour the plan's precision levels
-inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33; }
+inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39; }
 inline int x3_layout(int variant) { return (variant == 13 || variant == 14) ? 1 : 0; }
 // The sweep over the plan with the split operand; qx/qy must be readable in
 // whole 128-query blocks (padded to round_up(m, kBN)).  variant: 2 (4-7:
 // timing diagnostics with parts of the work left out).
+// Diagnostic build (SBO_OPT_KERNEL_VARIANT 39): summed phase cycles of the
+// split sweep since the last read (see g_x3_stamps), then reset.
+hipError_t read_x3_stamps(double *out, int n);
 hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, const int4 *desc,
                              const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
                              const float *qy, int64_t m, int64_t ldp, float cexp, float m0, float *part, float *mean,

@@ -1,0 +1,53 @@
+"""Phase shares of the split sweep from its stamp build (variant 39; diagnostic, GPU).
+
+  python tools/x3_stamps.py --config C4
+Prints the share of wave-cycles per phase and the body cycles per half-step
+by precision level.  Read shares, not lengths: the stamps' waits forbid some
+overlap the real kernel has."""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--config", default="C4")
+    a = p.parse_args()
+    import torch
+    from safe_bayesian_optimization_amd import TerrainMapper, synthetic
+    from safe_bayesian_optimization_amd import _native as N
+    from safe_bayesian_optimization_amd.terrain import CONFIGS
+    n, gw, gh = CONFIGS[a.config]
+    wl = synthetic(n, gw, gh, seed=0)
+    dev = torch.device("cuda:0")
+    t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
+    gm = TerrainMapper(0, wl.hyper)
+    gm.fit(t(wl.x), t(wl.y), t(wl.obs))
+    qx, qy = t(wl.qx), t(wl.qy)
+    lib = N.lib()
+    buf = (ctypes.c_double * 12)()
+    for v in (3, 39):
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, v)
+        gm.tick(qx, qy, wl.beta, wl.f_min)
+    lib.sbo_debug_x3_stamps(gm.ctx.handle, buf, 12)  # reset
+    gm.tick(qx, qy, wl.beta, wl.f_min)
+    lib.sbo_debug_x3_stamps(gm.ctx.handle, buf, 12)
+    c = list(buf)
+    tot = c[5]
+    names = ["step top (flush, stage)", "half-step body", "item end", "vmcnt wait", "barrier"]
+    for i, nm in enumerate(names):
+        print(f"{nm:26s} {100 * c[i] / tot:6.2f} %")
+    hs = c[9] + c[10] + c[11]
+    print(f"half-steps {hs:.0f}, wave-cycles per half-step {tot / max(hs, 1):.0f}")
+    for lv, nm in enumerate(("six", "three", "one")):
+        if c[9 + lv]:
+            print(f"body at {nm:5s} product(s): {c[6 + lv] / c[9 + lv]:7.0f} cycles per half-step ({c[9 + lv]:.0f})")
+
+
+if __name__ == "__main__":
+    main()
