@@ -410,7 +410,9 @@ def test_sweep_partition_and_outer_variant(mapper):
     with pytest.raises(N.SboError):
         gm.set_option(N.SBO_OPT_SWEEP_GROUPS, -1)
     with pytest.raises(N.SboError):
-        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 34)
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 1000)
+    with pytest.raises(N.SboError):
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, -1)
 
 
 @pytest.mark.parametrize("variant", [2, 3, 9, 13])
