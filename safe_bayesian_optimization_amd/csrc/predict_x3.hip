@@ -864,8 +864,14 @@ hipError_t read_x3_stamps(double *out, int n) {
     hipError_t e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_x3_stamps), h.size() * sizeof(unsigned long long));
     if (e != hipSuccess) return e;
     for (int j = 0; j < n; ++j) out[j] = 0.0;
+    // out[0..11]: summed over all waves; out[12 + 12 w + j]: over wave index w of every workgroup
     for (size_t sl = 0; sl < (size_t)kStampSlots; ++sl)
-        for (int j = 0; j < n && j < kStampFields; ++j) out[j] += (double)h[sl * kStampFields + j];
+        for (int j = 0; j < 12; ++j) {
+            const double v = (double)h[sl * kStampFields + j];
+            if (j < n) out[j] += v;
+            const int o = 12 + 12 * (int)(sl % 8) + j;
+            if (o < n) out[o] += v;
+        }
     std::fill(h.begin(), h.end(), 0ull);  // reset for the next read
     return hipMemcpyToSymbol(HIP_SYMBOL(g_x3_stamps), h.data(), h.size() * sizeof(unsigned long long));
 }

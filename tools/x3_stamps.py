@@ -17,6 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--config", default="C4")
+    p.add_argument("--variant", type=int, default=39)
     a = p.parse_args()
     import torch
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
@@ -30,13 +31,13 @@ def main():
     gm.fit(t(wl.x), t(wl.y), t(wl.obs))
     qx, qy = t(wl.qx), t(wl.qy)
     lib = N.lib()
-    buf = (ctypes.c_double * 12)()
-    for v in (3, 39):
+    buf = (ctypes.c_double * 108)()
+    for v in (3, a.variant):
         gm.set_option(N.SBO_OPT_KERNEL_VARIANT, v)
         gm.tick(qx, qy, wl.beta, wl.f_min)
-    lib.sbo_debug_x3_stamps(gm.ctx.handle, buf, 12)  # reset
+    lib.sbo_debug_x3_stamps(gm.ctx.handle, buf, 108)  # reset
     gm.tick(qx, qy, wl.beta, wl.f_min)
-    lib.sbo_debug_x3_stamps(gm.ctx.handle, buf, 12)
+    lib.sbo_debug_x3_stamps(gm.ctx.handle, buf, 108)
     c = list(buf)
     tot = c[5]
     names = ["step top (flush, stage)", "half-step body", "item end", "vmcnt wait", "barrier"]
@@ -47,6 +48,11 @@ def main():
     for lv, nm in enumerate(("six", "three", "one")):
         if c[9 + lv]:
             print(f"body at {nm:5s} product(s): {c[6 + lv] / c[9 + lv]:7.0f} cycles per half-step ({c[9 + lv]:.0f})")
+    print("per wave index: cycles per half-step in step top / body / item end / vmcnt / barrier")
+    for w in range(8):
+        cw = c[12 + 12 * w: 24 + 12 * w]
+        hw = max(cw[9] + cw[10] + cw[11], 1)
+        print(f"  wave {w}: " + " / ".join(f"{cw[i] / hw:6.0f}" for i in range(5)))
 
 
 if __name__ == "__main__":
