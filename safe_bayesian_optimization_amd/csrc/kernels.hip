@@ -742,8 +742,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, const unsigned long long *__restrict__ key,
     const unsigned long long *__restrict__ scan, const unsigned char *__restrict__ thr, int4 *__restrict__ desc,
-    unsigned short *__restrict__ tl, int prod_full, unsigned long long *__restrict__ products) {
-    // products (may be null): [0] += MFMA products, [1], [2] += tiles at level 1, 2
+    unsigned short *__restrict__ tl, int prod_full, unsigned long long *__restrict__ partial) {
+    // partial (may be null): per wave [MFMA products, tiles at level 1, at level 2]
+    // (summed by plan_counts_reduce_kernel: no contended global atomics)
     __shared__ float d2s[kPlanD2], kns[kPlanD2];
     __shared__ float red[4 * kPlanWaves];
     const int64_t qb = blockIdx.x;
@@ -778,19 +779,42 @@ __global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
         }
         if (lane == 0) desc[ne] = make_int4(I, (int)qb, (int)(uint32_t)off, cnt | (int)((off >> 32) << 16));
     }
-    if (products) {
+    if (partial) {
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             prod += __shfl_xor(prod, o);
             nl1 += __shfl_xor(nl1, o);
             nl2 += __shfl_xor(nl2, o);
         }
-        if (lane == 0 && prod) {
-            atomicAdd(products, prod);
-            atomicAdd(products + 1, nl1);
-            atomicAdd(products + 2, nl2);
+        if (lane == 0) {
+            unsigned long long *p = partial + 3 * (qb * kPlanWaves + wave);
+            p[0] = prod;
+            p[1] = nl1;
+            p[2] = nl2;
         }
     }
+}
+
+// One workgroup: the per-wave level counts of plan_write into the profile counters.
+__global__ __launch_bounds__(256) void plan_counts_reduce_kernel(const unsigned long long *__restrict__ partial,
+                                                                 int64_t n, unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long red[3][256];
+    unsigned long long v[3] = {0, 0, 0};
+    for (int64_t i = threadIdx.x; i < n; i += 256)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v[j] += partial[3 * i + j];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) red[j][threadIdx.x] = v[j];
+    __syncthreads();
+    for (int o = 128; o >= 1; o >>= 1) {
+        if ((int)threadIdx.x < o)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) out[j] += red[j][0];
 }
 
 // One thread per sweep workgroup: cut the non-empty item list into P
@@ -1368,7 +1392,7 @@ hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int6
 
 namespace {
 struct PlanLayout {
-    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes, wkey, wscan;
+    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes, wkey, wscan, lvcnt;
     // XCD-interleaved order (P % 8 == 0): the sweep reads desc2 / tl2 / seg2
     bool xcd;
     size_t xseg, pos_of, cnt2, off2, desc2, tl2, seg2, temp2, temp2_bytes;
@@ -1392,6 +1416,7 @@ PlanLayout plan_layout(int64_t nI, int64_t nQ, int P) {
     L.thr = take((size_t)items);
     L.wkey = take(8 * (size_t)items);
     L.wscan = take(8 * (size_t)items);
+    L.lvcnt = take(8 * 3 * (size_t)(nQ * kPlanWaves));
     L.desc = take(16 * (size_t)(items + 2 * kDescWindow));
     L.tl = take(2 * (size_t)(cap + 2 * kListWindow));
     L.seg = take(4 * (size_t)(P + 1));
@@ -1473,7 +1498,10 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn,
                        levels, make_float2(skip.lvl_key[0], skip.lvl_key[1]), nI, nQ, qx, qy,
                        m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, key, scan, thr, desc, tl, skip.prod_full,
-                       tiles_done ? tiles_done + 1 : nullptr);
+                       tiles_done ? reinterpret_cast<unsigned long long *>(w + L.lvcnt) : nullptr);
+    if (tiles_done)
+        hipLaunchKernelGGL(plan_counts_reduce_kernel, dim3(1), dim3(256), 0, s,
+                           reinterpret_cast<const unsigned long long *>(w + L.lvcnt), nQ * kPlanWaves, tiles_done + 1);
     if (!L.xcd) {
         hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done, wkey,
                            wscan, nI, nQ);
