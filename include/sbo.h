@@ -176,6 +176,28 @@ SBO_API sbo_status sbo_subgoal(sbo_ctx *ctx, const double *Dx, const double *Dy,
                                int height_cells, double goal_x, double goal_y, int64_t *index,
                                uint32_t flags);
 
+/* Post-selection geometry, host, f64.  Rings are the
+ * exterior ring as Boost stores it: x[] / y[], closing point included.
+ * sbo_polygon_correct: bg::correct for polygon<point, false, true> (the
+ * node's :682): closes an open ring (needs cap >= n + 1) and reverses a
+ * clockwise one; *n_out = new length.
+ * sbo_polydist: polydist (src/libraries/polygeom_lib.cpp:401-474) including
+ * its nearest-vertex quirk (:439-440); SBO_E_EMPTY for fewer than 2 ring
+ * points, with the reference's intended dist 1e8 and point (0, 0).
+ * sbo_point_within: bg::within(point, polygon) (:657), 1 strictly inside,
+ * 0 outside or on the boundary.
+ * sbo_project_subgoal: the node's step after GetNextSubgoal (:651-704): the
+ * goal when within the ring (returns 1); else (Dx, Dy)[subgoal_index]
+ * projected by polydist onto the corrected ring (returns 0); -1 when there
+ * is no subgoal (index < 0) or the ring is empty. */
+SBO_API sbo_status sbo_polygon_correct(double *rx, double *ry, int64_t n, int64_t cap, int64_t *n_out);
+SBO_API sbo_status sbo_polydist(const double *rx, const double *ry, int64_t n, double px, double py,
+                                double *proj_x, double *proj_y, double *dist);
+SBO_API int sbo_point_within(const double *rx, const double *ry, int64_t n, double px, double py);
+SBO_API int sbo_project_subgoal(const double *rx, const double *ry, int64_t n, double goal_x, double goal_y,
+                                int64_t subgoal_index, const double *Dx, const double *Dy, int64_t m,
+                                double *out_x, double *out_y, double *out_dist);
+
 /* Fitted predictive state as one device blob (fit on one
  * rank, broadcast the operand to the others instead of refitting there).
  * sbo_state_bytes gives the size (the packed sf2 L^-1 tiles dominate:

@@ -183,6 +183,23 @@ public:
                                      terrain_width_cells_, terrain_height_cells_, goal_.first, goal_.second);
     }
 
+    // The node's subgoal step (:651-704): the goal when it lies inside the
+    // eroded safe ring, else the frontier subgoal projected by polydist onto
+    // it.  ring_x/ring_y: the polygon's outer() (closing point included).
+    // Returns 1 (goal), 0 (projected) or -1 (no subgoal); *xy, *dist out.
+    int ProjectSubgoal(const std::vector<double> &ring_x, const std::vector<double> &ring_y, double *x, double *y,
+                       double *dist) const {
+        const int64_t n = (int64_t)ring_x.size();
+        if (sbo_point_within(ring_x.data(), ring_y.data(), n, goal_.first, goal_.second)) {  // no frontier needed
+            *x = goal_.first;
+            *y = goal_.second;
+            *dist = 0.0;
+            return 1;
+        }
+        return sbo_project_subgoal(ring_x.data(), ring_y.data(), (int64_t)ring_x.size(), goal_.first, goal_.second,
+                                   GetNextSubgoal(), Dx_.data(), Dy_.data(), (int64_t)Dx_.size(), x, y, dist);
+    }
+
     const std::vector<double> &Qlo() const { return Qlo_; }
     const std::vector<double> &Qhi() const { return Qhi_; }
     const std::vector<uint8_t> &S() const { return S_; }

@@ -216,3 +216,84 @@ def next_subgoal(Dx, Dy, lo, hi, safe, width, height, gx=0.0, gy=0.0):
     return int(lib().orc_next_subgoal(_c(Dx, np.float64), _c(Dy, np.float64), _c(lo, np.float64),
                                       _c(hi, np.float64), _c(safe, np.uint8), len(Dx),
                                       int(width), int(height), float(gx), float(gy)))
+
+
+# ------------------------------------------ post-selection geometry (8(f)4)
+# Pure-Python restatements (IEEE double, no FMA: the same roundings as the
+# reference's plain C++ double arithmetic).  Small rings only.
+def ring_area2(x, y):
+    """Twice the signed area of a closed ring (> 0 counter-clockwise)."""
+    s = 0.0
+    for i in range(len(x) - 1):
+        s += float(x[i]) * float(y[i + 1]) - float(x[i + 1]) * float(y[i])
+    return s
+
+
+def polygon_correct(x, y):
+    """bg::correct for polygon<point, false, true> (node :682): close an open
+    ring of > 2 points, reverse a clockwise one."""
+    x = [float(v) for v in x]
+    y = [float(v) for v in y]
+    if len(x) > 2 and (x[0] != x[-1] or y[0] != y[-1]):
+        x.append(x[0])
+        y.append(y[0])
+    if ring_area2(x, y) < 0.0:
+        x.reverse()
+        y.reverse()
+    return np.array(x, np.float64), np.array(y, np.float64)
+
+
+def polydist(x, y, px, py):
+    """polydist, src/libraries/polygeom_lib.cpp:401-474, line by line:
+    closing point dropped (:431), dxy/diff_norm with the wrap and 0 -> 1
+    (:434-447), w clamped to [0, 1] and the candidate blended from
+    VertexList[i] and VertexListRolled[i] == VertexList[i] (:439-440, :453-461),
+    first minimum of the distances (:465-468).  None for an empty ring (the
+    reference's :420-431 ends in pop_back on an empty vector)."""
+    import math
+    if len(x) <= 1:
+        return None
+    V = [(float(x[i]), float(y[i])) for i in range(len(x) - 1)]
+    n = len(V)
+    dxy = [(0.0, 0.0)] * n
+    dn = [0.0] * n
+    for i in range(n):
+        j = (i + 1) % n
+        dxy[j] = (V[j][0] - V[i][0], V[j][1] - V[i][1])
+        d = math.sqrt(dxy[j][0] * dxy[j][0] + dxy[j][1] * dxy[j][1])
+        dn[j] = 1.0 if d == 0.0 else d
+    px, py = float(px), float(py)
+    best = None
+    for i in range(n):
+        n2 = dn[i] * dn[i]
+        wt = (px - V[i][0]) * (dxy[i][0] / n2) + (py - V[i][1]) * (dxy[i][1] / n2)
+        w = max(min(wt, 1.0), 0.0)
+        cx = (1 - w) * V[i][0] + w * V[i][0]
+        cy = (1 - w) * V[i][1] + w * V[i][1]
+        ex, ey = px - cx, py - cy
+        d = math.sqrt(ex * ex + ey * ey)
+        if best is None or d < best[2]:
+            best = (cx, cy, d)
+    return best
+
+
+def point_within(x, y, px, py):
+    """bg::within(point, polygon) (node :657): winding number, boundary -> 0."""
+    n = len(x)
+    if n < 3:
+        return 0
+    wn = 0
+    for i in range(n):
+        j = (i + 1) % n
+        ax, ay, bx, by = float(x[i]), float(y[i]), float(x[j]), float(y[j])
+        if ax == bx and ay == by:
+            continue
+        s = (bx - ax) * (py - ay) - (by - ay) * (px - ax)
+        if s == 0.0 and min(ax, bx) <= px <= max(ax, bx) and min(ay, by) <= py <= max(ay, by):
+            return 0
+        if ay <= py:
+            if by > py and s > 0.0:
+                wn += 1
+        elif by <= py and s < 0.0:
+            wn -= 1
+    return int(wn != 0)

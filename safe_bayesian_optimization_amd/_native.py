@@ -31,6 +31,7 @@ EXPORTS = (
     "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
     "sbo_get_order", "sbo_profile_work", "sbo_profile_mfma", "sbo_debug_x3_stamps", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
     "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
+    "sbo_polygon_correct", "sbo_polydist", "sbo_point_within", "sbo_project_subgoal",
 )
 SBO_OPT_INVERSE_BITS = 1
 SBO_OPT_SPATIAL_ORDER = 2
@@ -150,6 +151,15 @@ def lib():
     L.sbo_profile_mfma.restype = st
     L.sbo_debug_x3_stamps.argtypes = [vp, ctypes.POINTER(dbl), ctypes.c_int]
     L.sbo_debug_x3_stamps.restype = st
+    pd = ctypes.POINTER(dbl)
+    L.sbo_polygon_correct.argtypes = [vp, vp, i64, i64, ctypes.POINTER(i64)]
+    L.sbo_polygon_correct.restype = st
+    L.sbo_polydist.argtypes = [vp, vp, i64, dbl, dbl, pd, pd, pd]
+    L.sbo_polydist.restype = st
+    L.sbo_point_within.argtypes = [vp, vp, i64, dbl, dbl]
+    L.sbo_point_within.restype = ctypes.c_int
+    L.sbo_project_subgoal.argtypes = [vp, vp, i64, dbl, dbl, i64, vp, vp, i64, pd, pd, pd]
+    L.sbo_project_subgoal.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -153,3 +153,51 @@ def next_subgoal(Dx, Dy, lo, hi, safe, width: int, height: int, gx: float = 0.0,
     safe = c(safe, np.uint8)
     return int(N.lib().sbo_next_subgoal(_ptr(Dx), _ptr(Dy), _ptr(lo), _ptr(hi), _ptr(safe), Dx.size, int(width),
                                         int(height), float(gx), float(gy)))
+
+
+# ---- post-selection geometry (csrc/polygeom.cpp) ----------
+def _f64(a):
+    return np.ascontiguousarray(a, np.float64)
+
+
+def polygon_correct(rx, ry):
+    """bg::correct of the node's ring copy (:676-682): returns the closed,
+    counter-clockwise ring as new arrays."""
+    n = len(rx)
+    cx = np.zeros(n + 1, np.float64)
+    cy = np.zeros(n + 1, np.float64)
+    cx[:n] = rx
+    cy[:n] = ry
+    out = ctypes.c_int64(0)
+    N.check(N.lib().sbo_polygon_correct(_ptr(cx), _ptr(cy), n, n + 1, ctypes.byref(out)))
+    return cx[:out.value].copy(), cy[:out.value].copy()
+
+
+def polydist(rx, ry, px: float, py: float, status: bool = False):
+    """polydist (src/libraries/polygeom_lib.cpp:401-474) -> (x, y, dist);
+    with status=True the sbo_status is appended instead of raised."""
+    rx, ry = _f64(rx), _f64(ry)
+    ox, oy, od = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    st = N.lib().sbo_polydist(_ptr(rx), _ptr(ry), rx.size, float(px), float(py), ctypes.byref(ox),
+                              ctypes.byref(oy), ctypes.byref(od))
+    if status:
+        return ox.value, oy.value, od.value, int(st)
+    N.check(st)
+    return ox.value, oy.value, od.value
+
+
+def point_within(rx, ry, px: float, py: float) -> int:
+    """bg::within(point, polygon) (:657): 1 strictly inside, else 0."""
+    rx, ry = _f64(rx), _f64(ry)
+    return int(N.lib().sbo_point_within(_ptr(rx), _ptr(ry), rx.size, float(px), float(py)))
+
+
+def project_subgoal(rx, ry, goal, subgoal_index: int, Dx, Dy):
+    """The node's subgoal step after GetNextSubgoal (:651-704) ->
+    (code, x, y, dist): code 1 = goal used, 0 = projected frontier point, -1 = none."""
+    rx, ry, Dx, Dy = _f64(rx), _f64(ry), _f64(Dx), _f64(Dy)
+    ox, oy, od = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    code = N.lib().sbo_project_subgoal(_ptr(rx), _ptr(ry), rx.size, float(goal[0]), float(goal[1]),
+                                       int(subgoal_index), _ptr(Dx), _ptr(Dy), Dx.size, ctypes.byref(ox),
+                                       ctypes.byref(oy), ctypes.byref(od))
+    return int(code), ox.value, oy.value, od.value
