@@ -274,10 +274,10 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * walking one tile-balanced range of the tick's plan; 0 = default (one per
  * CU).  Results do not depend on it (bitwise). */
 #define SBO_OPT_SWEEP_GROUPS 6
-/* SBO_OPT_SKIP_BUDGET (B in [10, 60], default 22): the automatic K* cutoff
+/* SBO_OPT_SKIP_BUDGET (B in [10, 60], default 20): the automatic K* cutoff
  * (SBO_OPT_TILE_SKIP = -1) keeps its worst-case error below 2^-B sf2 on any
- * variance and 2^-B sf2^(1/2) on any mean (2^-22 = 2.4e-7: under 3 % of the
- * 1e-5 contract; the measured effect at B = 20..27 is below the f32
+ * variance and 2^-B sf2^(1/2) on any mean (2^-20 = 9.5e-7: under 10 % of the
+ * 1e-5 contract; the measured effect at B = 18..27 is below the f32
  * rounding of the sweep itself).  Takes effect at the next sbo_fit /
  * sbo_append. */
 #define SBO_OPT_SKIP_BUDGET 7

@@ -100,7 +100,7 @@ struct sbo_ctx {
     int auto_skip_mean_log2 = 160;  // auto cutoff the last row block keeps for the mean
     float lg_tau_v = -1000.0f;   // log2 of each row block's |dV_I|_2 budget (tile-norm test)
     sbo::DevBuf tile_lgn;        // per packed tile: log2 of its two 2-norm gain bounds (float2, auto cutoff)
-    int skip_budget = 22;        // SBO_OPT_SKIP_BUDGET: the auto cutoff keeps the skip error below 2^-B
+    int skip_budget = 20;        // SBO_OPT_SKIP_BUDGET: the auto cutoff keeps the skip error below 2^-B
     double max_row_l1 = 0.0;     // max_i sum_j |A_ij|, A = sf2 L^-1
     double alpha_l1 = 0.0;       // sum_j |sf2 alpha_j|
     std::vector<int64_t> order;  // internal row -> caller's training index

@@ -338,7 +338,7 @@ def test_tile_skip_exact_and_bounded(dev, mapper):
     mu, sd and the key bitwise identical to the dense sweep.  Cutoff 2^-64:
     at most 1 ulp on a vanishing fraction of points.  Auto cutoff (default):
     within its stated error budget (2^-B sf2 on sigma^2, 2^-B sf on mu, B =
-    SBO_OPT_SKIP_BUDGET, default 22; also checked at B = 27)
+    SBO_OPT_SKIP_BUDGET, default 20; also checked at B = 27)
     of the dense sweep, same argmax."""
     wl = synthetic(8192, 200, 160, seed=21)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
@@ -362,14 +362,14 @@ def test_tile_skip_exact_and_bounded(dev, mapper):
         assert dmu <= 2.0 ** -B + 2 * ulp * np.abs(res[0][0]).max()   # f32 output rounding on top
         assert dvar <= 2.0 ** -B + 4 * ulp
         assert r[2] == res[0][2]
-    within(res[-1], 22)
+    within(res[-1], 20)
     gm.set_option(N.SBO_OPT_SKIP_BUDGET, 27)          # a stricter budget, refit: a larger L
     gm.fit(wl.x, wl.y, wl.obs)
     out = dict(mu=np.empty(m, np.float32), sd=np.empty(m, np.float32))
     k = gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
     assert gm.skip_info()[0] > L
     within((out["mu"], out["sd"], k.idx, k.score), 27)
-    gm.set_option(N.SBO_OPT_SKIP_BUDGET, 22)
+    gm.set_option(N.SBO_OPT_SKIP_BUDGET, 20)
     assert np.array_equal(res[0][0], res[160][0]) and np.array_equal(res[0][1], res[160][1])
     assert res[0][2:] == res[160][2:]
     for a, b in ((res[0][0], res[64][0]), (res[0][1], res[64][1])):
@@ -644,7 +644,7 @@ def test_precision_levels(mapper):
     instead of six, charged to the same error budget as the skipped tiles:
     the issued-product counter is 6 l0 + 3 l1 + l2 of the per-level tile
     counts, both levels occur on a spread-out workload, and the result stays
-    within the budget (2^-22 sf2 on sigma^2) of the all-six-products sweep
+    within the budget (2^-20 sf2 on sigma^2) of the all-six-products sweep
     (variant 22) -- itself within the budget of the dense sweep."""
     wl = synthetic(8192, 200, 160, seed=21)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
@@ -674,6 +674,6 @@ def test_precision_levels(mapper):
     ulp = np.finfo(np.float32).eps
     dvar = np.abs(res[3][1].astype(np.float64) ** 2 - res[22][1].astype(np.float64) ** 2).max()
     dmu = np.abs(res[3][0].astype(np.float64) - res[22][0]).max()
-    assert dvar <= 2 * 2.0 ** -22 + 4 * ulp
-    assert dmu <= 2 * 2.0 ** -22 + 2 * ulp * np.abs(res[22][0]).max()
+    assert dvar <= 2 * 2.0 ** -20 + 4 * ulp
+    assert dmu <= 2 * 2.0 ** -20 + 2 * ulp * np.abs(res[22][0]).max()
     assert res[3][2] == res[22][2]
