@@ -2,29 +2,43 @@
 
 One "step" = one planning tick over this rank's shard of the grid (SURVEY.md
 3.1 without ROS): the fused predictive sweep (K* generated in registers,
-V = sf2 L^-1 K*^T on f32 MFMA, mean alongside), ComputeSets in f64, the masked
-argmax of the confidence width over the safe set, and the cross-rank key
-reduction (one RCCL all-gather of 16-byte keys when N > 1).  Inputs (query
-coordinates) are resident in HBM before timing starts; mu/sd/lo/hi/S are
-written to HBM every step.  The fit (RBF fill + rocSOLVER potrf + dtrtri +
-operand pack) runs once, replicated on every rank, and is reported separately.
+V = sf2 L^-1 K*^T on bf16 MFMA with three-way split operands and f32
+accumulation, the mean alongside), ComputeSets in f64, the masked argmax of
+the confidence width over the safe set, and the cross-rank key exchange (one
+RCCL all-gather of 16-byte keys when N > 1).  Inputs (query coordinates) are
+resident in HBM before timing starts; mu/sd/lo/hi/S are written to HBM every
+step.  The fit (RBF fill + rocSOLVER potrf + dtrtri + operand pack) runs
+once, replicated on every rank, and is reported separately.
 
 Default workload = BASELINE.json configs[3] (C4: N=16384, 1000x1000 grid),
 the north-star target size, on 1 GPU; with --gpus P the same 10^6-point grid
-is split into P contiguous row blocks (strong scaling).  --config C5 runs the
-streaming loop instead (configs[4]: 50 iterations, N 1000 -> 8000 by
-incremental Cholesky appends, 512x512 grid, 1 GPU): a step is one append +
-one tick.
+is split into P contiguous, cost-balanced row blocks (strong scaling).
+--config C5 runs the streaming loop instead (configs[4]: 50 iterations, N
+1000 -> 8000 by incremental Cholesky appends, 512x512 grid, 1 GPU): a step is
+one append + one tick.
+
+At N = 1 the same JSON line also carries two regimes measured in the same
+run (``regimes``): the C4 sweep with tile skipping off (executed work = the
+dense N^2 M of SURVEY.md 8(d)) and the lpsc.yaml stress box
+([0, 1] x [0, 2.5], config/lpsc.yaml:32-33) where almost nothing can be
+skipped -- so the algorithmic speed-up (skipping) and the hardware speed-up
+(GPU vs the dense CPU path) are reported apart.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
-  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+  (--gpus N > 1 without WORLD_SIZE launches N ranks itself through
+   torch.distributed.run on 127.0.0.1; the driver's own
+   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+   is accepted as is)
 """
+
 from __future__ import annotations
 
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -43,7 +57,8 @@ DATA = "synthetic (SplitMix64 smooth field + N(0,sn2) noise in BASELINE config s
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU); > 1 without WORLD_SIZE launches them itself")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
@@ -56,6 +71,11 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-outputs", action="store_true", help="skip writing mu/sd/lo/hi/S (argmax only)")
+    p.add_argument("--no-regimes", action="store_true",
+                   help="N = 1: skip the dense (no tile skipping) and lpsc stress-box measurements")
+    p.add_argument("--regime-steps", type=int, default=2, help="timed ticks per regime (after one warmup)")
+    p.add_argument("--launch-check", action="store_true",
+                   help="CPU rehearsal of the multi-rank path (gloo): launcher, shard cut broadcast, key all-gather")
     p.add_argument("--variant", type=int, default=3,
                    help="predictive kernel (SBO_OPT_KERNEL_VARIANT): 3 split-operand bf16 sweep (default), 0 f32 MFMA")
     return p.parse_args()
@@ -81,14 +101,39 @@ class Prof:
                     predict_flops=w.value, mfma_flops=mf.value, tiles_by_level=list(lv))
 
 
+def _free_port():
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch(a):
+    """--gpus N > 1 without a launcher: start N ranks (one process per GPU)
+    through torch.distributed.run on 127.0.0.1 and return its exit code.  No
+    GPU call has been made in this process (only the children touch it)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # RCCL on this host needs dmabuf IPC
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
-    import torch
-    import torch.distributed as dist
-
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
+        return launch(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus is not None and a.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.launch_check:
+        return run_launch_check(a, world, rank)
+    import torch
+    import torch.distributed as dist
+
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
@@ -108,6 +153,53 @@ def main():
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
+    return 0
+
+
+def dist_info(backend):
+    """What the collective actually saw (not what was asked for)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+                "collective": "all_gather_into_tensor of 16-byte (f64 score, i64 index) keys, one per tick"}
+    return {"world_size": 1, "backend": None, "collective": None}
+
+
+def run_launch_check(a, world, rank):
+    """The multi-rank path without a GPU (gloo on CPU tensors): the same cut
+    broadcast and key all-gather the GPU ranks run, on synthetic per-query
+    costs and scores; rank 0 prints a JSON line with what the ranks saw."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from safe_bayesian_optimization_amd.dist import allreduce_key, balanced_cuts, combine_keys
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    m = 1 << 16
+    rng = np.random.default_rng(123)
+    cost = rng.uniform(0.5, 2.0, m)
+    score = np.round(rng.uniform(0.0, 4.0, m), 2)   # ties across shards
+    cuts = torch.tensor(balanced_cuts(cost, world) if rank == 0 else [0] * (world + 1), dtype=torch.int64)
+    if world > 1:
+        dist.broadcast(cuts, 0)
+    lo, hi = int(cuts[rank]), int(cuts[rank + 1])
+    j = int(np.argmax(score[lo:hi])) if hi > lo else -1
+    s = float(score[lo + j]) if j >= 0 else 0.0
+    key = torch.tensor([np.array([s]).view(np.int64)[0], lo + j if j >= 0 else -1], dtype=torch.int64)
+    best = allreduce_key(key)
+    ok = best == combine_keys([(float(score.max()), int(np.argmax(score)))])
+    info = dist_info(a.backend)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "grid-points/s", "n_gpus": world,
+                          "launch_check": True, "argmax_matches_global": bool(ok), "cuts": [int(c) for c in cuts],
+                          "config": {"workload": "launch-check", "parallelism": f"m-shard{world}" if world > 1
+                                     else "single"}, **info}), flush=True)
+    return 0 if ok else 1
 
 
 def _max_over_ranks(vals, dev, world, backend):
@@ -247,6 +339,7 @@ def run_sweep(a, dev, world, rank):
     mfma_flops_launch = pr["mfma_flops"] / max(pr["predict_launches"], 1)
     levels_launch = [x / max(pr["predict_launches"], 1) for x in pr["tiles_by_level"]]
     elapsed, pred_ms_max = _max_over_ranks([elapsed, pred_ms], dev, world, a.backend)
+    winfo = dist_info(a.backend)
     if rank != 0:
         return None
 
@@ -278,10 +371,24 @@ def run_sweep(a, dev, world, rank):
                    "how": "sbo_subgoal: device raster/owner map, host border follow of the w x h image"}
     cpu = cpu_baseline(gm, wl, a.cpu_seconds) if world == 1 and not a.no_cpu else None
     traffic, traffic_src = pmc_traffic(a.config, n, m_total, m)
+    regimes = None
+    if world == 1 and not a.no_regimes:
+        regimes = {"dense": run_regime_dense(a, gm, prof, step, n, m),
+                   "lpsc_stress_box": run_regime_stress(a, gm, prof, dev, n, gw, gh)}
+    if cpu is not None:
+        cpu["gpu_over_cpu"] = value / cpu["value"]
+        if regimes:
+            d = regimes["dense"]
+            cpu["gpu_dense_over_cpu"] = d["value"] / cpu["value"]
+            cpu["gpu_default_over_gpu_dense"] = value / d["value"]
+            cpu["ratios"] = ("gpu_dense_over_cpu: hardware (the same dense algorithm on both); "
+                             "gpu_default_over_gpu_dense: algorithmic (error-budgeted tile skipping and "
+                             "precision levels); gpu_over_cpu = their product")
     return {
         "metric": METRIC, "value": value, "unit": "grid-points/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": a.scaling,
         "vs_baseline": None, "dtype": dtype_of(a.variant), "data": DATA,
+        "world_size": winfo["world_size"], "backend": winfo["backend"], "collective": winfo["collective"],
         "config": {"workload": a.config, "n_train": n, "grid": [gw, gh], "M": m_total, "M_per_rank": m,
                    "beta": wl.beta, "f_min": round(wl.f_min, 6),
                    "hyper": [wl.hyper.length_scale, wl.hyper.sigma_f, wl.hyper.noise_level],
@@ -292,6 +399,7 @@ def run_sweep(a, dev, world, rank):
                          traffic=traffic,
                          traffic_source=traffic_src, avg_launch_ms=pred_ms, max_rank_launch_ms=pred_ms_max,
                          dense_flops_per_launch=dense_flops_launch,
+                         executed_fraction_of_dense=exec_flops_launch / dense_flops_launch,
                          dense_equivalent_tflops=dense_flops_launch / (pred_ms * 1e-3) / 1e12),
         "fill_roofline": {"kernel": "rbf_fill_kernel", "bound": "hbm", "achieved": fill_gbs, "peak": PEAK_HBM_GBS,
                           "unit": "GB/s", "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None,
@@ -300,7 +408,81 @@ def run_sweep(a, dev, world, rank):
         "argmax": {"index": best[1], "score": best[0]},
         "subgoal": subgoal,
         "cpu_baseline": cpu,
+        "regimes": regimes,
     }
+
+
+def _timed_ticks(prof, step, steps):
+    """One warmup tick, then `steps` ticks: (wall s per tick, sweep counters per launch)."""
+    import torch
+    step()
+    prof.reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    pr = prof.read()
+    prof.reset(False)
+    k = max(pr["predict_launches"], 1)
+    return wall, pr["predict_ms"] / k, pr["predict_flops"] / k, pr["mfma_flops"] / k, [x / k for x in pr["tiles_by_level"]]
+
+
+def _regime_line(a, name, how, m, n, wall, ms, flops, mflops, levels, extra=None):
+    dense = float(n) * float(n) * m
+    r = {"what": how, "value": m / wall, "unit": "grid-points/s", "ms_per_step": wall * 1e3,
+         "roofline": dict(predict_roofline(a.variant, flops, ms, mflops, levels), avg_launch_ms=ms,
+                          dense_flops_per_launch=dense, executed_fraction_of_dense=flops / dense,
+                          dense_equivalent_tflops=dense / (ms * 1e-3) / 1e12)}
+    if extra:
+        r.update(extra)
+    return r
+
+
+def run_regime_dense(a, gm, prof, step, n, m):
+    """The same C4 tick with tile skipping off (SBO_OPT_TILE_SKIP = 0): every
+    k-tile of the lower triangle multiplied at six bf16 products, so executed
+    work is the dense N^2 flop per grid point of SURVEY.md 8(d)."""
+    from safe_bayesian_optimization_amd import _native as N
+    gm.set_option(N.SBO_OPT_TILE_SKIP, 0)
+    try:
+        res = _timed_ticks(prof, step, a.regime_steps)
+    finally:
+        gm.set_option(N.SBO_OPT_TILE_SKIP, -1)
+    return _regime_line(a, "dense", f"{a.config} tick, SBO_OPT_TILE_SKIP=0 (no skipping, all tiles at six products)",
+                        m, n, *res)
+
+
+def run_regime_stress(a, gm, prof, dev, n, gw, gh):
+    """SURVEY.md 8(d) stress variant: the same N and grid size on the mapping
+    node's own box [0, 1] x [0, 2.5] (config/lpsc.yaml:32-33), default plan:
+    with l = 0.4 almost no tile is negligible.  Refits the context."""
+    import torch
+
+    from safe_bayesian_optimization_amd import _native as N
+    from safe_bayesian_optimization_amd.terrain import synthetic_box
+    wl = synthetic_box(n, gw, gh, seed=0, name=f"{a.config}-lpsc-box")
+    f32 = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gm.fit(f32(wl.x), f32(wl.y), f32(wl.obs))
+    torch.cuda.synchronize()
+    fit_ms = (time.perf_counter() - t0) * 1e3
+    qx, qy = f32(wl.qx), f32(wl.qy)
+    m = qx.numel()
+    key = torch.empty(2, dtype=torch.int64, device=dev)
+    outs = dict(mu=torch.empty(m, dtype=torch.float32, device=dev), sd=torch.empty(m, dtype=torch.float32, device=dev),
+                lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
+                safe=torch.empty(m, dtype=torch.uint8, device=dev))
+
+    def step():
+        gm.tick(qx, qy, wl.beta, wl.f_min, score=N.SCORE_WIDTH, outputs=outs, key_out=key, async_=True)
+
+    res = _timed_ticks(prof, step, a.regime_steps)
+    return _regime_line(a, "lpsc_stress_box", "N points and the grid on x [0, 1] x y [0, 2.5] (config/lpsc.yaml:32-33), "
+                        "default plan (variant 3, auto cutoff, B = 20)", m, n, *res,
+                        extra={"fit_ms": fit_ms, "kstar_cutoff_log2": gm.skip_info()[0]})
 
 
 def dtype_of(variant):
@@ -420,38 +602,56 @@ def pmc_traffic(config, n, m_total, m):
         return None, None
 
 
+def host_cores():
+    """Cores the CPU comparator may use: `nproc` (the CPUs this process may
+    run on, honouring OMP_NUM_THREADS as GNU nproc does), and the machine's
+    total beside it."""
+    try:
+        n = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=10).stdout.strip())
+    except Exception:
+        n = len(os.sched_getaffinity(0))
+    return max(1, n), os.cpu_count() or n
+
+
 def cpu_baseline(gm, wl, budget_s):
-    """The oracle's f32 predictive path (dense blocked TRSM, OpenMP) +
-    ComputeSets + argmax on a contiguous sample of the grid, given the device
-    factor; points/s extrapolated linearly (the M axis is embarrassingly parallel)."""
+    """The Eigen-class dense CPU path on the host's cores: K*^T per query block
+    (numpy), mu by sgemv, V = L^-1 K*^T by OpenBLAS strsm (level-3, `nproc`
+    threads), var, ComputeSets + argmax (oracle C), given the device's own
+    factor; timed on a bounded contiguous sample of the grid and extrapolated
+    linearly (the M axis is embarrassingly parallel).  Dense: it does not skip
+    tiles -- the gpu_dense_over_cpu ratio compares like with like."""
+    from threadpoolctl import threadpool_info, threadpool_limits
+
     from oracle import oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads, total = host_cores()
     O.set_threads(threads)
     L, alpha = gm.factor()
     o = gm.order()                           # internal training order of the factor
-    Lcm = np.ascontiguousarray(L.T)          # column-major buffer of the lower factor
-    del L
     h = wl.hyper
-    x, y = wl.x.astype(np.float32)[o], wl.y.astype(np.float32)[o]
+    bp = O.BlasPredictor(L, alpha, wl.x.astype(np.float32)[o], wl.y.astype(np.float32)[o], h.length_scale, h.sf2,
+                         h.prior_mean)
+    del L
 
     def run(k):
-        qx = wl.qx[:k].astype(np.float32)
-        qy = wl.qy[:k].astype(np.float32)
         t0 = time.perf_counter()
-        mu, var = O.predict_f32(Lcm, alpha, x, y, qx, qy, h.length_scale, h.sf2, h.prior_mean)
-        lo_, hi_, s_ = O.compute_sets(mu, np.sqrt(np.maximum(var, 0)), wl.beta, wl.f_min)
-        O.argmax(hi_ - lo_, s_)
+        bp.tick(wl.qx[:k], wl.qy[:k], wl.beta, wl.f_min)
         return time.perf_counter() - t0
 
-    k = 64 * threads
-    t = run(k)
-    k2 = int(min(wl.qx.size, max(k, k * max(budget_s - t, 0.0) / max(t, 1e-6))))
-    k2 = max(64, (k2 // 64) * 64)
-    t2 = run(k2)
-    return {"value": k2 / t2, "unit": "grid-points/s", "cores": threads, "kind": "port",
-            "sample": f"{k2} contiguous grid points of {wl.name} (N={wl.x.size}), f32 dense blocked TRSM predictive "
-                      f"+ ComputeSets + argmax (oracle, OpenMP), given the device L/alpha; {t2:.1f} s wall"}
+    with threadpool_limits(limits=threads, user_api="blas"):
+        blas = [f"{i.get('internal_api')} {i.get('version')} ({i.get('architecture')}, {i.get('num_threads')} threads)"
+                for i in threadpool_info() if i.get("user_api") == "blas"]
+        k = bp.block
+        run(k)                               # warm: thread pool, page-in of L
+        t = run(k)
+        k2 = int(min(wl.qx.size, max(k, k * max(budget_s - 2 * t, 0.0) / max(t, 1e-6))))
+        k2 = max(k, (k2 // k) * k)
+        t2 = run(k2)
+    return {"value": k2 / t2, "unit": "grid-points/s", "cores": threads, "host_cpus": total, "kind": "port",
+            "blas": blas[0] if blas else None,
+            "sample": f"{k2} contiguous grid points of {wl.name} (N={wl.x.size}): dense f32 K*^T + sgemv mean + "
+                      f"OpenBLAS strsm variance (oracle.BlasPredictor, the Eigen LLT-solve class) + ComputeSets + "
+                      f"argmax, given the device L/alpha; {t2:.1f} s wall, extrapolated linearly"}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -112,6 +112,12 @@ SBO_API sbo_status sbo_predict(sbo_ctx *ctx, const float *qx, const float *qy, i
 SBO_API sbo_status sbo_compute_sets(sbo_ctx *ctx, const float *mu, const float *sd, int64_t m,
                                     double beta, double f_min, double *lo, double *hi,
                                     uint8_t *safe, uint32_t flags);
+/* The same on f64 inputs: the node's own mu_/std_ (Eigen::VectorXd,
+ * node.cpp:129-130, filled at :641-643) passed as they are -- lossless for
+ * any service value, bit-exact with ComputeSets() (:411-416). */
+SBO_API sbo_status sbo_compute_sets_f64(sbo_ctx *ctx, const double *mu, const double *sd, int64_t m,
+                                        double beta, double f_min, double *lo, double *hi,
+                                        uint8_t *safe, uint32_t flags);
 
 /* Grid acquisition argmax (a10): argmax of score over mask (mask may be NULL),
  * lowest index on ties, NaN never wins.  index_offset is added to local
@@ -198,6 +204,12 @@ SBO_API int sbo_project_subgoal(const double *rx, const double *ry, int64_t n, d
                                 int64_t subgoal_index, const double *Dx, const double *Dy, int64_t m,
                                 double *out_x, double *out_y, double *out_dist);
 
+/* Bounding box of the fitted training points (x0, x1, y0, y1), widened by
+ * every sbo_append and carried through sbo_export_state / sbo_import_state:
+ * the extent the service grid spans by default (mapper side of :583-586).
+ * SBO_E_STATE before the first fit. */
+SBO_API sbo_status sbo_get_bounds(const sbo_ctx *ctx, double *bounds);
+
 /* Fitted predictive state as one device blob (fit on one
  * rank, broadcast the operand to the others instead of refitting there).
  * sbo_state_bytes gives the size (the packed sf2 L^-1 tiles dominate:
@@ -205,7 +217,9 @@ SBO_API int sbo_project_subgoal(const double *rx, const double *ry, int64_t n, d
  * sbo_import_state restores it into another context on any device.  An
  * imported context predicts, ticks and reports like the original (bitwise
  * identical sweeps) but holds no factor: sbo_append / sbo_get_factor return
- * SBO_E_STATE until the next sbo_fit. */
+ * SBO_E_STATE until the next sbo_fit.  sbo_import_state rejects
+ * (SBO_E_INVAL) a blob whose magic, size, section offsets, header fields
+ * or training order do not match what (n, npad) implies. */
 SBO_API sbo_status sbo_state_bytes(sbo_ctx *ctx, int64_t *bytes);
 SBO_API sbo_status sbo_export_state(sbo_ctx *ctx, void *dev_buf, int64_t cap);
 SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t bytes);
@@ -267,8 +281,9 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * MFMA (16x16x4) with an f32 cross-tile accumulator; 1 = variant 0 with an
  * f64 one; 9, 10 = variant 22 with the A stage issued in one burst per
  * step, resp. A fragments read one row block ahead; 13 = the 32x32x16
- * shape.  4-8, 11, 12, 14-21: timing diagnostics (some with parts of the
- * work left out: wrong results). */
+ * shape.  Any other value: SBO_E_INVAL.  (The timing diagnostics -- some
+ * leave parts of the work out -- exist only in the diagnostic build
+ * lib/libsbo_diag.so, never in this library.) */
 #define SBO_OPT_KERNEL_VARIANT 5
 /* SBO_OPT_SWEEP_GROUPS: workgroups of the persistent predictive sweep, each
  * walking one tile-balanced range of the tick's plan; 0 = default (one per
@@ -310,8 +325,9 @@ SBO_API sbo_status sbo_profile_work(sbo_ctx *ctx, double *predict_flops);
  * precision levels (variant 3), one for the f32 sweeps (variants 0, 1);
  * tiles_by_level (may be NULL): the multiplied tiles at six, three, one
  * product(s). */
-/* Diagnostic: with SBO_OPT_KERNEL_VARIANT 39 (the default sweep with phase
- * stamps, s_memtime; never timed as the product) the summed cycles of every
+/* Diagnostic build only (libsbo_diag.so; the product returns zeros): with
+ * SBO_OPT_KERNEL_VARIANT 39 (the default sweep with phase stamps,
+ * s_memtime; never timed as the product) the summed cycles of every
  * sweep wave since the last call, cycles[0..11]: step top, half-step body,
  * item end, vmcnt wait, barrier, whole half-steps, body at six / three / one
  * product(s), half-steps at six / three / one product(s); then reset. */

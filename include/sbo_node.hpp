@@ -146,8 +146,8 @@ public:
         terrain_height_cells_ = r.n_height_cells;
         Dx_ = r.x_coords;
         Dy_ = r.y_coords;
-        mu_ = r.values;
-        std_ = r.uncertainties;
+        mu_.assign(r.values.begin(), r.values.end());               // :641-643: widened into VectorXd
+        std_.assign(r.uncertainties.begin(), r.uncertainties.end());
         return ComputeSets();
     }
 
@@ -158,7 +158,7 @@ public:
         Qhi_.assign(m, 0.0);
         S_.assign(m, 0);
         if (m == 0) return true;
-        const sbo_status st = sbo_compute_sets(ctx_.get(), mu_.data(), std_.data(), (int64_t)m, beta_, f_min_,
+        const sbo_status st = sbo_compute_sets_f64(ctx_.get(), mu_.data(), std_.data(), (int64_t)m, beta_, f_min_,
                                                Qlo_.data(), Qhi_.data(), S_.data(), 0);
         if (st != SBO_OK) {
             err_ = ctx_.last_error();
@@ -209,7 +209,7 @@ private:
     Context &ctx_;
     double beta_, f_min_;
     std::vector<double> Dx_, Dy_, Qlo_, Qhi_;
-    std::vector<float> mu_, std_;
+    std::vector<double> mu_, std_;   // Eigen::VectorXd mu_, std_ (:129-130)
     std::vector<uint8_t> S_;
     int terrain_width_cells_ = 0, terrain_height_cells_ = 0;
     std::pair<double, double> goal_{0.0, 0.0};

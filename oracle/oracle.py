@@ -297,3 +297,46 @@ def point_within(x, y, px, py):
         elif by <= py and s < 0.0:
             wn -= 1
     return int(wn != 0)
+
+
+# ------------------------------------------- Eigen-class CPU path (bench only)
+class BlasPredictor:
+    """The dense CPU predictive path a node would run on its host with Eigen
+    (``LLT::matrixL().solve(K*^T)`` is a blocked TRSM, SURVEY.md 8(d) CPU
+    comparator): given the lower factor L (f32) and alpha, for each block of
+    queries build K*^T (N x k, f32, numpy exp), mu = m0 + K*^T alpha (sgemv),
+    V = L^-1 K*^T by OpenBLAS ``strsm`` (level-3, multithreaded), var = sf2 -
+    colsum(V^2); then ComputeSets + argmax (orc_compute_sets / orc_argmax).
+    Dense: no tile skipping.  TEST/BENCH INFRASTRUCTURE: only bench.py's
+    cpu_baseline leg uses it, as the timed CPU comparator."""
+
+    def __init__(self, L, alpha, x, y, ell, sf2, m0, block=2048):
+        self.Lf = np.asfortranarray(L, dtype=np.float32)       # lower factor, Fortran order for strsm
+        self.alpha = np.ascontiguousarray(alpha, np.float32)
+        self.x = np.ascontiguousarray(x, np.float32)[:, None]
+        self.y = np.ascontiguousarray(y, np.float32)[:, None]
+        self.c = np.float32(-1.0 / (2.0 * ell * ell))
+        self.sf2, self.m0 = np.float32(sf2), np.float32(m0)
+        self.block = int(block)
+
+    def predict(self, qx, qy):
+        from scipy.linalg.blas import strsm
+        qx = np.ascontiguousarray(qx, np.float32)
+        qy = np.ascontiguousarray(qy, np.float32)
+        m = qx.size
+        mu = np.empty(m, np.float32)
+        var = np.empty(m, np.float32)
+        for a in range(0, m, self.block):
+            b = min(m, a + self.block)
+            dx = self.x - qx[None, a:b]
+            dy = self.y - qy[None, a:b]
+            K = np.asfortranarray(self.sf2 * np.exp((dx * dx + dy * dy) * self.c))   # N x k
+            mu[a:b] = self.m0 + self.alpha @ K
+            V = strsm(1.0, self.Lf, K, lower=1, overwrite_b=1)
+            var[a:b] = np.maximum(self.sf2 - np.einsum("ij,ij->j", V, V), 0.0)
+        return mu, var
+
+    def tick(self, qx, qy, beta, f_min):
+        mu, var = self.predict(qx, qy)
+        lo, hi, s = compute_sets(mu, np.sqrt(var), beta, f_min)
+        return argmax(hi - lo, s)

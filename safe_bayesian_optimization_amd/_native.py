@@ -19,6 +19,7 @@ SBO_DEVICE_PTRS = 0x1
 SBO_ASYNC = 0x2
 SCORE_WIDTH = 0
 SCORE_UCB = 1
+SBO_E_STATE = 6
 
 STATUS = {0: "SBO_OK", 1: "SBO_E_INVAL", 2: "SBO_E_NOT_SPD", 3: "SBO_E_DEVICE", 4: "SBO_E_OOM",
           5: "SBO_E_EMPTY", 6: "SBO_E_STATE"}
@@ -26,11 +27,11 @@ STATUS = {0: "SBO_OK", 1: "SBO_E_INVAL", 2: "SBO_E_NOT_SPD", 3: "SBO_E_DEVICE", 
 # Every symbol include/sbo.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "sbo_version", "sbo_status_string", "sbo_create", "sbo_destroy", "sbo_set_stream", "sbo_last_error",
-    "sbo_fit", "sbo_append", "sbo_num_train", "sbo_predict", "sbo_compute_sets", "sbo_argmax", "sbo_tick",
+    "sbo_fit", "sbo_append", "sbo_num_train", "sbo_predict", "sbo_compute_sets", "sbo_compute_sets_f64", "sbo_argmax", "sbo_tick",
     "sbo_key_combine", "sbo_find_safety_contour_indices", "sbo_next_subgoal", "sbo_find_contours_external",
     "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
     "sbo_get_order", "sbo_profile_work", "sbo_profile_mfma", "sbo_debug_x3_stamps", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
-    "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
+    "sbo_get_bounds", "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
     "sbo_polygon_correct", "sbo_polydist", "sbo_point_within", "sbo_project_subgoal",
 )
 SBO_OPT_INVERSE_BITS = 1
@@ -104,6 +105,8 @@ def lib():
     L.sbo_predict.restype = st
     L.sbo_compute_sets.argtypes = [vp, vp, vp, i64, dbl, dbl, vp, vp, vp, u32]
     L.sbo_compute_sets.restype = st
+    L.sbo_compute_sets_f64.argtypes = [vp, vp, vp, i64, dbl, dbl, vp, vp, vp, u32]
+    L.sbo_compute_sets_f64.restype = st
     L.sbo_argmax.argtypes = [vp, vp, vp, i64, i64, ctypes.POINTER(sbo_key), u32]
     L.sbo_argmax.restype = st
     L.sbo_tick.argtypes = [vp, vp, vp, i64, dbl, dbl, i32, i64, vp, vp, vp, vp, vp, vp, u32]
@@ -120,6 +123,8 @@ def lib():
     L.sbo_frontier.restype = st
     L.sbo_subgoal.argtypes = [vp, vp, vp, vp, vp, vp, i64, i32, i32, dbl, dbl, ctypes.POINTER(i64), u32]
     L.sbo_subgoal.restype = st
+    L.sbo_get_bounds.argtypes = [vp, vp]
+    L.sbo_get_bounds.restype = st
     L.sbo_state_bytes.argtypes = [vp, ctypes.POINTER(i64)]
     L.sbo_state_bytes.restype = st
     L.sbo_export_state.argtypes = [vp, vp, i64]

@@ -1207,7 +1207,10 @@ __device__ __forceinline__ void block_reduce_key(double &s, int64_t &i, sbo_key 
 
 // node.cpp:411-416 and :409 in IEEE double, no contraction:
 //   confidence = beta * std;  lo = mu - confidence;  hi = mu + confidence;  S = lo > f_min
-__device__ __forceinline__ void compute_sets_one(float mu, float sd, double beta, double f_min,
+// T = float (the tick's own f32 outputs, widened exactly) or double (the
+// node's f64 mu_/std_, node.cpp:129-130, :641-643)
+template <typename T>
+__device__ __forceinline__ void compute_sets_one(T mu, T sd, double beta, double f_min,
                                                  double &lo, double &hi, bool &safe) {
     const double c = __dmul_rn(beta, (double)sd);
     lo = __dsub_rn((double)mu, c);
@@ -1246,8 +1249,9 @@ __global__ __launch_bounds__(kAcqThreads) void acquire_kernel(
     block_reduce_key(bs, bi, keys + blockIdx.x);
 }
 
-__global__ __launch_bounds__(kAcqThreads) void sets_kernel(const float *__restrict__ mu,
-                                                           const float *__restrict__ sd, int64_t m,
+template <typename T>
+__global__ __launch_bounds__(kAcqThreads) void sets_kernel(const T *__restrict__ mu,
+                                                           const T *__restrict__ sd, int64_t m,
                                                            double beta, double f_min,
                                                            double *__restrict__ lo,
                                                            double *__restrict__ hi,
@@ -1591,8 +1595,15 @@ hipError_t launch_acquire(hipStream_t s, const float *part, const float *mean, i
 
 hipError_t launch_sets(hipStream_t s, const float *mu, const float *sd, int64_t m, double beta,
                        double f_min, double *lo, double *hi, uint8_t *safe) {
-    hipLaunchKernelGGL(sets_kernel, dim3((unsigned)acq_blocks(m)), dim3(kAcqThreads), 0, s, mu, sd, m, beta,
+    hipLaunchKernelGGL(sets_kernel<float>, dim3((unsigned)acq_blocks(m)), dim3(kAcqThreads), 0, s, mu, sd, m, beta,
                        f_min, lo, hi, safe);
+    return hipGetLastError();
+}
+
+hipError_t launch_sets(hipStream_t s, const double *mu, const double *sd, int64_t m, double beta,
+                       double f_min, double *lo, double *hi, uint8_t *safe) {
+    hipLaunchKernelGGL(sets_kernel<double>, dim3((unsigned)acq_blocks(m)), dim3(kAcqThreads), 0, s, mu, sd, m,
+                       beta, f_min, lo, hi, safe);
     return hipGetLastError();
 }
 

@@ -885,16 +885,18 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
                        seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean)
     switch (variant) {
         case 2: SBO_X3_LAUNCH(2, 16); break;   // four waves of 32 queries
+        case 9: SBO_X3_LAUNCH(1, 0); break;    // A pieces in a burst at the top of the step
+        case 10: SBO_X3_LAUNCH(1, 48); break;  // A fragments one row block ahead
+        case 13: SBO_X3_LAUNCH(3, 16); break;  // wide shape: 32x32x16 MFMA, four waves of 32 queries
+        case 22: SBO_X3_LAUNCH(1, 16); break;    // variant 3 with every tile at full precision
+#ifdef SBO_DIAG
         case 4: SBO_X3_LAUNCH(2, 17); break;   // diagnostics: no next-step K*
         case 5: SBO_X3_LAUNCH(2, 18); break;   //   no A pieces
         case 6: SBO_X3_LAUNCH(1, 17); break;   //   no next-step K*
         case 7: SBO_X3_LAUNCH(1, 18); break;   //   no A pieces
         case 8: SBO_X3_LAUNCH(1, 24); break;   //   every stage from the first tile
-        case 9: SBO_X3_LAUNCH(1, 0); break;    // A pieces in a burst at the top of the step
-        case 10: SBO_X3_LAUNCH(1, 48); break;  // A fragments one row block ahead
         case 11: SBO_X3_LAUNCH(1, 80); break;  // diagnostics: one chain per item, no outer sums
         case 12: SBO_X3_LAUNCH(1, 81); break;  //   and no next-step K*
-        case 13: SBO_X3_LAUNCH(3, 16); break;  // wide shape: 32x32x16 MFMA, four waves of 32 queries
         case 14: SBO_X3_LAUNCH(3, 17); break;  //   diagnostics: no next-step K*
         case 15: SBO_X3_LAUNCH(1, 144); break;  // schedule A/B: four VALU per MFMA gap
         case 16: SBO_X3_LAUNCH(1, 272); break;  //   the compiler's own interleave
@@ -903,7 +905,6 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 19: SBO_X3_LAUNCH(1, 1040); break;  // A stage loaded by waves 4-7 only (12 pieces each)
         case 20: SBO_X3_LAUNCH(1, 2064); break;  // diagnostics: 3 of the 6 split products
         case 21: SBO_X3_LAUNCH(1, 4112); break;  //   1 of the 6
-        case 22: SBO_X3_LAUNCH(1, 16); break;    // variant 3 with every tile at full precision
         case 23: SBO_X3_LAUNCH(1, 8208); break;  // variant 3 with A fragments two row blocks ahead
         case 24: SBO_X3_LAUNCH(1, 24624); break;  // variant 3 issuing only the A pieces a level reads
         case 25: SBO_X3_LAUNCH(1, 4113); break;   // diagnostics: 1 product, no next-step K*
@@ -921,6 +922,7 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 37: SBO_X3_LAUNCH(1, 70163); break;  //   and no barrier
         case 38: SBO_X3_LAUNCH(1, 69655); break;  //   no K*, no A pieces, no outer sums
         case 39: SBO_X3_LAUNCH(1, 335920); break;  // variant 3 with phase stamps (sbo_debug_x3_stamps)
+#endif
         default: SBO_X3_LAUNCH(1, 73776); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead
     }
 #undef SBO_X3_LAUNCH

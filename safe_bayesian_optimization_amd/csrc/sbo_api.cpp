@@ -7,6 +7,7 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -407,8 +408,11 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         plan.L = ctx->skip_log2;
     }
     plan.prod_full = ctx->kernel_variant >= 2 ? 6 : 1;
-    // timing diagnostic: the drop-only plan with every kept tile at level SBO_LVL_FORCE
+#ifdef SBO_DIAG
+    // timing diagnostic (diagnostic build only): the drop-only plan
+    // with every kept tile at level SBO_LVL_FORCE -- outside the error budget
     if (const char *e = getenv("SBO_LVL_FORCE"); e && plan.levels) plan.levels = 2 + std::clamp(atoi(e), 0, 2);
+#endif
     if (ctx->query_order && plan.L > 0 && m > sbo::kBN) {
         const size_t wb = sbo::query_order_bytes(m);
         SBO_HIP(ctx->qwork.reserve(wb));
@@ -481,6 +485,38 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     return SBO_OK;
 }
 
+}  // namespace
+
+namespace {
+// ComputeSets on f32 (the tick's own outputs) or f64 (the node's mu_/std_)
+template <typename T>
+sbo_status compute_sets_impl(sbo_ctx *ctx, const T *mu, const T *sd, int64_t m, double beta, double f_min,
+                             double *lo, double *hi, uint8_t *safe, uint32_t flags) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(mu && sd, SBO_E_INVAL, "sbo_compute_sets: null mu/sd");
+    SBO_CHECK(m >= 0, SBO_E_INVAL, "sbo_compute_sets: m must be >= 0");
+    if (m == 0) return SBO_OK;
+    SBO_HIP(hipSetDevice(ctx->device));
+    if (dev(flags)) {
+        SBO_HIP(sbo::launch_sets(ctx->stream, mu, sd, m, beta, f_min, lo, hi, safe));
+        return finish(ctx, flags);
+    }
+    const size_t need = Carve::need(m, sizeof(T)) * 2 + Carve::need(m, 8) * 2 + Carve::need(m, 1);
+    SBO_HIP(ctx->hq.reserve(need));
+    Carve c(ctx->hq.as<void>());
+    T *dmu = c.take<T>(m), *dsd = c.take<T>(m);
+    double *dlo = c.take<double>(m), *dhi = c.take<double>(m);
+    uint8_t *ds = c.take<uint8_t>(m);
+    SBO_HIP(hipMemcpyAsync(dmu, mu, sizeof(T) * m, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(dsd, sd, sizeof(T) * m, hipMemcpyHostToDevice, ctx->stream));
+    SBO_HIP(sbo::launch_sets(ctx->stream, (const T *)dmu, (const T *)dsd, m, beta, f_min, lo ? dlo : nullptr,
+                             hi ? dhi : nullptr, safe ? ds : nullptr));
+    if (lo) SBO_HIP(hipMemcpyAsync(lo, dlo, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (hi) SBO_HIP(hipMemcpyAsync(hi, dhi, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (safe) SBO_HIP(hipMemcpyAsync(safe, ds, m, hipMemcpyDeviceToHost, ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    return SBO_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -730,32 +766,15 @@ SBO_API sbo_status sbo_tick(sbo_ctx *ctx, const float *qx, const float *qy, int6
     return SBO_OK;
 }
 
+
 SBO_API sbo_status sbo_compute_sets(sbo_ctx *ctx, const float *mu, const float *sd, int64_t m, double beta,
                                     double f_min, double *lo, double *hi, uint8_t *safe, uint32_t flags) {
-    if (!ctx) return SBO_E_INVAL;
-    SBO_CHECK(mu && sd, SBO_E_INVAL, "sbo_compute_sets: null mu/sd");
-    SBO_CHECK(m >= 0, SBO_E_INVAL, "sbo_compute_sets: m must be >= 0");
-    if (m == 0) return SBO_OK;
-    SBO_HIP(hipSetDevice(ctx->device));
-    if (dev(flags)) {
-        SBO_HIP(sbo::launch_sets(ctx->stream, mu, sd, m, beta, f_min, lo, hi, safe));
-        return finish(ctx, flags);
-    }
-    const size_t need = Carve::need(m, 4) * 2 + Carve::need(m, 8) * 2 + Carve::need(m, 1);
-    SBO_HIP(ctx->hq.reserve(need));
-    Carve c(ctx->hq.as<void>());
-    float *dmu = c.take<float>(m), *dsd = c.take<float>(m);
-    double *dlo = c.take<double>(m), *dhi = c.take<double>(m);
-    uint8_t *ds = c.take<uint8_t>(m);
-    SBO_HIP(hipMemcpyAsync(dmu, mu, sizeof(float) * m, hipMemcpyHostToDevice, ctx->stream));
-    SBO_HIP(hipMemcpyAsync(dsd, sd, sizeof(float) * m, hipMemcpyHostToDevice, ctx->stream));
-    SBO_HIP(sbo::launch_sets(ctx->stream, dmu, dsd, m, beta, f_min, lo ? dlo : nullptr, hi ? dhi : nullptr,
-                             safe ? ds : nullptr));
-    if (lo) SBO_HIP(hipMemcpyAsync(lo, dlo, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
-    if (hi) SBO_HIP(hipMemcpyAsync(hi, dhi, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
-    if (safe) SBO_HIP(hipMemcpyAsync(safe, ds, m, hipMemcpyDeviceToHost, ctx->stream));
-    SBO_HIP(hipStreamSynchronize(ctx->stream));
-    return SBO_OK;
+    return compute_sets_impl(ctx, mu, sd, m, beta, f_min, lo, hi, safe, flags);
+}
+
+SBO_API sbo_status sbo_compute_sets_f64(sbo_ctx *ctx, const double *mu, const double *sd, int64_t m, double beta,
+                                        double f_min, double *lo, double *hi, uint8_t *safe, uint32_t flags) {
+    return compute_sets_impl(ctx, mu, sd, m, beta, f_min, lo, hi, safe, flags);
 }
 
 SBO_API sbo_status sbo_argmax(sbo_ctx *ctx, const double *score, const uint8_t *mask, int64_t m,
@@ -942,7 +961,8 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->sweep_groups = (int)value;
             return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
-            SBO_CHECK(value >= 0 && value <= 39, SBO_E_INVAL, "SBO_OPT_KERNEL_VARIANT must be in [0, 39]");
+            SBO_CHECK(sbo::variant_allowed((int)value), SBO_E_INVAL,
+                      "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22)");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
         case SBO_OPT_TILE_SKIP:
@@ -1106,6 +1126,22 @@ struct StateHeader {
     int64_t off_order, off_aug, off_kcoord, off_kbox, off_lgn, total;
 };
 
+static_assert(offsetof(StateHeader, off_aug) == 112 && sizeof(StateHeader) <= 256,
+              "state blob header layout (tests/test_gpu_parity.py tampers off_aug at byte 112)");
+
+// Section offsets of a blob holding n points (npad = round_up(n, kBM)):
+// export writes them, import recomputes them from (n, npad) and rejects any
+// blob whose stored offsets disagree.
+void state_offsets(StateHeader &h) {
+    const int64_t nt = h.npad / sbo::kBK;
+    h.off_order = 256;
+    h.off_aug = sbo::round_up(h.off_order + 8 * h.n, 256);
+    h.off_kcoord = sbo::round_up(h.off_aug + 4 * sbo::total_tiles(h.npad / sbo::kBM) * sbo::kTileFloats, 256);
+    h.off_kbox = sbo::round_up(h.off_kcoord + 4 * nt * 3 * sbo::kBK, 256);
+    h.off_lgn = sbo::round_up(h.off_kbox + 16 * nt, 256);
+    h.total = sbo::round_up(h.off_lgn + 16 * sbo::total_tiles(h.npad / sbo::kBM), 256);
+}
+
 StateHeader state_layout(const sbo_ctx *ctx) {
     StateHeader h{};
     h.magic = kStateMagic;
@@ -1122,19 +1158,20 @@ StateHeader state_layout(const sbo_ctx *ctx) {
     h.auto_skip_mean_log2 = ctx->auto_skip_mean_log2;
     h.lg_tau_v = ctx->lg_tau_v;
     h.spatial_order = ctx->spatial_order;
-    const int64_t nt = ctx->npad / sbo::kBK;
-    h.off_order = 256;
-    h.off_aug = sbo::round_up(h.off_order + 8 * h.n, 256);
-    h.off_kcoord = sbo::round_up(h.off_aug + 4 * sbo::total_tiles(ctx->npad / sbo::kBM) * sbo::kTileFloats, 256);
-    h.off_kbox = sbo::round_up(h.off_kcoord + 4 * nt * 3 * sbo::kBK, 256);
-    h.off_lgn = sbo::round_up(h.off_kbox + 16 * nt, 256);
-    h.total = sbo::round_up(h.off_lgn + 16 * sbo::total_tiles(ctx->npad / sbo::kBM), 256);
+    state_offsets(h);
     return h;
 }
 
 }  // namespace
 
 extern "C" {
+
+SBO_API sbo_status sbo_get_bounds(const sbo_ctx *ctx, double *bounds) {
+    if (!ctx || !bounds) return SBO_E_INVAL;
+    if (!ctx->fitted) return SBO_E_STATE;
+    for (int i = 0; i < 4; ++i) bounds[i] = (double)ctx->bbox[i];
+    return SBO_OK;
+}
 
 SBO_API sbo_status sbo_state_bytes(sbo_ctx *ctx, int64_t *bytes) {
     if (!ctx || !bytes) return SBO_E_INVAL;
@@ -1174,8 +1211,20 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
     StateHeader h;
     SBO_HIP(hipMemcpyAsync(&h, b, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
-    SBO_CHECK(h.magic == kStateMagic && h.total <= bytes && h.n > 0 && h.npad == sbo::round_up(h.n, sbo::kBM),
-              SBO_E_INVAL, "sbo_import_state: not an sbo state blob (or truncated)");
+    SBO_CHECK(h.magic == kStateMagic && h.n > 0 && h.n <= (int64_t)1 << 32 && h.npad == sbo::round_up(h.n, sbo::kBM),
+              SBO_E_INVAL, "sbo_import_state: not an sbo state blob");
+    {
+        StateHeader e = h;
+        state_offsets(e);
+        SBO_CHECK(e.off_order == h.off_order && e.off_aug == h.off_aug && e.off_kcoord == h.off_kcoord &&
+                      e.off_kbox == h.off_kbox && e.off_lgn == h.off_lgn && e.total == h.total,
+                  SBO_E_INVAL, "sbo_import_state: section offsets do not match the blob's (n, npad)");
+        SBO_CHECK(h.total <= bytes, SBO_E_INVAL, "sbo_import_state: truncated blob");
+        SBO_CHECK(h.spatial_order >= 0 && h.spatial_order <= 2 && std::isfinite(h.lg_tau_v) &&
+                      std::isfinite(h.hyper[0]) && h.hyper[0] > 0.0 && std::isfinite(h.hyper[1]) &&
+                      std::isfinite(h.hyper[3]) && h.bbox[0] <= h.bbox[1] && h.bbox[2] <= h.bbox[3],
+                  SBO_E_INVAL, "sbo_import_state: header fields out of range");
+    }
     ctx->fitted = false;
     ctx->has_factor = false;
     ctx->linv_n = 0;
@@ -1195,6 +1244,18 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
     SBO_HIP(hipMemcpyAsync(ctx->tile_lgn.as<void>(), b + h.off_lgn, 16 * (size_t)sbo::total_tiles(h.npad / sbo::kBM),
                            hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
+    {   // the order must be a permutation of 0..n-1 (it indexes the caller's arrays)
+        std::vector<uint8_t> seen((size_t)h.n, 0);
+        for (int64_t v : ctx->order) {
+            if (v < 0 || v >= h.n || seen[(size_t)v]) {
+                ctx->order.clear();
+                ctx->n = 0;
+                ctx->err = "sbo_import_state: training order is not a permutation";
+                return SBO_E_INVAL;
+            }
+            seen[(size_t)v] = 1;
+        }
+    }
     ctx->n = h.n;
     ctx->npad = h.npad;
     ctx->hyper = sbo_hyper{h.hyper[0], h.hyper[1], h.hyper[2], h.hyper[3]};

@@ -224,6 +224,17 @@ hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, 
 constexpr int kLevelShift = 14;
 // the split sweeps that honour the plan's precision levels
 inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39; }
+// Sweeps the product library accepts (all compute the full result; 3 is the
+// default).  The timing diagnostics (parts of the work left out, forced
+// precision levels, phase stamps) exist only in the diagnostic build
+// (-DSBO_DIAG, lib/libsbo_diag.so, selected by SBO_LIB for tools/).
+inline bool variant_allowed(int v) {
+#ifdef SBO_DIAG
+    return v >= 0 && v <= 39;
+#else
+    return v == 0 || v == 1 || v == 2 || v == 3 || v == 9 || v == 10 || v == 13 || v == 22;
+#endif
+}
 inline int x3_layout(int variant) { return (variant == 13 || variant == 14) ? 1 : 0; }
 // The sweep over the plan with the split operand; qx/qy must be readable in
 // whole 128-query blocks (padded to round_up(m, kBN)).  variant: 2 (4-7:
@@ -261,6 +272,8 @@ hipError_t launch_query_order(hipStream_t s, const float *qx, const float *qy, i
                               void *work, size_t work_bytes, int32_t **perm, float **sqx, float **sqy);
 // ComputeSets from given mu/sd (staged API).
 hipError_t launch_sets(hipStream_t s, const float *mu, const float *sd, int64_t m, double beta,
+                       double f_min, double *lo, double *hi, uint8_t *safe);
+hipError_t launch_sets(hipStream_t s, const double *mu, const double *sd, int64_t m, double beta,
                        double f_min, double *lo, double *hi, uint8_t *safe);
 // Masked argmax over f64 scores -> block keys.
 hipError_t launch_argmax_blocks(hipStream_t s, const double *score, const uint8_t *mask, int64_t m,

@@ -127,7 +127,6 @@ class TerrainMapper:
         self.ctx = ctx or Context(device)
         self.hyper = hyper or Hyper()
         self._lib = N.lib()
-        self._bounds = None
 
     # -------------------------------------------------------------- fitting
     def fit(self, x, y, obs, *, async_: bool = False) -> None:
@@ -135,7 +134,6 @@ class TerrainMapper:
         if async_:
             fl |= N.SBO_ASYNC
         n = int(x.numel() if _is_dev(x) else x.size)
-        self._bounds = ((float(x.min()), float(x.max())), (float(y.min()), float(y.max()))) if n else None
         self.ctx.check(self._lib.sbo_fit(self.ctx.handle, _ptr(x), _ptr(y), _ptr(obs), n,
                                          _to_hyper(self.hyper), fl))
 
@@ -218,6 +216,16 @@ class TerrainMapper:
         self.ctx.check(self._lib.sbo_get_order(self.ctx.handle, _ptr(o)))
         return o
 
+    def bounds(self):
+        """((x0, x1), (y0, y1)) of every fitted or appended training point
+        (sbo_get_bounds; survives export/import), or None before a fit."""
+        b = np.zeros(4, np.float64)
+        st = self._lib.sbo_get_bounds(self.ctx.handle, _ptr(b))
+        if st == N.SBO_E_STATE:
+            return None
+        self.ctx.check(st)
+        return (float(b[0]), float(b[1])), (float(b[2]), float(b[3]))
+
     def skip_info(self):
         """(cutoff exponent L in effect, max_i |A_i|_1, |sf2 alpha|_1)."""
         L, r, a = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
@@ -272,13 +280,14 @@ class TerrainMapper:
         the training-data bounds (or the given ranges) with
         n = floor(extent / resolution) + 1 cells per axis, stored row-major
         (y outer, x inner).  Parity of this rule is unpinned."""
-        if self.n == 0 or self._bounds is None:
+        bounds = self.bounds() if self.n else None
+        if bounds is None:
             return TerrainMapResponse(False, "no measurements", 0, 0)
         rx, ry = (float(np.float32(r)) for r in resolution)
         if not (rx > 0 and ry > 0):
             return TerrainMapResponse(False, "resolution must be > 0", 0, 0)
-        x0, x1 = x_range if x_range is not None else self._bounds[0]
-        y0, y1 = y_range if y_range is not None else self._bounds[1]
+        x0, x1 = x_range if x_range is not None else bounds[0]
+        y0, y1 = y_range if y_range is not None else bounds[1]
         w = int(np.floor((x1 - x0) / rx)) + 1
         h = int(np.floor((y1 - y0) / ry)) + 1
         gx = x0 + rx * np.arange(w)

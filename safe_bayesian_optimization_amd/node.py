@@ -12,10 +12,13 @@
     FindSafetyContourIndices                   :418-497
     GetNextSubgoal                             :499-550
 
-ComputeSets runs on the GPU (libsbo ``sbo_compute_sets``, IEEE double, no
-FMA); the frontier and the subgoal selection run in libsbo's host code.  The
-ROS transport, the CGAL/Boost safe-set geometry and the polydist projection
-(:649-723, :725-1200) are out of scope.
+ComputeSets runs on the GPU (libsbo ``sbo_compute_sets_f64`` on the node's
+f64 ``mu_``/``std_``, IEEE double, no FMA); the frontier and the subgoal
+selection run in libsbo's host code, as do the post-selection geometry the
+node applies to the subgoal (``bg::within`` goal short-circuit, ring
+``bg::correct``, ``polydist`` projection: ``ProjectSubgoal``, :649-723).  The
+ROS transport and the construction of the eroded safe-set hull (CGAL alpha
+shapes, Boost buffer, :725-1200) are out of scope.
 """
 from __future__ import annotations
 
@@ -35,8 +38,8 @@ class OptimizerCore:
         self.ctx = ctx
         self._device = device
         self.D_ = np.zeros((0, 2), np.float64)
-        self.mu_ = np.zeros(0, np.float32)
-        self.std_ = np.zeros(0, np.float32)
+        self.mu_ = np.zeros(0, np.float64)    # Eigen::VectorXd (:129-130)
+        self.std_ = np.zeros(0, np.float64)
         self.Q_ = np.zeros((0, 2), np.float64)
         self.S_ = np.zeros(0, np.uint8)
         self.terrain_width_cells_ = 0
@@ -59,8 +62,8 @@ class OptimizerCore:
         D[:, 0] = np.asarray(response.x_coords, np.float64)
         D[:, 1] = np.asarray(response.y_coords, np.float64)
         self.D_ = D
-        self.mu_ = np.ascontiguousarray(response.values, np.float32)
-        self.std_ = np.ascontiguousarray(response.uncertainties, np.float32)
+        self.mu_ = np.ascontiguousarray(response.values, np.float64)          # :641-643, widened as Eigen does
+        self.std_ = np.ascontiguousarray(response.uncertainties, np.float64)
         self.ComputeSets()
 
     # ---------------------------------------------------------- acquisition
@@ -73,8 +76,8 @@ class OptimizerCore:
         s = np.empty(m, np.uint8)
         if m:
             ctx = self._context()
-            ctx.check(self._lib.sbo_compute_sets(ctx.handle, _ptr(self.mu_), _ptr(self.std_), m, self.beta_,
-                                                 self.f_min_, _ptr(lo), _ptr(hi), _ptr(s), 0))
+            ctx.check(self._lib.sbo_compute_sets_f64(ctx.handle, _ptr(self.mu_), _ptr(self.std_), m, self.beta_,
+                                                     self.f_min_, _ptr(lo), _ptr(hi), _ptr(s), 0))
         self.Q_ = np.stack([lo, hi], axis=1)
         self.S_ = s
 

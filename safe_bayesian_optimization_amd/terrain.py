@@ -123,6 +123,29 @@ def synthetic(n: int, grid_w: int, grid_h: int | None = None, seed: int = 0,
                     grid_w, grid_h, hyper, f_min)
 
 
+def synthetic_box(n: int, grid_w: int, grid_h: int, x_range=(0.0, 1.0), y_range=(0.0, 2.5), seed: int = 0,
+                  hyper: Hyper | None = None, name: str | None = None) -> Workload:
+    """The stress variant of SURVEY.md 8(d): N points uniform over the mapping
+    node's own box (config/lpsc.yaml:32-33, x_range [0, 1], y_range [0, 2.5]),
+    the same smooth field + N(0, sn2) observations, a grid_w x grid_h query
+    grid over the box.  With l = 0.4 the box is only 2.5 x 6.25 length scales,
+    so at large N almost no K* tile is negligible (the skip-free regime) and
+    K is ill-conditioned (cond ~1e4-1e5)."""
+    hyper = hyper or Hyper()
+    (x0, x1), (y0, y1) = x_range, y_range
+    u = uniform(seed, 2 * n)
+    x = x0 + u[0::2] * (x1 - x0)
+    y = y0 + u[1::2] * (y1 - y0)
+    side = max(x1 - x0, y1 - y0)
+    obs = smooth_field(x - x0, y - y0, side, hyper.length_scale, seed) + math.sqrt(hyper.sn2) * normal(seed + 1, n)
+    gx = np.linspace(x0, x1, grid_w)
+    gy = np.linspace(y0, y1, grid_h)
+    QY, QX = np.meshgrid(gy, gx, indexing="ij")
+    f_min = float(np.percentile(obs, 40.0))
+    return Workload(name or f"lpsc_box_n{n}_g{grid_w}x{grid_h}", x, y, obs, QX.reshape(-1), QY.reshape(-1),
+                    grid_w, grid_h, hyper, f_min)
+
+
 def make_terrain_csv(rows: int = 48, cols: int = 64, seed: int = 7) -> np.ndarray:
     """Stand-in for the missing data/terrain.csv: a smooth stiffness-like field
     in [700, 1100] (config/lpsc.yaml:5 stiffness_range)."""

@@ -136,3 +136,37 @@ def test_gloo_world2_cost_balanced_shards():
     want = O.argmax(score, mask)
     for s, i in (k0, k1):
         assert i == want[0] and s == want[1]
+
+
+# ------------------------------------------------ bench.py's own launcher
+def _bench(*args, env=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                          "MASTER_PORT")}
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=e, cwd=root)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_launches_its_own_ranks(world):
+    """`python bench.py --gpus N` with no WORLD_SIZE starts N ranks itself
+    (torch.distributed.run on 127.0.0.1); the JSON line reports the world
+    size and backend the collective saw, the cut broadcast and key all-gather
+    give the global argmax (gloo, CPU rehearsal of the GPU path)."""
+    rc, line, r = _bench("--gpus", str(world), "--launch-check")
+    assert rc == 0, r.stderr[-2000:]
+    assert line["n_gpus"] == world and line["world_size"] == world and line["backend"] == "gloo"
+    assert line["config"]["parallelism"] == f"m-shard{world}"
+    assert line["argmax_matches_global"] is True
+    assert line["cuts"][0] == 0 and line["cuts"][-1] == 1 << 16 and len(line["cuts"]) == world + 1
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    rc, line, r = _bench("--gpus", "2", "--launch-check", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and line is None and "WORLD_SIZE=1" in r.stderr

@@ -249,6 +249,49 @@ def test_compute_sets_bit_exact(mapper, seed):
     assert np.array_equal(lo, olo) and np.array_equal(hi, ohi) and np.array_equal(s, os_)
 
 
+@pytest.mark.parametrize("dev_ptrs", [False, True])
+def test_compute_sets_f64_bit_exact(dev, mapper, dev_ptrs):
+    """sbo_compute_sets_f64: the node's own f64 mu_/std_ (node.cpp:129-130)
+    as they are -- values that no f32 can hold give the oracle's
+    ComputeSets bit for bit (and differ from the f32-narrowed call)."""
+    rng = np.random.default_rng(7)
+    m = 65537
+    mu = rng.normal(size=m) * 3 + 1e-9 * rng.normal(size=m)
+    sd = rng.uniform(0, 1, m) + 1e-12
+    mu[:4] = [0.0, -0.0, 1e-300, 1e300]
+    assert np.mean(mu.astype(np.float32).astype(np.float64) != mu) > 0.99
+    beta, fmin = 2.0, float(np.percentile(mu, 40))
+    olo, ohi, os_ = O.compute_sets(mu, sd, beta, fmin)
+    if dev_ptrs:
+        t = lambda a: torch.tensor(a, device=dev)  # noqa: E731
+        dmu, dsd = t(mu), t(sd)
+        lo_t = torch.empty(m, dtype=torch.float64, device=dev)
+        hi_t = torch.empty_like(lo_t)
+        s_t = torch.empty(m, dtype=torch.uint8, device=dev)
+        mapper.ctx.check(N.lib().sbo_compute_sets_f64(mapper.ctx.handle, dmu.data_ptr(), dsd.data_ptr(), m, beta,
+                                                      fmin, lo_t.data_ptr(), hi_t.data_ptr(), s_t.data_ptr(),
+                                                      N.SBO_DEVICE_PTRS))
+        lo, hi, s = lo_t.cpu().numpy(), hi_t.cpu().numpy(), s_t.cpu().numpy()
+    else:
+        lo = np.empty(m); hi = np.empty(m); s = np.empty(m, np.uint8)
+        mapper.ctx.check(N.lib().sbo_compute_sets_f64(mapper.ctx.handle, mu.ctypes.data, sd.ctypes.data, m, beta,
+                                                      fmin, lo.ctypes.data, hi.ctypes.data, s.ctypes.data, 0))
+    assert np.array_equal(lo, olo) and np.array_equal(hi, ohi) and np.array_equal(s, os_)
+    nlo, _, _ = O.compute_sets(mu.astype(np.float32), sd.astype(np.float32), beta, fmin)
+    assert not np.array_equal(nlo, olo)   # the narrowing the f64 entry point avoids is visible
+
+
+def test_product_rejects_diagnostic_variants(mapper):
+    """libsbo.so accepts only the sweeps that compute the full result; the
+    timing diagnostics (work left out, phase stamps) live in libsbo_diag.so."""
+    gm = TerrainMapper(0, ctx=mapper.ctx)
+    for v in (4, 5, 6, 7, 8, 11, 12, 14, 15, 16, 17, 18, 19, 20, 21, 23, 25, 29, 30, 35, 37, 39, 40):
+        with pytest.raises(N.SboError):
+            gm.set_option(N.SBO_OPT_KERNEL_VARIANT, v)
+    for v in (0, 1, 2, 9, 10, 13, 22, 3):
+        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, v)
+
+
 def test_node_compute_sets_and_subgoal(mapper, c1_case):
     from safe_bayesian_optimization_amd import OptimizerCore
     from safe_bayesian_optimization_amd.gp import TerrainMapResponse
@@ -607,8 +650,30 @@ def test_state_export_import(dev, mapper):
     bad[:8] = 0
     with pytest.raises(N.SboError):
         b.import_state(bad)
+    # a stored section offset that disagrees with (n, npad): rejected before any copy
+    off = 8 * 3 + 8 * 4 + 8 * 2 + 4 * 4 + 4 * 3 + 4 + 8   # header: ... off_order, off_aug
+    bad = blob.clone()
+    v = blob[off:off + 8].cpu().numpy().view(np.int64)[0]
+    bad[off:off + 8] = torch.tensor(np.array([v + 256], np.int64).view(np.uint8), device=bad.device)
+    with pytest.raises(N.SboError):
+        b.import_state(bad)
+    # a training order that is not a permutation
+    bad = blob.clone()
+    bad[256:264] = bad[264:272]
+    with pytest.raises(N.SboError):
+        b.import_state(bad)
+    # the training bounds travel with the state (the service grid's default extent)
+    b.import_state(blob)
+    assert b.bounds() == a.bounds()
+    assert a.get_terrain_map_with_uncertainty((0.5, 0.5)).success
+    assert b.get_terrain_map_with_uncertainty((0.5, 0.5)).n_width_cells == \
+        a.get_terrain_map_with_uncertainty((0.5, 0.5)).n_width_cells
     b.fit(wl.x, wl.y, wl.obs)      # a refit restores the full state
     b.append(wl.x[:5] + 0.01, wl.y[:5], wl.obs[:5])
+    # appends widen the bounds
+    (x0, x1), (y0, y1) = b.bounds()
+    b.append(np.array([x1 + 3.0], np.float32), np.array([y0 - 2.0], np.float32), np.zeros(1, np.float32))
+    assert b.bounds() == ((x0, float(np.float32(x1 + 3.0))), (float(np.float32(y0 - 2.0)), y1))
     b.close()
 
 
