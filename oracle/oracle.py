@@ -16,7 +16,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_LIB_PATH = os.environ.get("ORC_LIB") or os.path.join(_HERE, "liboracle.so")   # ORC_LIB: sanitizer build
 _lib = None
 
 _f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
