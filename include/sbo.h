@@ -309,6 +309,13 @@ SBO_API sbo_status sbo_get_order(const sbo_ctx *ctx, int64_t *order);
  * dense n x n ROW-major f32 host array (upper triangle left untouched). */
 SBO_API sbo_status sbo_get_inverse(sbo_ctx *ctx, float *Linv);
 
+/* Test accessor: the plan's per packed tile gain bounds, 8 floats per tile in
+ * packed-tile order (row block I, k-tile t at tile_start(I) + t):
+ * log2 of (16 max row 1-norm, spectral-norm bound, Frobenius norm, 0) of
+ * A_It, then (16 max row 1-norm, spectral-norm bound) of its bf16 pieces A1
+ * and A2 (-1000 for an all-zero matrix).  cap >= 8 * tiles. */
+SBO_API sbo_status sbo_get_tile_bounds(sbo_ctx *ctx, float *bounds, int64_t cap);
+
 /* Kernel timing (bench.py): when enabled, hipEvents are recorded on the
  * context's stream around every predictive-sweep and RBF-fill launch.
  * sbo_profile(ctx, 1) enables and resets; sbo_profile_read sums the elapsed

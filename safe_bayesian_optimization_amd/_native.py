@@ -31,7 +31,7 @@ EXPORTS = (
     "sbo_key_combine", "sbo_find_safety_contour_indices", "sbo_next_subgoal", "sbo_find_contours_external",
     "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
     "sbo_get_order", "sbo_profile_work", "sbo_profile_mfma", "sbo_debug_x3_stamps", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
-    "sbo_get_bounds", "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
+    "sbo_get_bounds", "sbo_get_tile_bounds", "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
     "sbo_polygon_correct", "sbo_polydist", "sbo_point_within", "sbo_project_subgoal",
 )
 SBO_OPT_INVERSE_BITS = 1
@@ -123,6 +123,8 @@ def lib():
     L.sbo_frontier.restype = st
     L.sbo_subgoal.argtypes = [vp, vp, vp, vp, vp, vp, i64, i32, i32, dbl, dbl, ctypes.POINTER(i64), u32]
     L.sbo_subgoal.restype = st
+    L.sbo_get_tile_bounds.argtypes = [vp, vp, i64]
+    L.sbo_get_tile_bounds.restype = st
     L.sbo_get_bounds.argtypes = [vp, vp]
     L.sbo_get_bounds.restype = st
     L.sbo_state_bytes.argtypes = [vp, ctypes.POINTER(i64)]

@@ -159,98 +159,132 @@ __global__ __launch_bounds__(kBM) void row_l1_kernel(const float *__restrict__ a
     atomicAdd(row_l1 + I * kBM + r, s);
 }
 
-// Per packed tile, gain bounds (log2, rounded up):
-// .x = log2(16 max_r |A_r|_1)  (|A k|_2 <= sqrt(256) |A k|_inf <= 16 max_r |A_r|_1 max|k|)
-// .y = log2 of a bound on the spectral norm ||A_It||_2  (|A k|_2 <= ||A||_2 |k|_2):
-//      with the 64x64 Gram matrix G = A^T A (PSD, f64), ||A||_2^2 = lambda_max(G)
-//      <= ||G^8||_inf^(1/8) (any induced norm bounds the spectral radius),
-//      also <= |A|_F^2 = trace G; the smaller of the two;
-// .z = log2(|A_It|_F), which also bounds || |A_It| ||_2 (the entrywise
-//      absolute values: the bound on the split products a tile's lower
-//      precision levels leave out).
-// the plan pairs .x with the largest K* of the tile and .y with a bound on
-// |k|_2 from the tile's points.  One workgroup per tile, f64 arithmetic.
+// The split of an f32 value into three bf16 pieces, v = v0 + v1 + v2 (+ a
+// remainder below 2^-24 |v|), exactly as pack_x3_kernel splits the operand
+// (the same round-to-nearest-even conversion instruction).
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float bf16_rn(float a) {
+    const f32x2_t v = {a, 0.0f};
+    const uint32_t w = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+    return __uint_as_float(w << 16);
+}
+__device__ __forceinline__ float split_piece(float a, int plane) {
+    const float a0 = bf16_rn(a);
+    if (plane == 0) return a0;
+    const float r1 = a - a0, a1 = bf16_rn(r1);
+    if (plane == 1) return a1;
+    return bf16_rn(r1 - a1);
+}
+
+// Per packed tile, gain bounds (log2, rounded up), two float4 per tile:
+// lgn[2T]   .x = log2(16 max_r |A_r|_1)  (|A k|_2 <= sqrt(256) |A k|_inf <= 16 max_r |A_r|_1 max|k|)
+//           .y = log2 of a bound on the spectral norm ||A_It||_2  (|A k|_2 <= ||A||_2 |k|_2):
+//                with the 64x64 Gram matrix G = A^T A (PSD, f64), ||A||_2^2 = lambda_max(G)
+//                <= ||G^8||_inf^(1/8) (any induced norm bounds the spectral radius),
+//                also <= |A|_F^2 = trace G; the smaller of the two;
+//           .z = log2(|A_It|_F), which also bounds || |A_It| ||_2;
+// lgn[2T+1] the same two bounds for the bf16 pieces the split sweep
+//           multiplies (A = A0 + A1 + A2, pack_x3_kernel): .x, .y of A1 and
+//           .z, .w of A2 (16 max row 1-norm, spectral) -- the products a
+//           tile's lower precision levels leave out are A2 K0 + A1 K1 + A0 K2
+//           (three products) and also A1 K0 + A0 K1 (one product), bounded
+//           plane by plane in tile_increments.
+// The plan pairs the row-sum bounds with the largest K* of the tile and the
+// spectral ones with a bound on |k|_2 from the tile's points.  One workgroup
+// per tile, f64 arithmetic; the three matrices one after the other.
 __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
                                                         float4 *__restrict__ lgn) {
-    __shared__ float at[kBM * kBK];            // the tile, [row][k]  (64 KiB)
+    __shared__ float at[kBM * kBK];            // the tile (or one of its pieces), [row][k]  (64 KiB)
     __shared__ double gm[kBK * kBK];           // G, then its powers (32 KiB)
     __shared__ double hm[kBK * kBK];           // squaring scratch  (32 KiB)
     __shared__ double red[2][kBM / 64];
     const int64_t tile = t0 + blockIdx.x;
     const float *t = aug + tile * kTileFloats;
     const int tid = threadIdx.x;
-    double s = 0.0;
-    for (int k = 0; k < kBK; ++k) {
-        const float a = t[tile_offset(k, tid)];
-        at[tid * kBK + k] = a;
-        s += fabs((double)a);
-    }
+    const int gi = tid >> 2, gj = (tid & 3) * 16;  // G[i][j], thread: i = tid / 4, j = 16 (tid % 4) + 0..15
+    float out[6];                                // (rows, spectral) of A; of A1; of A2
+    double lg_fro_a = -1000.0;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s = fmax(s, __shfl_xor(s, o));
-    if ((tid & 63) == 0) red[0][tid >> 6] = s;
-    __syncthreads();
-    // G[i][j], thread: i = tid / 4, j = 16 (tid % 4) + 0..15
-    const int gi = tid >> 2, gj = (tid & 3) * 16;
-    {
-        double acc[16];
-#pragma unroll
-        for (int c = 0; c < 16; ++c) acc[c] = 0.0;
-        for (int r = 0; r < kBM; ++r) {
-            const double ai = (double)at[r * kBK + gi];
-#pragma unroll
-            for (int c = 0; c < 16; ++c) acc[c] = fma(ai, (double)at[r * kBK + gj + c], acc[c]);
-        }
-#pragma unroll
-        for (int c = 0; c < 16; ++c) gm[gi * kBK + gj + c] = acc[c];
-    }
-    __syncthreads();
-    const double fro2 = [&] {  // trace G = |A|_F^2 (every thread reads it)
-        double tr = 0.0;
-        for (int i = 0; i < kBK; ++i) tr += gm[i * kBK + i];
-        return tr;
-    }();
-    // three squarings, G <- (G/c)^2 with c = the largest entry (exact power-of-two
-    // rescale), tracking log2 of the scale: G^8 = 2^e8 * gm
-    double e8 = 0.0;
-    for (int it = 0; it < 3; ++it) {
-        double mx = 0.0;
-        for (int i = tid; i < kBK * kBK; i += kBM) mx = fmax(mx, fabs(gm[i]));
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-        if ((tid & 63) == 0) red[1][tid >> 6] = mx;
-        __syncthreads();
-        mx = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
-        __syncthreads();
-        if (!(mx > 0.0)) break;
-        const int ex = ilogb(mx);
-        double acc[16];
-#pragma unroll
-        for (int c = 0; c < 16; ++c) acc[c] = 0.0;
+    for (int pi = 0; pi < 3; ++pi) {
+        const int plane = pi == 0 ? -1 : pi;     // -1: A itself, then A1, A2
+        double s = 0.0;
         for (int k = 0; k < kBK; ++k) {
-            const double g1 = ldexp(gm[gi * kBK + k], -ex);
-#pragma unroll
-            for (int c = 0; c < 16; ++c) acc[c] = fma(g1, ldexp(gm[k * kBK + gj + c], -ex), acc[c]);
+            const float a0 = t[tile_offset(k, tid)];
+            const float a = plane < 0 ? a0 : split_piece(a0, plane);
+            at[tid * kBK + k] = a;
+            s += fabs((double)a);
         }
 #pragma unroll
-        for (int c = 0; c < 16; ++c) hm[gi * kBK + gj + c] = acc[c];
-        e8 = 2.0 * (e8 + (double)ex);  // (2^e G')^2 = 2^(2e) G'^2
+        for (int o = 32; o >= 1; o >>= 1) s = fmax(s, __shfl_xor(s, o));
+        if ((tid & 63) == 0) red[0][tid >> 6] = s;
         __syncthreads();
-        for (int i = tid; i < kBK * kBK; i += kBM) gm[i] = hm[i];
-        __syncthreads();
-    }
-    // ||G^8||_inf: largest absolute row sum
-    double rs = 0.0;
-    if (tid < kBK)
-        for (int j = 0; j < kBK; ++j) rs += fabs(gm[tid * kBK + j]);
+        {
+            double acc[16];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) rs = fmax(rs, __shfl_xor(rs, o));
-    if (tid == 0) {
+            for (int c = 0; c < 16; ++c) acc[c] = 0.0;
+            for (int r = 0; r < kBM; ++r) {
+                const double ai = (double)at[r * kBK + gi];
+#pragma unroll
+                for (int c = 0; c < 16; ++c) acc[c] = fma(ai, (double)at[r * kBK + gj + c], acc[c]);
+            }
+#pragma unroll
+            for (int c = 0; c < 16; ++c) gm[gi * kBK + gj + c] = acc[c];
+        }
+        __syncthreads();
+        const double fro2 = [&] {  // trace G = |A|_F^2 (every thread reads it)
+            double tr = 0.0;
+            for (int i = 0; i < kBK; ++i) tr += gm[i * kBK + i];
+            return tr;
+        }();
+        // three squarings, G <- (G/c)^2 with c = the largest entry (exact power-of-two
+        // rescale), tracking log2 of the scale: G^8 = 2^e8 * gm
+        double e8 = 0.0;
+        for (int it = 0; it < 3; ++it) {
+            double mx = 0.0;
+            for (int i = tid; i < kBK * kBK; i += kBM) mx = fmax(mx, fabs(gm[i]));
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+            if ((tid & 63) == 0) red[1][tid >> 6] = mx;
+            __syncthreads();
+            mx = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+            __syncthreads();
+            if (!(mx > 0.0)) break;
+            const int ex = ilogb(mx);
+            double acc[16];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) acc[c] = 0.0;
+            for (int k = 0; k < kBK; ++k) {
+                const double g1 = ldexp(gm[gi * kBK + k], -ex);
+#pragma unroll
+                for (int c = 0; c < 16; ++c) acc[c] = fma(g1, ldexp(gm[k * kBK + gj + c], -ex), acc[c]);
+            }
+#pragma unroll
+            for (int c = 0; c < 16; ++c) hm[gi * kBK + gj + c] = acc[c];
+            e8 = 2.0 * (e8 + (double)ex);  // (2^e G')^2 = 2^(2e) G'^2
+            __syncthreads();
+            for (int i = tid; i < kBK * kBK; i += kBM) gm[i] = hm[i];
+            __syncthreads();
+        }
+        // ||G^8||_inf: largest absolute row sum
+        double rs = 0.0;
+        if (tid < kBK)
+            for (int j = 0; j < kBK; ++j) rs += fabs(gm[tid * kBK + j]);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) rs = fmax(rs, __shfl_xor(rs, o));
         s = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
         // log2 ||A||_2 <= (log2 ||G^8||_inf) / 16, with a margin for the f64 rounding
         const double lg_spec = rs > 0.0 ? (log2(rs) + e8) / 16.0 + 1e-4 : -1000.0;
         const double lg_fro = fro2 > 0.0 ? 0.5 * log2(fro2) : -1000.0;
-        lgn[tile] = make_float4(s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f,
-                                (float)fmin(lg_spec, lg_fro) + 1e-5f, (float)lg_fro + 1e-5f, 0.0f);
+        const int o = 2 * pi;                    // A: 0, A1: 2, A2: 4
+        out[o] = s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f;
+        out[o + 1] = (float)fmin(lg_spec, lg_fro) + 1e-5f;
+        if (plane < 0) lg_fro_a = lg_fro;
+        __syncthreads();   // gm / red / at are rewritten for the next matrix
+    }
+    if (tid == 0) {
+        lgn[2 * tile] = make_float4(out[0], out[1], (float)lg_fro_a + 1e-5f, 0.0f);
+        lgn[2 * tile + 1] = make_float4(out[2], out[3], out[4], out[5]);
     }
 }
 
@@ -472,25 +506,34 @@ __device__ __forceinline__ float tile_box_d2(const float4 b, const QBox &q) {
 }
 
 // A kept tile runs at one of three precision levels: all six split
-// products (code 0), the three largest a1 k0 + a0 k1 + a0 k0 (code 1: the
-// dropped terms are below 3.1 2^-16 |a| |k| per product), or a0 k0 alone
-// (code 2: below 2.03 2^-8 + 3.1 2^-16).  Lowering a tile's level, or
-// dropping it, costs part of the row block's error budget: with
-// b_abs = min(2^x K*max, 2^z |k|_2) bounding | |A_It| |k_t| |_2 and
-// b = min(2^x K*max, 2^y |k|_2) bounding |A_It k_t|_2, the three increments
-//     code 0 -> 1:  c3 = 3.1 2^-16 b_abs
-//     code 1 -> 2:  c1 - c3,  c1 = (2.03 2^-8 + 3.1 2^-16) b_abs
-//     code 2 -> drop: b - c1
+// products (code 0), the three largest a1 k0 + a0 k1 + a0 k0 (code 1), or
+// a0 k0 alone (code 2).  With A = A0 + A1 + A2 and K = K0 + K1 + K2 the
+// bf16 pieces (round to nearest at each step, so |K1| <= 2^-9 (1 + 2^-9) |K|
+// and |K2| <= 2^-18 (1 + 2^-9)^2 |K| entrywise), the products code 1 leaves
+// out are A2 K0 + A1 K1 + A0 K2 and code 2 also A1 K0 + A0 K1; each is
+// bounded plane by plane, |A_p K_j|_2 <= min(R_p K*max, S_p |k|_2) rho_j with
+// R_p = 16 max row 1-norm and S_p the spectral bound of piece p (lgn[2T+1];
+// for A0: R = R_A (1 + 2^-9), S = S_A + 2^-9 |A|_F).  Lowering a tile's
+// level, or dropping it, costs part of the row block's error budget; the
+// three increments
+//     code 0 -> 1:  c3 = |A2 K0| + |A1 K1| + |A0 K2|   (bounds as above)
+//     code 1 -> 2:  c1 = |A1 K0| + |A0 K1|
+//     code 2 -> drop:  b - c3 - c1,  b = min(R_A K*max, S_A |k|_2) >= |A_It k_t|_2
 // sum to the tile's drop bound and are spent greedily over all tiles of the
 // row block, cheapest first by error per sweep time saved (the increments
 // are ranked by log2(error) + kLvlKey[j], kLvlKey from the measured per-tile
 // time of the three levels and of the drop; a tile's keys never go down, so
-// its spent increments are a prefix).
+// its spent increments are a prefix).  (Earlier rule, still an upper bound
+// of these: c3 <= 3.1 2^-16 |A|_F |k|_2, c3 + c1 <= 2.03 2^-8 |A|_F |k|_2 --
+// far_tile relies on it.)
 // For each increment: its bin relative to the budget 2^lg_tau (bin 0 = below
 // 2^-kBudgetFloor of it, bin kBudgetBins-1 = over the whole budget, never
 // spent) and its weight in fixed point (2^32 = the budget), rounded up.
 constexpr float kLg3 = -14.36f;  // log2(3.1 2^-16), rounded up
 constexpr float kLg1 = -6.96f;   // log2(2.03 2^-8 + 3.1 2^-16), rounded up
+constexpr float kRho0 = 0.0029f;          // log2(1 + 2^-9), rounded up
+constexpr float kRho1 = -9.0f + 0.0029f;  // log2(2^-9 (1 + 2^-9))
+constexpr float kRho2 = -18.0f + 0.0058f; // log2(2^-18 (1 + 2^-9)^2)
 
 __device__ __forceinline__ int inc_bin(float l, unsigned long long &w, float key = 0.0f) {  // l = log2(inc / budget)
     const float f = (l + key + (float)kBudgetFloor) * (float)kBinsPerBit + 1.0f;
@@ -499,15 +542,27 @@ __device__ __forceinline__ int inc_bin(float l, unsigned long long &w, float key
     return bi;
 }
 
-__device__ __forceinline__ void tile_increments(float d2, float kn, float4 lgn_t, float cexp, float lg_tau,
-                                                float2 key, int (&bi)[3], unsigned long long (&w)[3]) {
+// log2(2^a + 2^b), rounded up
+__device__ __forceinline__ float lg_add(float a, float b) {
+    const float hi = fmaxf(a, b), lo = fminf(a, b);
+    return hi + __log2f(1.0f + exp2f(lo - hi)) + 1e-4f;
+}
+
+__device__ __forceinline__ void tile_increments(float d2, float kn, float4 lgn_t, float4 lgp_t, float cexp,
+                                                float lg_tau, float2 key, int (&bi)[3],
+                                                unsigned long long (&w)[3]) {
     const float kmax = cexp * d2 * 0.999f;
     const float b = fminf(lgn_t.x + kmax, lgn_t.y + kn) - lg_tau + 0.01f;
-    const float babs = fminf(lgn_t.x + kmax, lgn_t.z + kn) - lg_tau + 0.01f;
-    const float r3 = babs + kLg3, r1 = babs + kLg1;
+    // |A_p k|_2 bounds of the three pieces (relative to the budget)
+    const float n0 = fminf(lgn_t.x + kRho0 + kmax, lg_add(lgn_t.y, lgn_t.z - 9.0f) + kn) - lg_tau + 0.01f;
+    const float n1 = fminf(lgp_t.x + kmax, lgp_t.y + kn) - lg_tau + 0.01f;
+    const float n2 = fminf(lgp_t.z + kmax, lgp_t.w + kn) - lg_tau + 0.01f;
+    const float r3 = lg_add(lg_add(n2 + kRho0, n1 + kRho1), n0 + kRho2);   // A2 K0 + A1 K1 + A0 K2
+    const float r1 = lg_add(n1 + kRho0, n0 + kRho1);                       // A1 K0 + A0 K1
+    const float r31 = lg_add(r3, r1);
     bi[0] = inc_bin(r3, w[0], key.x);
-    bi[1] = inc_bin(r1 + __log2f(1.0f - exp2f(r3 - r1)), w[1], key.y);
-    const float dl = r1 - b;  // <= -3.96: |A|_F <= 8 ||A||_2
+    bi[1] = inc_bin(r1, w[1], key.y);
+    const float dl = r31 - b;
     bi[2] = dl < -0.01f ? inc_bin(b + __log2f(1.0f - exp2f(dl)), w[2]) : inc_bin(b, w[2]);
     // monotone: the three bins never go down (so a tile's spent increments are a prefix)
     bi[1] = max(bi[1], bi[0]);
@@ -518,7 +573,7 @@ __device__ __forceinline__ void tile_increments(float d2, float kn, float4 lgn_t
 // distance of every k-tile, and the per-item selection rule.
 struct PlanRule {
     const float4 *kbox;
-    const float4 *lgn;  // per packed tile log2 gain bounds (null: distance test)
+    const float4 *lgn;  // per packed tile log2 gain bounds, two float4 (null: distance test)
     float cexp, skip_d2, skip_d2_mean, lg_tau;
     int nI;
     QBox box;
@@ -539,25 +594,58 @@ struct PlanRule {
     // evaluating the bounds -- most candidate tiles of a row block.
     __device__ __forceinline__ bool far_tile(int I, int t, float dd) const {
         const float kf = fmaxf(0.0f, fmaxf(key.x + kLg3, key.y + kLg1));
-        return lgn[tile_start(I) + t].x + cexp * dd * 0.999f - lg_tau + 0.01f + kf < -(float)kBudgetFloor;
+        return lgn[2 * (tile_start(I) + t)].x + cexp * dd * 0.999f - lg_tau + 0.01f + kf < -(float)kBudgetFloor;
     }
 
     __device__ __forceinline__ void incs(int I, int t, int (&bi)[3], unsigned long long (&w)[3]) const {
-        tile_increments(d2(t), kn(t), lgn[tile_start(I) + t], cexp, lg_tau, key, bi, w);
+        const int64_t T = tile_start(I) + t;
+        tile_increments(d2(t), kn(t), lgn[2 * T], lgn[2 * T + 1], cexp, lg_tau, key, bi, w);
         if (levels != 1) {  // only the whole drop: the first two increments free, the third the whole drop bound
             bi[0] = bi[1] = 0;
             w[0] = w[1] = 0ull;
             const float kmax = cexp * d2(t) * 0.999f;
-            const float4 l = lgn[tile_start(I) + t];
+            const float4 l = lgn[2 * T];
             bi[2] = inc_bin(fminf(l.x + kmax, l.y + kn(t)) - lg_tau + 0.01f, w[2]);
         }
+    }
+
+    // Total weight of every increment of row block I (wave-wide): what the
+    // row block would spend dropping all its tiles; `over` is set when some
+    // increment is larger than the whole reference budget (it never drops
+    // everything).  The same increments and fixed-point weights as threshold.
+    __device__ unsigned long long total_weight(int I, int lane, bool &over) const {
+        const int T = kTilesPerRowBlockStep * (I + 1);
+        unsigned long long wsum = 0;
+        int ov = 0;
+        for (int t = lane; t < T; t += 64) {
+            if (far_tile(I, t, d2(t))) {
+                wsum += 6ull;
+                continue;
+            }
+            int bi[3];
+            unsigned long long w[3];
+            incs(I, t, bi, w);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                if (bi[j] < kBudgetBins - 1) wsum += w[j];
+                else ov = 1;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            wsum += __shfl_xor(wsum, o);
+            ov |= __shfl_xor(ov, o);
+        }
+        over = ov != 0;
+        return wsum;
     }
 
     // Greedy budget threshold of row block I (wave-wide; bins is wave-private
     // LDS): the largest prefix of bins, smallest increments first, whose
     // summed weights (integer adds: order-independent) stay within the
-    // budget.  Returns the last spent bin (-1: none).
-    __device__ int threshold(int I, unsigned long long *bins, int lane) const {
+    // row block's budget (fixed point, 2^32 = the reference budget 2^lg_tau).
+    // Returns the last spent bin (-1: none).
+    __device__ int threshold(int I, unsigned long long *bins, int lane, unsigned long long budget) const {
         if (!lgn) return -1;
         const int T = kTilesPerRowBlockStep * (I + 1);
         for (int i = lane; i < kBudgetBins; i += 64) bins[i] = 0ull;
@@ -596,7 +684,7 @@ struct PlanRule {
 #pragma unroll
         for (int j = 0; j < per; ++j) {
             pre += v[j];
-            ok += pre <= (1ull << 32) ? 1 : 0;
+            ok += pre <= budget ? 1 : 0;
         }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) ok += __shfl_xor(ok, o);
@@ -629,6 +717,11 @@ struct PlanRule {
         return code;
     }
 };
+
+// The plan's reference budget 2^lg_ref = tau2, the whole query block's
+// |dV|_2 budget, from lg_tau = log2(tau2 / sqrt(nI)) (the even share).
+__device__ __forceinline__ float plan_ref(float lg_tau, int nI) { return lg_tau + 0.5f * __log2f((float)nI) - 1e-4f; }
+constexpr int kPlanMaxI = 512;   // water-filling of the budget for nI <= this (N <= 131072), else even shares
 
 // Query box of block qb (threads 0..127 hold its queries, 128..255 repeat
 // them) and the distance cache.
@@ -697,14 +790,55 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     __shared__ float d2s[kPlanD2], kns[kPlanD2];
     __shared__ float red[4 * kPlanWaves];
     __shared__ unsigned long long bins[kPlanWaves][kBudgetBins];
+    __shared__ unsigned long long wtot[kPlanMaxI];
+    __shared__ unsigned long long budget_exp;
     const int64_t qb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nkt = kTilesPerRowBlockStep * nI;
-    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns, levels, lvl_key};
+    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, plan_ref(lg_tau, nI), nI, {}, d2s, kns, levels, lvl_key};
     R.box = plan_setup(qx, qy, m, qb, kbox, lgn ? kcoord : nullptr, cexp, nkt, d2s, kns, red);
+    // The error budget of the query block, |dV(q)|_2^2 = sum_I |dV_I(q)|_2^2
+    // <= tau2^2 = 2^(2 lg_ref) for every query q of the block, shared over
+    // its row blocks by water-filling instead of evenly (tau2 / sqrt(nI)
+    // each): a row block whose tiles can all be dropped within the common
+    // share drops them and spends only what they cost; the rest of tau2^2 is
+    // split evenly over the others (iterated: a larger share can make more
+    // row blocks cheap).  Fixed point, 2^32 = 2^lg_ref.
+    const bool fill = lgn && nI <= kPlanMaxI;
+    if (fill) {
+        for (int I = wave; I < nI; I += kPlanWaves) {
+            bool over;
+            const unsigned long long w = R.total_weight(I, lane, over);
+            if (lane == 0) wtot[I] = over ? ~0ull : w;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const double one = 4294967296.0;
+            double share = 1.0 / sqrt((double)nI);   // the even split, in units of 2^lg_ref
+            for (int it = 0; it < 4; ++it) {
+                double cheap2 = 0.0;
+                int nexp = 0;
+                for (int I = 0; I < nI; ++I) {
+                    const double w = wtot[I] == ~0ull ? 2.0 : (double)wtot[I] / one;
+                    if (w <= share) cheap2 += w * w;
+                    else ++nexp;
+                }
+                if (nexp == 0) break;
+                const double s2 = fmax(0.0, (1.0 - cheap2) * (1.0 - 1e-9)) / (double)nexp;
+                const double sn = sqrt(s2) * (1.0 - 1e-9);
+                if (!(sn > share)) break;
+                share = sn;
+            }
+            budget_exp = (unsigned long long)floor(share * one);
+        }
+        __syncthreads();
+    }
     for (int I = wave; I < nI; I += kPlanWaves) {
         const int T = kTilesPerRowBlockStep * (I + 1);
-        const int drop_max = R.threshold(I, bins[wave], lane);
+        // a cheap row block (everything within the share) spends its own total
+        const unsigned long long bud = !fill ? (unsigned long long)floor(4294967296.0 / sqrt((double)nI))
+                                       : (wtot[I] <= budget_exp ? ~0ull : budget_exp);
+        const int drop_max = R.threshold(I, bins[wave], lane, bud);
         int cnt = 0;
         unsigned wsum = 0;
         for (int t0 = 0; t0 < T; t0 += 64) {
@@ -750,7 +884,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
     const int64_t qb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nkt = kTilesPerRowBlockStep * nI;
-    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, lg_tau, nI, {}, d2s, kns, levels, lvl_key};
+    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, plan_ref(lg_tau, nI), nI, {}, d2s, kns, levels, lvl_key};
     R.box = plan_setup(qx, qy, m, qb, kbox, lgn ? kcoord : nullptr, cexp, nkt, d2s, kns, red);
     unsigned long long prod = 0, nl1 = 0, nl2 = 0;
     for (int I = wave; I < nI; I += kPlanWaves) {

@@ -328,8 +328,8 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     {
         SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)npad));
         SBO_HIP(sbo::launch_row_l1(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->scratch.as<double>()));
-        SBO_HIP(grow_keep(ctx, ctx->tile_lgn, sizeof(float4) * (size_t)sbo::total_tiles(nI),
-                          sizeof(float4) * old_tiles));
+        SBO_HIP(grow_keep(ctx, ctx->tile_lgn, 2 * sizeof(float4) * (size_t)sbo::total_tiles(nI),
+                          2 * sizeof(float4) * old_tiles));
         SBO_HIP(sbo::launch_tile_norms(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->tile_lgn.as<float4>()));
         const int64_t r0 = I0 * sbo::kBM;
         std::vector<double> rl1((size_t)(npad - r0));
@@ -1013,6 +1013,18 @@ SBO_API sbo_status sbo_get_inverse(sbo_ctx *ctx, float *Linv) {
     return SBO_OK;
 }
 
+SBO_API sbo_status sbo_get_tile_bounds(sbo_ctx *ctx, float *bounds, int64_t cap) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(ctx->fitted && bounds, SBO_E_STATE, "sbo_get_tile_bounds: call sbo_fit first");
+    const int64_t need = 8 * sbo::total_tiles(ctx->npad / sbo::kBM);
+    SBO_CHECK(cap >= need, SBO_E_INVAL, "sbo_get_tile_bounds: cap < 8 floats per packed tile");
+    SBO_HIP(hipSetDevice(ctx->device));
+    SBO_HIP(hipMemcpyAsync(bounds, ctx->tile_lgn.as<void>(), sizeof(float) * (size_t)need, hipMemcpyDeviceToHost,
+                           ctx->stream));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    return SBO_OK;
+}
+
 }  // extern "C"
 
 // ----------------------------------------------------------- frontier 8(f)1
@@ -1113,7 +1125,7 @@ SBO_API sbo_status sbo_subgoal(sbo_ctx *ctx, const double *Dx, const double *Dy,
 // ------------------------------------------------- fitted state, 8(e)
 namespace {
 
-constexpr uint64_t kStateMagic = 0x3453544154534253ull;  // "SBSTATS4" (three tile norms, 16 B per tile)
+constexpr uint64_t kStateMagic = 0x3553544154534253ull;  // "SBSTATS5" (tile and piece norms, 32 B per tile)
 
 struct StateHeader {
     uint64_t magic;
@@ -1139,7 +1151,7 @@ void state_offsets(StateHeader &h) {
     h.off_kcoord = sbo::round_up(h.off_aug + 4 * sbo::total_tiles(h.npad / sbo::kBM) * sbo::kTileFloats, 256);
     h.off_kbox = sbo::round_up(h.off_kcoord + 4 * nt * 3 * sbo::kBK, 256);
     h.off_lgn = sbo::round_up(h.off_kbox + 16 * nt, 256);
-    h.total = sbo::round_up(h.off_lgn + 16 * sbo::total_tiles(h.npad / sbo::kBM), 256);
+    h.total = sbo::round_up(h.off_lgn + 32 * sbo::total_tiles(h.npad / sbo::kBM), 256);
 }
 
 StateHeader state_layout(const sbo_ctx *ctx) {
@@ -1198,7 +1210,7 @@ SBO_API sbo_status sbo_export_state(sbo_ctx *ctx, void *dev_buf, int64_t cap) {
     SBO_HIP(hipMemcpyAsync(b + h.off_kbox, ctx->kbox.as<void>(), 16 * (size_t)nt, hipMemcpyDeviceToDevice,
                            ctx->stream));
     SBO_HIP(hipMemcpyAsync(b + h.off_lgn, ctx->tile_lgn.as<void>(),
-                           16 * (size_t)sbo::total_tiles(ctx->npad / sbo::kBM), hipMemcpyDeviceToDevice, ctx->stream));
+                           32 * (size_t)sbo::total_tiles(ctx->npad / sbo::kBM), hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));  // the header and order live on this host stack
     return SBO_OK;
 }
@@ -1233,7 +1245,7 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
     SBO_HIP(ctx->aug.reserve(aug_bytes));
     SBO_HIP(ctx->kcoord.reserve(4 * (size_t)nt * 3 * sbo::kBK));
     SBO_HIP(ctx->kbox.reserve(16 * (size_t)nt));
-    SBO_HIP(ctx->tile_lgn.reserve(16 * (size_t)sbo::total_tiles(h.npad / sbo::kBM)));
+    SBO_HIP(ctx->tile_lgn.reserve(32 * (size_t)sbo::total_tiles(h.npad / sbo::kBM)));
     ctx->order.resize((size_t)h.n);
     SBO_HIP(hipMemcpyAsync(ctx->order.data(), b + h.off_order, 8 * (size_t)h.n, hipMemcpyDeviceToHost, ctx->stream));
     SBO_HIP(hipMemcpyAsync(ctx->aug.as<void>(), b + h.off_aug, aug_bytes, hipMemcpyDeviceToDevice, ctx->stream));
@@ -1241,7 +1253,7 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
                            hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipMemcpyAsync(ctx->kbox.as<void>(), b + h.off_kbox, 16 * (size_t)nt, hipMemcpyDeviceToDevice,
                            ctx->stream));
-    SBO_HIP(hipMemcpyAsync(ctx->tile_lgn.as<void>(), b + h.off_lgn, 16 * (size_t)sbo::total_tiles(h.npad / sbo::kBM),
+    SBO_HIP(hipMemcpyAsync(ctx->tile_lgn.as<void>(), b + h.off_lgn, 32 * (size_t)sbo::total_tiles(h.npad / sbo::kBM),
                            hipMemcpyDeviceToDevice, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
     {   // the order must be a permutation of 0..n-1 (it indexes the caller's arrays)

@@ -99,7 +99,7 @@ struct sbo_ctx {
     int auto_skip_log2 = 160;    // auto K* cutoff for V (half the budget), computed at fit (refresh_operand)
     int auto_skip_mean_log2 = 160;  // auto cutoff the last row block keeps for the mean
     float lg_tau_v = -1000.0f;   // log2 of each row block's |dV_I|_2 budget (tile-norm test)
-    sbo::DevBuf tile_lgn;        // per packed tile: log2 of its two 2-norm gain bounds (float2, auto cutoff)
+    sbo::DevBuf tile_lgn;        // per packed tile: log2 gain bounds of A_It and of its bf16 pieces (2 x float4)
     int skip_budget = 20;        // SBO_OPT_SKIP_BUDGET: the auto cutoff keeps the skip error below 2^-B
     double max_row_l1 = 0.0;     // max_i sum_j |A_ij|, A = sf2 L^-1
     double alpha_l1 = 0.0;       // sum_j |sf2 alpha_j|
@@ -246,8 +246,10 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
                              const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
                              const float *qy, int64_t m, int64_t ldp, float cexp, float m0, float *part, float *mean,
                              int variant);
-// lgn[tile_start(I) + t] = (log2 16 max_r |A_It[r]|_1, log2 |A_It|_F) (f64
-// sums, rounded up) for row blocks I >= I0 (-1000 for an all-zero tile).
+// lgn[2 (tile_start(I) + t)] = log2 bounds (16 max row 1-norm, spectral,
+// Frobenius) of A_It, lgn[2 (..) + 1] = (16 max row 1-norm, spectral) of its
+// bf16 pieces A1 and A2 (f64 sums, rounded up) for row blocks I >= I0 (-1000
+// for an all-zero matrix).
 hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float4 *lgn);
 // d = (double)in - v;  out = (float)d
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);

@@ -421,6 +421,93 @@ def test_tile_skip_exact_and_bounded(dev, mapper):
     assert res[0][2] == res[64][2]
 
 
+@pytest.mark.parametrize("budget", [10, 13])
+def test_loose_budgets_hold(mapper, budget):
+    """At loose budgets (B = 10, 13: 2^-B sf2 = 1e-3, 1.2e-4) most tiles run
+    at reduced precision or are dropped, so the effect of the plan's bounds is
+    far above the f32 noise: mu and sigma^2 still stay within 2^-B of the
+    dense all-six-products sweep, i.e. the per-piece level increments and the
+    drop bounds are upper bounds in practice too."""
+    wl = synthetic(4096, 160, 120, seed=33)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    m = wl.qx.size
+    gm.set_option(N.SBO_OPT_TILE_SKIP, 0)
+    ref = dict(mu=np.empty(m, np.float32), sd=np.empty(m, np.float32))
+    gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=ref)
+    gm.set_option(N.SBO_OPT_TILE_SKIP, -1)
+    gm.set_option(N.SBO_OPT_SKIP_BUDGET, budget)
+    gm.fit(wl.x, wl.y, wl.obs)
+    lib = N.lib()
+    lib.sbo_profile(gm.ctx.handle, 1)
+    out = dict(mu=np.empty(m, np.float32), sd=np.empty(m, np.float32))
+    gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
+    mf = ctypes.c_double()
+    lv = (ctypes.c_int64 * 3)()
+    lib.sbo_profile_mfma(gm.ctx.handle, ctypes.byref(mf), lv)
+    lib.sbo_profile(gm.ctx.handle, 0)
+    gm.set_option(N.SBO_OPT_SKIP_BUDGET, 20)
+    ulp = np.finfo(np.float32).eps
+    dmu = np.abs(out["mu"].astype(np.float64) - ref["mu"]).max()
+    dvar = np.abs(out["sd"].astype(np.float64) ** 2 - ref["sd"].astype(np.float64) ** 2).max()
+    print(f"B={budget}: levels {list(lv)}  |dmu| {dmu:.2e}  |dvar| {dvar:.2e}  (budget {2.0 ** -budget:.2e})")
+    assert lv[1] > 0 and lv[2] > 0
+    assert dmu <= 2.0 ** -budget + 2 * ulp * np.abs(ref["mu"]).max()
+    assert dvar <= 2.0 ** -budget + 4 * ulp
+
+
+def test_tile_gain_bounds_are_bounds(mapper):
+    """sbo_get_tile_bounds: every packed tile's log2 bounds are upper bounds
+    of the exact norms of A_It = (sf2 L^-1)_It and of its bf16 pieces A1, A2
+    (the same round-to-nearest split as the sweep's operand), and the
+    spectral bounds are within the ||G^8||^(1/16) slack (<= 64^(1/16) = 1.30x)."""
+    wl = synthetic(1100, 8, seed=17)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    n = gm.n
+    A = np.zeros((n, n), np.float32)
+    gm.ctx.check(N.lib().sbo_get_inverse(gm.ctx.handle, A.ctypes.data))
+    A = np.tril(A)
+    nI = (n + 255) // 256
+    tiles = sum(4 * (I + 1) for I in range(nI))
+    b = np.empty(8 * tiles, np.float32)
+    gm.ctx.check(N.lib().sbo_get_tile_bounds(gm.ctx.handle, b.ctypes.data, b.size))
+    b = b.reshape(tiles, 8).astype(np.float64)
+
+    def bf16(v):
+        return torch.from_numpy(np.ascontiguousarray(v, np.float32)).to(torch.bfloat16).to(torch.float32).numpy()
+
+    def norms(T):
+        if not np.any(T):
+            return -1000.0, -1000.0
+        return (np.log2(16 * np.abs(T.astype(np.float64)).sum(1).max()),
+                np.log2(np.linalg.norm(T.astype(np.float64), 2)))
+    T0 = 0
+    checked = 0
+    for I in range(nI):
+        for t in range(4 * (I + 1)):
+            Tpad = np.zeros((256, 64), np.float32)
+            blk = A[I * 256:(I + 1) * 256, t * 64:(t + 1) * 64]
+            Tpad[:blk.shape[0], :blk.shape[1]] = blk
+            a0 = bf16(Tpad)
+            r1 = Tpad - a0
+            a1 = bf16(r1)
+            a2 = bf16(r1 - a1)
+            e = [*norms(Tpad), *norms(a1), *norms(a2)]
+            g = [b[T0, 0], b[T0, 1], b[T0, 4], b[T0, 5], b[T0, 6], b[T0, 7]]
+            for ex, gb in zip(e, g):
+                if ex > -1000.0:
+                    assert gb >= ex - 1e-6, (I, t, e, g)
+            for ex, gb in ((e[1], g[1]), (e[3], g[3]), (e[5], g[5])):
+                if ex > -1000.0:
+                    assert gb <= ex + np.log2(1.31), (I, t, e, g)
+            if np.any(Tpad):
+                assert b[T0, 2] >= np.log2(np.linalg.norm(Tpad.astype(np.float64))) - 1e-6
+                checked += 1
+            T0 += 1
+    assert T0 == tiles and checked > 20
+
+
 def test_sweep_partition_and_outer_variant(mapper):
     """The persistent sweep's partition of the plan does not change the
     arithmetic: 1, 3, 7 or 1000 workgroups (more than there are non-empty

@@ -18,6 +18,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--config", default="C4")
     p.add_argument("--variant", type=int, default=39)
+    p.add_argument("--opt", nargs="*", default=[], help="NAME=VAL sbo options, e.g. SBO_OPT_TILE_SKIP=0")
     a = p.parse_args()
     import torch
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
@@ -28,6 +29,9 @@ def main():
     dev = torch.device("cuda:0")
     t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
     gm = TerrainMapper(0, wl.hyper)
+    for kv in a.opt:
+        k, v = kv.split("=")
+        gm.set_option(getattr(N, k), int(v))
     gm.fit(t(wl.x), t(wl.y), t(wl.obs))
     qx, qy = t(wl.qx), t(wl.qy)
     lib = N.lib()
