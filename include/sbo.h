@@ -296,6 +296,12 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * rounding of the sweep itself).  Takes effect at the next sbo_fit /
  * sbo_append. */
 #define SBO_OPT_SKIP_BUDGET 7
+/* SBO_OPT_CHOLESKY (1 default | 0): the fit's factorization -- 1 the
+ * library's blocked right-looking Cholesky (a one-workgroup kernel per
+ * 128-column diagonal block, rocBLAS strsm + ssyrk for the panel and the
+ * trailing update), 0 rocSOLVER spotrf.  Same f32 algorithm class and the
+ * same NOT_SPD reporting (leading minor). */
+#define SBO_OPT_CHOLESKY 8
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The K* tile cutoff in effect (auto or fixed) and the norms it was derived from. */

@@ -41,6 +41,7 @@ SBO_OPT_QUERY_ORDER = 4
 SBO_OPT_KERNEL_VARIANT = 5
 SBO_OPT_SWEEP_GROUPS = 6
 SBO_OPT_SKIP_BUDGET = 7
+SBO_OPT_CHOLESKY = 8
 
 
 class SboError(RuntimeError):

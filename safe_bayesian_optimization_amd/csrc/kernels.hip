@@ -140,6 +140,71 @@ __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__r
     c[2 * kBK + o] = in ? sf2 * alpha[k] : 0.0f;
 }
 
+// ---- blocked Cholesky (a2), the factorization step rocSOLVER's spotrf
+// spends most of its time in (unblocked potf2 panels, one small workgroup
+// each): the kb x kb diagonal block of step k0, in LDS, right-looking by
+// columns (column j: sqrt of the pivot, scale the column into a separate
+// array, rank-1 update of the trailing lower triangle with 256 / kCholNB
+// threads per row and four independent updates in flight per thread).  f32
+// as spotrf, correctly rounded sqrt and division.  A pivot that is not > 0
+// (or NaN) stops the factorization: info = k0 + j + 1 (the leading minor,
+// rocSOLVER's convention); later blocks see info != 0 and leave their data
+// alone.  Column-major, lda = ld; only i >= j is written.
+__global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, int64_t ld, int kb, int64_t k0,
+                                                        int *__restrict__ info) {
+    constexpr int T = 256 / kCholNB;  // threads per row
+    __shared__ float a[kCholNB][kCholNB + 1];
+    __shared__ float col[kCholNB];   // the scaled column j (a separate array: the update's reads never alias its writes)
+    if (*info != 0) return;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < kb * kb; e += 256) {
+        const int i = e % kb, j = e / kb;
+        if (i >= j) a[i][j] = A[i + (int64_t)j * ld];
+    }
+    __syncthreads();
+    int bad = 0;
+    const int r = tid % kCholNB, par = tid / kCholNB;
+    for (int j = 0; j < kb; ++j) {
+        const float djj = a[j][j];
+        if (!(djj > 0.0f) || !(djj < __builtin_huge_valf())) {   // uniform: every thread read the same pivot
+            bad = j + 1;
+            break;
+        }
+        const float d = __fsqrt_rn(djj);
+        for (int i = j + 1 + tid; i < kb; i += 256) {
+            const float v = __fdiv_rn(a[i][j], d);
+            a[i][j] = v;
+            col[i] = v;
+        }
+        __syncthreads();
+        if (tid == 0) a[j][j] = d;
+        const int i = j + 1 + r;
+        if (i < kb) {
+            const float aij = col[i];
+            float *ai = a[i];
+            int l = j + 1 + par;
+            for (; l + 3 * T <= i; l += 4 * T) {   // four independent updates in flight
+                const float c0 = col[l], c1 = col[l + T], c2 = col[l + 2 * T], c3 = col[l + 3 * T];
+                const float v0 = ai[l], v1 = ai[l + T], v2 = ai[l + 2 * T], v3 = ai[l + 3 * T];
+                ai[l] = fmaf(-aij, c0, v0);
+                ai[l + T] = fmaf(-aij, c1, v1);
+                ai[l + 2 * T] = fmaf(-aij, c2, v2);
+                ai[l + 3 * T] = fmaf(-aij, c3, v3);
+            }
+            for (; l <= i; l += T) ai[l] = fmaf(-aij, col[l], ai[l]);
+        }
+        __syncthreads();
+    }
+    if (bad) {
+        if (tid == 0) atomicCAS(info, 0, (int)(k0 + bad));
+        return;
+    }
+    for (int e = tid; e < kb * kb; e += 256) {
+        const int i = e % kb, j = e / kb;
+        if (i >= j) A[i + (int64_t)j * ld] = a[i][j];
+    }
+}
+
 // Row 1-norms of the packed operand: block I, thread r sums |A[I*BM + r][:]|.
 // Row 1-norms of the packed operand, |A[I*BM + r][:]|_1: block (c, I)
 // sums row r over k-tiles [c*kRowL1Tiles, (c+1)*kRowL1Tiles) of row block I
@@ -1501,6 +1566,12 @@ hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t 
     if (e != hipSuccess) return e;
     const int64_t chunks = (nI * kTilesPerRowBlockStep + kRowL1Tiles - 1) / kRowL1Tiles;
     hipLaunchKernelGGL(row_l1_kernel, dim3((unsigned)chunks, (unsigned)(nI - I0)), dim3(kBM), 0, s, aug, I0, row_l1);
+    return hipGetLastError();
+}
+
+hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info) {
+    if (kb <= 0 || kb > kCholNB) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, s, A, ld, kb, k0, info);
     return hipGetLastError();
 }
 

@@ -367,10 +367,40 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
 }
 
 // Factor K in L (already filled, lda = cap) and refresh the operand.
+// Right-looking blocked Cholesky of the n x n lower triangle at L (lda = ld):
+// per step of kCholNB columns the diagonal block in one workgroup
+// (chol_diag_kernel), the panel below it by rocBLAS strsm (L21 = A21 L11^-T)
+// and the trailing update by ssyrk (A22 -= L21 L21^T) -- the same
+// factorization as spotrf, without its unblocked potf2 panels (which were 23 %
+// of a C4 fit, profiles/r2_c4_fit_kernel_stats.csv).  info: rocSOLVER's.
+sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_int *info) {
+    SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), ctx->stream));
+    SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
+    const float one = 1.0f, minus_one = -1.0f;
+    for (int64_t k = 0; k < n; k += sbo::kCholNB) {
+        const int64_t kb = std::min<int64_t>(sbo::kCholNB, n - k);
+        float *L11 = L + k + k * ld;
+        SBO_HIP(sbo::launch_chol_diag(ctx->stream, L11, ld, (int)kb, k, info));
+        const int64_t m2 = n - k - kb;
+        if (m2 <= 0) break;
+        float *A21 = L11 + kb, *A22 = L11 + kb + kb * ld;
+        SBO_BLAS(rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                               rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11, (rocblas_int)ld,
+                               A21, (rocblas_int)ld));
+        SBO_BLAS(rocblas_ssyrk(ctx->blas, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)m2, (rocblas_int)kb,
+                               &minus_one, A21, (rocblas_int)ld, &one, A22, (rocblas_int)ld));
+    }
+    return SBO_OK;
+}
+
 sbo_status factor_and_refresh(sbo_ctx *ctx) {
     rocblas_int *info = ctx->info.as<rocblas_int>();
-    SBO_BLAS(rocsolver_spotrf(ctx->blas, rocblas_fill_lower, (rocblas_int)ctx->n, ctx->L.as<float>(),
-                              (rocblas_int)ctx->cap, info));
+    if (ctx->chol_blocked) {
+        if (sbo_status st = blocked_potrf(ctx, ctx->L.as<float>(), ctx->n, ctx->cap, info); st != SBO_OK) return st;
+    } else {
+        SBO_BLAS(rocsolver_spotrf(ctx->blas, rocblas_fill_lower, (rocblas_int)ctx->n, ctx->L.as<float>(),
+                                  (rocblas_int)ctx->cap, info));
+    }
     rocblas_int hinfo = 0;
     SBO_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
@@ -941,6 +971,10 @@ SBO_API sbo_status sbo_profile_read(sbo_ctx *ctx, double *predict_ms, int64_t *p
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
     if (!ctx) return SBO_E_INVAL;
     switch (option) {
+        case SBO_OPT_CHOLESKY:
+            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_CHOLESKY must be 0 or 1");
+            ctx->chol_blocked = value != 0;
+            return SBO_OK;
         case SBO_OPT_INVERSE_BITS:
             SBO_CHECK(value == 32 || value == 64, SBO_E_INVAL, "SBO_OPT_INVERSE_BITS must be 32 or 64");
             ctx->inverse_bits = (int)value;

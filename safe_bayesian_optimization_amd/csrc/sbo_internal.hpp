@@ -94,6 +94,7 @@ struct sbo_ctx {
     sbo::DevBuf Linv;            // L^-1 (strtri f32 workspace, or dtrtri f64 kept for appends), lda = cap
     int64_t linv_n = 0;          // rows of the f64 L^-1 held in Linv (0: none; appends extend it)
     int inverse_bits = 64;       // SBO_OPT_INVERSE_BITS: precision of the L^-1 computation
+    bool chol_blocked = true;    // SBO_OPT_CHOLESKY: 1 own blocked factorization, 0 rocSOLVER spotrf
     int spatial_order = 1;       // SBO_OPT_SPATIAL_ORDER: 0 caller order, 1 Hilbert, 2 Morton
     int skip_log2 = -1;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-L (-1: auto)
     int auto_skip_log2 = 160;    // auto K* cutoff for V (half the budget), computed at fit (refresh_operand)
@@ -251,6 +252,10 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
 // bf16 pieces A1 and A2 (f64 sums, rounded up) for row blocks I >= I0 (-1000
 // for an all-zero matrix).
 hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float4 *lgn);
+// Blocked Cholesky: factor the kb x kb diagonal block at A (column-major,
+// lda = ld) of step k0 in place (kb <= kCholNB); info as rocSOLVER's.
+constexpr int kCholNB = 128;
+hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info);
 // d = (double)in - v;  out = (float)d
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out);

@@ -105,6 +105,42 @@ def test_cholesky_backward_error(mapper, n):
     assert np.linalg.norm(r) / np.linalg.norm(wl.obs) < 1e-3
 
 
+@pytest.mark.parametrize("n", [129, 300, 2048, 4100])
+def test_blocked_cholesky_matches_spotrf(mapper, n):
+    """The library's blocked Cholesky (SBO_OPT_CHOLESKY = 1, default) and
+    rocSOLVER spotrf (0): both within the backward-error bound, factors equal
+    to f32 rounding, the same posterior to the contract."""
+    wl = synthetic(n, 24, 20, seed=n + 3)
+    res = {}
+    for ch in (0, 1):
+        gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+        gm.set_option(N.SBO_OPT_CHOLESKY, ch)
+        gm.fit(wl.x, wl.y, wl.obs)
+        L, alpha = gm.factor()
+        o = gm.order()
+        K = O.rbf_fill_f32in(f32(wl.x)[o], f32(wl.y)[o])
+        L64 = L.astype(np.float64)
+        be = np.linalg.norm(L64 @ L64.T - K) / np.linalg.norm(K)
+        assert be <= 10 * n * EPS32, (ch, be)
+        res[ch] = (L64, gm.predict(wl.qx, wl.qy))
+    gm.set_option(N.SBO_OPT_CHOLESKY, 1)
+    assert np.abs(res[0][0] - res[1][0]).max() <= 1e-4 * np.abs(res[0][0]).max()
+    assert nrel(res[1][1][0], res[0][1][0].astype(np.float64)) < REL_TOL
+    assert nrel(res[1][1][1].astype(np.float64) ** 2, res[0][1][1].astype(np.float64) ** 2) < REL_TOL
+
+
+def test_blocked_cholesky_not_spd_past_first_block(mapper):
+    """A leading minor that fails beyond the first 128-column block is
+    reported as NOT_SPD by the blocked factorization too."""
+    wl = synthetic(300, 8, seed=4)
+    x, y = f32(wl.x), f32(wl.y)
+    x[200], y[200] = x[10], y[10]          # a duplicated point with no noise: K singular
+    gm = TerrainMapper(0, Hyper(noise_level=0.0), ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_CHOLESKY, 1)
+    with pytest.raises(N.NotSPDError):
+        gm.fit(x, y, wl.obs)
+
+
 def test_not_spd_is_reported(mapper):
     x = np.array([0.0, 0.0, 1.0], np.float32)
     with pytest.raises(N.NotSPDError):

@@ -14,15 +14,18 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--n", type=int, nargs="+", default=[8192, 16384])
     p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--chol", type=int, nargs="+", default=[1], help="SBO_OPT_CHOLESKY values to time (1 own, 0 rocSOLVER)")
     a = p.parse_args()
     import torch
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
     dev = torch.device("cuda:0")
-    for n in a.n:
+    from safe_bayesian_optimization_amd import _native as N
+    for n, ch in [(n, c) for n in a.n for c in a.chol]:
         wl = synthetic(n, 64, 64, seed=0)
         t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
         X, Y, O = t(wl.x), t(wl.y), t(wl.obs)
         gm = TerrainMapper(0, wl.hyper)
+        gm.set_option(N.SBO_OPT_CHOLESKY, ch)
         ts = []
         for _ in range(a.reps + 1):
             torch.cuda.synchronize()
@@ -30,7 +33,7 @@ def main():
             gm.fit(X, Y, O)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
-        print(f"N={n}: first fit {ts[0]:.1f} ms, warm refits {', '.join(f'{v:.1f}' for v in ts[1:])} ms", flush=True)
+        print(f"N={n} cholesky={'own blocked' if ch else 'rocSOLVER spotrf'}: first fit {ts[0]:.1f} ms, warm refits {', '.join(f'{v:.1f}' for v in ts[1:])} ms", flush=True)
         gm.close()
 
 
