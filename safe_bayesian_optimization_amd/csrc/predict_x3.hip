@@ -206,7 +206,13 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 uint32_t w0, w1, w2;
-                split3(e[c].x, e[c].y, w0, w1, w2);
+                if constexpr ((DIAG & 1048576) != 0) {  // timing diagnostic: kh only (results wrong beyond level 2)
+                    w0 = pk_bf16(e[c].x, e[c].y);
+                    w1 = w0;
+                    w2 = w0;
+                } else {
+                    split3(e[c].x, e[c].y, w0, w1, w2);
+                }
                 SBO_PIN(w0);
                 SBO_PIN(w1);
                 SBO_PIN(w2);
@@ -922,6 +928,7 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 37: SBO_X3_LAUNCH(1, 70163); break;  //   and no barrier
         case 38: SBO_X3_LAUNCH(1, 69655); break;  //   no K*, no A pieces, no outer sums
         case 39: SBO_X3_LAUNCH(1, 335920); break;  // variant 3 with phase stamps (sbo_debug_x3_stamps)
+        case 41: SBO_X3_LAUNCH(1, 1122352); break;  // diagnostics: variant 3 with the K* split reduced to kh
 #endif
         default: SBO_X3_LAUNCH(1, 73776); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead
     }

@@ -224,14 +224,14 @@ hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, 
 // tile-list entry of the plan: k-tile index | precision level code << kLevelShift
 constexpr int kLevelShift = 14;
 // the split sweeps that honour the plan's precision levels
-inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39; }
+inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39 || variant == 41; }
 // Sweeps the product library accepts (all compute the full result; 3 is the
 // default).  The timing diagnostics (parts of the work left out, forced
 // precision levels, phase stamps) exist only in the diagnostic build
 // (-DSBO_DIAG, lib/libsbo_diag.so, selected by SBO_LIB for tools/).
 inline bool variant_allowed(int v) {
 #ifdef SBO_DIAG
-    return v >= 0 && v <= 39;
+    return v >= 0 && v <= 41;
 #else
     return v == 0 || v == 1 || v == 2 || v == 3 || v == 9 || v == 10 || v == 13 || v == 22;
 #endif
