@@ -15,6 +15,7 @@ def main():
     p.add_argument("--grid", type=int)
     p.add_argument("--ticks", type=int, default=3)
     p.add_argument("--opt", nargs="*", default=[], help="NAME=VALUE library options (e.g. SBO_OPT_TILE_SKIP=0)")
+    p.add_argument("--box", action="store_true", help="the lpsc.yaml stress box [0,1] x [0,2.5] (SURVEY 8(d))")
     a = p.parse_args()
     import torch
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
@@ -23,7 +24,11 @@ def main():
     n = a.n or n
     if a.grid:
         gw = gh = a.grid
-    wl = synthetic(n, gw, gh, seed=0)
+    if a.box:
+        from safe_bayesian_optimization_amd.terrain import synthetic_box
+        wl = synthetic_box(n, gw, gh, seed=0)
+    else:
+        wl = synthetic(n, gw, gh, seed=0)
     dev = torch.device("cuda:0")
     t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
     gm = TerrainMapper(0, wl.hyper)
