@@ -455,6 +455,7 @@ constexpr int kPredictWaves = kBN / 16;
 constexpr int kPredictThreads = 64 * kPredictWaves;
 constexpr int kDescWindow = 64;          // item descriptors (int4) per 1 KiB LDS window
 constexpr int kListWindow = 512;         // tile indices (u16) per 1 KiB LDS window
+constexpr int kRecWindow = 64;           // split-sweep step records (int4) per 1 KiB LDS window
 constexpr int kSmemFloats = 2 * kStageFloats + 2 * 256 + 2 * 256;  // stages + 2 desc + 2 list windows
 constexpr int kBudgetFloor = 40;        // bounds below 2^-40 of the budget share bin 0
 constexpr int kBinsPerBit = 4;
@@ -1096,6 +1097,29 @@ __global__ __launch_bounds__(256) void plan_move_kernel(const unsigned long long
     if (lane == 0) desc2[p] = make_int4(d.x, d.y, (int)(uint32_t)o2, cnt | (int)((o2 >> 32) << 16));
 }
 
+// Step records of the split sweep (kRecFirst in sbo_internal.hpp), one
+// wave per non-empty item, in the order the sweep walks the list (after the
+// XCD permutation): the kernel then stages a tile from one record instead of
+// re-deriving offsets from the descriptor and tile list in every wave.
+__global__ __launch_bounds__(256) void plan_rec_kernel(const unsigned long long *__restrict__ scan, int64_t n_items,
+                                                       const int4 *__restrict__ desc,
+                                                       const unsigned short *__restrict__ tl, int4 *__restrict__ rec) {
+    const int64_t nne = (int64_t)(scan[n_items - 1] >> kPlanKeyShift);
+    const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (k >= nne) return;
+    const int4 d = desc[k];
+    const int cnt = d.w & 0xffff;
+    const uint64_t off = (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
+    const int64_t ts = tile_start(d.x);
+    for (int i = lane; i < cnt; i += 64) {
+        const int te = tl[off + i];
+        const int t = te & ((1 << kLevelShift) - 1);
+        const int w = d.x | ((te >> kLevelShift) << 16) | (i == 0 ? kRecFirst : 0) | (i == cnt - 1 ? kRecLast : 0);
+        rec[off + i] = make_int4((int)(uint32_t)((ts + t) * 96), t * 256, d.y, w);
+    }
+}
+
 __global__ void plan_seg2_kernel(const int *__restrict__ xseg, int G, int P, int *__restrict__ seg2) {
     for (int r = threadIdx.x; r <= P; r += blockDim.x) {
         if (r == P) {
@@ -1601,7 +1625,7 @@ hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int6
 
 namespace {
 struct PlanLayout {
-    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes, wkey, wscan, lvcnt;
+    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes, wkey, wscan, lvcnt, rec;
     // XCD-interleaved order (P % 8 == 0): the sweep reads desc2 / tl2 / seg2
     bool xcd;
     size_t xseg, pos_of, cnt2, off2, desc2, tl2, seg2, temp2, temp2_bytes;
@@ -1629,6 +1653,7 @@ PlanLayout plan_layout(int64_t nI, int64_t nQ, int P) {
     L.desc = take(16 * (size_t)(items + 2 * kDescWindow));
     L.tl = take(2 * (size_t)(cap + 2 * kListWindow));
     L.seg = take(4 * (size_t)(P + 1));
+    L.rec = take(16 * (size_t)(cap + 2 * kRecWindow));
     size_t tb = 0;
     (void)rocprim::inclusive_scan(nullptr, tb, (const unsigned long long *)nullptr, (unsigned long long *)nullptr,
                                   (size_t)items, rocprim::plus<unsigned long long>());
@@ -1711,9 +1736,13 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     if (tiles_done)
         hipLaunchKernelGGL(plan_counts_reduce_kernel, dim3(1), dim3(256), 0, s,
                            reinterpret_cast<const unsigned long long *>(w + L.lvcnt), nQ * kPlanWaves, tiles_done + 1);
+    auto *rec = reinterpret_cast<int4 *>(w + L.rec);
     if (!L.xcd) {
         hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done, wkey,
                            wscan, nI, nQ);
+        if (skip.records)
+            hipLaunchKernelGGL(plan_rec_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, scan, items, desc,
+                               tl, rec);
         return hipGetLastError();
     }
     auto *xseg = reinterpret_cast<int *>(w + L.xseg);
@@ -1740,16 +1769,20 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     hipLaunchKernelGGL(plan_move_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, scan, items, desc, tl,
                        pos_of, off2, desc2, tl2);
     hipLaunchKernelGGL(plan_seg2_kernel, dim3(1), dim3(256), 0, s, xseg, G, P, seg2);
+    if (skip.records)
+        hipLaunchKernelGGL(plan_rec_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, scan, items, desc2,
+                           tl2, rec);
     return hipGetLastError();
 }
 
 void plan_views(int64_t npad, int64_t m, int P, const void *work, const int4 **desc, const unsigned short **tl,
-                const int **seg) {
+                const int **seg, const int4 **rec) {
     const PlanLayout L = plan_layout(npad / kBM, (m + kBN - 1) / kBN, P);
     const char *w = static_cast<const char *>(work);
     *desc = reinterpret_cast<const int4 *>(w + (L.xcd ? L.desc2 : L.desc));
     *tl = reinterpret_cast<const unsigned short *>(w + (L.xcd ? L.tl2 : L.tl));
     *seg = reinterpret_cast<const int *>(w + (L.xcd ? L.seg2 : L.seg));
+    if (rec) *rec = reinterpret_cast<const int4 *>(w + L.rec);
 }
 
 float exp2_coef_f(float ell) { return (float)exp2_coef(ell); }

@@ -54,7 +54,7 @@ constexpr int kXSlot = kXA + kXC + kXQ;  // 50,688 B
 constexpr int kXSlots = 3;
 constexpr int kXWin = kXSlots * kXSlot;  // descriptor and tile-list windows follow the slots
 constexpr int kXSmem = kXWin + 4096;
-constexpr int kDescWin = 64, kListWin = 512;
+constexpr int kRecWin = 64;  // step records (int4) per 1 KiB LDS window
 
 __device__ __forceinline__ float fast_exp2(float v) { return __builtin_amdgcn_exp2f(v); }
 __device__ __forceinline__ float lo_f32(uint32_t w) { return __uint_as_float(w << 16); }
@@ -163,6 +163,10 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
     constexpr int EL = (DIAG & 4096) ? 2 : ((DIAG & 2048) ? 1 : LV);
     constexpr bool P1 = EL <= 1, P2 = EL == 0;  // planes a1, a2 in use
     constexpr int NPROD = EL == 0 ? 6 : (EL == 1 ? 3 : 1);
+    // DIR: this level's products accumulate straight into the outer sums
+    // (no per-tile chain, no outer add): DIAG & 2097152 one product,
+    // DIAG & 4194304 three products as well
+    constexpr bool DIR = (EL == 2 && (DIAG & 2097152)) || (EL == 1 && (DIAG & 4194304));
     constexpr int LAG = (DIAG & 32768) ? 2 : (EL == 0 ? 2 : (EL == 1 ? 4 : 8));
     const int npu = __builtin_amdgcn_readfirstlane(npieces);
     // A fragments of row block r are read AH blocks ahead of their use: the
@@ -251,7 +255,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
         // the finished chains of block rb - LAG (LAG row blocks = 2 (six
         // products), 4 (three) or 8 (one) x NPROD MFMAs ago: off the MFMA
         // result latency)
-        if (!FRESH && !(DIAG & 68) && rb >= LAG) {
+        if (!FRESH && !(DIAG & 68) && !DIR && rb >= LAG) {
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 outer[c][rb - LAG] += acc[c][rb - LAG];
@@ -261,7 +265,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             // (DIAG & 64: one chain over the whole item, no outer sums -- timing only)
-            f32x4 v = (FRESH && !(DIAG & 64)) ? zero : acc[c][rb];
+            f32x4 v = DIR ? outer[c][rb] : ((FRESH && !(DIAG & 64)) ? zero : acc[c][rb]);
             if constexpr (P2) {
                 v = mfma(a2, kb.h[c], v);
                 v = mfma(a1, kb.m[c], v);
@@ -272,7 +276,8 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                 v = mfma(a0, kb.m[c], v);
             }
             v = mfma(a0, kb.h[c], v);
-            acc[c][rb] = v;
+            if constexpr (DIR) outer[c][rb] = v;
+            else acc[c][rb] = v;
         }
         // interleave: each MFMA followed by two VALU and one LDS read, so the
         // vector work issues in the matrix pipe's shadow (a bf16 MFMA holds
@@ -301,7 +306,16 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                 dma16(voff, asrc + rb * kStride, adst + rb * kStride);
         }
     }
-    if (!FRESH && !(DIAG & 68)) {
+    if constexpr (DIR && FRESH) {
+        // a tile's halves share its level: the second half of a DIR tile
+        // never reads acc, so leave it undefined here (else its stale value
+        // stays live through this path into the other levels' second halves)
+#pragma unroll
+        for (int rb = 0; rb < 16; ++rb)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[c][rb] = __builtin_nondeterministic_value(acc[c][rb]);
+    }
+    if (!FRESH && !(DIAG & 68) && !DIR) {
 #pragma unroll
         for (int rb = 16 - LAG; rb < 16; ++rb)
 #pragma unroll
@@ -473,7 +487,7 @@ constexpr int kFirst = 2, kLast = 4, kValid = 8;
 template <int NC, int DIAG>
 __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     const char *__restrict__ ax3, const float *__restrict__ kc3, const int4 *__restrict__ desc,
-    const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P, int n_items, int nI,
+    const int4 *__restrict__ rec, const int *__restrict__ seg, int P, int n_items, int nI, uint32_t a_max,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp, float cexp, float m0,
     float *__restrict__ part, float *__restrict__ mean) {
     __shared__ __attribute__((aligned(16))) char smem[kXSmem];
@@ -496,8 +510,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     const int g = lane >> 4, r = lane & 15;
 
     const lds_char *lds = (const lds_char *)smem;
-    const int4 *dwin = reinterpret_cast<const int4 *>(smem + kXWin);
-    const unsigned short *lwin = reinterpret_cast<const unsigned short *>(smem + kXWin + 2048);
+    const int4 *rwin = reinterpret_cast<const int4 *>(smem + kXWin);
     // LDS-DMA with an SGPR base (global_load_lds_dwordx4 v_off, s_base): the
     // only per-lane operand is the byte offset lane*16
     const uint32_t voff = (uint32_t)lane * 16u;
@@ -505,8 +518,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     const int ldr = HALF_LOAD ? lw - 4 : lw;  // loader index (< 0: no A pieces)
     const bool is_loader = ldr >= 0;
     const uint32_t lds_wave = lds_smem + (uint32_t)(is_loader ? ldr : 0) * 1024u;
-    const uint32_t lds_dwin = lds_smem + (uint32_t)kXWin;
-    const uint32_t lds_lwin = lds_dwin + 2048u;
+    const uint32_t lds_rwin = lds_smem + (uint32_t)kXWin;
 #define SBO_DMA16(sbase, ldst)                                                                          \
     asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"((const void *)(sbase)),     \
                  "{m0}"(ldst)                                                                           \
@@ -515,15 +527,15 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     // queries (lanes 0-31 qx, 32-63 qy) and the half-tile's coordinates
     // first, then every wave its A pieces (the youngest kPieces of its
     // vector-memory operations)
-#define SBO_X3_STAGE(Tg_, t_, h_, qb_, sl_, burst_)                                                     \
+#define SBO_X3_STAGE(akib_, kcf_, h_, qb_, sl_, burst_)                                                 \
     do {                                                                                                \
         const uint32_t d_ = lds_smem + (uint32_t)(sl_) * kXSlot;                                        \
         if (lw == 0) {                                                                                  \
             if (lane < 32) SBO_DMA16(qx + (int64_t)(qb_) * kBN, d_ + kXA + kXC);                        \
             else SBO_DMA16(qy + (int64_t)(qb_) * kBN - 128, d_ + kXA + kXC);                            \
-            if (lane < 32) SBO_DMA16(kc3 + (int64_t)(t_) * (2 * kXC / 4) + (h_) * (kXC / 4), d_ + kXA);  \
+            if (lane < 32) SBO_DMA16(kc3 + (uint32_t)(kcf_) + (h_) * (kXC / 4), d_ + kXA);              \
         }                                                                                               \
-        const char *s_ = ax3 + ((DIAG & 8) ? 0 : ((Tg_) * 2 + (h_)) * (int64_t)kXA) + (is_loader ? ldr : 0) * 1024; \
+        const char *s_ = a_base + ((DIAG & 8) ? 0 : (uint64_t)((akib_) + (h_) * (kXA / 1024)) * 1024u);  \
         const uint32_t w_ = lds_wave + (uint32_t)(sl_) * kXSlot;                                        \
         a_src = s_;                                                                                     \
         a_dst = w_;                                                                                     \
@@ -531,69 +543,53 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
             _Pragma("unroll") for (int j = 0; j < kPieces; ++j)                                         \
                 SBO_DMA16(s_ + j * kLoaders * 1024, w_ + (uint32_t)(j * kLoaders * 1024));              \
     } while (0)
-#define SBO_DESC_WINDOW(w_)                                                                             \
+    // the range's step records (plan_rec_kernel: one int4 per kept tile, in
+    // sweep order) arrive in 1 KiB LDS windows of kRecWin, one window ahead
+#define SBO_REC_WINDOW(w_)                                                                              \
     do {                                                                                                \
-        if (lw == 1) SBO_DMA16(reinterpret_cast<const char *>(desc) + (int64_t)(w_) * 1024, lds_dwin + (uint32_t)((w_) & 1) * 1024u);     \
+        if (lw == 1) SBO_DMA16(reinterpret_cast<const char *>(rec) + (uint64_t)(w_) * 1024u, lds_rwin + (uint32_t)((w_) & 1) * 1024u); \
     } while (0)
-#define SBO_LIST_WINDOW(w_)                                                                             \
-    do {                                                                                                \
-        if (lw == 2) SBO_DMA16(reinterpret_cast<const char *>(tl) + (int64_t)(w_) * 1024, lds_lwin + (uint32_t)((w_) & 1) * 1024u);     \
-    } while (0)
-    auto desc_at = [&](int k) {
-        const int4 d = dwin[((k / kDescWin) & 1) * kDescWin + k % kDescWin];
-        const int I = min(max(__builtin_amdgcn_readfirstlane(d.x), 0), nI - 1);
-        return make_int4(I, __builtin_amdgcn_readfirstlane(d.y), __builtin_amdgcn_readfirstlane(d.z),
-                         __builtin_amdgcn_readfirstlane(d.w));
+    auto rec_at = [&](uint32_t e) {
+        const int4 d = rwin[((e / kRecWin) & 1) * kRecWin + e % kRecWin];
+        return make_int4(__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
+                         __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w));
     };
-    auto entry_off = [](const int4 &d) { return (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32); };
-    auto list_at = [&](uint64_t e) {  // (tile index, level code) of list entry e
-        return __builtin_amdgcn_readfirstlane((int)lwin[((e / kListWin) & 1) * kListWin + e % kListWin]);
-    };
-
-    // ---- lookahead cursor: the step being staged
-    SBO_DESC_WINDOW(k0 / kDescWin);
-    SBO_DESC_WINDOW(k0 / kDescWin + 1);
+    // the range's first and one-past-last list entries
+    uint32_t la_e, e_end;
+    {
+        const int4 da = desc[k0], db = desc[k1 - 1];
+        la_e = (uint32_t)__builtin_amdgcn_readfirstlane(da.z);
+        e_end = (uint32_t)__builtin_amdgcn_readfirstlane(db.z) + (uint32_t)(__builtin_amdgcn_readfirstlane(db.w) & 0xffff);
+    }
+    SBO_REC_WINDOW(la_e / kRecWin);
+    SBO_REC_WINDOW(la_e / kRecWin + 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int la_k = k0, la_j = 0, la_h = 0;
-    int4 la_d = desc_at(k0);
-    uint64_t la_e = entry_off(la_d);
-    SBO_LIST_WINDOW(la_e / kListWin);
-    SBO_LIST_WINDOW(la_e / kListWin + 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    int la_h = 0;
 
+    // this wave's share of every A stage starts at a_base (+ the stage's offset)
+    const char *a_base = ax3 + (is_loader ? ldr : 0) * 1024;
     const char *a_src = ax3;  // this wave's A pieces of the last staged step (spread mode)
     uint32_t a_dst = 0;
     auto stage = [&](int sl, bool burst) {
-        const int cnt = la_d.w & 0xffff;
+        const int4 r = rec_at(la_e);
         XStep s;
-        s.I = la_d.x;
-        s.qb = la_d.y;
-        s.flags = la_h | (la_j == 0 && la_h == 0 ? kFirst : 0) | (la_j == cnt - 1 && la_h == 1 ? kLast : 0) | kValid;
-        const int te = list_at(la_e);
-        const int t = min(te & ((1 << kLevelShift) - 1), kTilesPerRowBlockStep * (la_d.x + 1) - 1);
-        s.lv = LEVELS ? min(te >> kLevelShift, 2) : 0;
-        SBO_X3_STAGE(tile_start(la_d.x) + t, t, la_h, la_d.y, sl, burst);
+        s.I = min(r.w & 0xffff, nI - 1);
+        s.qb = r.z;
+        s.flags = la_h | ((r.w & kRecFirst) && la_h == 0 ? kFirst : 0) | ((r.w & kRecLast) && la_h == 1 ? kLast : 0) |
+                  kValid;
+        s.lv = LEVELS ? min((r.w >> 16) & 3, 2) : 0;
+        SBO_X3_STAGE(min((uint32_t)r.x, a_max), r.y, la_h, r.z, sl, burst);
         la_h ^= 1;
         if (la_h == 0) {
-            ++la_j;
             ++la_e;
-            if (la_j >= cnt) {
-                ++la_k;
-                la_j = 0;
-                if (la_k < k1) {
-                    la_d = desc_at(la_k);
-                    if (la_k % kDescWin == 0) SBO_DESC_WINDOW(la_k / kDescWin + 1);
-                }
-            }
-            if (la_e % kListWin == 0) SBO_LIST_WINDOW(la_e / kListWin + 1);
+            if (la_e % kRecWin == 0) SBO_REC_WINDOW(la_e / kRecWin + 1);
         }
         return s;
     };
 
     XStep s0 = stage(0, true), s1 = {0, 0, 0, 0}, s2 = {0, 0, 0, 0};
-    if (la_k < k1) s1 = stage(1, true);
+    if (la_e < e_end) s1 = stage(1, true);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
@@ -662,7 +658,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;
         if constexpr (STAMP) SBO_STAMP(t0);
         if (FRESH) flush();
-        const bool issue = la_k < k1;
+        const bool issue = la_e < e_end;
         const int nslot = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
         s2 = issue ? stage(nslot, false) : XStep{0, 0, 0, 0};
         // A pieces the staged tile's level needs (plane p = pieces p*kPieces/3 ..)
@@ -796,8 +792,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     }
 #undef SBO_STAMP
 #undef SBO_X3_STAGE
-#undef SBO_DESC_WINDOW
-#undef SBO_LIST_WINDOW
+#undef SBO_REC_WINDOW
 #undef SBO_DMA16
 }
 
@@ -882,13 +877,16 @@ hipError_t read_x3_stamps(double *out, int n) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_x3_stamps), h.data(), h.size() * sizeof(unsigned long long));
 }
 
-hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, const int4 *desc,
-                             const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
-                             const float *qy, int64_t m, int64_t ldp, float cexp, float m0, float *part, float *mean,
-                             int variant) {
+hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, const int4 *desc, const int4 *rec,
+                             const int *seg, int P, int n_items, int nI, const float *qx, const float *qy, int64_t m,
+                             int64_t ldp, float cexp, float m0, float *part, float *mean, int variant) {
+    // the largest tile offset a record may name (KiB): keeps every staged address inside ax3
+    const int64_t amax = (total_tiles(nI) - 1) * (2 * kXA / 1024);
+    if (nI <= 0 || amax > 0xffffffffll) return hipErrorInvalidValue;
+    const uint32_t a_max = (uint32_t)amax;
 #define SBO_X3_LAUNCH(NC, D) \
-    hipLaunchKernelGGL((predict_x3_kernel<NC, D>), dim3((unsigned)P), dim3(NC == 1 ? 512 : 256), 0, s, ax3, kc3, desc, tl, \
-                       seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean)
+    hipLaunchKernelGGL((predict_x3_kernel<NC, D>), dim3((unsigned)P), dim3(NC == 1 ? 512 : 256), 0, s, ax3, kc3, desc, rec, \
+                       seg, P, n_items, nI, a_max, qx, qy, m, ldp, cexp, m0, part, mean)
     switch (variant) {
         case 2: SBO_X3_LAUNCH(2, 16); break;   // four waves of 32 queries
         case 9: SBO_X3_LAUNCH(1, 0); break;    // A pieces in a burst at the top of the step
@@ -929,6 +927,9 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 38: SBO_X3_LAUNCH(1, 69655); break;  //   no K*, no A pieces, no outer sums
         case 39: SBO_X3_LAUNCH(1, 335920); break;  // variant 3 with phase stamps (sbo_debug_x3_stamps)
         case 41: SBO_X3_LAUNCH(1, 1122352); break;  // diagnostics: variant 3 with the K* split reduced to kh
+        // A/B (correct results, measured no faster: DESIGN.md section 10):
+        case 42: SBO_X3_LAUNCH(1, 73776 + 2097152); break;  // variant 3, one-product tiles straight into the outer sums
+        case 43: SBO_X3_LAUNCH(1, 73776 + 6291456); break;  //   and three-product tiles too
 #endif
         default: SBO_X3_LAUNCH(1, 73776); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead
     }

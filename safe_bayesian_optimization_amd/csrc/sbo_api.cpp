@@ -438,6 +438,7 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         plan.L = ctx->skip_log2;
     }
     plan.prod_full = ctx->kernel_variant >= 2 ? 6 : 1;
+    plan.records = ctx->kernel_variant >= 2;
 #ifdef SBO_DIAG
     // timing diagnostic (diagnostic build only): the drop-only plan
     // with every kept tile at level SBO_LVL_FORCE -- outside the error budget
@@ -494,9 +495,10 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         const int4 *desc = nullptr;
         const unsigned short *tl = nullptr;
         const int *seg = nullptr;
-        sbo::plan_views(ctx->npad, m, P, ctx->plan_work.as<void>(), &desc, &tl, &seg);
+        const int4 *rec = nullptr;
+        sbo::plan_views(ctx->npad, m, P, ctx->plan_work.as<void>(), &desc, &tl, &seg, &rec);
         Bracket br(ctx, ctx->ev_predict);
-        SBO_HIP(sbo::launch_predict_x3(ctx->stream, ctx->ax3.as<char>(), ctx->kc3.as<float>(), desc, tl, seg, P,
+        SBO_HIP(sbo::launch_predict_x3(ctx->stream, ctx->ax3.as<char>(), ctx->kc3.as<float>(), desc, rec, seg, P,
                                        (int)(nIc * ((m + sbo::kBN - 1) / sbo::kBN)), (int)nIc, qx, qy, m, ldp,
                                        sbo::exp2_coef_f((float)ctx->hyper.length_scale),
                                        (float)ctx->hyper.prior_mean, ctx->part.as<float>(), ctx->mean.as<float>(),

@@ -186,6 +186,7 @@ struct SkipPlan {
     float lg_tau_v = 0.0f;
     int levels = 0;     // with lgn: tiles may run at the reduced precision levels (split sweep)
     int prod_full = 1;  // MFMA products per full-precision tile (6: split sweep), for the counter
+    bool records = false;  // also write the split sweep's step records (plan_views' rec)
     // rank of a tile's two level increments against drops: log2(time a drop
     // saves / time the level step saves), per-tile sweep time at C4 of six,
     // three, one product(s) 18.6, 12.9, 9.9 ns (variants 22, 20, 21)
@@ -212,7 +213,7 @@ hipError_t launch_plan_cost(hipStream_t s, int64_t npad, int64_t m, int P, const
                             float *bcost, float *cost);
 // The plan's descriptors, tile lists and per-workgroup ranges inside `work`.
 void plan_views(int64_t npad, int64_t m, int P, const void *work, const int4 **desc, const unsigned short **tl,
-                const int **seg);
+                const int **seg, const int4 **rec = nullptr);
 // Split-operand (bf16 x3) predictive sweep, predict_x3.hip: the packed
 // operand split into three bf16 planes per half-tile and the per-k-tile
 // coordinates in natural order, for row blocks >= I0 (coordinates: all).
@@ -223,15 +224,21 @@ hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, 
 // the split operand's layout a kernel variant reads (1: the wide 32x32x16 shape)
 // tile-list entry of the plan: k-tile index | precision level code << kLevelShift
 constexpr int kLevelShift = 14;
+// Step record of the split sweep (plan_rec_kernel), one int4 per kept tile in
+// sweep order: x = the packed tile's offset in the split operand (KiB, two
+// half-tiles of 48), y = its k-tile's coordinate offset in kc3 (floats),
+// z = query block, w = row block | level code << 16 | first / last tile of
+// its item (kRecFirst, kRecLast).
+constexpr int kRecFirst = 1 << 20, kRecLast = 1 << 21;
 // the split sweeps that honour the plan's precision levels
-inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39 || variant == 41; }
+inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39 || variant == 41 || variant == 42 || variant == 43; }
 // Sweeps the product library accepts (all compute the full result; 3 is the
 // default).  The timing diagnostics (parts of the work left out, forced
 // precision levels, phase stamps) exist only in the diagnostic build
 // (-DSBO_DIAG, lib/libsbo_diag.so, selected by SBO_LIB for tools/).
 inline bool variant_allowed(int v) {
 #ifdef SBO_DIAG
-    return v >= 0 && v <= 41;
+    return v >= 0 && v <= 43;
 #else
     return v == 0 || v == 1 || v == 2 || v == 3 || v == 9 || v == 10 || v == 13 || v == 22;
 #endif
@@ -243,10 +250,9 @@ inline int x3_layout(int variant) { return (variant == 13 || variant == 14) ? 1 
 // Diagnostic build (SBO_OPT_KERNEL_VARIANT 39): summed phase cycles of the
 // split sweep since the last read (see g_x3_stamps), then reset.
 hipError_t read_x3_stamps(double *out, int n);
-hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, const int4 *desc,
-                             const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
-                             const float *qy, int64_t m, int64_t ldp, float cexp, float m0, float *part, float *mean,
-                             int variant);
+hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, const int4 *desc, const int4 *rec,
+                             const int *seg, int P, int n_items, int nI, const float *qx, const float *qy, int64_t m,
+                             int64_t ldp, float cexp, float m0, float *part, float *mean, int variant);
 // lgn[2 (tile_start(I) + t)] = log2 bounds (16 max row 1-norm, spectral,
 // Frobenius) of A_It, lgn[2 (..) + 1] = (16 max row 1-norm, spectral) of its
 // bf16 pieces A1 and A2 (f64 sums, rounded up) for row blocks I >= I0 (-1000
