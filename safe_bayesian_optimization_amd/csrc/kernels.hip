@@ -12,6 +12,8 @@
 //
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit,
 // so the f64 acquisition arithmetic is the node's plain IEEE double sequence.
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 
@@ -469,6 +471,16 @@ constexpr unsigned long long kPlanCountMask = (1ull << kPlanKeyShift) - 1ull;
 // (forced-level C4 sweeps: 20.6, 13.5, 10.6 ns per tile): the weight the
 // workgroup ranges and sbo_query_cost balance
 constexpr unsigned kLevelWeight0 = 64, kLevelWeight1 = 42, kLevelWeight2 = 33;
+// The mean's row block (the last) sweeps slower per tile than the others --
+// stamp build at C4 with every tile forced to one level: the XCD chunk that
+// holds it balanced at 125 / 107 / 100 % of the six- / three- / one-product
+// weights -- and lower row blocks somewhat faster (their A operand fits the
+// XCD's L2): tile weights of the mean's row block, and the slope, percent at
+// I = nI - 1 over I = 0, of a linear per-row-block factor (diagnostic build:
+// SBO_MEAN_W = "w0,w1,w2", SBO_RB_SLOPE)
+constexpr unsigned kMeanWeight0 = 80, kMeanWeight1 = 45, kMeanWeight2 = 33;
+__device__ unsigned g_mean_w[3] = {kMeanWeight0, kMeanWeight1, kMeanWeight2};
+__device__ unsigned g_rb_slope = 0;
 constexpr int kSteps = kBK / 4;          // 16x16x4 k steps per tile
 constexpr int kRowBlocks = kBM / 16;     // 16-row MFMA blocks per wave
 
@@ -913,8 +925,12 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
             const int n0 = __popcll(__ballot(code == 0)), n1 = __popcll(__ballot(code == 1)),
                       n2 = __popcll(__ballot(code == 2));
             cnt += n0 + n1 + n2;
-            wsum += kLevelWeight0 * n0 + kLevelWeight1 * n1 + kLevelWeight2 * n2;
+            wsum += I == nI - 1 ? g_mean_w[0] * n0 + g_mean_w[1] * n1 + g_mean_w[2] * n2
+                                : kLevelWeight0 * n0 + kLevelWeight1 * n1 + kLevelWeight2 * n2;
         }
+        if (g_rb_slope)
+            wsum = (unsigned)((unsigned long long)wsum * (100u * (unsigned)nI + g_rb_slope * (unsigned)I) /
+                              (100u * (unsigned)nI));
         const int64_t item = plan_item(I, nI, nQ, qb);
         if (lane == 0) {
             key[item] = (unsigned long long)cnt | ((cnt > 0 ? 1ull : 0ull) << kPlanKeyShift);
@@ -1711,6 +1727,17 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     auto *seg = reinterpret_cast<int *>(w + L.seg);
     auto *wkey = reinterpret_cast<unsigned long long *>(w + L.wkey);
     auto *wscan = reinterpret_cast<unsigned long long *>(w + L.wscan);
+#ifdef SBO_DIAG
+    if (const char *ev = getenv("SBO_MEAN_W")) {
+        unsigned v[3] = {kMeanWeight0, kMeanWeight1, kMeanWeight2};
+        if (sscanf(ev, "%u,%u,%u", &v[0], &v[1], &v[2]) == 3)
+            (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mean_w), v, sizeof(v), 0, hipMemcpyHostToDevice, s);
+    }
+    if (const char *ev = getenv("SBO_RB_SLOPE")) {
+        const unsigned v = (unsigned)std::max(0, atoi(ev));
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_rb_slope), &v, sizeof(v), 0, hipMemcpyHostToDevice, s);
+    }
+#endif
     const double ce = exp2_coef(ell);
     const float cexp = (float)ce;
     const float skip_d2 = cutoff_d2(skip.L, ce);

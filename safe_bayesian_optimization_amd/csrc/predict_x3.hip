@@ -30,6 +30,7 @@
 // the A pieces of stage i+2 in flight has retired them -- the K* of step
 // i+1 is computed during step i, beside its MFMAs.
 #include <cstdint>
+#include <cstdlib>
 #include <algorithm>
 #include <type_traits>
 #include <vector>
@@ -487,7 +488,7 @@ constexpr int kFirst = 2, kLast = 4, kValid = 8;
 template <int NC, int DIAG>
 __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     const char *__restrict__ ax3, const float *__restrict__ kc3, const int4 *__restrict__ desc,
-    const int4 *__restrict__ rec, const int *__restrict__ seg, int P, int n_items, int nI, uint32_t a_max,
+    const int4 *__restrict__ rec, const int *__restrict__ seg, int P, int n_items, int nI, uint32_t a_max, int rot,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp, float cexp, float m0,
     float *__restrict__ part, float *__restrict__ mean) {
     __shared__ __attribute__((aligned(16))) char smem[kXSmem];
@@ -502,9 +503,14 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     constexpr int kPieces = (kXA / 1024) / kLoaders;  // A pieces per loader wave per stage (6 or 12)
     static_assert(kPieces == 6 || kPieces == 12, "the end-of-step wait below counts 6 or 12 pieces");
     const int bid = blockIdx.x;
-    const int rng = (P % 8 == 0) ? (bid % 8) * (P / 8) + bid / 8 : bid;
+    // (rot: diagnostic build only -- XCD b % 8 takes chunk (b + rot) % 8)
+    const int rng = (P % 8 == 0) ? ((bid + rot) % 8) * (P / 8) + bid / 8 : bid;
     const int k0 = max(seg[rng], 0), k1 = min(seg[rng + 1], n_items);
     if (k0 >= k1) return;
+    // DIAG & 8388608: only the workgroup's span (first to last instruction), per wave
+    constexpr bool SPAN = (DIAG & 8388608) != 0;
+    unsigned long long span_t0 = 0;
+    if constexpr (SPAN) span_t0 = __builtin_amdgcn_s_memtime();
     const int tid = threadIdx.x, lane = tid & 63;
     const int lw = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave = loader index
     const int g = lane >> 4, r = lane & 15;
@@ -583,7 +589,11 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         la_h ^= 1;
         if (la_h == 0) {
             ++la_e;
-            if (la_e % kRecWin == 0) SBO_REC_WINDOW(la_e / kRecWin + 1);
+            // window w + 1 goes into the buffer of window w - 1 once entry
+            // 64 w + 1 is current: every wave read that buffer's last entry
+            // (64 w - 1) at least one barrier ago (at 64 w the slower waves
+            // may still be reading it in this same step)
+            if (la_e % kRecWin == 1) SBO_REC_WINDOW(la_e / kRecWin + 1);
         }
         return s;
     };
@@ -784,6 +794,14 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     } while (more);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
     flush();
+    if constexpr (SPAN) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        const int slot = bid * 8 + lw;
+        if (lane == 0 && slot < kStampSlots) {
+            g_x3_stamps[(size_t)slot * kStampFields + 5] = t1 - span_t0;
+            g_x3_stamps[(size_t)slot * kStampFields + 9] = 1;
+        }
+    }
     if constexpr (STAMP) {
         const int slot = bid * 8 + lw;
         if (lane == 0 && slot < kStampSlots)
@@ -865,14 +883,18 @@ hipError_t read_x3_stamps(double *out, int n) {
     hipError_t e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_x3_stamps), h.size() * sizeof(unsigned long long));
     if (e != hipSuccess) return e;
     for (int j = 0; j < n; ++j) out[j] = 0.0;
-    // out[0..11]: summed over all waves; out[12 + 12 w + j]: over wave index w of every workgroup
-    for (size_t sl = 0; sl < (size_t)kStampSlots; ++sl)
+    // out[0..11]: summed over all waves; out[12 + 12 w + j]: over wave index w
+    // of every workgroup; out[108 + b]: workgroup b's loop cycles (mean over its waves)
+    for (size_t sl = 0; sl < (size_t)kStampSlots; ++sl) {
         for (int j = 0; j < 12; ++j) {
             const double v = (double)h[sl * kStampFields + j];
             if (j < n) out[j] += v;
             const int o = 12 + 12 * (int)(sl % 8) + j;
             if (o < n) out[o] += v;
         }
+        const int o = 108 + (int)(sl / 8);
+        if (o < n) out[o] += (double)h[sl * kStampFields + 5] / 8.0;
+    }
     std::fill(h.begin(), h.end(), 0ull);  // reset for the next read
     return hipMemcpyToSymbol(HIP_SYMBOL(g_x3_stamps), h.data(), h.size() * sizeof(unsigned long long));
 }
@@ -884,9 +906,13 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
     const int64_t amax = (total_tiles(nI) - 1) * (2 * kXA / 1024);
     if (nI <= 0 || amax > 0xffffffffll) return hipErrorInvalidValue;
     const uint32_t a_max = (uint32_t)amax;
+    int rot = 0;
+#ifdef SBO_DIAG
+    if (const char *e = getenv("SBO_XCD_ROT")) rot = std::clamp(atoi(e), 0, 7);
+#endif
 #define SBO_X3_LAUNCH(NC, D) \
     hipLaunchKernelGGL((predict_x3_kernel<NC, D>), dim3((unsigned)P), dim3(NC == 1 ? 512 : 256), 0, s, ax3, kc3, desc, rec, \
-                       seg, P, n_items, nI, a_max, qx, qy, m, ldp, cexp, m0, part, mean)
+                       seg, P, n_items, nI, a_max, rot, qx, qy, m, ldp, cexp, m0, part, mean)
     switch (variant) {
         case 2: SBO_X3_LAUNCH(2, 16); break;   // four waves of 32 queries
         case 9: SBO_X3_LAUNCH(1, 0); break;    // A pieces in a burst at the top of the step
@@ -930,6 +956,7 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         // A/B (correct results, measured no faster: DESIGN.md section 10):
         case 42: SBO_X3_LAUNCH(1, 73776 + 2097152); break;  // variant 3, one-product tiles straight into the outer sums
         case 43: SBO_X3_LAUNCH(1, 73776 + 6291456); break;  //   and three-product tiles too
+        case 46: SBO_X3_LAUNCH(1, 73776 + 8388608); break;  // variant 3 recording only each workgroup's span
 #endif
         default: SBO_X3_LAUNCH(1, 73776); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead
     }

@@ -19,6 +19,7 @@ def main():
     p.add_argument("--config", default="C4")
     p.add_argument("--variant", type=int, default=39)
     p.add_argument("--opt", nargs="*", default=[], help="NAME=VAL sbo options, e.g. SBO_OPT_TILE_SKIP=0")
+    p.add_argument("--save", default="", help="save the per-workgroup loop cycles (.npy)")
     a = p.parse_args()
     import torch
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
@@ -35,13 +36,14 @@ def main():
     gm.fit(t(wl.x), t(wl.y), t(wl.obs))
     qx, qy = t(wl.qx), t(wl.qy)
     lib = N.lib()
-    buf = (ctypes.c_double * 108)()
+    nwg = 1024
+    buf = (ctypes.c_double * (108 + nwg))()
     for v in (3, a.variant):
         gm.set_option(N.SBO_OPT_KERNEL_VARIANT, v)
         gm.tick(qx, qy, wl.beta, wl.f_min)
-    lib.sbo_debug_x3_stamps(gm.ctx.handle, buf, 108)  # reset
+    lib.sbo_debug_x3_stamps(gm.ctx.handle, buf, 108 + nwg)  # reset
     gm.tick(qx, qy, wl.beta, wl.f_min)
-    lib.sbo_debug_x3_stamps(gm.ctx.handle, buf, 108)
+    lib.sbo_debug_x3_stamps(gm.ctx.handle, buf, 108 + nwg)
     c = list(buf)
     tot = c[5]
     names = ["step top (flush, stage)", "half-step body", "item end", "vmcnt wait", "barrier"]
@@ -57,6 +59,17 @@ def main():
         cw = c[12 + 12 * w: 24 + 12 * w]
         hw = max(cw[9] + cw[10] + cw[11], 1)
         print(f"  wave {w}: " + " / ".join(f"{cw[i] / hw:6.0f}" for i in range(5)))
+    wg = np.array(c[108:108 + nwg])
+    wg = wg[:np.count_nonzero(wg)]
+    if a.save:
+        np.save(a.save, wg)
+    if wg.size % 8 == 0 and wg.size:
+        x = wg.reshape(-1, 8)  # workgroup b runs on XCD b % 8
+        print("per XCD mean/mean: " + " ".join(f"{v:.3f}" for v in x.mean(0) / wg.mean()) +
+              "  | within-XCD max/XCD-mean: " + " ".join(f"{v:.3f}" for v in x.max(0) / x.mean(0)))
+    if wg.size:
+        print(f"workgroups {wg.size}: loop cycles mean {wg.mean():.4g}, max/mean {wg.max() / wg.mean():.3f}, "
+              f"min/mean {wg.min() / wg.mean():.3f}, p90/mean {np.percentile(wg, 90) / wg.mean():.3f}")
 
 
 if __name__ == "__main__":
