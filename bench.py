@@ -59,8 +59,8 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=None,
                    help="ranks (one per GPU); > 1 without WORLD_SIZE launches them itself")
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
     p.add_argument("--n", type=int, default=None, help="override N")
     p.add_argument("--grid", type=int, default=None, help="override grid side")

@@ -521,7 +521,9 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     // only per-lane operand is the byte offset lane*16
     const uint32_t voff = (uint32_t)lane * 16u;
     const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
-    const int ldr = HALF_LOAD ? lw - 4 : lw;  // loader index (< 0: no A pieces)
+    // (DIAG & 16777216 with HALF_LOAD: waves 0-3 load instead -- the older
+    // wave of each SIMD pair, which waits at the barrier for the younger)
+    const int ldr = HALF_LOAD ? ((DIAG & 16777216) ? (lw < 4 ? lw : -1) : lw - 4) : lw;  // loader index (< 0: no A pieces)
     const bool is_loader = ldr >= 0;
     const uint32_t lds_wave = lds_smem + (uint32_t)(is_loader ? ldr : 0) * 1024u;
     const uint32_t lds_rwin = lds_smem + (uint32_t)kXWin;
@@ -957,6 +959,8 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 42: SBO_X3_LAUNCH(1, 73776 + 2097152); break;  // variant 3, one-product tiles straight into the outer sums
         case 43: SBO_X3_LAUNCH(1, 73776 + 6291456); break;  //   and three-product tiles too
         case 46: SBO_X3_LAUNCH(1, 73776 + 8388608); break;  // variant 3 recording only each workgroup's span
+        case 47: SBO_X3_LAUNCH(1, 73776 + 1024 + 16777216); break;  // variant 3, A stage loaded by waves 0-3 only
+        case 48: SBO_X3_LAUNCH(1, 73776 + 1024); break;     // variant 3, A stage loaded by waves 4-7 only
 #endif
         default: SBO_X3_LAUNCH(1, 73776); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead
     }
