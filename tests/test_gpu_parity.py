@@ -821,9 +821,11 @@ def test_query_cost_is_the_plan(mapper):
     lib.sbo_profile(gm.ctx.handle, 0)
     tiles = w.value / (2.0 * 256 * 128 * 64)
     assert tiles > 0 and sum(lv) == round(tiles)
-    # tiles weighted by their precision level's sweep time (64 / 42 / 33 of 64)
+    # tiles weighted by their precision level's sweep time (64 / 42 / 33 of 64;
+    # the mean's row block 80 / 45 / 33: its tiles sweep slower, kernels.hip)
     weighted = (64 * lv[0] + 42 * lv[1] + 33 * lv[2]) / 64.0
-    assert abs(float(cost.astype(np.float64).sum()) - weighted) <= 1e-4 * weighted
+    total = float(cost.astype(np.float64).sum())
+    assert weighted * (1 - 1e-4) <= total <= (80 * lv[0] + 45 * lv[1] + 33 * lv[2]) / 64.0 * (1 + 1e-4)
     assert np.array_equal(mu0, mu1) and np.array_equal(sd0, sd1)
 
 
