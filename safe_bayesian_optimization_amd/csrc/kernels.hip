@@ -144,61 +144,112 @@ __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__r
 
 // ---- blocked Cholesky (a2), the factorization step rocSOLVER's spotrf
 // spends most of its time in (unblocked potf2 panels, one small workgroup
-// each): the kb x kb diagonal block of step k0, in LDS, right-looking by
-// columns (column j: sqrt of the pivot, scale the column into a separate
-// array, rank-1 update of the trailing lower triangle with 256 / kCholNB
-// threads per row and four independent updates in flight per thread).  f32
-// as spotrf, correctly rounded sqrt and division.  A pivot that is not > 0
-// (or NaN) stops the factorization: info = k0 + j + 1 (the leading minor,
-// rocSOLVER's convention); later blocks see info != 0 and leave their data
-// alone.  Column-major, lda = ld; only i >= j is written.
+// each): the kb x kb diagonal block of step k0, in LDS, right-looking in
+// panels of kCholPanel columns.  A panel is factored by wave 0 alone in
+// registers (lane l holds rows jb + l and jb + 64 + l of the panel; the pivot
+// row's values come from their lane by v_readlane, no barrier per column);
+// the trailing lower triangle then takes the panel's rank-kCholPanel update
+// from all four waves in 4 x 4 element tiles.  Every element sees the same
+// fmaf sequence as the column-by-column algorithm (column j ascending,
+// fmaf(-L[i][j], L[l][j], a)), so the factor is bitwise that of a plain
+// right-looking Cholesky of the block.  f32 as spotrf, correctly rounded sqrt
+// and division.  A pivot that is not > 0 (or NaN) stops the factorization:
+// info = k0 + j + 1 (the leading minor, rocSOLVER's convention); later blocks
+// see info != 0 and leave their data alone.  Column-major, lda = ld; only
+// i >= j is written.
+constexpr int kCholPanel = 8;
+__device__ __forceinline__ float lane_value(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, int64_t ld, int kb, int64_t k0,
                                                         int *__restrict__ info) {
-    constexpr int T = 256 / kCholNB;  // threads per row
+    static_assert(kCholNB <= 128, "two panel rows per lane of wave 0");
     __shared__ float a[kCholNB][kCholNB + 1];
-    __shared__ float col[kCholNB];   // the scaled column j (a separate array: the update's reads never alias its writes)
+    __shared__ int s_bad;
     if (*info != 0) return;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int e = tid; e < kb * kb; e += 256) {
         const int i = e % kb, j = e / kb;
         if (i >= j) a[i][j] = A[i + (int64_t)j * ld];
     }
+    if (tid == 0) s_bad = 0;
     __syncthreads();
-    int bad = 0;
-    const int r = tid % kCholNB, par = tid / kCholNB;
-    for (int j = 0; j < kb; ++j) {
-        const float djj = a[j][j];
-        if (!(djj > 0.0f) || !(djj < __builtin_huge_valf())) {   // uniform: every thread read the same pivot
-            bad = j + 1;
-            break;
-        }
-        const float d = __fsqrt_rn(djj);
-        for (int i = j + 1 + tid; i < kb; i += 256) {
-            const float v = __fdiv_rn(a[i][j], d);
-            a[i][j] = v;
-            col[i] = v;
+    for (int jb = 0; jb < kb; jb += kCholPanel) {
+        const int w = min(kCholPanel, kb - jb);
+        if (wave == 0) {
+            const int r0 = jb + lane, r1 = jb + 64 + lane;
+            float p0[kCholPanel], p1[kCholPanel];
+#pragma unroll
+            for (int c = 0; c < kCholPanel; ++c) {
+                p0[c] = (r0 < kb && c < w) ? a[r0][jb + c] : 0.0f;
+                p1[c] = (r1 < kb && c < w) ? a[r1][jb + c] : 0.0f;
+            }
+            int bad = 0;
+#pragma unroll
+            for (int c = 0; c < kCholPanel; ++c) {
+                if (c >= w || bad) continue;   // uniform
+                const int j = jb + c;
+                const float djj = lane_value(p0[c], c);   // row j is lane c's first row
+                if (!(djj > 0.0f) || !(djj < __builtin_huge_valf())) {
+                    bad = j + 1;
+                    continue;
+                }
+                const float d = __fsqrt_rn(djj);
+                if (r0 > j) p0[c] = __fdiv_rn(p0[c], d);
+                else if (r0 == j) p0[c] = d;
+                p1[c] = __fdiv_rn(p1[c], d);   // r1 > j always
+#pragma unroll
+                for (int c2 = c + 1; c2 < kCholPanel; ++c2) {
+                    if (c2 >= w) continue;
+                    const float lc2 = lane_value(p0[c], c2);   // L[jb + c2][j], lane c2's (already scaled)
+                    if (r0 >= jb + c2) p0[c2] = fmaf(-p0[c], lc2, p0[c2]);
+                    p1[c2] = fmaf(-p1[c], lc2, p1[c2]);
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < kCholPanel; ++c) {
+                if (c < w && r0 < kb && r0 >= jb + c) a[r0][jb + c] = p0[c];
+                if (c < w && r1 < kb) a[r1][jb + c] = p1[c];
+            }
+            if (lane == 0 && bad) s_bad = bad;
         }
         __syncthreads();
-        if (tid == 0) a[j][j] = d;
-        const int i = j + 1 + r;
-        if (i < kb) {
-            const float aij = col[i];
-            float *ai = a[i];
-            int l = j + 1 + par;
-            for (; l + 3 * T <= i; l += 4 * T) {   // four independent updates in flight
-                const float c0 = col[l], c1 = col[l + T], c2 = col[l + 2 * T], c3 = col[l + 3 * T];
-                const float v0 = ai[l], v1 = ai[l + T], v2 = ai[l + 2 * T], v3 = ai[l + 3 * T];
-                ai[l] = fmaf(-aij, c0, v0);
-                ai[l + T] = fmaf(-aij, c1, v1);
-                ai[l + 2 * T] = fmaf(-aij, c2, v2);
-                ai[l + 3 * T] = fmaf(-aij, c3, v3);
-            }
-            for (; l <= i; l += T) ai[l] = fmaf(-aij, col[l], ai[l]);
+        if (s_bad) break;
+        // rank-w update of the trailing lower triangle [t0, kb) in 4 x 4 tiles
+        const int t0 = jb + w, n2 = kb - t0;
+        const int nt = (n2 + 3) >> 2, ntiles = nt * (nt + 1) / 2;
+        for (int q = tid; q < ntiles; q += 256) {
+            int ti = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+            while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
+            while (ti * (ti + 1) / 2 > q) --ti;
+            const int tl = q - ti * (ti + 1) / 2;
+            const int i0 = t0 + 4 * ti, l0 = t0 + 4 * tl;
+            float li[4][kCholPanel], ll[4][kCholPanel];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < kCholPanel; ++c) {
+                    li[r][c] = (i0 + r < kb && c < w) ? a[i0 + r][jb + c] : 0.0f;
+                    ll[r][c] = (l0 + r < kb && c < w) ? a[l0 + r][jb + c] : 0.0f;
+                }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = i0 + r, l = l0 + u;
+                    if (i < kb && l <= i) {
+                        float v = a[i][l];
+#pragma unroll
+                        for (int c = 0; c < kCholPanel; ++c)
+                            if (c < w) v = fmaf(-li[r][c], ll[u][c], v);
+                        a[i][l] = v;
+                    }
+                }
         }
         __syncthreads();
     }
-    if (bad) {
-        if (tid == 0) atomicCAS(info, 0, (int)(k0 + bad));
+    if (s_bad) {
+        if (tid == 0) atomicCAS(info, 0, (int)(k0 + s_bad));
         return;
     }
     for (int e = tid; e < kb * kb; e += 256) {
