@@ -18,13 +18,14 @@ def main():
     p.add_argument("--variants", type=int, nargs="+", default=[0, 1])
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--opt", nargs="*", default=[])
+    p.add_argument("--box", action="store_true", help="the config's N and grid on the lpsc.yaml box (stress variant)")
     a = p.parse_args()
     import torch
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
     from safe_bayesian_optimization_amd import _native as N
-    from safe_bayesian_optimization_amd.terrain import CONFIGS
+    from safe_bayesian_optimization_amd.terrain import CONFIGS, synthetic_box
     n, gw, gh = CONFIGS[a.config]
-    wl = synthetic(n, gw, gh, seed=0)
+    wl = synthetic_box(n, gw, gh, seed=0) if a.box else synthetic(n, gw, gh, seed=0)
     dev = torch.device("cuda:0")
     t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
     gm = TerrainMapper(0, wl.hyper)
