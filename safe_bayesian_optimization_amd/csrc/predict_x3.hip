@@ -169,6 +169,8 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
     // DIAG & 4194304 three products as well
     constexpr bool DIR = (EL == 2 && (DIAG & 2097152)) || (EL == 1 && (DIAG & 4194304));
     constexpr int LAG = (DIAG & 32768) ? 2 : (EL == 0 ? 2 : (EL == 1 ? 4 : 8));
+    // DIAG & 33554432: the next pair's coordinates read at ph 1 instead of ph 3
+    constexpr bool EARLY_XY = (DIAG & 33554432) != 0;
     const int npu = __builtin_amdgcn_readfirstlane(npieces);
     // A fragments of row block r are read AH blocks ahead of their use: the
     // fewer MFMAs a block has, the more blocks ahead (DIAG & 65536: 4 at one
@@ -207,6 +209,11 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                 SBO_PIN(ev);
                 if (ph == 0) e[c].x = ev; else e[c].y = ev;
             }
+            // EARLY_XY: the next pair's x, y two row blocks earlier than at ph 3
+            if (EARLY_XY && ph == 1 && i < 3) {
+                xk = lds_f2(pcn + g * 32 + (i + 1) * 8);
+                yk = lds_f2(pcn + 128 + g * 32 + (i + 1) * 8);
+            }
         } else if (ph == 2) {
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
@@ -236,8 +243,10 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                 }
             }
             if (i < 3) {
-                xk = lds_f2(pcn + g * 32 + (i + 1) * 8);
-                yk = lds_f2(pcn + 128 + g * 32 + (i + 1) * 8);
+                if (!EARLY_XY) {
+                    xk = lds_f2(pcn + g * 32 + (i + 1) * 8);
+                    yk = lds_f2(pcn + 128 + g * 32 + (i + 1) * 8);
+                }
                 ak = lds_f2(pcn + 256 + g * 32 + (i + 1) * 8);
             }
         }
@@ -953,16 +962,17 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 36: SBO_X3_LAUNCH(1, 69651); break;  //   1 product, no next-step K*, no A pieces
         case 37: SBO_X3_LAUNCH(1, 70163); break;  //   and no barrier
         case 38: SBO_X3_LAUNCH(1, 69655); break;  //   no K*, no A pieces, no outer sums
-        case 39: SBO_X3_LAUNCH(1, 335920); break;  // variant 3 with phase stamps (sbo_debug_x3_stamps)
+        case 39: SBO_X3_LAUNCH(1, 335920 + 33554432); break;  // variant 3 with phase stamps (sbo_debug_x3_stamps)
         case 41: SBO_X3_LAUNCH(1, 1122352); break;  // diagnostics: variant 3 with the K* split reduced to kh
         // A/B (correct results, measured no faster: DESIGN.md section 10):
         case 42: SBO_X3_LAUNCH(1, 73776 + 2097152); break;  // variant 3, one-product tiles straight into the outer sums
         case 43: SBO_X3_LAUNCH(1, 73776 + 6291456); break;  //   and three-product tiles too
-        case 46: SBO_X3_LAUNCH(1, 73776 + 8388608); break;  // variant 3 recording only each workgroup's span
+        case 46: SBO_X3_LAUNCH(1, 73776 + 33554432 + 8388608); break;  // variant 3 recording only each workgroup's span
         case 47: SBO_X3_LAUNCH(1, 73776 + 1024 + 16777216); break;  // variant 3, A stage loaded by waves 0-3 only
         case 48: SBO_X3_LAUNCH(1, 73776 + 1024); break;     // variant 3, A stage loaded by waves 4-7 only
+        case 49: SBO_X3_LAUNCH(1, 73776); break;  // variant 3 with the next K* coordinates read at ph 3 (round-2 default)
 #endif
-        default: SBO_X3_LAUNCH(1, 73776); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead
+        default: SBO_X3_LAUNCH(1, 73776 + 33554432); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead, next coordinates at ph 1
     }
 #undef SBO_X3_LAUNCH
     return hipGetLastError();
