@@ -588,8 +588,11 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     const char *a_base = ax3 + (is_loader ? ldr : 0) * 1024;
     const char *a_src = ax3;  // this wave's A pieces of the last staged step (spread mode)
     uint32_t a_dst = 0;
+    // the record of entry la_e, read when la_e became current (one stage call
+    // ahead of its use: the LDS latency off the step top)
+    int4 r_cur = rec_at(la_e);
     auto stage = [&](int sl, bool burst) {
-        const int4 r = rec_at(la_e);
+        const int4 r = r_cur;
         XStep s;
         s.I = min(r.w & 0xffff, nI - 1);
         s.qb = r.z;
@@ -605,6 +608,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
             // (64 w - 1) at least one barrier ago (at 64 w the slower waves
             // may still be reading it in this same step)
             if (la_e % kRecWin == 1) SBO_REC_WINDOW(la_e / kRecWin + 1);
+            if (la_e < e_end) r_cur = rec_at(la_e);
         }
         return s;
     };
