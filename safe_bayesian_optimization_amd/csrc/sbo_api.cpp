@@ -268,13 +268,24 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)b, L22i,
                                       (rocblas_int)ld, info));
             SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
-            // T = L21 L11^-1, then T = -L22^-1 T
-            SBO_BLAS(rocblas_dtrmm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_none,
-                                   rocblas_diagonal_non_unit, (rocblas_int)b, (rocblas_int)n_old, &one, Li,
-                                   (rocblas_int)ld, T, (rocblas_int)ld, T, (rocblas_int)ld));
-            SBO_BLAS(rocblas_dtrmm(ctx->blas, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none,
-                                   rocblas_diagonal_non_unit, (rocblas_int)b, (rocblas_int)n_old, &minus_one, L22i,
-                                   (rocblas_int)ld, T, (rocblas_int)ld, T, (rocblas_int)ld));
+            // S = L21 L11^-1, then T = -L22^-1 S, as two dgemms on the
+            // triangles with their zero halves (one f64 MFMA GEMM each:
+            // rocBLAS's in-place dtrmm ran as ~200 small launches per append).
+            // The strictly upper part of L^-1 is zero: widen() writes it for
+            // the initial inverse and for L22^-1, rocSOLVER dtrtri leaves it,
+            // and the columns an append adds are zeroed above the new rows here.
+            SBO_HIP(hipMemset2DAsync(Li + n_old * ld, sizeof(double) * (size_t)ld, 0, sizeof(double) * (size_t)n_old,
+                                     (size_t)b, ctx->stream));
+            // (sized by the capacity, so that the appends of a streaming loop do not regrow it)
+            SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)sbo::round_up(b, 256) * (size_t)ld));
+            double *S = ctx->scratch.as<double>();
+            const double zero = 0.0;
+            SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)b,
+                                   (rocblas_int)n_old, (rocblas_int)n_old, &one, T, (rocblas_int)ld, Li,
+                                   (rocblas_int)ld, &zero, S, (rocblas_int)b));
+            SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)b,
+                                   (rocblas_int)n_old, (rocblas_int)b, &minus_one, L22i, (rocblas_int)ld, S,
+                                   (rocblas_int)b, &zero, T, (rocblas_int)ld));
         } else {
             SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)ld * (size_t)ld));
             Li = ctx->Linv.as<double>();
@@ -707,10 +718,18 @@ SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, cons
     SBO_BLAS(rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
                            rocblas_diagonal_non_unit, (rocblas_int)b, (rocblas_int)n0, &one, L, (rocblas_int)ld, L21,
                            (rocblas_int)ld));
-    SBO_BLAS(rocblas_ssyrk(ctx->blas, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)b, (rocblas_int)n0,
-                           &minus_one, L21, (rocblas_int)ld, &one, L22, (rocblas_int)ld));
+    // K22 -= L21 L21^T as a full b x b sgemm (rocBLAS's ssyrk ran its
+    // small-n kernels at ~250 us here; the strict upper half it also writes
+    // is never read), then the block's own factorization
+    SBO_BLAS(rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)b,
+                           (rocblas_int)b, (rocblas_int)n0, &minus_one, L21, (rocblas_int)ld, L21, (rocblas_int)ld,
+                           &one, L22, (rocblas_int)ld));
     rocblas_int *info = ctx->info.as<rocblas_int>();
-    SBO_BLAS(rocsolver_spotrf(ctx->blas, rocblas_fill_lower, (rocblas_int)b, L22, (rocblas_int)ld, info));
+    if (ctx->chol_blocked) {
+        if (sbo_status st = blocked_potrf(ctx, L22, b, ld, info); st != SBO_OK) return st;
+    } else {
+        SBO_BLAS(rocsolver_spotrf(ctx->blas, rocblas_fill_lower, (rocblas_int)b, L22, (rocblas_int)ld, info));
+    }
     rocblas_int hinfo = 0;
     SBO_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
