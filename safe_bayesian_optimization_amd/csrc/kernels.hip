@@ -310,7 +310,14 @@ __device__ __forceinline__ float split_piece(float a, int plane) {
 //           plane by plane in tile_increments.
 // The plan pairs the row-sum bounds with the largest K* of the tile and the
 // spectral ones with a bound on |k|_2 from the tile's points.  One workgroup
-// per tile, f64 arithmetic; the three matrices one after the other.
+// per tile, f64 arithmetic; the three matrices one after the other.  The
+// Gram matrix and its squarings are f64 MFMA products
+// (v_mfma_f64_16x16x4_f64; wave w owns rows 16w .. 16w+15 of G, four 16 x 16
+// accumulators).
+typedef double f64x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f64x4_t mfma_f64(double a, double b, f64x4_t c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
 __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
                                                         float4 *__restrict__ lgn) {
     __shared__ float at[kBM * kBK];            // the tile (or one of its pieces), [row][k]  (64 KiB)
@@ -319,8 +326,7 @@ __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict_
     __shared__ double red[2][kBM / 64];
     const int64_t tile = t0 + blockIdx.x;
     const float *t = aug + tile * kTileFloats;
-    const int tid = threadIdx.x;
-    const int gi = tid >> 2, gj = (tid & 3) * 16;  // G[i][j], thread: i = tid / 4, j = 16 (tid % 4) + 0..15
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     float out[6];                                // (rows, spectral) of A; of A1; of A2
     double lg_fro_a = -1000.0;
 #pragma unroll
@@ -338,16 +344,21 @@ __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict_
         if ((tid & 63) == 0) red[0][tid >> 6] = s;
         __syncthreads();
         {
-            double acc[16];
+            // G = A^T A: lane l of wave w feeds A^T[i = 16w + (l&15)][r] and
+            // A[r][j = 16 bj + (l&15)] at r = r0 + (l>>4)
+            f64x4_t acc[4];
 #pragma unroll
-            for (int c = 0; c < 16; ++c) acc[c] = 0.0;
-            for (int r = 0; r < kBM; ++r) {
-                const double ai = (double)at[r * kBK + gi];
+            for (int bj = 0; bj < 4; ++bj) acc[bj] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+            for (int r0 = 0; r0 < kBM; r0 += 4) {
+                const float *row = at + (r0 + (lane >> 4)) * kBK + (lane & 15);
+                const double a = (double)row[16 * wave];
 #pragma unroll
-                for (int c = 0; c < 16; ++c) acc[c] = fma(ai, (double)at[r * kBK + gj + c], acc[c]);
+                for (int bj = 0; bj < 4; ++bj) acc[bj] = mfma_f64(a, (double)row[16 * bj], acc[bj]);
             }
 #pragma unroll
-            for (int c = 0; c < 16; ++c) gm[gi * kBK + gj + c] = acc[c];
+            for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) gm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = acc[bj][v];
         }
         __syncthreads();
         const double fro2 = [&] {  // trace G = |A|_F^2 (every thread reads it)
@@ -369,16 +380,22 @@ __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict_
             __syncthreads();
             if (!(mx > 0.0)) break;
             const int ex = ilogb(mx);
-            double acc[16];
+            // G' = 2^-ex G in place (exact), then hm = G'^2 by MFMA
+            for (int i = tid; i < kBK * kBK; i += kBM) gm[i] = ldexp(gm[i], -ex);
+            __syncthreads();
+            f64x4_t acc[4];
 #pragma unroll
-            for (int c = 0; c < 16; ++c) acc[c] = 0.0;
-            for (int k = 0; k < kBK; ++k) {
-                const double g1 = ldexp(gm[gi * kBK + k], -ex);
+            for (int bj = 0; bj < 4; ++bj) acc[bj] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+            for (int k0 = 0; k0 < kBK; k0 += 4) {
+                const double a = gm[(16 * wave + (lane & 15)) * kBK + k0 + (lane >> 4)];
+                const double *brow = gm + (k0 + (lane >> 4)) * kBK + (lane & 15);
 #pragma unroll
-                for (int c = 0; c < 16; ++c) acc[c] = fma(g1, ldexp(gm[k * kBK + gj + c], -ex), acc[c]);
+                for (int bj = 0; bj < 4; ++bj) acc[bj] = mfma_f64(a, brow[16 * bj], acc[bj]);
             }
 #pragma unroll
-            for (int c = 0; c < 16; ++c) hm[gi * kBK + gj + c] = acc[c];
+            for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) hm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = acc[bj][v];
             e8 = 2.0 * (e8 + (double)ex);  // (2^e G')^2 = 2^(2e) G'^2
             __syncthreads();
             for (int i = tid; i < kBK * kBK; i += kBM) gm[i] = hm[i];
