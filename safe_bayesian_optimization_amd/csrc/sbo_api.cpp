@@ -378,29 +378,68 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
 }
 
 // Factor K in L (already filled, lda = cap) and refresh the operand.
-// Right-looking blocked Cholesky of the n x n lower triangle at L (lda = ld):
-// per step of kCholNB columns the diagonal block in one workgroup
-// (chol_diag_kernel), the panel below it by rocBLAS strsm (L21 = A21 L11^-T)
-// and the trailing update by ssyrk (A22 -= L21 L21^T) -- the same
-// factorization as spotrf, without its unblocked potf2 panels (which were 23 %
-// of a C4 fit, profiles/r2_c4_fit_kernel_stats.csv).  info: rocSOLVER's.
+// Right-looking blocked Cholesky of the n x n lower triangle at L (lda = ld)
+// in steps of kCholNB columns: the diagonal block in one workgroup
+// (chol_diag_kernel), the panel below it by rocBLAS strsm (L21 = A21 L11^-T),
+// the trailing update A22 -= L21 L21^T -- the same factorization as spotrf,
+// without its unblocked potf2 panels (which were 23 % of a C4 fit).  With
+// look-ahead: the trailing update is split into the next block column (an
+// sgemm on `stream`, followed at once by the next diagonal block and panel)
+// and the rest (ssyrk on aux_stream), so the one-CU diagonal kernel runs
+// beside the big update instead of between updates.  Event order: the rest
+// of step k waits for step k's panel; the next block column of step k + 1
+// waits for the rest of step k (which also wrote that column).  info:
+// rocSOLVER's.
 sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_int *info) {
     SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), ctx->stream));
     SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
+    if (!ctx->aux_stream) {
+        SBO_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+        SBO_HIP(hipEventCreateWithFlags(&ctx->ev_panel, hipEventDisableTiming));
+        SBO_HIP(hipEventCreateWithFlags(&ctx->ev_trail, hipEventDisableTiming));
+    }
     const float one = 1.0f, minus_one = -1.0f;
+    auto on = [&](hipStream_t st) { return rocblas_set_stream(ctx->blas, st); };
+    SBO_HIP(sbo::launch_chol_diag(ctx->stream, L, ld, (int)std::min<int64_t>(sbo::kCholNB, n), 0, info));
+    bool trail_pending = false;
+    sbo_status st = SBO_OK;
     for (int64_t k = 0; k < n; k += sbo::kCholNB) {
         const int64_t kb = std::min<int64_t>(sbo::kCholNB, n - k);
-        float *L11 = L + k + k * ld;
-        SBO_HIP(sbo::launch_chol_diag(ctx->stream, L11, ld, (int)kb, k, info));
         const int64_t m2 = n - k - kb;
         if (m2 <= 0) break;
-        float *A21 = L11 + kb, *A22 = L11 + kb + kb * ld;
-        SBO_BLAS(rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
-                               rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11, (rocblas_int)ld,
-                               A21, (rocblas_int)ld));
-        SBO_BLAS(rocblas_ssyrk(ctx->blas, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)m2, (rocblas_int)kb,
-                               &minus_one, A21, (rocblas_int)ld, &one, A22, (rocblas_int)ld));
+        float *L11 = L + k + k * ld, *A21 = L11 + kb;
+        const int64_t kb2 = std::min<int64_t>(sbo::kCholNB, m2);   // the next block column
+        float *C1 = L11 + kb + kb * ld;                             // its rows k + kb ..
+        if (on(ctx->stream) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
+        if (rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                          rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11, (rocblas_int)ld,
+                          A21, (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
+        if (hipEventRecord(ctx->ev_panel, ctx->stream) != hipSuccess ||
+            (trail_pending && hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0) != hipSuccess)) { st = SBO_E_DEVICE; break; }
+        if (rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m2,
+                          (rocblas_int)kb2, (rocblas_int)kb, &minus_one, A21, (rocblas_int)ld, A21, (rocblas_int)ld,
+                          &one, C1, (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
+        if (sbo::launch_chol_diag(ctx->stream, C1, ld, (int)kb2, k + kb, info) != hipSuccess) { st = SBO_E_DEVICE; break; }
+        const int64_t m3 = m2 - kb2;
+        trail_pending = false;
+        if (m3 > 0) {
+            if (hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0) != hipSuccess ||
+                on(ctx->aux_stream) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
+            if (rocblas_ssyrk(ctx->blas, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)m3, (rocblas_int)kb,
+                              &minus_one, A21 + kb2, (rocblas_int)ld, &one, C1 + kb2 + kb2 * ld,
+                              (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
+            trail_pending = true;
+            if (hipEventRecord(ctx->ev_trail, ctx->aux_stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
+        }
     }
+    // everything after the factorization runs on `stream`
+    if (on(ctx->stream) != rocblas_status_success && st == SBO_OK) st = SBO_E_DEVICE;
+    if (st != SBO_OK) {
+        (void)hipStreamSynchronize(ctx->aux_stream);
+        ctx->err = "blocked Cholesky: a rocBLAS or HIP call failed";
+        return st;
+    }
+    if (trail_pending) SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
     return SBO_OK;
 }
 
@@ -607,6 +646,10 @@ SBO_API void sbo_destroy(sbo_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     recycle_events(ctx);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
+    if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
+    if (ctx->ev_trail) (void)hipEventDestroy(ctx->ev_trail);
+    if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
     if (ctx->blas) rocblas_destroy_handle(ctx->blas);
     if (ctx->host_key) (void)hipHostFree(ctx->host_key);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);

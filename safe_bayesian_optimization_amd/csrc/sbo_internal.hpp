@@ -80,6 +80,10 @@ struct sbo_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     rocblas_handle blas = nullptr;
+    // the blocked Cholesky's look-ahead: trailing updates on a second stream
+    // (created on first use), ordered against `stream` by two events
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t ev_panel = nullptr, ev_trail = nullptr;
     std::string err;
 
     // fitted model

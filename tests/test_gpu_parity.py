@@ -196,6 +196,21 @@ def strtrs_var_error(gm, wl, ovar):
     return nrel(h.sf2 - (V * V).sum(0), ovar)
 
 
+def sgemv_mean_error(gm, wl, omu):
+    """Normwise mean error of the reference class's f32 mean, m0 + K*^T alpha
+    as one f32 matrix-vector product (BLAS sgemv, f32 accumulation) on the
+    device's own alpha and the f32 K* -- the yardstick where K is badly
+    conditioned (|alpha| large, the sum cancels)."""
+    h = wl.hyper
+    _, alpha = gm.factor()
+    o = gm.order()
+    xs, ys, qx, qy = (f32(v).astype(np.float64) for v in (wl.x[o], wl.y[o], wl.qx, wl.qy))
+    Ks = np.exp(-((xs[:, None] - qx[None, :]) ** 2 + (ys[:, None] - qy[None, :]) ** 2)
+                / (2 * h.length_scale ** 2)).astype(np.float32)
+    mu32 = np.float32(h.prior_mean) + Ks.T @ (np.float32(h.sf2) * alpha.astype(np.float32))
+    return nrel(mu32.astype(np.float64), omu)
+
+
 @pytest.mark.parametrize("ell", [0.05, 1.6])
 def test_predict_length_scale_extremes(mapper, ell):
     """l = 0.05 on the default domain: nearly every K* tile is skipped
@@ -207,7 +222,10 @@ def test_predict_length_scale_extremes(mapper, ell):
     triangular solve is; measured 0.9x-1.8x of strtrs over l = 1.0-1.6 and
     both training orders (2.6e-5 vs 1.4e-5 at l = 1.6, Hilbert order).  The
     error is the f32 rounding of A and K*: it does not move with the outer
-    accumulator type or the tile cutoff.  Bound: 2.5x strtrs."""
+    accumulator type or the tile cutoff.  Bound: 2.5x strtrs.  The mean at
+    l = 1.6 sums K*_i alpha_i with |alpha| ~ 10^3 |mu|: it sits at the 1e-5
+    line (0.9-1.1e-5 depending on the factorization's rounding order), so it
+    is held to max(1e-5, 2.5x the f32 sgemv mean of the same K* and alpha)."""
     h = Hyper(length_scale=ell, sigma_f=1.0, noise_level=0.1, prior_mean=0.0)
     wl = synthetic(2048, 64, 48, seed=42)
     gm = TerrainMapper(0, h, ctx=mapper.ctx)
@@ -218,8 +236,9 @@ def test_predict_length_scale_extremes(mapper, ell):
     emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
     L, rl1, al1 = gm.skip_info()
     estrsm = strtrs_var_error(gm, wl, ovar)
-    print(f"l={ell}: cutoff 2^-{L}: mu {emu:.2e} var {evar:.2e} (f32 strtrs {estrsm:.2e})")
-    assert emu < REL_TOL
+    esgemv = sgemv_mean_error(gm, wl, omu)
+    print(f"l={ell}: cutoff 2^-{L}: mu {emu:.2e} (f32 sgemv {esgemv:.2e}) var {evar:.2e} (f32 strtrs {estrsm:.2e})")
+    assert emu < max(REL_TOL, 2.5 * esgemv)
     assert evar < max(REL_TOL, 2.5 * estrsm)
 
 
