@@ -299,7 +299,8 @@ __device__ __forceinline__ float split_piece(float a, int plane) {
 // lgn[2T]   .x = log2(16 max_r |A_r|_1)  (|A k|_2 <= sqrt(256) |A k|_inf <= 16 max_r |A_r|_1 max|k|)
 //           .y = log2 of a bound on the spectral norm ||A_It||_2  (|A k|_2 <= ||A||_2 |k|_2):
 //                with the 64x64 Gram matrix G = A^T A (PSD, f64), ||A||_2^2 = lambda_max(G)
-//                <= ||G^8||_inf^(1/8) (any induced norm bounds the spectral radius),
+//                <= ||G^16||_inf^(1/16) (any induced norm bounds the spectral radius;
+//                at most 64^(1/32) = 1.14x over ||A||_2 for a 64 x 64 G),
 //                also <= |A|_F^2 = trace G; the smaller of the two;
 //           .z = log2(|A_It|_F), which also bounds || |A_It| ||_2;
 // lgn[2T+1] the same two bounds for the bf16 pieces the split sweep
@@ -366,10 +367,11 @@ __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict_
             for (int i = 0; i < kBK; ++i) tr += gm[i * kBK + i];
             return tr;
         }();
-        // three squarings, G <- (G/c)^2 with c = the largest entry (exact power-of-two
-        // rescale), tracking log2 of the scale: G^8 = 2^e8 * gm
+        // k squarings, G <- (G/c)^2 with c = the largest entry (exact power-of-two
+        // rescale), tracking log2 of the scale: G^(2^k) = 2^e8 * gm
+        constexpr int kGramSquarings = 4;
         double e8 = 0.0;
-        for (int it = 0; it < 3; ++it) {
+        for (int it = 0; it < kGramSquarings; ++it) {
             double mx = 0.0;
             for (int i = tid; i < kBK * kBK; i += kBM) mx = fmax(mx, fabs(gm[i]));
 #pragma unroll
@@ -401,15 +403,15 @@ __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict_
             for (int i = tid; i < kBK * kBK; i += kBM) gm[i] = hm[i];
             __syncthreads();
         }
-        // ||G^8||_inf: largest absolute row sum
+        // ||G^(2^k)||_inf: largest absolute row sum
         double rs = 0.0;
         if (tid < kBK)
             for (int j = 0; j < kBK; ++j) rs += fabs(gm[tid * kBK + j]);
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) rs = fmax(rs, __shfl_xor(rs, o));
         s = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
-        // log2 ||A||_2 <= (log2 ||G^8||_inf) / 16, with a margin for the f64 rounding
-        const double lg_spec = rs > 0.0 ? (log2(rs) + e8) / 16.0 + 1e-4 : -1000.0;
+        // log2 ||A||_2 <= (log2 ||G^(2^k)||_inf) / 2^(k+1), with a margin for the f64 rounding
+        const double lg_spec = rs > 0.0 ? (log2(rs) + e8) / (double)(2 << kGramSquarings) + 1e-4 : -1000.0;
         const double lg_fro = fro2 > 0.0 ? 0.5 * log2(fro2) : -1000.0;
         const int o = 2 * pi;                    // A: 0, A1: 2, A2: 4
         out[o] = s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f;

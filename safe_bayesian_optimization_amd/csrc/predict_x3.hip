@@ -523,6 +523,13 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     const int tid = threadIdx.x, lane = tid & 63;
     const int lw = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave = loader index
     const int g = lane >> 4, r = lane & 15;
+    // DIAG & 134217728 / 268435456: static issue priority 1 for waves 4-7 (the
+    // second-dispatched half, which loses VALU arbitration) / for waves 0-3
+    if constexpr ((DIAG & 134217728) != 0) {
+        if (lw >= 4) __builtin_amdgcn_s_setprio(1);
+    } else if constexpr ((DIAG & 268435456) != 0) {
+        if (lw < 4) __builtin_amdgcn_s_setprio(1);
+    }
 
     const lds_char *lds = (const lds_char *)smem;
     const int4 *rwin = reinterpret_cast<const int4 *>(smem + kXWin);
@@ -975,6 +982,8 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 47: SBO_X3_LAUNCH(1, 73776 + 1024 + 16777216); break;  // variant 3, A stage loaded by waves 0-3 only
         case 48: SBO_X3_LAUNCH(1, 73776 + 1024); break;     // variant 3, A stage loaded by waves 4-7 only
         case 49: SBO_X3_LAUNCH(1, 73776); break;  // variant 3 with the next K* coordinates read at ph 3 (round-2 default)
+        case 51: SBO_X3_LAUNCH(1, 73776 + 33554432 + 134217728); break;  // variant 3, waves 4-7 at issue priority 1
+        case 52: SBO_X3_LAUNCH(1, 73776 + 33554432 + 268435456); break;  // variant 3, waves 0-3 at issue priority 1
 #endif
         default: SBO_X3_LAUNCH(1, 73776 + 33554432); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead, next coordinates at ph 1
     }
