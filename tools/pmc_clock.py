@@ -9,11 +9,14 @@ import glob
 import sys
 
 
-def main(d, cus=256):
+def main(d, cus=256, kernel=None):
     per = {}
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "predict_kernel" not in r["Kernel_Name"] and "predict_x3_kernel" not in r["Kernel_Name"]:
+            if kernel:
+                if kernel not in r["Kernel_Name"]:
+                    continue
+            elif "predict_kernel" not in r["Kernel_Name"] and "predict_x3_kernel" not in r["Kernel_Name"]:
                 continue
             e = per.setdefault(r["Dispatch_Id"], {"ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
             e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -33,4 +36,4 @@ def main(d, cus=256):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], kernel=sys.argv[2] if len(sys.argv) > 2 else None)
