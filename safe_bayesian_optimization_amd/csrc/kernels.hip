@@ -535,6 +535,8 @@ constexpr int kBudgetBins = kBudgetFloor * kBinsPerBit + 2;
 constexpr int kPlanThreads = 256;       // plan kernels: one query block, one row block per wave
 constexpr int kPlanWaves = kPlanThreads / 64;
 constexpr int kPlanD2 = 2048;           // k-tile distances cached in LDS (N <= 131072; beyond: recomputed)
+constexpr int kPlanBinCache = 256;
+constexpr int kPlanWriteBlocks = 4096;  // plan_write grid cap (four waves each, grid-stride over items)      // per wave: the increment bins of a row block's first tiles (nI <= 64: all)
 constexpr int kPlanKeyShift = 40;       // plan key: kept-tile count (low 40 bits) | non-empty (high bits)
 constexpr unsigned long long kPlanCountMask = (1ull << kPlanKeyShift) - 1ull;
 // Sweep time of a kept tile by precision level, in 1/64 of a full tile
@@ -793,7 +795,8 @@ struct PlanRule {
     // summed weights (integer adds: order-independent) stay within the
     // row block's budget (fixed point, 2^32 = the reference budget 2^lg_tau).
     // Returns the last spent bin (-1: none).
-    __device__ int threshold(int I, unsigned long long *bins, int lane, unsigned long long budget) const {
+    __device__ int threshold(int I, unsigned long long *bins, int lane, unsigned long long budget,
+                             unsigned *bc = nullptr) const {
         if (!lgn) return -1;
         const int T = kTilesPerRowBlockStep * (I + 1);
         for (int i = lane; i < kBudgetBins; i += 64) bins[i] = 0ull;
@@ -802,11 +805,13 @@ struct PlanRule {
         for (int t = lane; t < T; t += 64) {
             if (far_tile(I, t, d2(t))) {
                 ++nfar;
+                if (bc && t < kPlanBinCache) bc[t] = 0u;  // all three increments in bin 0
                 continue;
             }
             int bi[3];
             unsigned long long w[3];
             incs(I, t, bi, w);
+            if (bc && t < kPlanBinCache) bc[t] = (unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16);
 #pragma unroll
             for (int j = 0; j < 3; ++j)
                 if (bi[j] < kBudgetBins - 1) atomicAdd(bins + bi[j], w[j]);
@@ -841,13 +846,18 @@ struct PlanRule {
     }
 
     // The tile's level code (0 full, 1 three products, 2 one product) or -1
-    // (dropped) under the row block's threshold.
-    __device__ __forceinline__ int level(int I, int t, int drop_max) const {
+    // (dropped) under the row block's threshold.  bc: the bins threshold()
+    // cached for this row block (a far tile's are all 0, as booked there).
+    __device__ __forceinline__ int level(int I, int t, int drop_max, const unsigned *bc = nullptr) const {
         const float dd = d2(t);
         int code;
         if (lgn) {
             int spent;
-            if (far_tile(I, t, dd)) {
+            if (bc && t < kPlanBinCache) {
+                const unsigned c = bc[t];
+                spent = ((int)(c & 0xffu) <= drop_max) + ((int)((c >> 8) & 0xffu) <= drop_max) +
+                        ((int)(c >> 16) <= drop_max);
+            } else if (far_tile(I, t, dd)) {
                 spent = drop_max >= 0 ? 3 : 0;
             } else {
                 int bi[3];
@@ -923,6 +933,8 @@ __device__ QBox plan_setup(const float *__restrict__ qx, const float *__restrict
 __device__ __forceinline__ int64_t plan_item(int I, int nI, int64_t nQ, int64_t qb) {
     return (int64_t)(nI - 1 - I) * nQ + qb;
 }
+// 64-tile chunks of the longest item (the code bitmap's stride per item)
+__host__ __device__ __forceinline__ int plan_chunks(int nI) { return (kTilesPerRowBlockStep * nI + 63) / 64; }
 
 // Pass 1, one workgroup per query block, one row block per wave at a time:
 // the budget threshold and the kept-tile count of every item.  key packs
@@ -934,8 +946,11 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     int64_t nQ,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, float m0, int64_t ldp, float *__restrict__ part, float *__restrict__ mean,
-    unsigned long long *__restrict__ key, unsigned char *__restrict__ thr, unsigned long long *__restrict__ wkey) {
-    __shared__ float d2s[kPlanD2], kns[kPlanD2];
+    unsigned long long *__restrict__ key, unsigned char *__restrict__ thr, unsigned long long *__restrict__ wkey,
+    unsigned long long *__restrict__ bits) {
+    // dynamic LDS: the increment-bin cache [kPlanWaves][kPlanBinCache], then
+    // the distance and |k|_2 caches of min(nkt, kPlanD2) tiles each
+    extern __shared__ unsigned plan_dyn[];
     __shared__ float red[4 * kPlanWaves];
     __shared__ unsigned long long bins[kPlanWaves][kBudgetBins];
     __shared__ unsigned long long wtot[kPlanMaxI];
@@ -943,6 +958,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     const int64_t qb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nkt = kTilesPerRowBlockStep * nI;
+    unsigned *bc = plan_dyn + wave * kPlanBinCache;
+    float *d2s = reinterpret_cast<float *>(plan_dyn + kPlanWaves * kPlanBinCache);
+    float *kns = d2s + min(nkt, kPlanD2);
     PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, plan_ref(lg_tau, nI), nI, {}, d2s, kns, levels, lvl_key};
     R.box = plan_setup(qx, qy, m, qb, kbox, lgn ? kcoord : nullptr, cexp, nkt, d2s, kns, red);
     // The error budget of the query block, |dV(q)|_2^2 = sum_I |dV_I(q)|_2^2
@@ -986,14 +1004,19 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
         // a cheap row block (everything within the share) spends its own total
         const unsigned long long bud = !fill ? (unsigned long long)floor(4294967296.0 / sqrt((double)nI))
                                        : (wtot[I] <= budget_exp ? ~0ull : budget_exp);
-        const int drop_max = R.threshold(I, bins[wave], lane, bud);
+        const int drop_max = R.threshold(I, bins[wave], lane, bud, bc);
+        const int64_t item = plan_item(I, nI, nQ, qb);
+        // the item's codes, 64 tiles per chunk: kept / level 1 / level 2 masks (read by plan_write)
+        unsigned long long *ib = bits + item * (int64_t)plan_chunks(nI) * 3;
         int cnt = 0;
         unsigned wsum = 0;
+#pragma unroll 1
         for (int t0 = 0; t0 < T; t0 += 64) {
             const int t = t0 + lane;
-            const int code = t < T ? R.level(I, t, drop_max) : -1;
-            const int n0 = __popcll(__ballot(code == 0)), n1 = __popcll(__ballot(code == 1)),
-                      n2 = __popcll(__ballot(code == 2));
+            const int code = t < T ? R.level(I, t, drop_max, bc) : -1;
+            const unsigned long long b0 = __ballot(code == 0), b1 = __ballot(code == 1), b2 = __ballot(code == 2);
+            if (lane < 3) ib[(t0 >> 6) * 3 + lane] = lane == 0 ? (b0 | b1 | b2) : (lane == 1 ? b1 : b2);
+            const int n0 = __popcll(b0), n1 = __popcll(b1), n2 = __popcll(b2);
             cnt += n0 + n1 + n2;
             wsum += I == nI - 1 ? g_mean_w[0] * n0 + g_mean_w[1] * n1 + g_mean_w[2] * n2
                                 : kLevelWeight0 * n0 + kLevelWeight1 * n1 + kLevelWeight2 * n2;
@@ -1001,7 +1024,6 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
         if (g_rb_slope)
             wsum = (unsigned)((unsigned long long)wsum * (100u * (unsigned)nI + g_rb_slope * (unsigned)I) /
                               (100u * (unsigned)nI));
-        const int64_t item = plan_item(I, nI, nQ, qb);
         if (lane == 0) {
             key[item] = (unsigned long long)cnt | ((cnt > 0 ? 1ull : 0ull) << kPlanKeyShift);
             thr[item] = (unsigned char)(drop_max + 1);
@@ -1020,50 +1042,47 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
 
 // Pass 2 (after the inclusive scan of key): the kept tile indices of every
 // non-empty item, ascending, at its offset, and its descriptor
-// (I, qb, offset low 32 bits, count | offset high bits << 16).
-__global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
-    const float4 *__restrict__ kbox, const float *__restrict__ kcoord, const float4 *__restrict__ lgn, int levels,
-    float2 lvl_key, int nI,
-    int64_t nQ,
-    const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
-    float skip_d2_mean, float lg_tau, const unsigned long long *__restrict__ key,
-    const unsigned long long *__restrict__ scan, const unsigned char *__restrict__ thr, int4 *__restrict__ desc,
-    unsigned short *__restrict__ tl, int prod_full, unsigned long long *__restrict__ partial) {
+// (I, qb, offset low 32 bits, count | offset high bits << 16) -- from the
+// code bitmap plan_count left (bits: per item and 64-tile chunk, the kept /
+// level-1 / level-2 masks), so no tile's bounds are evaluated twice.  Each
+// wave walks items gw, gw + W, .. (W = all waves of the grid).
+__global__ __launch_bounds__(256) void plan_write_kernel(
+    int nI, int64_t nQ, const unsigned long long *__restrict__ key, const unsigned long long *__restrict__ scan,
+    const unsigned long long *__restrict__ bits, int4 *__restrict__ desc, unsigned short *__restrict__ tl,
+    int prod_full, unsigned long long *__restrict__ partial) {
     // partial (may be null): per wave [MFMA products, tiles at level 1, at level 2]
     // (summed by plan_counts_reduce_kernel: no contended global atomics)
-    __shared__ float d2s[kPlanD2], kns[kPlanD2];
-    __shared__ float red[4 * kPlanWaves];
-    const int64_t qb = blockIdx.x;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nkt = kTilesPerRowBlockStep * nI;
-    PlanRule R{kbox, lgn, cexp, skip_d2, skip_d2_mean, plan_ref(lg_tau, nI), nI, {}, d2s, kns, levels, lvl_key};
-    R.box = plan_setup(qx, qy, m, qb, kbox, lgn ? kcoord : nullptr, cexp, nkt, d2s, kns, red);
+    const int lane = threadIdx.x & 63;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+    const int64_t items = (int64_t)nI * nQ;
     unsigned long long prod = 0, nl1 = 0, nl2 = 0;
-    for (int I = wave; I < nI; I += kPlanWaves) {
-        const int64_t item = plan_item(I, nI, nQ, qb);
+    for (int64_t item = gw; item < items; item += nw) {
         const unsigned long long k = key[item];
         const int cnt = (int)(k & kPlanCountMask);
-        if (cnt == 0) continue;
-        const unsigned long long ex = scan[item] - k;
-        const uint64_t off = ex & kPlanCountMask;
-        const int64_t ne = (int64_t)(ex >> kPlanKeyShift);
-        const int drop_max = (int)thr[item] - 1;
-        const int T = kTilesPerRowBlockStep * (I + 1);
-        uint64_t base = off;
-        for (int t0 = 0; t0 < T; t0 += 64) {
-            const int t = t0 + lane;
-            const int code = t < T ? R.level(I, t, drop_max) : -1;
-            const bool kp = code >= 0;
-            const unsigned long long bal = __ballot(kp);
-            if (kp) {
-                tl[base + __popcll(bal & ((1ull << lane) - 1ull))] = (unsigned short)(t | (code << kLevelShift));
-                prod += code == 0 ? prod_full : (code == 1 ? 3 : 1);
-                nl1 += code == 1 ? 1 : 0;
-                nl2 += code == 2 ? 1 : 0;
+        if (cnt > 0) {
+            const int I = nI - 1 - (int)(item / nQ);
+            const int64_t qb = item % nQ;
+            const unsigned long long ex = scan[item] - k;
+            const uint64_t off = ex & kPlanCountMask;
+            const int64_t ne = (int64_t)(ex >> kPlanKeyShift);
+            const int T = kTilesPerRowBlockStep * (I + 1);
+            const unsigned long long *ib = bits + item * (int64_t)plan_chunks(nI) * 3;
+            uint64_t base = off;
+            for (int t0 = 0; t0 < T; t0 += 64) {
+                const unsigned long long kept = ib[(t0 >> 6) * 3], l1 = ib[(t0 >> 6) * 3 + 1],
+                                         l2 = ib[(t0 >> 6) * 3 + 2];
+                if ((kept >> lane) & 1ull) {
+                    const int code = ((l1 >> lane) & 1ull) ? 1 : (((l2 >> lane) & 1ull) ? 2 : 0);
+                    tl[base + __popcll(kept & ((1ull << lane) - 1ull))] =
+                        (unsigned short)((t0 + lane) | (code << kLevelShift));
+                    prod += code == 0 ? prod_full : (code == 1 ? 3 : 1);
+                    nl1 += code == 1 ? 1 : 0;
+                    nl2 += code == 2 ? 1 : 0;
+                }
+                base += __popcll(kept);
             }
-            base += __popcll(bal);
+            if (lane == 0) desc[ne] = make_int4(I, (int)qb, (int)(uint32_t)off, cnt | (int)((off >> 32) << 16));
         }
-        if (lane == 0) desc[ne] = make_int4(I, (int)qb, (int)(uint32_t)off, cnt | (int)((off >> 32) << 16));
     }
     if (partial) {
 #pragma unroll
@@ -1073,7 +1092,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_write_kernel(
             nl2 += __shfl_xor(nl2, o);
         }
         if (lane == 0) {
-            unsigned long long *p = partial + 3 * (qb * kPlanWaves + wave);
+            unsigned long long *p = partial + 3 * gw;
             p[0] = prod;
             p[1] = nl1;
             p[2] = nl2;
@@ -1711,7 +1730,7 @@ hipError_t launch_tile_boxes(hipStream_t s, const float *x, const float *y, int6
 
 namespace {
 struct PlanLayout {
-    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes, wkey, wscan, lvcnt, rec;
+    size_t key, scan, thr, desc, tl, seg, temp, temp_bytes, wkey, wscan, lvcnt, rec, bits;
     // XCD-interleaved order (P % 8 == 0): the sweep reads desc2 / tl2 / seg2
     bool xcd;
     size_t xseg, pos_of, cnt2, off2, desc2, tl2, seg2, temp2, temp2_bytes;
@@ -1735,7 +1754,8 @@ PlanLayout plan_layout(int64_t nI, int64_t nQ, int P) {
     L.thr = take((size_t)items);
     L.wkey = take(8 * (size_t)items);
     L.wscan = take(8 * (size_t)items);
-    L.lvcnt = take(8 * 3 * (size_t)(nQ * kPlanWaves));
+    L.lvcnt = take(8 * 3 * 4 * (size_t)kPlanWriteBlocks);
+    L.bits = take(8 * 3 * (size_t)items * (size_t)plan_chunks((int)nI));
     L.desc = take(16 * (size_t)(items + 2 * kDescWindow));
     L.tl = take(2 * (size_t)(cap + 2 * kListWindow));
     L.seg = take(4 * (size_t)(P + 1));
@@ -1814,10 +1834,13 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     const float skip_d2_mean = skip.L > 0 && skip.L_mean > skip.L ? cutoff_d2(skip.L_mean, ce) : skip_d2;
     const float4 *lgn = skip.L > 0 ? skip.lgn : nullptr;
     const int levels = lgn ? skip.levels : 0;
-    hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn,
+    auto *bits = reinterpret_cast<unsigned long long *>(w + L.bits);
+    const int nc = std::min(kTilesPerRowBlockStep * nI, kPlanD2);
+    const size_t plan_lds = 4 * (size_t)kPlanWaves * kPlanBinCache + 8 * (size_t)nc;
+    hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), plan_lds, s, kbox, skip.kcoord, lgn,
                        levels, make_float2(skip.lvl_key[0], skip.lvl_key[1]), nI,
                        nQ, qx, qy,
-                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr, wkey);
+                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr, wkey, bits);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t tb = L.temp_bytes;
@@ -1826,13 +1849,12 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     tb = L.temp_bytes;
     e = rocprim::inclusive_scan(w + L.temp, tb, wkey, wscan, (size_t)items, rocprim::plus<unsigned long long>(), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), 0, s, kbox, skip.kcoord, lgn,
-                       levels, make_float2(skip.lvl_key[0], skip.lvl_key[1]), nI, nQ, qx, qy,
-                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, key, scan, thr, desc, tl, skip.prod_full,
-                       tiles_done ? reinterpret_cast<unsigned long long *>(w + L.lvcnt) : nullptr);
+    const int64_t wblocks = std::min<int64_t>((items + 3) / 4, kPlanWriteBlocks);
+    hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)wblocks), dim3(256), 0, s, nI, nQ, key, scan, bits,
+                       desc, tl, skip.prod_full, tiles_done ? reinterpret_cast<unsigned long long *>(w + L.lvcnt) : nullptr);
     if (tiles_done)
         hipLaunchKernelGGL(plan_counts_reduce_kernel, dim3(1), dim3(256), 0, s,
-                           reinterpret_cast<const unsigned long long *>(w + L.lvcnt), nQ * kPlanWaves, tiles_done + 1);
+                           reinterpret_cast<const unsigned long long *>(w + L.lvcnt), wblocks * 4, tiles_done + 1);
     auto *rec = reinterpret_cast<int4 *>(w + L.rec);
     if (!L.xcd) {
         hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done, wkey,
