@@ -767,19 +767,25 @@ struct PlanRule {
         const int T = kTilesPerRowBlockStep * (I + 1);
         unsigned long long wsum = 0;
         int ov = 0;
-        for (int t = lane; t < T; t += 64) {
-            if (far_tile(I, t, d2(t))) {
-                wsum += 6ull;
-                continue;
-            }
-            int bi[3];
-            unsigned long long w[3];
-            incs(I, t, bi, w);
+        for (int t0 = 0; t0 < T; t0 += 64) {
+            const int t = t0 + lane;
+            if (t < T) {
+                if (far_tile(I, t, d2(t))) {
+                    wsum += 6ull;
+                } else {
+                    int bi[3];
+                    unsigned long long w[3];
+                    incs(I, t, bi, w);
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                if (bi[j] < kBudgetBins - 1) wsum += w[j];
-                else ov = 1;
+                    for (int j = 0; j < 3; ++j) {
+                        if (bi[j] < kBudgetBins - 1) wsum += w[j];
+                        else ov = 1;
+                    }
+                }
             }
+            // an increment over the whole budget decides the row block (never
+            // cheap): the rest of its tiles cannot change that
+            if (__ballot(ov)) break;
         }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
