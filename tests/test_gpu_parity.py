@@ -511,6 +511,44 @@ def test_loose_budgets_hold(mapper, budget):
     assert dvar <= 2.0 ** -budget + 4 * ulp
 
 
+def test_plan_beyond_the_bin_cache(mapper):
+    """N = 20480 (80 row blocks): row blocks past 64 have more k-tiles than
+    plan_count caches increment bins for (kPlanBinCache = 256; the rest are
+    re-evaluated) and five 64-tile chunks in the plan's code bitmap.  At a
+    loose budget (B = 13: every level and drops in use) and at the default
+    B = 20, mu and sigma^2 stay within 2^-B of the dense all-six-products
+    sweep, as in test_loose_budgets_hold."""
+    wl = synthetic(20480, 96, 96, seed=35)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    m = wl.qx.size
+    gm.set_option(N.SBO_OPT_TILE_SKIP, 0)
+    ref = dict(mu=np.empty(m, np.float32), sd=np.empty(m, np.float32))
+    gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=ref)
+    gm.set_option(N.SBO_OPT_TILE_SKIP, -1)
+    lib = N.lib()
+    ulp = np.finfo(np.float32).eps
+    try:
+        for budget in (13, 20):
+            gm.set_option(N.SBO_OPT_SKIP_BUDGET, budget)
+            gm.fit(wl.x, wl.y, wl.obs)
+            lib.sbo_profile(gm.ctx.handle, 1)
+            out = dict(mu=np.empty(m, np.float32), sd=np.empty(m, np.float32))
+            gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
+            mf = ctypes.c_double()
+            lv = (ctypes.c_int64 * 3)()
+            lib.sbo_profile_mfma(gm.ctx.handle, ctypes.byref(mf), lv)
+            lib.sbo_profile(gm.ctx.handle, 0)
+            dmu = np.abs(out["mu"].astype(np.float64) - ref["mu"]).max()
+            dvar = np.abs(out["sd"].astype(np.float64) ** 2 - ref["sd"].astype(np.float64) ** 2).max()
+            print(f"N=20480 B={budget}: levels {list(lv)}  |dmu| {dmu:.2e}  |dvar| {dvar:.2e}")
+            assert lv[0] + lv[1] + lv[2] > 0
+            assert dmu <= 2.0 ** -budget + 2 * ulp * np.abs(ref["mu"]).max()
+            assert dvar <= 2.0 ** -budget + 4 * ulp
+    finally:
+        gm.set_option(N.SBO_OPT_SKIP_BUDGET, 20)
+
+
 def test_tile_gain_bounds_are_bounds(mapper):
     """sbo_get_tile_bounds: every packed tile's log2 bounds are upper bounds
     of the exact norms of A_It = (sf2 L^-1)_It and of its bf16 pieces A1, A2
