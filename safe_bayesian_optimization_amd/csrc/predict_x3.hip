@@ -205,7 +205,9 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
         } else if (ph <= 1) {
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
-                float ev = kstar1(ph == 0 ? xk.x : xk.y, ph == 0 ? yk.x : yk.y, xq[c], yq[c], cexp);
+                // (DIAG & 536870912: timing bound of a one-multiply K*, wrong results)
+                float ev = (DIAG & 536870912) ? (ph == 0 ? xk.x : xk.y) * xq[c]
+                                              : kstar1(ph == 0 ? xk.x : xk.y, ph == 0 ? yk.x : yk.y, xq[c], yq[c], cexp);
                 SBO_PIN(ev);
                 if (ph == 0) e[c].x = ev; else e[c].y = ev;
             }
@@ -984,6 +986,8 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 49: SBO_X3_LAUNCH(1, 73776); break;  // variant 3 with the next K* coordinates read at ph 3 (round-2 default)
         case 51: SBO_X3_LAUNCH(1, 73776 + 33554432 + 134217728); break;  // variant 3, waves 4-7 at issue priority 1
         case 52: SBO_X3_LAUNCH(1, 73776 + 33554432 + 268435456); break;  // variant 3, waves 0-3 at issue priority 1
+        case 53: SBO_X3_LAUNCH(1, 73776 + 33554432 + 536870912); break;  // diagnostics: variant 3 with a one-multiply K*
+        case 54: SBO_X3_LAUNCH(1, 73776 + 33554432 + 536870912 + 1048576); break;  //   and the split reduced to kh
 #endif
         default: SBO_X3_LAUNCH(1, 73776 + 33554432); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead, next coordinates at ph 1
     }
