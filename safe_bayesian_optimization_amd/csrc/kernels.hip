@@ -168,9 +168,23 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, i
     __shared__ int s_bad;
     if (*info != 0) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int e = tid; e < kb * kb; e += 256) {
-        const int i = e % kb, j = e / kb;
-        if (i >= j) a[i][j] = A[i + (int64_t)j * ld];
+    // the block in, kCholLoad independent loads per thread in flight at a time
+    // (one at a time, the reads' latency was most of this kernel)
+    constexpr int kCholLoad = 16;
+    for (int e0 = 0; e0 < kb * kb; e0 += 256 * kCholLoad) {
+        float v[kCholLoad];
+#pragma unroll
+        for (int u = 0; u < kCholLoad; ++u) {
+            const int e = e0 + u * 256 + tid;
+            const int i = e % kb, j = e / kb;
+            v[u] = (e < kb * kb && i >= j) ? A[i + (int64_t)j * ld] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kCholLoad; ++u) {
+            const int e = e0 + u * 256 + tid;
+            const int i = e % kb, j = e / kb;
+            if (e < kb * kb && i >= j) a[i][j] = v[u];
+        }
     }
     if (tid == 0) s_bad = 0;
     __syncthreads();

@@ -9,5 +9,5 @@ TAILN=2 step cmp 400 python tools/compare_libs.py $L/libsbo_base.so $L/libsbo.so
 TAILN=4 step fit_base 300 env SBO_LIB=$L/libsbo_base.so python tools/fit_timing.py --n 8192 16384 --reps 3
 TAILN=4 step fit_new 300 python tools/fit_timing.py --n 8192 16384 --reps 3 --chol 1 0
 step prof_fit 300 rocprofv3 --kernel-trace --stats -d $O/prof_fit -o run --output-format csv -- python tools/fit_timing.py --n 16384 --reps 2
-step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+[ -n "$NOTESTS" ] || step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 echo done
