@@ -760,14 +760,17 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
             constexpr int kE = WIDE ? 16 : 4;
 #pragma unroll
             for (int c = 0; c < kCB; ++c) {
-                double sv = 0.0;
+                // four independent f64 chains (element e of every block), then
+                // combined: the 64-term sum off one dependent fma chain
+                double sq[kE > 4 ? 4 : kE] = {};
 #pragma unroll
                 for (int rb = 0; rb < kRB; ++rb)
 #pragma unroll
                     for (int e = 0; e < kE; ++e) {
-                        sv = fma((double)outer[c][rb][e], (double)outer[c][rb][e], sv);
+                        sq[e & 3] = fma((double)outer[c][rb][e], (double)outer[c][rb][e], sq[e & 3]);
                         outer[c][rb][e] = 0.0f;
                     }
+                double sv = (sq[0] + sq[1]) + (sq[2] + sq[3]);
                 if (!WIDE) sv += __shfl_xor(sv, 16);
                 sv += __shfl_xor(sv, 32);
                 pend_s[c] = (float)sv;
