@@ -146,7 +146,11 @@ __device__ __forceinline__ float kstar1(float xk, float yk, float xq, float yq, 
 //   LV: the tile's precision level (the plan's code): 0 all six products,
 //   1 the three largest (a1 kh + a0 km + a0 kh), 2 a0 kh alone; the A planes
 //   a level leaves out are not read from LDS.
-template <int NC, bool FRESH, int DIAG, int PIECES, int LV = 0>
+//   KHN: the next step is a one-product step too (DIAG & 1073741824 selects
+//   this body then): its K* pieces are kh alone, the split is skipped (a
+//   one-product step reads no other piece, so the results are bitwise those
+//   of the full split).
+template <int NC, bool FRESH, int DIAG, int PIECES, int LV = 0, bool KHN = false>
 __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn, const float (&xq)[NC],
                                         const float (&yq)[NC], int g, float cexp, float msc, const KPieces<NC> &kb,
                                         f32x4 (&acc)[NC][16], f32x4 (&outer)[NC][16], KPieces<NC> &nx,
@@ -224,6 +228,11 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                     w0 = pk_bf16(e[c].x, e[c].y);
                     w1 = w0;
                     w2 = w0;
+                } else if constexpr (KHN) {  // the next step runs at one product: kh alone
+                    w0 = pk_bf16(e[c].x, e[c].y);
+                    SBO_PIN(w0);
+                    nx.h[c][i] = w0;
+                    continue;
                 } else {
                     split3(e[c].x, e[c].y, w0, w1, w2);
                 }
@@ -731,9 +740,15 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         if constexpr (WIDE)
             x3w_half<FRESH, DIAG>(pa, pcn, xq[0], yq[0], lane >> 5, cexp, msc, kb, acc[0], outer[0], nx, mu[0],
                                   voff, a_src, a_dst);
+        else if (LEVELS && s0.lv == 2 && (DIAG & 1073741824) && nvalid && s1.lv == 2)
+            x3_half<NC, FRESH, DIAG, kPieces, 2, true>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff,
+                                                       a_src, a_dst, is_loader, np2);
         else if (LEVELS && s0.lv == 2)
             x3_half<NC, FRESH, DIAG, kPieces, 2>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
                                                  a_dst, is_loader, np2);
+        else if (LEVELS && s0.lv == 1 && (DIAG & 1073741824) && (DIAG & 524288) && nvalid && s1.lv == 2)
+            x3_half<NC, FRESH, DIAG, kPieces, 1, true>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff,
+                                                       a_src, a_dst, is_loader, np2);
         else if (LEVELS && s0.lv == 1)
             x3_half<NC, FRESH, DIAG, kPieces, 1>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
                                                  a_dst, is_loader, np2);
@@ -978,12 +993,12 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 36: SBO_X3_LAUNCH(1, 69651); break;  //   1 product, no next-step K*, no A pieces
         case 37: SBO_X3_LAUNCH(1, 70163); break;  //   and no barrier
         case 38: SBO_X3_LAUNCH(1, 69655); break;  //   no K*, no A pieces, no outer sums
-        case 39: SBO_X3_LAUNCH(1, 335920 + 33554432); break;  // variant 3 with phase stamps (sbo_debug_x3_stamps)
+        case 39: SBO_X3_LAUNCH(1, 335920 + 33554432 + 1073741824); break;  // variant 3 with phase stamps (sbo_debug_x3_stamps)
         case 41: SBO_X3_LAUNCH(1, 1122352); break;  // diagnostics: variant 3 with the K* split reduced to kh
         // A/B (correct results, measured no faster: DESIGN.md section 10):
         case 42: SBO_X3_LAUNCH(1, 73776 + 2097152); break;  // variant 3, one-product tiles straight into the outer sums
         case 43: SBO_X3_LAUNCH(1, 73776 + 6291456); break;  //   and three-product tiles too
-        case 46: SBO_X3_LAUNCH(1, 73776 + 33554432 + 8388608); break;  // variant 3 recording only each workgroup's span
+        case 46: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 8388608); break;  // variant 3 recording only each workgroup's span
         case 47: SBO_X3_LAUNCH(1, 73776 + 1024 + 16777216); break;  // variant 3, A stage loaded by waves 0-3 only
         case 48: SBO_X3_LAUNCH(1, 73776 + 1024); break;     // variant 3, A stage loaded by waves 4-7 only
         case 49: SBO_X3_LAUNCH(1, 73776); break;  // variant 3 with the next K* coordinates read at ph 3 (round-2 default)
@@ -991,8 +1006,10 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 52: SBO_X3_LAUNCH(1, 73776 + 33554432 + 268435456); break;  // variant 3, waves 0-3 at issue priority 1
         case 53: SBO_X3_LAUNCH(1, 73776 + 33554432 + 536870912); break;  // diagnostics: variant 3 with a one-multiply K*
         case 54: SBO_X3_LAUNCH(1, 73776 + 33554432 + 536870912 + 1048576); break;  //   and the split reduced to kh
+        case 55: SBO_X3_LAUNCH(1, 73776 + 33554432); break;  // variant 3 without the kh-only split (the default before it)
+        case 56: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 524288); break;  // variant 3, kh-only split from three-product steps too (slower)
 #endif
-        default: SBO_X3_LAUNCH(1, 73776 + 33554432); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead, next coordinates at ph 1
+        default: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead, next coordinates at ph 1, kh-only split between one-product steps
     }
 #undef SBO_X3_LAUNCH
     return hipGetLastError();
