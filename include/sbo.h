@@ -264,10 +264,16 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * sqrt(sf2)), B = SBO_OPT_SKIP_BUDGET, computed from the fitted factor
  * (sbo_get_skip reports it). */
 #define SBO_OPT_TILE_SKIP 3
-/* SBO_OPT_QUERY_ORDER (0 | 1, default 1): sweep the queries of a tick in
- * Morton order (device radix sort, ~0.1 ms per 10^6 points) so each
- * workgroup's 128 queries are spatially compact and skip more k-tiles;
- * outputs and argmax indices stay in the caller's order. */
+/* SBO_OPT_QUERY_ORDER (0 | 1 | 2, default 1): the order the queries of a
+ * tick are swept in, so that each workgroup's 128 queries are spatially
+ * compact and skip more k-tiles -- 0 the caller's order; 2 Morton order
+ * (device radix sort, ~0.1 ms per 10^6 points); 1 (default) 8 x 16 grid
+ * patches when the queries are a raster grid (rows of one coordinate, the
+ * other repeating row by row; a contiguous run of rows cut anywhere
+ * qualifies; detected with one stream synchronization per new query
+ * buffer, and the patch layout is a valid order for whatever the buffer
+ * later holds), else Morton order.  Outputs and argmax indices stay in the
+ * caller's order. */
 #define SBO_OPT_QUERY_ORDER 4
 /* SBO_OPT_KERNEL_VARIANT, the predictive sweep: 3 (default) = split
  * operands on bf16 MFMA -- sf2 L^-1 and K* as three bf16 pieces each, up to

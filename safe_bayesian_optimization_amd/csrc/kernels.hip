@@ -1269,13 +1269,19 @@ __global__ void plan_block_cost_kernel(const unsigned long long *__restrict__ wk
     bcost[qb] = (float)((double)c / (double)kLevelWeight0);  // in full-precision tiles
 }
 
-__global__ void plan_query_cost_kernel(const float *__restrict__ bcost, int64_t m, const int32_t *__restrict__ perm,
-                                       float *__restrict__ cost) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const int64_t qb = i / kBN;
-    const int64_t nb = (m - qb * kBN) < kBN ? (m - qb * kBN) : kBN;
-    cost[perm ? (int64_t)perm[i] : i] = bcost[qb] / (float)nb;
+// a block's cost is shared by its queries (a grid patch's padded positions,
+// perm -1, take no share): one block per workgroup of kBN threads
+__global__ __launch_bounds__(kBN) void plan_query_cost_kernel(const float *__restrict__ bcost, int64_t m,
+                                                              const int32_t *__restrict__ perm,
+                                                              float *__restrict__ cost) {
+    __shared__ int nv;
+    const int64_t qb = blockIdx.x, i = qb * kBN + threadIdx.x;
+    const int64_t o = i < m ? (perm ? (int64_t)perm[i] : i) : -1;  // (-1: padding)
+    if (threadIdx.x == 0) nv = 0;
+    __syncthreads();
+    if (o >= 0) atomicAdd(&nv, 1);
+    __syncthreads();
+    if (o >= 0) cost[o] = bcost[qb] / (float)nv;
 }
 
 // ---- the sweep (persistent: one workgroup per CU)
@@ -1575,7 +1581,8 @@ __global__ __launch_bounds__(kAcqThreads) void acquire_kernel(
     const int64_t i = (int64_t)blockIdx.x * kAcqThreads + threadIdx.x;
     double bs = 0.0;
     int64_t bi = -1;
-    if (i < m) {
+    // (perm -1: a padded grid-patch position, no output)
+    if (i < m && (!perm || perm[i] >= 0)) {
         double s = 0.0;
         for (int I = 0; I < nI; ++I) s += (double)part[(int64_t)I * ldp + i];
         double vd = (double)sf2 - s;
@@ -1935,8 +1942,7 @@ hipError_t launch_plan_cost(hipStream_t s, int64_t npad, int64_t m, int P, const
     const auto *wkey = reinterpret_cast<const unsigned long long *>(static_cast<const char *>(work) + L.wkey);
     hipLaunchKernelGGL(plan_block_cost_kernel, dim3((unsigned)((nQ + 255) / 256)), dim3(256), 0, s, wkey, nI, nQ,
                        bcost);
-    hipLaunchKernelGGL(plan_query_cost_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, bcost, m, perm,
-                       cost);
+    hipLaunchKernelGGL(plan_query_cost_kernel, dim3((unsigned)nQ), dim3(kBN), 0, s, bcost, m, perm, cost);
     return hipGetLastError();
 }
 

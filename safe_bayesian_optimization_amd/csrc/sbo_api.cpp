@@ -468,14 +468,10 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
                     int score_kind, int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
                     uint8_t *safe, sbo_key *key_dev, float *cost = nullptr) {
     const int64_t nI = ctx->npad / sbo::kBM;
-    const int64_t ldp = sbo::round_up(m, 64);
-    SBO_HIP(ctx->part.reserve(sizeof(float) * (size_t)nI * (size_t)ldp));
-    SBO_HIP(ctx->mean.reserve(sizeof(float) * (size_t)ldp));
-    const int64_t nb = sbo::acq_blocks(m);
-    SBO_HIP(ctx->keys.reserve(sizeof(sbo_key) * (size_t)(nb + 1)));
-    sbo_key *bkeys = ctx->keys.as<sbo_key>();
-    // sweep the queries in Morton order (compact 128-query blocks skip more k-tiles)
+    // sweep the queries in grid patches or Morton order (compact 128-query
+    // blocks skip more k-tiles); ms sweep positions (>= m: padded patches)
     const int32_t *perm = nullptr;
+    int64_t ms = m;
     sbo::SkipPlan plan;
     if (ctx->skip_log2 < 0) {
         plan.L = ctx->auto_skip_log2;
@@ -495,25 +491,50 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     if (const char *e = getenv("SBO_LVL_FORCE"); e && plan.levels) plan.levels = 2 + std::clamp(atoi(e), 0, 2);
 #endif
     if (ctx->query_order && plan.L > 0 && m > sbo::kBN) {
-        const size_t wb = sbo::query_order_bytes(m);
-        SBO_HIP(ctx->qwork.reserve(wb));
         int32_t *p = nullptr;
         float *sx = nullptr, *sy = nullptr;
-        SBO_HIP(sbo::launch_query_order(ctx->stream, qx, qy, m, ctx->bbox, ctx->qwork.as<void>(), wb, &p, &sx, &sy));
+        if (ctx->query_order == 1) {
+            // a raster grid's shape, read once per query buffer (one stream
+            // sync); the patch layout is valid for any data, so a reused
+            // buffer holding other points still gets correct outputs
+            SBO_HIP(ctx->qgwork.reserve(sbo::query_grid_bytes(m)));
+            if (qx != ctx->qgrid_x || qy != ctx->qgrid_y || m != ctx->qgrid_m) {
+                unsigned long long g[6];
+                SBO_HIP(sbo::launch_grid_detect(ctx->stream, qx, qy, m, ctx->qgwork.as<void>(), g));
+                sbo::grid_layout(g, m, ctx->qgrid);
+                ctx->qgrid_x = qx;
+                ctx->qgrid_y = qy;
+                ctx->qgrid_m = m;
+            }
+        }
+        if (ctx->query_order == 1 && ctx->qgrid.ok) {
+            SBO_HIP(sbo::launch_query_grid(ctx->stream, qx, qy, m, ctx->qgrid, ctx->qgwork.as<void>(), &p, &sx, &sy));
+            ms = ctx->qgrid.ms;
+        } else {
+            const size_t wb = sbo::query_order_bytes(m);
+            SBO_HIP(ctx->qwork.reserve(wb));
+            SBO_HIP(sbo::launch_query_order(ctx->stream, qx, qy, m, ctx->bbox, ctx->qwork.as<void>(), wb, &p, &sx, &sy));
+        }
         perm = p;
         qx = sx;
         qy = sy;
     }
+    const int64_t ldp = sbo::round_up(ms, 64);
+    SBO_HIP(ctx->part.reserve(sizeof(float) * (size_t)nI * (size_t)ldp));
+    SBO_HIP(ctx->mean.reserve(sizeof(float) * (size_t)ldp));
+    const int64_t nb = sbo::acq_blocks(ms);
+    SBO_HIP(ctx->keys.reserve(sizeof(sbo_key) * (size_t)(nb + 1)));
+    sbo_key *bkeys = ctx->keys.as<sbo_key>();
     const int P = ctx->sweep_groups > 0 ? ctx->sweep_groups : std::max(1, ctx->num_cu);
-    SBO_HIP(ctx->plan_work.reserve(sbo::predict_work_bytes(ctx->npad, m, P)));
-    SBO_HIP(sbo::launch_plan(ctx->stream, ctx->kbox.as<float4>(), ctx->npad, qx, qy, m, ldp,
+    SBO_HIP(ctx->plan_work.reserve(sbo::predict_work_bytes(ctx->npad, ms, P)));
+    SBO_HIP(sbo::launch_plan(ctx->stream, ctx->kbox.as<float4>(), ctx->npad, qx, qy, ms, ldp,
                              (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan, ctx->part.as<float>(),
                              ctx->mean.as<float>(),
                              ctx->prof && !cost ? ctx->counters.as<unsigned long long>() : nullptr, P,
                              ctx->plan_work.as<void>(), ctx->plan_work.capacity()));
     if (cost) {  // sbo_query_cost: the plan's work per query, no sweep
-        SBO_HIP(ctx->qcost.reserve(sizeof(float) * (size_t)((m + sbo::kBN - 1) / sbo::kBN)));
-        SBO_HIP(sbo::launch_plan_cost(ctx->stream, ctx->npad, m, P, ctx->plan_work.as<void>(), perm,
+        SBO_HIP(ctx->qcost.reserve(sizeof(float) * (size_t)((ms + sbo::kBN - 1) / sbo::kBN)));
+        SBO_HIP(sbo::launch_plan_cost(ctx->stream, ctx->npad, ms, P, ctx->plan_work.as<void>(), perm,
                                       ctx->qcost.as<float>(), cost));
         return SBO_OK;
     }
@@ -546,22 +567,22 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         const unsigned short *tl = nullptr;
         const int *seg = nullptr;
         const int4 *rec = nullptr;
-        sbo::plan_views(ctx->npad, m, P, ctx->plan_work.as<void>(), &desc, &tl, &seg, &rec);
+        sbo::plan_views(ctx->npad, ms, P, ctx->plan_work.as<void>(), &desc, &tl, &seg, &rec);
         Bracket br(ctx, ctx->ev_predict);
         SBO_HIP(sbo::launch_predict_x3(ctx->stream, ctx->ax3.as<char>(), ctx->kc3.as<float>(), desc, rec, seg, P,
-                                       (int)(nIc * ((m + sbo::kBN - 1) / sbo::kBN)), (int)nIc, qx, qy, m, ldp,
+                                       (int)(nIc * ((ms + sbo::kBN - 1) / sbo::kBN)), (int)nIc, qx, qy, ms, ldp,
                                        sbo::exp2_coef_f((float)ctx->hyper.length_scale),
                                        (float)ctx->hyper.prior_mean, ctx->part.as<float>(), ctx->mean.as<float>(),
                                        ctx->kernel_variant));
     } else {
         Bracket br(ctx, ctx->ev_predict);
         SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(), ctx->npad, qx, qy,
-                                    m, ldp, (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean,
+                                    ms, ldp, (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean,
                                     ctx->part.as<float>(), ctx->mean.as<float>(), ctx->kernel_variant, P,
                                     ctx->plan_work.as<void>()));
     }
     const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
-    SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<float>(), ctx->mean.as<float>(), (int)nI, ldp, m, sf2,
+    SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<float>(), ctx->mean.as<float>(), (int)nI, ldp, ms, sf2,
                                 beta, f_min, score_kind, index_offset, perm, mu, sd, lo, hi, safe, bkeys));
     SBO_HIP(sbo::launch_reduce_keys(ctx->stream, bkeys, nb, key_dev ? key_dev : bkeys + nb));
     return SBO_OK;
@@ -1048,7 +1069,8 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->spatial_order = (int)value;
             return SBO_OK;
         case SBO_OPT_QUERY_ORDER:
-            ctx->query_order = value != 0;
+            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_QUERY_ORDER must be 0, 1 or 2");
+            ctx->query_order = (int)value;
             return SBO_OK;
         case SBO_OPT_SKIP_BUDGET:
             SBO_CHECK(value >= 10 && value <= 60, SBO_E_INVAL, "SBO_OPT_SKIP_BUDGET must be in [10, 60]");

@@ -31,6 +31,15 @@ __host__ __device__ inline int64_t round_up(int64_t v, int64_t m) { return (v + 
 // First packed tile of row block I: sum_{I'<I} (I'+1)*(BM/BK).
 __host__ __device__ inline int64_t tile_start(int64_t I) { return kTilesPerRowBlockStep * I * (I + 1) / 2; }
 inline int64_t total_tiles(int64_t nI) { return tile_start(nI); }
+// raster-grid query blocks (query_order.hip): kGridPatchFast points along
+// the grid's fast axis x kGridPatchSlow rows
+constexpr int kGridPatchFast = 8, kGridPatchSlow = 16;
+static_assert(kGridPatchFast * kGridPatchSlow == kBN, "a grid patch is one query block");
+struct QueryGrid {
+    bool ok = false;
+    int64_t W = 0, c0 = 0, R = 0, npf = 0, ms = 0;  // row length, first row's column, rows, patches per row, positions
+};
+inline int64_t grid_max_positions(int64_t m) { return round_up(m + m / 8 + kBN, kBN); }
 // Element offset inside a packed [BK][BM] tile of A[row][k] (row < BM, k < BK).
 // The MFMA is 16x16x4: lane (k&3, row&15) of a k step needs A of the sixteen
 // 16-row blocks of its row; blocks 4jj..4jj+3 sit side by side, so four
@@ -110,7 +119,12 @@ struct sbo_ctx {
     double alpha_l1 = 0.0;       // sum_j |sf2 alpha_j|
     std::vector<int64_t> order;  // internal row -> caller's training index
     float bbox[4] = {0.f, 0.f, 0.f, 0.f};  // training bounding box (x0, x1, y0, y1)
-    bool query_order = true;     // SBO_OPT_QUERY_ORDER: sweep queries in Morton order
+    int query_order = 1;         // SBO_OPT_QUERY_ORDER: 0 caller order, 1 grid patches or Morton, 2 Morton
+    // grid layout of the last query buffers seen (the layout depends on (m, W, c0) only)
+    const float *qgrid_x = nullptr, *qgrid_y = nullptr;
+    int64_t qgrid_m = -1;
+    sbo::QueryGrid qgrid;
+    sbo::DevBuf qgwork;          // grid detection + patch layout workspace
     int kernel_variant = 3;      // SBO_OPT_KERNEL_VARIANT: predictive kernel (3: split-operand bf16 sweep)
     int sweep_groups = 0;        // SBO_OPT_SWEEP_GROUPS: persistent sweep workgroups (0: one per CU)
     int num_cu = 0;              // compute units of the device
@@ -287,6 +301,19 @@ hipError_t launch_acquire(hipStream_t s, const float *part, const float *mean, i
 size_t query_order_bytes(int64_t m);
 hipError_t launch_query_order(hipStream_t s, const float *qx, const float *qy, int64_t m, const float bbox[4],
                               void *work, size_t work_bytes, int32_t **perm, float **sqx, float **sqy);
+// Raster-grid queries (query_order.hip): blocks of kGridPatchFast points
+// along the grid's fast axis x kGridPatchSlow rows, patches in raster order,
+// padded positions with perm = -1.  launch_grid_detect (workspace
+// query_grid_bytes(m), synchronizes the stream) reads the raster's shape;
+// grid_layout turns it into a layout (false: not a raster, or more padding
+// than grid_max_positions allows -- Morton then); launch_query_grid
+// gathers the q.ms sweep positions.
+size_t query_grid_bytes(int64_t m);
+hipError_t launch_grid_detect(hipStream_t s, const float *qx, const float *qy, int64_t m, void *work,
+                              unsigned long long host_g[6]);
+bool grid_layout(const unsigned long long g[6], int64_t m, QueryGrid &q);
+hipError_t launch_query_grid(hipStream_t s, const float *qx, const float *qy, int64_t m, const QueryGrid &q,
+                             void *work, int32_t **perm, float **sqx, float **sqy);
 // ComputeSets from given mu/sd (staged API).
 hipError_t launch_sets(hipStream_t s, const float *mu, const float *sd, int64_t m, double beta,
                        double f_min, double *lo, double *hi, uint8_t *safe);

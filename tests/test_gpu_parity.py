@@ -678,6 +678,56 @@ def test_split_operand_sweep(mapper, variant):
     gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 3)
 
 
+def _grid_tick(gm, qx, qy, wl):
+    m = qx.size
+    out = dict(mu=np.empty(m, np.float32), sd=np.empty(m, np.float32), lo=np.empty(m), hi=np.empty(m),
+               safe=np.empty(m, np.uint8))
+    key = gm.tick(np.ascontiguousarray(qx, np.float32), np.ascontiguousarray(qy, np.float32), wl.beta, wl.f_min,
+                  outputs=out)
+    return out, (float(key.score), int(key.idx))
+
+
+def test_grid_query_blocks(mapper):
+    """Raster-grid queries are swept in 8 x 16 grid patches (partial patches
+    padded, their positions write nothing): outputs match the caller-order
+    sweep within 1e-5 and the acquisition is consistent with them, for a
+    full grid with odd sides, a shard of its rows cut mid-row, the same grid
+    column-major, and a reused query buffer whose contents are no longer a
+    grid (the cached patch layout is a valid permutation for any points)."""
+    wl = synthetic(3000, 203, 157, seed=27)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    W, H = 203, 157
+    qx, qy = wl.qx, wl.qy
+    rng = np.random.default_rng(5)
+    cases = {
+        "grid": (qx, qy),
+        "rows cut mid-row": (qx[W * 3 + 50: W * 120 + 17], qy[W * 3 + 50: W * 120 + 17]),
+        "column-major": (qx.reshape(H, W).T.ravel(), qy.reshape(H, W).T.ravel()),
+        "reused buffer, scattered points": (rng.permutation(qx), rng.permutation(qy)),
+    }
+    try:
+        for name, (x, y) in cases.items():
+            gm.set_option(N.SBO_OPT_QUERY_ORDER, 0)
+            ref, rkey = _grid_tick(gm, x, y, wl)
+            gm.set_option(N.SBO_OPT_QUERY_ORDER, 1)
+            out, key = _grid_tick(gm, x, y, wl)
+            e_mu = nrel(out["mu"], ref["mu"].astype(np.float64))
+            e_var = nrel(out["sd"].astype(np.float64) ** 2, ref["sd"].astype(np.float64) ** 2)
+            print(f"{name}: m {x.size}  mu {e_mu:.2e}  var {e_var:.2e}  key {key} vs {rkey}")
+            assert e_mu < 1e-5 and e_var < 1e-5, name
+            # every caller index written, sets consistent with the tick's own mu/sd
+            olo, ohi, osafe = O.compute_sets(out["mu"], out["sd"], wl.beta, wl.f_min)
+            assert np.array_equal(out["lo"], olo) and np.array_equal(out["hi"], ohi), name
+            assert np.array_equal(out["safe"], osafe), name
+            oi, os_ = O.argmax(ohi - olo, osafe)
+            assert key[1] == oi, name
+    finally:
+        gm.set_option(N.SBO_OPT_QUERY_ORDER, 1)
+    with pytest.raises(N.SboError):
+        gm.set_option(N.SBO_OPT_QUERY_ORDER, 3)
+
+
 def test_spatial_order_does_not_change_the_posterior(mapper):
     wl = synthetic(3000, 64, 48, seed=22)
     out = {}
