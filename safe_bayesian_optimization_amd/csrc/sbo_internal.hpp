@@ -108,7 +108,7 @@ struct sbo_ctx {
     int64_t linv_n = 0;          // rows of the f64 L^-1 held in Linv (0: none; appends extend it)
     int inverse_bits = 64;       // SBO_OPT_INVERSE_BITS: precision of the L^-1 computation
     bool chol_blocked = true;    // SBO_OPT_CHOLESKY: 1 own blocked factorization, 0 rocSOLVER spotrf
-    int spatial_order = 1;       // SBO_OPT_SPATIAL_ORDER: 0 caller order, 1 Hilbert, 2 Morton
+    int spatial_order = 3;       // SBO_OPT_SPATIAL_ORDER: 0 caller order, 1 Hilbert, 2 Morton, 3 k-d
     int skip_log2 = -1;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-L (-1: auto)
     int auto_skip_log2 = 160;    // auto K* cutoff for V (half the budget), computed at fit (refresh_operand)
     int auto_skip_mean_log2 = 160;  // auto cutoff the last row block keeps for the mean

@@ -731,7 +731,7 @@ def test_grid_query_blocks(mapper):
 def test_spatial_order_does_not_change_the_posterior(mapper):
     wl = synthetic(3000, 64, 48, seed=22)
     out = {}
-    for order in (1, 2, 0):   # Hilbert (default), Morton, caller order
+    for order in (3, 1, 2, 0):   # k-d (default), Hilbert, Morton, caller order
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
         gm.set_option(N.SBO_OPT_SPATIAL_ORDER, order)
         gm.fit(wl.x, wl.y, wl.obs)
@@ -740,12 +740,12 @@ def test_spatial_order_does_not_change_the_posterior(mapper):
         else:
             assert np.array_equal(np.sort(gm.order()), np.arange(3000))
         out[order] = gm.predict(wl.qx, wl.qy)
-    gm.set_option(N.SBO_OPT_SPATIAL_ORDER, 1)
-    for order in (1, 2):
+    gm.set_option(N.SBO_OPT_SPATIAL_ORDER, 3)
+    for order in (3, 1, 2):
         assert nrel(out[order][0], out[0][0].astype(np.float64)) < 1e-5
         assert nrel(out[order][1].astype(np.float64) ** 2, out[0][1].astype(np.float64) ** 2) < 1e-5
     with pytest.raises(N.SboError):
-        gm.set_option(N.SBO_OPT_SPATIAL_ORDER, 3)
+        gm.set_option(N.SBO_OPT_SPATIAL_ORDER, 4)
 
 
 # ---------------------------------------------------------------- (C5) append
