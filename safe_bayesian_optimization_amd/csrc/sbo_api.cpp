@@ -106,14 +106,16 @@ uint32_t hilbert2(uint32_t a, uint32_t b) {
 }
 
 // k-d order (SBO_OPT_SPATIAL_ORDER 3): recursive bisection of p[0, cnt)
-// across the longer side of its box, the left part a whole number of k-tiles
-// (kBK points) closest to half, down to single k-tiles, each leaf then in
-// caller order (deterministic: the comparator is a total order on
-// (coordinate, index), non-finite coordinates first).  Its 64-point k-tile
-// boxes are ~16 % smaller in semi-perimeter than Hilbert's on scattered
-// points (C4: 2.21 vs 2.65 length units).
-void kd_order(const std::vector<float> &hx, const std::vector<float> &hy, int64_t *p, int64_t cnt) {
-    if (cnt <= sbo::kBK) {
+// across the longer side of its box, each cut on a k-tile boundary of the
+// stored array (off = the first point's position modulo kBK: an appended
+// batch's first leaf fills the partial tile before it) and closest to half,
+// down to single k-tiles, each leaf then in caller order (deterministic:
+// the comparator is a total order on (coordinate, index), non-finite
+// coordinates first).  Its 64-point k-tile boxes are ~16 % smaller in
+// semi-perimeter than Hilbert's on scattered points (C4: 2.21 vs 2.65
+// length units).
+void kd_order(const std::vector<float> &hx, const std::vector<float> &hy, int64_t *p, int64_t cnt, int64_t off) {
+    if (off + cnt <= sbo::kBK) {
         std::sort(p, p + cnt);
         return;
     }
@@ -125,14 +127,15 @@ void kd_order(const std::vector<float> &hx, const std::vector<float> &hy, int64_
         y0 = std::min(y0, b); y1 = std::max(y1, b);
     }
     const std::vector<float> &c = ((double)x1 - x0 >= (double)y1 - y0) ? hx : hy;
-    int64_t left = (cnt / 2 + sbo::kBK / 2) / sbo::kBK * sbo::kBK;
-    left = std::min(std::max<int64_t>(left, sbo::kBK), cnt - 1);
+    // the cut: a tile boundary (off + left a multiple of kBK) closest to half
+    int64_t left = (off + cnt / 2 + sbo::kBK / 2) / sbo::kBK * sbo::kBK - off;
+    left = std::min(std::max<int64_t>(left, sbo::kBK - off), cnt - 1);
     std::nth_element(p, p + left, p + cnt, [&](int64_t a, int64_t b) {
         const float ka = key(c[a]), kb = key(c[b]);
         return ka < kb || (ka == kb && a < b);
     });
-    kd_order(hx, hy, p, left);
-    kd_order(hx, hy, p + left, cnt - left);
+    kd_order(hx, hy, p, left, off);
+    kd_order(hx, hy, p + left, cnt - left, (off + left) % sbo::kBK);
 }
 
 // Copy `count` measurements into the context's training buffers at `dst`,
@@ -150,7 +153,7 @@ sbo_status stage_training(sbo_ctx *ctx, const float *x, const float *y, const fl
     std::vector<int64_t> perm(count);
     for (int64_t i = 0; i < count; ++i) perm[i] = i;
     if (ctx->spatial_order == 3 && count > 1) {
-        kd_order(hx, hy, perm.data(), count);
+        kd_order(hx, hy, perm.data(), count, dst % sbo::kBK);
     } else if (ctx->spatial_order && count > 1) {
         const auto mx = std::minmax_element(hx.begin(), hx.end());
         const auto my = std::minmax_element(hy.begin(), hy.end());
