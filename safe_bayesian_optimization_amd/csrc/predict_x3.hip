@@ -189,7 +189,10 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
         if constexpr (P2) f2[r] = lds_b128(pa + 2 * kXPlane + r * 1024);
     }
     // coordinates of pair 0; pair i+1's are read while pair i is built
-    f32x2v xk = lds_f2(pcn + g * 32), yk = lds_f2(pcn + 128 + g * 32), ak = lds_f2(pcn + 256 + g * 32);
+    // DIAG & 67108864: sf2 alpha read only before the mean's row block (msc != 0)
+    constexpr bool AK_MEAN = (DIAG & 67108864) != 0;
+    f32x2v xk = lds_f2(pcn + g * 32), yk = lds_f2(pcn + 128 + g * 32), ak = {0.f, 0.f};
+    if (!AK_MEAN || msc != 0.0f) ak = lds_f2(pcn + 256 + g * 32);
     f32x2v e[NC];
 #pragma unroll
     for (int rb = 0; rb < 16; ++rb) {
@@ -258,7 +261,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                     xk = lds_f2(pcn + g * 32 + (i + 1) * 8);
                     yk = lds_f2(pcn + 128 + g * 32 + (i + 1) * 8);
                 }
-                ak = lds_f2(pcn + 256 + g * 32 + (i + 1) * 8);
+                if (!AK_MEAN || msc != 0.0f) ak = lds_f2(pcn + 256 + g * 32 + (i + 1) * 8);
             }
         }
         if (SPREAD && rb >= 1 && rb <= PIECES && loader) {
@@ -993,12 +996,12 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 36: SBO_X3_LAUNCH(1, 69651); break;  //   1 product, no next-step K*, no A pieces
         case 37: SBO_X3_LAUNCH(1, 70163); break;  //   and no barrier
         case 38: SBO_X3_LAUNCH(1, 69655); break;  //   no K*, no A pieces, no outer sums
-        case 39: SBO_X3_LAUNCH(1, 335920 + 33554432 + 1073741824); break;  // variant 3 with phase stamps (sbo_debug_x3_stamps)
+        case 39: SBO_X3_LAUNCH(1, 335920 + 33554432 + 1073741824 + 67108864); break;  // variant 3 with phase stamps (sbo_debug_x3_stamps)
         case 41: SBO_X3_LAUNCH(1, 1122352); break;  // diagnostics: variant 3 with the K* split reduced to kh
         // A/B (correct results, measured no faster: DESIGN.md section 10):
         case 42: SBO_X3_LAUNCH(1, 73776 + 2097152); break;  // variant 3, one-product tiles straight into the outer sums
         case 43: SBO_X3_LAUNCH(1, 73776 + 6291456); break;  //   and three-product tiles too
-        case 46: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 8388608); break;  // variant 3 recording only each workgroup's span
+        case 46: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 67108864 + 8388608); break;  // variant 3 recording only each workgroup's span
         case 47: SBO_X3_LAUNCH(1, 73776 + 1024 + 16777216); break;  // variant 3, A stage loaded by waves 0-3 only
         case 48: SBO_X3_LAUNCH(1, 73776 + 1024); break;     // variant 3, A stage loaded by waves 4-7 only
         case 49: SBO_X3_LAUNCH(1, 73776); break;  // variant 3 with the next K* coordinates read at ph 3 (round-2 default)
@@ -1008,8 +1011,9 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 54: SBO_X3_LAUNCH(1, 73776 + 33554432 + 536870912 + 1048576); break;  //   and the split reduced to kh
         case 55: SBO_X3_LAUNCH(1, 73776 + 33554432); break;  // variant 3 without the kh-only split (the default before it)
         case 56: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 524288); break;  // variant 3, kh-only split from three-product steps too (slower)
+        case 57: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824); break;  // variant 3 reading sf2 alpha before every step (the default before)
 #endif
-        default: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead, next coordinates at ph 1, kh-only split between one-product steps
+        default: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 67108864); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead, next coordinates at ph 1, kh-only split between one-product steps, sf2 alpha read only before the mean's row block
     }
 #undef SBO_X3_LAUNCH
     return hipGetLastError();

@@ -249,14 +249,14 @@ constexpr int kLevelShift = 14;
 // its item (kRecFirst, kRecLast).
 constexpr int kRecFirst = 1 << 20, kRecLast = 1 << 21;
 // the split sweeps that honour the plan's precision levels
-inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39 || variant == 41 || variant == 42 || variant == 43 || variant == 46 || variant == 47 || variant == 48 || variant == 49 || variant == 51 || variant == 52 || variant == 53 || variant == 54 || variant == 55 || variant == 56; }
+inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39 || variant == 41 || variant == 42 || variant == 43 || variant == 46 || variant == 47 || variant == 48 || variant == 49 || variant == 51 || variant == 52 || variant == 53 || variant == 54 || variant == 55 || variant == 56 || variant == 57; }
 // Sweeps the product library accepts (all compute the full result; 3 is the
 // default).  The timing diagnostics (parts of the work left out, forced
 // precision levels, phase stamps) exist only in the diagnostic build
 // (-DSBO_DIAG, lib/libsbo_diag.so, selected by SBO_LIB for tools/).
 inline bool variant_allowed(int v) {
 #ifdef SBO_DIAG
-    return v >= 0 && v <= 56;
+    return v >= 0 && v <= 57;
 #else
     return v == 0 || v == 1 || v == 2 || v == 3 || v == 9 || v == 10 || v == 13 || v == 22;
 #endif
