@@ -565,12 +565,14 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     // queries (lanes 0-31 qx, 32-63 qy) and the half-tile's coordinates
     // first, then every wave its A pieces (the youngest kPieces of its
     // vector-memory operations)
-#define SBO_X3_STAGE(akib_, kcf_, h_, qb_, sl_, burst_)                                                 \
+#define SBO_X3_STAGE(akib_, kcf_, h_, qb_, sl_, burst_, first_)                                         \
     do {                                                                                                \
         const uint32_t d_ = lds_smem + (uint32_t)(sl_) * kXSlot;                                        \
         if (lw == 0) {                                                                                  \
-            if (lane < 32) SBO_DMA16(qx + (int64_t)(qb_) * kBN, d_ + kXA + kXC);                        \
-            else SBO_DMA16(qy + (int64_t)(qb_) * kBN - 128, d_ + kXA + kXC);                            \
+            if ((first_) || WIDE) {  /* an item's queries: with its first step only */                  \
+                if (lane < 32) SBO_DMA16(qx + (int64_t)(qb_) * kBN, d_ + kXA + kXC);                    \
+                else SBO_DMA16(qy + (int64_t)(qb_) * kBN - 128, d_ + kXA + kXC);                        \
+            }                                                                                           \
             if (lane < 32) SBO_DMA16(kc3 + (uint32_t)(kcf_) + (h_) * (kXC / 4), d_ + kXA);              \
         }                                                                                               \
         const char *s_ = a_base + ((DIAG & 8) ? 0 : (uint64_t)((akib_) + (h_) * (kXA / 1024)) * 1024u);  \
@@ -620,7 +622,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         s.flags = la_h | ((r.w & kRecFirst) && la_h == 0 ? kFirst : 0) | ((r.w & kRecLast) && la_h == 1 ? kLast : 0) |
                   kValid;
         s.lv = LEVELS ? min((r.w >> 16) & 3, 2) : 0;
-        SBO_X3_STAGE(min((uint32_t)r.x, a_max), r.y, la_h, r.z, sl, burst);
+        SBO_X3_STAGE(min((uint32_t)r.x, a_max), r.y, la_h, r.z, sl, burst, (s.flags & kFirst) != 0);
         la_h ^= 1;
         if (la_h == 0) {
             ++la_e;
@@ -653,9 +655,11 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         }
     double mu[NQ];
     KPieces<WIDE ? 2 : NC> kb, nx;
+    // the lane's query coordinates of the item whose K* is being built: read
+    // from the slot of an item's first step only (its stage alone carries them)
+    float xq[NQ], yq[NQ];
     {
         const lds_char *pq = lds + kXA + kXC;
-        float xq[NQ], yq[NQ];
 #pragma unroll
         for (int c = 0; c < NQ; ++c) {
             mu[c] = 0.0;
@@ -733,11 +737,12 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
 #pragma unroll
                 for (int c = 0; c < NQ; ++c) mu[c] = 0.0;
         }
-        float xq[NQ], yq[NQ];
+        if (WIDE || (nvalid && (s1.flags & kFirst))) {
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) {
-            xq[c] = lds_f(pqn + (qo + 16 * c) * 4);
-            yq[c] = lds_f(pqn + (kBN + qo + 16 * c) * 4);
+            for (int c = 0; c < NQ; ++c) {
+                xq[c] = lds_f(pqn + (qo + 16 * c) * 4);
+                yq[c] = lds_f(pqn + (kBN + qo + 16 * c) * 4);
+            }
         }
         if constexpr (STAMP) SBO_STAMP(t1);
         if constexpr (WIDE)
