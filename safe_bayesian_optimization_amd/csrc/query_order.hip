@@ -11,9 +11,10 @@
 //
 // Raster grids (the node's terrain grid, or a contiguous shard of its rows)
 // get blocks that are whole grid patches instead: 8 points along the fast
-// axis x 16 rows, patches in raster order, partial patches padded (the
-// padded sweep positions repeat a nearby grid point and carry perm = -1, so
-// no output is written for them).  Morton blocks of a grid whose side is not
+// axis x 16 rows, patches in raster order, the last R % 16 rows in patches
+// of the next power-of-two height (as wide as it takes for 128), partial
+// patches padded (a padded sweep position repeats the nearest grid point of
+// its column and carries perm = -1, so no output is written for it).  Morton blocks of a grid whose side is not
 // a power of two are L-shaped or split; at C4 (1000^2) their boxes average
 // 3.2x the patches' area, and the patch blocks keep 6 % fewer k-tiles.  The
 // layout is a function of (m, W, c0) alone -- any data gets a valid
@@ -99,17 +100,26 @@ __global__ void grid_check_kernel(const float *__restrict__ qx, const float *__r
 }
 
 // Sweep position p of the patch layout (see launch_query_grid) -> caller index (or -1) and coordinates.
-__global__ void grid_gather_kernel(const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t W,
-                                   int64_t c0, int64_t R, int64_t npf, int64_t ms, int32_t *__restrict__ perm,
-                                   float *__restrict__ sx, float *__restrict__ sy) {
+__global__ void grid_gather_kernel(const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, QueryGrid q,
+                                   int32_t *__restrict__ perm, float *__restrict__ sx, float *__restrict__ sy) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= ms) return;
-    const int64_t patch = p / kBN, l = p % kBN;
-    const int64_t cf = (patch % npf) * kGridPatchFast + l % kGridPatchFast;
-    const int64_t rs = (patch / npf) * kGridPatchSlow + l / kGridPatchFast;
+    if (p >= q.ms) return;
+    const int64_t W = q.W, c0 = q.c0, R = q.R;
+    const int64_t patch = p / kBN, l = p % kBN, nfp = q.nfull * q.npf;
+    // whole patch rows, then the last rows (R % kGridPatchSlow of them) in
+    // patches q.wl wide and kBN / q.wl tall
+    const int64_t cf = patch < nfp ? (patch % q.npf) * kGridPatchFast + l % kGridPatchFast
+                                   : (patch - nfp) * q.wl + l % q.wl;
+    const int64_t rs = patch < nfp ? (patch / q.npf) * kGridPatchSlow + l / kGridPatchFast
+                                   : q.nfull * kGridPatchSlow + l / q.wl;
     const int64_t i = rs * W + cf - c0;
     const bool valid = cf < W && rs < R && i >= 0 && i < m;
+    // a padded position repeats the nearest grid point of its own column
+    // (the next row before the first row's start c0, the previous row past
+    // the last row's end), so the patch's box stays the patch's
     int64_t src = (rs < R ? rs : R - 1) * W + (cf < W ? cf : W - 1) - c0;
+    if (src < 0) src += W;
+    if (src >= m) src -= W;
     src = src < 0 ? 0 : (src >= m ? m - 1 : src);
     perm[p] = valid ? (int32_t)i : -1;
     sx[p] = qx[src];
@@ -146,10 +156,15 @@ bool grid_layout(const unsigned long long g[6], int64_t m, QueryGrid &q) {
         if (g[3 * o + 2] || j2 >= (unsigned long long)m || j2 - j1 < j1) continue;
         const int64_t W = (int64_t)(j2 - j1), c0 = W - (int64_t)j1;
         const int64_t R = (c0 + m + W - 1) / W;
-        const int64_t npf = (W + kGridPatchFast - 1) / kGridPatchFast, nps = (R + kGridPatchSlow - 1) / kGridPatchSlow;
-        const int64_t ms = npf * nps * kBN;
+        const int64_t npf = (W + kGridPatchFast - 1) / kGridPatchFast, nfull = R / kGridPatchSlow;
+        // the last R % kGridPatchSlow rows: patches of the next power-of-two height
+        const int64_t h = R % kGridPatchSlow;
+        int64_t hp = 1;
+        while (hp < h) hp <<= 1;
+        const int64_t wl = h ? kBN / hp : kBN, npl = h ? (W + wl - 1) / wl : 0;
+        const int64_t ms = (nfull * npf + npl) * kBN;
         if (W < kGridPatchFast || ms > grid_max_positions(m)) continue;  // too much padding: Morton instead
-        q = QueryGrid{true, W, c0, R, npf, ms};
+        q = QueryGrid{true, W, c0, R, npf, ms, nfull, wl};
         return true;
     }
     return false;
@@ -162,8 +177,8 @@ hipError_t launch_query_grid(hipStream_t s, const float *qx, const float *qy, in
     int32_t *perm = reinterpret_cast<int32_t *>(p);
     float *xs = reinterpret_cast<float *>(perm + a);
     float *ys = xs + a;
-    hipLaunchKernelGGL(grid_gather_kernel, dim3((unsigned)((q.ms + 255) / 256)), dim3(256), 0, s, qx, qy, m, q.W, q.c0,
-                       q.R, q.npf, q.ms, perm, xs, ys);
+    hipLaunchKernelGGL(grid_gather_kernel, dim3((unsigned)((q.ms + 255) / 256)), dim3(256), 0, s, qx, qy, m, q, perm,
+                       xs, ys);
     *perm_out = perm;
     *sqx = xs;
     *sqy = ys;

@@ -38,6 +38,7 @@ static_assert(kGridPatchFast * kGridPatchSlow == kBN, "a grid patch is one query
 struct QueryGrid {
     bool ok = false;
     int64_t W = 0, c0 = 0, R = 0, npf = 0, ms = 0;  // row length, first row's column, rows, patches per row, positions
+    int64_t nfull = 0, wl = 0;  // whole patch rows; the last rows' patch width (kBN / the next power of two >= R % 16)
 };
 inline int64_t grid_max_positions(int64_t m) { return round_up(m + m / 8 + kBN, kBN); }
 // Element offset inside a packed [BK][BM] tile of A[row][k] (row < BM, k < BK).
