@@ -311,6 +311,14 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * trailing update), 0 rocSOLVER spotrf.  Same f32 algorithm class and the
  * same NOT_SPD reporting (leading minor). */
 #define SBO_OPT_CHOLESKY 8
+/* SBO_OPT_INVERSE (1 default | 0): how the fit computes the f64 L^-1 of
+ * SBO_OPT_INVERSE_BITS = 64 -- 1 the library's block recursion (rocSOLVER
+ * dtrtri on diagonal blocks of <= 2048, the off-diagonal products as
+ * panelled dgemms that leave out the zero half of each triangular factor:
+ * n^3/3 flops), 0 rocsolver_dtrtri on the whole factor (its recursion
+ * multiplies the triangles as full matrices: 2n^3/3).  Same algorithm
+ * class; results agree to f64 rounding.  Takes effect at the next sbo_fit. */
+#define SBO_OPT_INVERSE 9
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The K* tile cutoff in effect (auto or fixed) and the norms it was derived from. */

@@ -42,6 +42,7 @@ SBO_OPT_KERNEL_VARIANT = 5
 SBO_OPT_SWEEP_GROUPS = 6
 SBO_OPT_SKIP_BUDGET = 7
 SBO_OPT_CHOLESKY = 8
+SBO_OPT_INVERSE = 9
 
 
 class SboError(RuntimeError):

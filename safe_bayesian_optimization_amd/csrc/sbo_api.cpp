@@ -57,6 +57,53 @@ sbo_status finish(sbo_ctx *ctx, uint32_t flags) {
     return SBO_OK;
 }
 
+// rocSOLVER info slots: slot 0 for single calls, 1..kInfoSlots-1 for the
+// base cases of the recursive inverse (one each, so a later success cannot
+// overwrite an earlier singular block); refresh_operand reads them all.
+constexpr int kInfoSlots = 64;
+
+// X = L^-1 in place for the lower-triangular f64 matrix at Li (column-major,
+// lda ld; its strictly upper part is zero), by the block recursion
+//     [A 0; B C]^-1 = [A^-1 0; -C^-1 B A^-1  C^-1].
+// rocSOLVER's dtrtri forms the two products with the triangular inverses as
+// full dgemms (2n^3/3 flops at the top of its recursion); here each product
+// is a row of dgemms over panels of width nb that leave out the zero part
+// of the triangle (n^3/3 + O(n^2 nb) flops):
+//     S[:, p] = B[:, p0:h] Ainv[p0:h, p]          (column panels p of A^-1)
+//     X21[p, :] = -Cinv[p, 0:p1] S[0:p1, :]       (row panels p of C^-1)
+// Each panel's diagonal block is multiplied in full; its strictly upper part
+// is zero (widen() writes it, neither rocSOLVER nor this recursion touches
+// it).  S: (n - h) x h doubles of scratch at the top level, reused below.
+sbo_status inverse_lower_f64(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld, double *S, int &slot) {
+    constexpr int64_t kBase = 2048;
+    if (n <= kBase) {
+        rocblas_int *info = ctx->info.as<rocblas_int>() + 1 + (slot++ % (kInfoSlots - 1));
+        SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
+                                  (rocblas_int)ld, info));
+        return SBO_OK;
+    }
+    const int64_t h = sbo::round_up(n / 2, 128), m = n - h;
+    double *B = Li + h, *C = Li + h + h * ld;
+    if (sbo_status st = inverse_lower_f64(ctx, Li, h, ld, S, slot); st != SBO_OK) return st;
+    if (sbo_status st = inverse_lower_f64(ctx, C, m, ld, S, slot); st != SBO_OK) return st;
+    SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
+    const double one = 1.0, minus_one = -1.0, zero = 0.0;
+    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / 8, 128));
+    for (int64_t p0 = 0; p0 < h; p0 += nb) {
+        const int64_t w = std::min(nb, h - p0);
+        SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)m,
+                               (rocblas_int)w, (rocblas_int)(h - p0), &one, B + p0 * ld, (rocblas_int)ld,
+                               Li + p0 + p0 * ld, (rocblas_int)ld, &zero, S + p0 * m, (rocblas_int)m));
+    }
+    for (int64_t p0 = 0; p0 < m; p0 += nb) {
+        const int64_t w = std::min(nb, m - p0);
+        SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)w,
+                               (rocblas_int)h, (rocblas_int)(p0 + w), &minus_one, C + p0, (rocblas_int)ld, S,
+                               (rocblas_int)m, &zero, B + p0, (rocblas_int)ld));
+    }
+    return SBO_OK;
+}
+
 sbo_status check_hyper(sbo_ctx *ctx, const sbo_hyper &h) {
     SBO_CHECK(std::isfinite(h.length_scale) && h.length_scale > 0.0, SBO_E_INVAL,
               "length_scale must be > 0");
@@ -292,6 +339,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                       sizeof(float) * old_tiles * sbo::kTileFloats));
     SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
     rocblas_int hinfo = 0;
+    SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int) * kInfoSlots, ctx->stream));
     if (ctx->inverse_bits == 64) {
         double *Li = ctx->Linv.as<double>();
         if (incr) {
@@ -326,8 +374,16 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)ld * (size_t)ld));
             Li = ctx->Linv.as<double>();
             SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
-            SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
-                                      (rocblas_int)ld, info));
+            if (ctx->inverse_rec) {
+                const int64_t h = sbo::round_up(n / 2, 128);
+                SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max<int64_t>(h * (n - h), 1)));
+                int slot = 0;
+                if (sbo_status st = inverse_lower_f64(ctx, Li, n, ld, ctx->scratch.as<double>(), slot); st != SBO_OK)
+                    return st;
+            } else {
+                SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n,
+                                          Li, (rocblas_int)ld, info));
+            }
         }
         ctx->linv_n = n;
         // alpha = K^-1 (y - m0) = L^-T L^-1 (y - m0), in f64 from the f64
@@ -403,8 +459,11 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     }
     SBO_HIP(ctx->kbox.reserve(sizeof(float4) * (size_t)(npad / sbo::kBK)));
     SBO_HIP(sbo::launch_tile_boxes(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, npad, ctx->kbox.as<float4>()));
-    SBO_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, ctx->stream));
+    rocblas_int hinfos[kInfoSlots];
+    SBO_HIP(hipMemcpyAsync(hinfos, info, sizeof(hinfos), hipMemcpyDeviceToHost, ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
+    for (rocblas_int v : hinfos)
+        if (hinfo == 0) hinfo = v;
     if (hinfo != 0) ctx->linv_n = 0;
     SBO_CHECK(hinfo == 0, SBO_E_NOT_SPD, "trtri: singular factor (info=" + std::to_string(hinfo) + ")");
     ctx->npad = npad;
@@ -1095,6 +1154,10 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
         case SBO_OPT_CHOLESKY:
             SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_CHOLESKY must be 0 or 1");
             ctx->chol_blocked = value != 0;
+            return SBO_OK;
+        case SBO_OPT_INVERSE:
+            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_INVERSE must be 0 or 1");
+            ctx->inverse_rec = value != 0;
             return SBO_OK;
         case SBO_OPT_INVERSE_BITS:
             SBO_CHECK(value == 32 || value == 64, SBO_E_INVAL, "SBO_OPT_INVERSE_BITS must be 32 or 64");

@@ -790,6 +790,36 @@ def test_append_incremental_inverse(mapper):
     assert nrel(mu, omu) < REL_TOL and nrel(sd.astype(np.float64) ** 2, ovar) < REL_TOL
 
 
+@pytest.mark.parametrize("n", [2049, 4100, 5000])
+def test_recursive_inverse_matches_dtrtri(mapper, n):
+    """The fit's f64 L^-1 by the library's block recursion (SBO_OPT_INVERSE =
+    1, default: panelled dgemms over the triangles' nonzero parts, rocSOLVER
+    dtrtri on <= 2048 diagonal blocks) and by rocsolver_dtrtri on the whole
+    factor (0): both equal sf2 * inv(L) of the device factor to f32 rounding
+    of the packed operand, and the posterior agrees with the oracle."""
+    from scipy.linalg import solve_triangular
+    wl = synthetic(n, 24, 20, seed=n + 7)
+    got = {}
+    for rec in (0, 1):
+        gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+        gm.set_option(N.SBO_OPT_INVERSE, rec)
+        gm.fit(wl.x, wl.y, wl.obs)
+        L, _ = gm.factor()
+        A = np.zeros((n, n), np.float32)
+        gm.ctx.check(N.lib().sbo_get_inverse(gm.ctx.handle, A.ctypes.data))
+        ref = wl.hyper.sf2 * solve_triangular(L.astype(np.float64), np.eye(n), lower=True)
+        err = np.abs(np.tril(A) - ref).max() / np.abs(ref).max()
+        print(f"n={n} inverse={rec}: max rel err {err:.2e}")
+        assert err < 1e-6, (rec, err)
+        assert not np.triu(A, 1).any()
+        mu, sd = gm.predict(wl.qx, wl.qy)
+        omu, ovar = oracle_given_factor(gm, wl)
+        assert nrel(mu, omu) < REL_TOL and nrel(sd.astype(np.float64) ** 2, ovar) < REL_TOL
+        got[rec] = np.tril(A)
+    gm.set_option(N.SBO_OPT_INVERSE, 1)
+    assert np.abs(got[0] - got[1]).max() <= 2e-6 * np.abs(got[0]).max()
+
+
 # ------------------------------------------------------ full-size properties
 def test_c3_properties(dev):
     """N=8192 with a 1024x1024 grid (C3): properties that hold at any size --
