@@ -59,7 +59,8 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=None,
                    help="ranks (one per GPU); > 1 without WORLD_SIZE launches them itself")
-    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--steps", type=int, default=300,
+                   help="timed ticks (default 300: ~7 s at C4, long enough for a 5 s utilisation sampler)")
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
     p.add_argument("--n", type=int, default=None, help="override N")
