@@ -210,6 +210,10 @@ SBO_API int sbo_project_subgoal(const double *rx, const double *ry, int64_t n, d
  * SBO_E_STATE before the first fit. */
 SBO_API sbo_status sbo_get_bounds(const sbo_ctx *ctx, double *bounds);
 
+/* The diagonal jitter added by SBO_OPT_JITTER_RETRIES to the current fit
+ * (0.0 when the first factorization succeeded).  SBO_E_STATE before a fit. */
+SBO_API sbo_status sbo_get_jitter(const sbo_ctx *ctx, double *jitter);
+
 /* Fitted predictive state as one device blob (fit on one
  * rank, broadcast the operand to the others instead of refitting there).
  * sbo_state_bytes gives the size (the packed sf2 L^-1 tiles dominate:
@@ -319,6 +323,14 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * multiplies the triangles as full matrices: 2n^3/3).  Same algorithm
  * class; results agree to f64 rounding.  Takes effect at the next sbo_fit. */
 #define SBO_OPT_INVERSE 9
+/* SBO_OPT_JITTER_RETRIES (R in [0, 8], default 0): an sbo_fit whose
+ * factorization fails (SBO_E_NOT_SPD: duplicate points with no noise, or a
+ * kernel matrix singular in f32) is retried up to R times with
+ * sf2 * 10^(r-7) added to the diagonal at retry r (1e-6 sf2, 1e-5 sf2, ...).
+ * The jitter that succeeded becomes part of the noise term (appends and
+ * exported state use it too) and sbo_get_jitter reports it; 0 keeps the
+ * reference's behaviour of reporting the failure. */
+#define SBO_OPT_JITTER_RETRIES 10
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The K* tile cutoff in effect (auto or fixed) and the norms it was derived from. */

@@ -31,7 +31,7 @@ EXPORTS = (
     "sbo_key_combine", "sbo_find_safety_contour_indices", "sbo_next_subgoal", "sbo_find_contours_external",
     "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
     "sbo_get_order", "sbo_profile_work", "sbo_profile_mfma", "sbo_debug_x3_stamps", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
-    "sbo_get_bounds", "sbo_get_tile_bounds", "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
+    "sbo_get_bounds", "sbo_get_jitter", "sbo_get_tile_bounds", "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
     "sbo_polygon_correct", "sbo_polydist", "sbo_point_within", "sbo_project_subgoal",
 )
 SBO_OPT_INVERSE_BITS = 1
@@ -43,6 +43,7 @@ SBO_OPT_SWEEP_GROUPS = 6
 SBO_OPT_SKIP_BUDGET = 7
 SBO_OPT_CHOLESKY = 8
 SBO_OPT_INVERSE = 9
+SBO_OPT_JITTER_RETRIES = 10
 
 
 class SboError(RuntimeError):
@@ -129,6 +130,8 @@ def lib():
     L.sbo_get_tile_bounds.restype = st
     L.sbo_get_bounds.argtypes = [vp, vp]
     L.sbo_get_bounds.restype = st
+    L.sbo_get_jitter.argtypes = [vp, ctypes.POINTER(dbl)]
+    L.sbo_get_jitter.restype = st
     L.sbo_state_bytes.argtypes = [vp, ctypes.POINTER(i64)]
     L.sbo_state_bytes.restype = st
     L.sbo_export_state.argtypes = [vp, vp, i64]

@@ -802,15 +802,36 @@ SBO_API sbo_status sbo_fit(sbo_ctx *ctx, const float *x, const float *y, const f
     SBO_HIP(ctx->alpha.reserve(sizeof(float) * n));
     SBO_HIP(ctx->L.reserve(sizeof(float) * (size_t)n * (size_t)n));
     if (sbo_status st = stage_training(ctx, x, y, obs, n, 0, 0, flags)) return st;
-    const float sf2 = (float)(hyper.sigma_f * hyper.sigma_f);
-    {
-        Bracket br(ctx, ctx->ev_fill);
-        SBO_HIP(sbo::launch_rbf_fill(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, ctx->x.as<float>(),
-                                     ctx->y.as<float>(), n, n, (float)hyper.length_scale, sf2,
-                                     (float)hyper.noise_level, true, ctx->L.as<float>()));
+    const double sf2 = hyper.sigma_f * hyper.sigma_f;
+    // SBO_OPT_JITTER_RETRIES = R > 0: a factorization that fails (NOT_SPD)
+    // is retried up to R times with sf2 * 10^(r-7) added to the diagonal
+    // (r = 1..R); the jitter that succeeded stays part of the noise term,
+    // so appends and exported state use the same K (sbo_get_jitter).
+    ctx->jitter = 0.0;
+    for (int r = 0;; ++r) {
+        const double jit = r == 0 ? 0.0 : sf2 * std::pow(10.0, r - 7);
+        {
+            Bracket br(ctx, ctx->ev_fill);
+            SBO_HIP(sbo::launch_rbf_fill(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, ctx->x.as<float>(),
+                                         ctx->y.as<float>(), n, n, (float)hyper.length_scale, (float)sf2,
+                                         (float)(hyper.noise_level + jit), true, ctx->L.as<float>()));
+        }
+        const sbo_status st = factor_and_refresh(ctx);
+        if (st == SBO_OK) {
+            ctx->jitter = jit;
+            ctx->hyper.noise_level = hyper.noise_level + jit;
+            break;
+        }
+        if (st != SBO_E_NOT_SPD || r >= ctx->jitter_retries) return st;
     }
-    if (sbo_status st = factor_and_refresh(ctx)) return st;
     return finish(ctx, flags);
+}
+
+SBO_API sbo_status sbo_get_jitter(const sbo_ctx *ctx, double *jitter) {
+    if (!ctx || !jitter) return SBO_E_INVAL;
+    if (!ctx->fitted) return SBO_E_STATE;
+    *jitter = ctx->jitter;
+    return SBO_OK;
 }
 
 SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, const float *obs, int64_t b,
@@ -1155,6 +1176,10 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_CHOLESKY must be 0 or 1");
             ctx->chol_blocked = value != 0;
             return SBO_OK;
+        case SBO_OPT_JITTER_RETRIES:
+            SBO_CHECK(value >= 0 && value <= 8, SBO_E_INVAL, "SBO_OPT_JITTER_RETRIES must be in [0, 8]");
+            ctx->jitter_retries = (int)value;
+            return SBO_OK;
         case SBO_OPT_INVERSE:
             SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_INVERSE must be 0 or 1");
             ctx->inverse_rec = value != 0;
@@ -1490,6 +1515,7 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
     ctx->n = h.n;
     ctx->npad = h.npad;
     ctx->hyper = sbo_hyper{h.hyper[0], h.hyper[1], h.hyper[2], h.hyper[3]};
+    ctx->jitter = 0.0;  // an exporter's jitter is already part of the imported noise term
     ctx->max_row_l1 = h.max_row_l1;
     ctx->alpha_l1 = h.alpha_l1;
     for (int i = 0; i < 4; ++i) ctx->bbox[i] = h.bbox[i];

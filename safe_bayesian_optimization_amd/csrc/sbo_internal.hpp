@@ -108,6 +108,8 @@ struct sbo_ctx {
     sbo::DevBuf Linv;            // L^-1 (strtri f32 workspace, or dtrtri f64 kept for appends), lda = cap
     int64_t linv_n = 0;          // rows of the f64 L^-1 held in Linv (0: none; appends extend it)
     int inverse_bits = 64;       // SBO_OPT_INVERSE_BITS: precision of the L^-1 computation
+    int jitter_retries = 0;      // SBO_OPT_JITTER_RETRIES: NOT_SPD fits retried with diagonal jitter
+    double jitter = 0.0;         // the diagonal jitter of the current fit (0 unless a retry succeeded)
     bool inverse_rec = true;     // SBO_OPT_INVERSE: 1 own recursive f64 inverse (panelled dgemms), 0 rocSOLVER dtrtri
     bool chol_blocked = true;    // SBO_OPT_CHOLESKY: 1 own blocked factorization, 0 rocSOLVER spotrf
     int spatial_order = 3;       // SBO_OPT_SPATIAL_ORDER: 0 caller order, 1 Hilbert, 2 Morton, 3 k-d

@@ -226,6 +226,13 @@ class TerrainMapper:
         self.ctx.check(st)
         return (float(b[0]), float(b[1])), (float(b[2]), float(b[3]))
 
+    def jitter(self) -> float:
+        """Diagonal jitter the current fit needed (SBO_OPT_JITTER_RETRIES; 0.0
+        when the first factorization succeeded)."""
+        j = ctypes.c_double()
+        self.ctx.check(self._lib.sbo_get_jitter(self.ctx.handle, ctypes.byref(j)))
+        return j.value
+
     def skip_info(self):
         """(cutoff exponent L in effect, max_i |A_i|_1, |sf2 alpha|_1)."""
         L, r, a = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()

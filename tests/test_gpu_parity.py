@@ -141,6 +141,41 @@ def test_blocked_cholesky_not_spd_past_first_block(mapper):
         gm.fit(x, y, wl.obs)
 
 
+def test_jitter_retry_recovers_not_spd(mapper):
+    """SBO_OPT_JITTER_RETRIES (failure recovery): a singular K
+    (a duplicated point, no noise) is reported as NOT_SPD by default; with
+    retries the fit succeeds with the smallest jitter sf2 * 10^(r-7) that
+    factors, L L^T = K + jitter I to the backward-error bound, and the
+    posterior is finite with sigma in [0, sf] (the jittered K is too
+    ill-conditioned in f32 for the 1e-5 contract against the oracle)."""
+    wl = synthetic(300, 24, 20, seed=4)
+    x, y = f32(wl.x), f32(wl.y)
+    x[200], y[200] = x[10], y[10]
+    hyper = Hyper(noise_level=0.0)
+    gm = TerrainMapper(0, hyper, ctx=mapper.ctx)
+    with pytest.raises(N.NotSPDError):
+        gm.fit(x, y, wl.obs)
+    gm.set_option(N.SBO_OPT_JITTER_RETRIES, 6)
+    try:
+        gm.fit(x, y, wl.obs)
+        jit = gm.jitter()
+        assert jit > 0.0 and any(np.isclose(jit, 10.0 ** (r - 7)) for r in range(1, 7)), jit
+        L, alpha = gm.factor()
+        o = gm.order()
+        K = O.rbf_fill_f32in(x[o], y[o]) + jit * np.eye(300)
+        L64 = L.astype(np.float64)
+        assert np.linalg.norm(L64 @ L64.T - K) / np.linalg.norm(K) <= 10 * 300 * EPS32
+        mu, sd = gm.predict(wl.qx, wl.qy)
+        assert np.isfinite(mu).all() and np.isfinite(alpha).all()
+        assert (sd >= 0).all() and (sd <= np.sqrt(hyper.sf2) * (1 + 1e-6)).all()
+        # a regular fit (with noise) on the same context reports no jitter
+        gm2 = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+        gm2.fit(wl.x, wl.y, wl.obs)
+        assert gm2.jitter() == 0.0
+    finally:
+        gm.set_option(N.SBO_OPT_JITTER_RETRIES, 0)
+
+
 def test_not_spd_is_reported(mapper):
     x = np.array([0.0, 0.0, 1.0], np.float32)
     with pytest.raises(N.NotSPDError):
