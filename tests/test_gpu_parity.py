@@ -162,7 +162,7 @@ def test_jitter_retry_recovers_not_spd(mapper):
         assert jit > 0.0 and any(np.isclose(jit, 10.0 ** (r - 7)) for r in range(1, 7)), jit
         L, alpha = gm.factor()
         o = gm.order()
-        K = O.rbf_fill_f32in(x[o], y[o]) + jit * np.eye(300)
+        K = O.rbf_fill_f32in(x[o], y[o], hyper.length_scale, hyper.sf2, 0.0) + jit * np.eye(300)
         L64 = L.astype(np.float64)
         assert np.linalg.norm(L64 @ L64.T - K) / np.linalg.norm(K) <= 10 * 300 * EPS32
         mu, sd = gm.predict(wl.qx, wl.qy)
