@@ -132,3 +132,57 @@ def allreduce_key(key_dev, group=None) -> tuple[float, int]:
     out = torch.empty(world * 2, dtype=torch.int64, device=key_dev.device)
     dist.all_gather_into_tensor(out, key_dev.reshape(2), group=group)
     return combine_keys(key_tensor_to_pairs(out))
+
+
+def rank_cuts(lo: int, hi: int, device="cpu", group=None) -> list[int]:
+    """Every rank's [lo, hi) as one cut list (one all-gather of two int64;
+    the blocks are contiguous and in rank order)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if world == 1:
+        return [lo, hi]
+    mine = torch.tensor([lo, hi], dtype=torch.int64, device=device)
+    out = torch.empty(2 * world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(out, mine, group=group)
+    p = [int(v) for v in out.cpu()]
+    cuts = [p[0]] + [p[2 * r + 1] for r in range(world)]
+    assert all(p[2 * r] == cuts[r] for r in range(world)), p
+    return cuts
+
+
+def gather_rows(local, cuts, group=None):
+    """The whole M-vector of a per-query output (S, lo, hi, mu, sigma) on
+    every rank from each rank's contiguous block [cuts[r], cuts[r+1])
+    (optional exchange: the node-parity frontier and a full
+    map need the whole grid): one all-gather of the blocks padded to the
+    longest -- RCCL on device tensors, gloo on CPU ones -- then the padding
+    dropped.  Off the headline path: the tick itself exchanges 16 bytes."""
+    import torch
+    import torch.distributed as dist
+    world = len(cuts) - 1
+    if world == 1:
+        return local
+    sizes = [b - a for a, b in zip(cuts, cuts[1:])]
+    w = max(sizes)
+    rank = dist.get_rank(group)
+    assert local.numel() == sizes[rank], (local.numel(), sizes, rank)
+    buf = torch.zeros(w, dtype=local.dtype, device=local.device)
+    buf[: sizes[rank]] = local.reshape(-1)
+    out = torch.empty(world * w, dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    return torch.cat([out[r * w: r * w + sizes[r]] for r in range(world)])
+
+
+def sharded_subgoal(subgoal_fn, Dx, Dy, lo, hi, safe, cuts, width: int, height: int, goal, group=None):
+    """GetNextSubgoal (node.cpp:499-550) over the whole grid when the tick is
+    sharded by rows: lo, hi (f64) and S (u8) gathered from every rank -- 17
+    bytes per point -- then ``subgoal_fn(Dx, Dy, lo, hi, S, width, height,
+    gx, gy)`` on the full arrays on every rank (the frontier trace is
+    deterministic, so every rank selects the same index; no second
+    collective).  Dx, Dy: the full grid coordinates (every rank holds the
+    query grid)."""
+    lo_all = gather_rows(lo, cuts, group)
+    hi_all = gather_rows(hi, cuts, group)
+    s_all = gather_rows(safe, cuts, group)
+    return subgoal_fn(Dx, Dy, lo_all, hi_all, s_all, width, height, *goal)

@@ -170,3 +170,56 @@ def test_bench_launches_its_own_ranks(world):
 def test_bench_rejects_gpus_world_mismatch():
     rc, line, r = _bench("--gpus", "2", "--launch-check", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert rc != 0 and line is None and "WORLD_SIZE=1" in r.stderr
+
+
+# ------------------------------------- full-grid exchange for the frontier
+def _subgoal_worker(rank, world, port, cuts, Dx, Dy, lo, hi, s, w, h, goal, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from safe_bayesian_optimization_amd import node as ND
+    from safe_bayesian_optimization_amd.dist import gather_rows, rank_cuts, sharded_subgoal
+    a, b = cuts[rank], cuts[rank + 1]
+    got_cuts = rank_cuts(a, b)
+    t = lambda v: torch.as_tensor(np.ascontiguousarray(v))  # noqa: E731
+    full_lo = gather_rows(t(lo[a:b]), got_cuts).numpy()
+
+    def fn(Dx_, Dy_, lo_, hi_, s_, w_, h_, gx, gy):
+        return ND.next_subgoal(Dx_, Dy_, lo_.numpy(), hi_.numpy(), s_.numpy(), w_, h_, gx, gy)
+
+    idx = sharded_subgoal(fn, Dx, Dy, t(lo[a:b]), t(hi[a:b]), t(s[a:b]), got_cuts, w, h, goal)
+    q.put((rank, got_cuts, bool(np.array_equal(full_lo, lo)), idx))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_subgoal_equals_full(world):
+    """Row shards of lo / hi / S (uneven, as cost-balanced cuts give) are
+    all-gathered into the full grid on every rank, and the subgoal selected
+    from them equals the single-rank GetNextSubgoal on the whole grid."""
+    from scipy.ndimage import gaussian_filter
+    from safe_bayesian_optimization_amd import node as ND
+    rng = np.random.default_rng(5 + world)
+    w, h = 48, 40
+    xs, ys = np.linspace(-2.0, 3.0, w), np.linspace(-1.0, 2.5, h)
+    Dx, Dy = np.tile(xs, h), np.repeat(ys, w)
+    m = Dx.size
+    mu = gaussian_filter(rng.normal(size=(h, w)), 2.0).reshape(-1) * 5
+    sd = rng.uniform(0.01, 1.0, size=m)
+    lo, hi, s = O.compute_sets(mu, sd, 2.0, float(np.percentile(mu, 30)))
+    cuts = [0] + sorted(rng.choice(np.arange(1, m), world - 1, replace=False).tolist()) + [m]
+    goal = (2.5, 2.0)
+    want = ND.next_subgoal(Dx, Dy, lo, hi, s, w, h, *goal)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgoal_worker, args=(r, world, port, cuts, Dx, Dy, lo, hi, s, w, h, goal, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert want >= 0
+    for _, got_cuts, lo_ok, idx in res:
+        assert got_cuts == cuts and lo_ok and idx == want
