@@ -340,6 +340,34 @@ def run_sweep(a, dev, world, rank):
     mfma_flops_launch = pr["mfma_flops"] / max(pr["predict_launches"], 1)
     levels_launch = [x / max(pr["predict_launches"], 1) for x in pr["tiles_by_level"]]
     elapsed, pred_ms_max = _max_over_ranks([elapsed, pred_ms], dev, world, a.backend)
+    subgoal_sharded = None
+    if world > 1 and not a.no_outputs and a.scaling == "strong":
+        # the node-parity frontier needs the whole grid: lo / hi / S of every
+        # rank all-gathered (17 B per point, SURVEY.md 8(e) optional exchange),
+        # then GetNextSubgoal on every rank -- timed apart from the tick
+        from safe_bayesian_optimization_amd.dist import rank_cuts, sharded_subgoal
+        on_dev = a.backend == "nccl"
+        Dx = torch.as_tensor(wl.qx, dtype=torch.float64, device=dev)
+        Dy = torch.as_tensor(wl.qy, dtype=torch.float64, device=dev)
+        goal = (float(wl.qx.mean()), float(wl.qy.mean()))
+        cuts = rank_cuts(lo, hi, device=dev if on_dev else "cpu")
+        loc = [outs[k] if on_dev else outs[k].cpu() for k in ("lo", "hi", "safe")]
+
+        def fn(Dx_, Dy_, lo_, hi_, s_, w_, h_, gx, gy):
+            return gm.ctx.subgoal(Dx_, Dy_, lo_.to(dev), hi_.to(dev), s_.to(dev), w_, h_, gx, gy)
+
+        sg = lambda: sharded_subgoal(fn, Dx, Dy, *loc, cuts, gw, gh, goal)  # noqa: E731
+        sg()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(3):
+            sidx = sg()
+        torch.cuda.synchronize()
+        sub_ms = _max_over_ranks([(time.perf_counter() - t1) * 1e3 / 3], dev, world, a.backend)[0]
+        subgoal_sharded = {"index": sidx, "ms": sub_ms, "goal": goal, "gathered_bytes": 17 * m_total,
+                           "how": "lo/hi/S all-gathered from the row shards (one all_gather each), then "
+                                  "sbo_subgoal on every rank (same index everywhere)"}
     winfo = dist_info(a.backend)
     if rank != 0:
         return None
@@ -370,33 +398,8 @@ def run_sweep(a, dev, world, rank):
         sub_ms = (time.perf_counter() - t1) * 1e3 / 3
         subgoal = {"index": sidx, "ms": sub_ms, "goal": goal,
                    "how": "sbo_subgoal: device raster/owner map, host border follow of the w x h image"}
-    elif world > 1 and not a.no_outputs and a.scaling == "strong":
-        # the node-parity frontier needs the whole grid: lo / hi / S of every
-        # rank all-gathered (17 B per point, SURVEY.md 8(e) optional exchange),
-        # then GetNextSubgoal on every rank -- timed apart from the tick
-        from safe_bayesian_optimization_amd.dist import rank_cuts, sharded_subgoal
-        on_dev = a.backend == "nccl"
-        Dx = torch.as_tensor(wl.qx, dtype=torch.float64, device=dev)
-        Dy = torch.as_tensor(wl.qy, dtype=torch.float64, device=dev)
-        goal = (float(wl.qx.mean()), float(wl.qy.mean()))
-        cuts = rank_cuts(lo, hi, device=dev if on_dev else "cpu")
-        loc = [outs[k] if on_dev else outs[k].cpu() for k in ("lo", "hi", "safe")]
-
-        def fn(Dx_, Dy_, lo_, hi_, s_, w_, h_, gx, gy):
-            return gm.ctx.subgoal(Dx_, Dy_, lo_.to(dev), hi_.to(dev), s_.to(dev), w_, h_, gx, gy)
-
-        sg = lambda: sharded_subgoal(fn, Dx, Dy, *loc, cuts, gw, gh, goal)  # noqa: E731
-        sg()
-        torch.cuda.synchronize()
-        dist.barrier()
-        t1 = time.perf_counter()
-        for _ in range(3):
-            sidx = sg()
-        torch.cuda.synchronize()
-        sub_ms = _max_over_ranks([(time.perf_counter() - t1) * 1e3 / 3], dev, world, a.backend)[0]
-        subgoal = {"index": sidx, "ms": sub_ms, "goal": goal, "gathered_bytes": 17 * m_total,
-                   "how": "lo/hi/S all-gathered from the row shards (one all_gather each), then sbo_subgoal "
-                          "on every rank (same index everywhere)"}
+    else:
+        subgoal = subgoal_sharded
     cpu = cpu_baseline(gm, wl, a.cpu_seconds) if world == 1 and not a.no_cpu else None
     traffic, traffic_src = pmc_traffic(a.config, n, m_total, m)
     regimes = None
