@@ -309,12 +309,11 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * rounding of the sweep itself).  Takes effect at the next sbo_fit /
  * sbo_append. */
 #define SBO_OPT_SKIP_BUDGET 7
-/* SBO_OPT_CHOLESKY (1 default | 2 | 0): the fit's factorization -- 1 the
+/* SBO_OPT_CHOLESKY (1 default | 0): the fit's factorization -- 1 the
  * library's blocked right-looking Cholesky (a one-workgroup kernel per
- * 128-column diagonal block that also inverts it, the panel below as one
- * sgemm with that inverse, rocBLAS ssyrk for the trailing update), 2 the
- * same with rocBLAS strsm for the panel, 0 rocSOLVER spotrf.  Same f32
- * algorithm class and the same NOT_SPD reporting (leading minor). */
+ * 128-column diagonal block, rocBLAS strsm + ssyrk for the panel and the
+ * trailing update), 0 rocSOLVER spotrf.  Same f32 algorithm class and the
+ * same NOT_SPD reporting (leading minor). */
 #define SBO_OPT_CHOLESKY 8
 /* SBO_OPT_INVERSE (1 default | 0): how the fit computes the f64 L^-1 of
  * SBO_OPT_INVERSE_BITS = 64 -- 1 the library's block recursion (rocSOLVER

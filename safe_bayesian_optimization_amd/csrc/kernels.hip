@@ -161,16 +161,10 @@ constexpr int kCholPanel = 8;
 __device__ __forceinline__ float lane_value(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
-// Xinv != nullptr: also L11^-1 (column-major, lda kCholNB, zero above the
-// diagonal) for the panel solve L21 = A21 L11^-T as one sgemm (see
-// blocked_potrf), by rows: X[i][:] = (e_i - L[i][0:i] X[0:i][:]) / L[i][i],
-// thread j owning column j, four partial sums per row (k mod 4), L[i][k]
-// read as an LDS broadcast.
 __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, int64_t ld, int kb, int64_t k0,
-                                                        int *__restrict__ info, float *__restrict__ Xinv) {
+                                                        int *__restrict__ info) {
     static_assert(kCholNB <= 128, "two panel rows per lane of wave 0");
     __shared__ float a[kCholNB][kCholNB + 1];
-    __shared__ float xs[kCholNB][kCholNB];
     __shared__ int s_bad;
     if (*info != 0) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -275,28 +269,6 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, i
     for (int e = tid; e < kb * kb; e += 256) {
         const int i = e % kb, j = e / kb;
         if (i >= j) A[i + (int64_t)j * ld] = a[i][j];
-    }
-    if (!Xinv) return;
-    const int j = tid;
-    for (int i = 0; i < kb; ++i) {
-        if (j < kb) {
-            float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
-            int k = j;   // X[k][j] = 0 for k < j
-            for (; k + 3 < i; k += 4) {
-                s0 = fmaf(a[i][k], xs[k][j], s0);
-                s1 = fmaf(a[i][k + 1], xs[k + 1][j], s1);
-                s2 = fmaf(a[i][k + 2], xs[k + 2][j], s2);
-                s3 = fmaf(a[i][k + 3], xs[k + 3][j], s3);
-            }
-            for (; k < i; ++k) s0 = fmaf(a[i][k], xs[k][j], s0);
-            const float r = (i == j ? 1.0f : 0.0f) - ((s0 + s1) + (s2 + s3));
-            xs[i][j] = i < j ? 0.0f : __fdiv_rn(r, a[i][i]);
-        }
-        __syncthreads();
-    }
-    for (int e = tid; e < kCholNB * kCholNB; e += 256) {
-        const int i = e % kCholNB, c = e / kCholNB;
-        Xinv[e] = (i < kb && c < kb) ? xs[i][c] : 0.0f;
     }
 }
 
@@ -1753,9 +1725,9 @@ hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t 
     return hipGetLastError();
 }
 
-hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info, float *Xinv) {
+hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info) {
     if (kb <= 0 || kb > kCholNB) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, s, A, ld, kb, k0, info, Xinv);
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, s, A, ld, kb, k0, info);
     return hipGetLastError();
 }
 

@@ -493,19 +493,9 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_panel, hipEventDisableTiming));
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_trail, hipEventDisableTiming));
     }
-    const float one = 1.0f, minus_one = -1.0f, zero = 0.0f;
+    const float one = 1.0f, minus_one = -1.0f;
     auto on = [&](hipStream_t st) { return rocblas_set_stream(ctx->blas, st); };
-    // panel solve by the diagonal block's inverse: L21 = A21 X^T, one sgemm
-    // into chol_w and a copy back (rocBLAS strsm builds the same inverse of
-    // the 128 x 128 block itself, in ~10 small launches per step)
-    float *Xinv = nullptr, *W = nullptr;
-    if (ctx->chol_inv_panel && n > sbo::kCholNB) {
-        SBO_HIP(ctx->chol_xinv.reserve(sizeof(float) * sbo::kCholNB * sbo::kCholNB));
-        SBO_HIP(ctx->chol_w.reserve(sizeof(float) * (size_t)(n - sbo::kCholNB) * sbo::kCholNB));
-        Xinv = ctx->chol_xinv.as<float>();
-        W = ctx->chol_w.as<float>();
-    }
-    SBO_HIP(sbo::launch_chol_diag(ctx->stream, L, ld, (int)std::min<int64_t>(sbo::kCholNB, n), 0, info, Xinv));
+    SBO_HIP(sbo::launch_chol_diag(ctx->stream, L, ld, (int)std::min<int64_t>(sbo::kCholNB, n), 0, info));
     bool trail_pending = false;
     sbo_status st = SBO_OK;
     for (int64_t k = 0; k < n; k += sbo::kCholNB) {
@@ -516,28 +506,15 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         const int64_t kb2 = std::min<int64_t>(sbo::kCholNB, m2);   // the next block column
         float *C1 = L11 + kb + kb * ld;                             // its rows k + kb ..
         if (on(ctx->stream) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
-        if (Xinv && kb == sbo::kCholNB) {
-            if (rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m2,
-                              (rocblas_int)kb, (rocblas_int)kb, &one, A21, (rocblas_int)ld, Xinv, sbo::kCholNB,
-                              &zero, W, (rocblas_int)m2) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
-            if (hipMemcpy2DAsync(A21, sizeof(float) * (size_t)ld, W, sizeof(float) * (size_t)m2,
-                                 sizeof(float) * (size_t)m2, (size_t)kb, hipMemcpyDeviceToDevice,
-                                 ctx->stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
-        } else if (rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
-                                 rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11,
-                                 (rocblas_int)ld, A21, (rocblas_int)ld) != rocblas_status_success) {
-            st = SBO_E_DEVICE;
-            break;
-        }
+        if (rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                          rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11, (rocblas_int)ld,
+                          A21, (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
         if (hipEventRecord(ctx->ev_panel, ctx->stream) != hipSuccess ||
             (trail_pending && hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0) != hipSuccess)) { st = SBO_E_DEVICE; break; }
         if (rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m2,
                           (rocblas_int)kb2, (rocblas_int)kb, &minus_one, A21, (rocblas_int)ld, A21, (rocblas_int)ld,
                           &one, C1, (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
-        if (sbo::launch_chol_diag(ctx->stream, C1, ld, (int)kb2, k + kb, info, Xinv) != hipSuccess) {
-            st = SBO_E_DEVICE;
-            break;
-        }
+        if (sbo::launch_chol_diag(ctx->stream, C1, ld, (int)kb2, k + kb, info) != hipSuccess) { st = SBO_E_DEVICE; break; }
         const int64_t m3 = m2 - kb2;
         trail_pending = false;
         if (m3 > 0) {
@@ -1196,9 +1173,8 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
     if (!ctx) return SBO_E_INVAL;
     switch (option) {
         case SBO_OPT_CHOLESKY:
-            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_CHOLESKY must be 0, 1 or 2");
+            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_CHOLESKY must be 0 or 1");
             ctx->chol_blocked = value != 0;
-            ctx->chol_inv_panel = value == 1;
             return SBO_OK;
         case SBO_OPT_JITTER_RETRIES:
             SBO_CHECK(value >= 0 && value <= 8, SBO_E_INVAL, "SBO_OPT_JITTER_RETRIES must be in [0, 8]");

@@ -111,10 +111,7 @@ struct sbo_ctx {
     int jitter_retries = 0;      // SBO_OPT_JITTER_RETRIES: NOT_SPD fits retried with diagonal jitter
     double jitter = 0.0;         // the diagonal jitter of the current fit (0 unless a retry succeeded)
     bool inverse_rec = true;     // SBO_OPT_INVERSE: 1 own recursive f64 inverse (panelled dgemms), 0 rocSOLVER dtrtri
-    bool chol_blocked = true;
-    bool chol_inv_panel = true;  // SBO_OPT_CHOLESKY 1: panels by the diagonal block's inverse (sgemm); 2: rocBLAS strsm
-    sbo::DevBuf chol_xinv;       // the current diagonal block's inverse (kCholNB^2 floats)
-    sbo::DevBuf chol_w;          // the panel product before it is copied into L    // SBO_OPT_CHOLESKY: 1 own blocked factorization, 0 rocSOLVER spotrf
+    bool chol_blocked = true;    // SBO_OPT_CHOLESKY: 1 own blocked factorization, 0 rocSOLVER spotrf
     int spatial_order = 3;       // SBO_OPT_SPATIAL_ORDER: 0 caller order, 1 Hilbert, 2 Morton, 3 k-d
     int skip_log2 = -1;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-L (-1: auto)
     int auto_skip_log2 = 160;    // auto K* cutoff for V (half the budget), computed at fit (refresh_operand)
@@ -285,11 +282,8 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
 hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float4 *lgn);
 // Blocked Cholesky: factor the kb x kb diagonal block at A (column-major,
 // lda = ld) of step k0 in place (kb <= kCholNB); info as rocSOLVER's.
-// Xinv (nullable): also its inverse, kCholNB x kCholNB column-major, zero
-// above the diagonal and outside kb x kb.
 constexpr int kCholNB = 128;
-hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info,
-                            float *Xinv = nullptr);
+hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info);
 // d = (double)in - v;  out = (float)d
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out);

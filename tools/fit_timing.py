@@ -35,7 +35,7 @@ def main():
             gm.fit(X, Y, O)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
-        print(f"N={n} cholesky={('rocSOLVER spotrf', 'own blocked (inverse panels)', 'own blocked (strsm panels)')[ch]} inverse={'own recursion' if inv else 'rocSOLVER dtrtri'}: first fit {ts[0]:.1f} ms, warm refits {', '.join(f'{v:.1f}' for v in ts[1:])} ms", flush=True)
+        print(f"N={n} cholesky={'own blocked' if ch else 'rocSOLVER spotrf'} inverse={'own recursion' if inv else 'rocSOLVER dtrtri'}: first fit {ts[0]:.1f} ms, warm refits {', '.join(f'{v:.1f}' for v in ts[1:])} ms", flush=True)
         gm.close()
 
 
