@@ -57,15 +57,13 @@ sbo_status finish(sbo_ctx *ctx, uint32_t flags) {
     return SBO_OK;
 }
 
-// rocSOLVER info slots: slot 0 for single calls, the base cases of the
-// recursive inverse one each (so a later success cannot overwrite an earlier
-// singular block) -- 1..31 on the fit's stream, 32..63 for the early half on
-// inv_stream; refresh_operand reads them all.
-constexpr int kInfoSlots = 64, kInfoEarly = 32;
+// rocSOLVER info slots: slot 0 for single calls, 1..kInfoSlots-1 for the
+// base cases of the recursive inverse (one each, so a later success cannot
+// overwrite an earlier singular block); refresh_operand reads them all.
+constexpr int kInfoSlots = 64;
 
-// The fit's f64 L^-1 in place for the lower-triangular matrix at Li
-// (column-major, lda ld; its strictly upper part is zero), by the block
-// recursion
+// X = L^-1 in place for the lower-triangular f64 matrix at Li (column-major,
+// lda ld; its strictly upper part is zero), by the block recursion
 //     [A 0; B C]^-1 = [A^-1 0; -C^-1 B A^-1  C^-1].
 // rocSOLVER's dtrtri forms the two products with the triangular inverses as
 // full dgemms (2n^3/3 flops at the top of its recursion); here each product
@@ -76,67 +74,34 @@ constexpr int kInfoSlots = 64, kInfoEarly = 32;
 // Each panel's diagonal block is multiplied in full; its strictly upper part
 // is zero (widen() writes it, neither rocSOLVER nor this recursion touches
 // it).  S: (n - h) x h doubles of scratch at the top level, reused below.
-// The first half (A^-1 and S) needs only the factor's left h columns, so the
-// fit runs it beside the Cholesky's last steps (inverse_first_half on
-// inv_stream); the second half (C^-1, X21) follows the factor.
-constexpr int64_t kInvBase = 2048;
-int64_t inverse_split(int64_t n) { return sbo::round_up(n / 2, 128); }
-
-sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                             int slot0, int &slot);
-
-sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                              int slot0, int &slot) {
-    const int64_t h = inverse_split(n), m = n - h;
-    if (sbo_status st = inverse_lower_f64(ctx, hb, Li, h, ld, S, slot0, slot); st != SBO_OK) return st;
-    SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
-    const double one = 1.0, zero = 0.0;
-    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / 8, 128));
-    for (int64_t p0 = 0; p0 < h; p0 += nb) {
-        const int64_t w = std::min(nb, h - p0);
-        SBO_BLAS(rocblas_dgemm(hb, rocblas_operation_none, rocblas_operation_none, (rocblas_int)m, (rocblas_int)w,
-                               (rocblas_int)(h - p0), &one, Li + h + p0 * ld, (rocblas_int)ld, Li + p0 + p0 * ld,
-                               (rocblas_int)ld, &zero, S + p0 * m, (rocblas_int)m));
-    }
-    return SBO_OK;
-}
-
-sbo_status inverse_second_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                               int slot0, int &slot) {
-    const int64_t h = inverse_split(n), m = n - h;
-    double *B = Li + h, *C = Li + h + h * ld;
-    // C^-1 uses scratch from S + h m on (S itself holds B A^-1 until the end)
-    if (sbo_status st = inverse_lower_f64(ctx, hb, C, m, ld, S + h * m, slot0, slot); st != SBO_OK) return st;
-    SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
-    const double minus_one = -1.0, zero = 0.0;
-    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / 8, 128));
-    for (int64_t p0 = 0; p0 < m; p0 += nb) {
-        const int64_t w = std::min(nb, m - p0);
-        SBO_BLAS(rocblas_dgemm(hb, rocblas_operation_none, rocblas_operation_none, (rocblas_int)w, (rocblas_int)h,
-                               (rocblas_int)(p0 + w), &minus_one, C + p0, (rocblas_int)ld, S, (rocblas_int)m, &zero,
-                               B + p0, (rocblas_int)ld));
-    }
-    return SBO_OK;
-}
-
-// Scratch the recursion needs below a product buffer of (n - h) x h: the
-// sub-problems' own buffers follow it (C^-1's at S + h m).
-int64_t inverse_scratch(int64_t n) {
-    if (n <= kInvBase) return 0;
-    const int64_t h = inverse_split(n), m = n - h;
-    return h * m + std::max(inverse_scratch(h), inverse_scratch(m));
-}
-
-sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                             int slot0, int &slot) {
-    if (n <= kInvBase) {
-        rocblas_int *info = ctx->info.as<rocblas_int>() + slot0 + (slot++ % (kInfoEarly - 1));
-        SBO_BLAS(rocsolver_dtrtri(hb, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
+sbo_status inverse_lower_f64(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld, double *S, int &slot) {
+    constexpr int64_t kBase = 2048;
+    if (n <= kBase) {
+        rocblas_int *info = ctx->info.as<rocblas_int>() + 1 + (slot++ % (kInfoSlots - 1));
+        SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
                                   (rocblas_int)ld, info));
         return SBO_OK;
     }
-    if (sbo_status st = inverse_first_half(ctx, hb, Li, n, ld, S, slot0, slot); st != SBO_OK) return st;
-    return inverse_second_half(ctx, hb, Li, n, ld, S, slot0, slot);
+    const int64_t h = sbo::round_up(n / 2, 128), m = n - h;
+    double *B = Li + h, *C = Li + h + h * ld;
+    if (sbo_status st = inverse_lower_f64(ctx, Li, h, ld, S, slot); st != SBO_OK) return st;
+    if (sbo_status st = inverse_lower_f64(ctx, C, m, ld, S, slot); st != SBO_OK) return st;
+    SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
+    const double one = 1.0, minus_one = -1.0, zero = 0.0;
+    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / 8, 128));
+    for (int64_t p0 = 0; p0 < h; p0 += nb) {
+        const int64_t w = std::min(nb, h - p0);
+        SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)m,
+                               (rocblas_int)w, (rocblas_int)(h - p0), &one, B + p0 * ld, (rocblas_int)ld,
+                               Li + p0 + p0 * ld, (rocblas_int)ld, &zero, S + p0 * m, (rocblas_int)m));
+    }
+    for (int64_t p0 = 0; p0 < m; p0 += nb) {
+        const int64_t w = std::min(nb, m - p0);
+        SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)w,
+                               (rocblas_int)h, (rocblas_int)(p0 + w), &minus_one, C + p0, (rocblas_int)ld, S,
+                               (rocblas_int)m, &zero, B + p0, (rocblas_int)ld));
+    }
+    return SBO_OK;
 }
 
 sbo_status check_hyper(sbo_ctx *ctx, const sbo_hyper &h) {
@@ -374,11 +339,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                       sizeof(float) * old_tiles * sbo::kTileFloats));
     SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
     rocblas_int hinfo = 0;
-    // the early inverse half ran beside the Cholesky (blocked_potrf): its
-    // info slots stay, the rest are cleared
-    const bool early = ctx->inverse_bits == 64 && !incr && ctx->early_inv_n == n;
-    ctx->early_inv_n = 0;
-    SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int) * (early ? kInfoEarly : kInfoSlots), ctx->stream));
+    SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int) * kInfoSlots, ctx->stream));
     if (ctx->inverse_bits == 64) {
         double *Li = ctx->Linv.as<double>();
         if (incr) {
@@ -412,26 +373,14 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         } else {
             SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)ld * (size_t)ld));
             Li = ctx->Linv.as<double>();
-            if (early) {
-                // A^-1 and S = B A^-1 are done: widen the right columns (rows
-                // 0..h-1 zero), then C^-1 and X21 = -C^-1 S
-                const int64_t h = inverse_split(n);
-                SBO_HIP(sbo::launch_widen(ctx->stream, L + h + h * ld, ld, n - h, n - h, true, Li + h + h * ld, ld));
-                SBO_HIP(hipMemset2DAsync(Li + h * ld, sizeof(double) * (size_t)ld, 0, sizeof(double) * (size_t)h,
-                                         (size_t)(n - h), ctx->stream));
+            SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
+            if (ctx->inverse_rec) {
+                const int64_t h = sbo::round_up(n / 2, 128);
+                SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max<int64_t>(h * (n - h), 1)));
                 int slot = 0;
-                if (sbo_status st = inverse_second_half(ctx, ctx->blas, Li, n, ld, ctx->scratch.as<double>(), 1, slot);
-                    st != SBO_OK)
-                    return st;
-            } else if (ctx->inverse_rec) {
-                SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
-                SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max<int64_t>(inverse_scratch(n), 1)));
-                int slot = 0;
-                if (sbo_status st = inverse_lower_f64(ctx, ctx->blas, Li, n, ld, ctx->scratch.as<double>(), 1, slot);
-                    st != SBO_OK)
+                if (sbo_status st = inverse_lower_f64(ctx, Li, n, ld, ctx->scratch.as<double>(), slot); st != SBO_OK)
                     return st;
             } else {
-                SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
                 SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n,
                                           Li, (rocblas_int)ld, info));
             }
@@ -536,39 +485,13 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
 // of step k waits for step k's panel; the next block column of step k + 1
 // waits for the rest of step k (which also wrote that column).  info:
 // rocSOLVER's.
-//
-// early_inv (the fit, SBO_OPT_INVERSE = 1 with the f64 inverse): once the
-// panel of the block column that ends at h = inverse_split(n) is done, the
-// factor's left h columns are final, and the first half of the recursive
-// inverse (widen them, A^-1, S = B A^-1: half of the inverse's flops) runs
-// on inv_stream with its own rocBLAS handle beside the Cholesky's last
-// steps, which leave most CUs idle (one-workgroup diagonal blocks, small
-// trailing updates).  refresh_operand finishes it (early_inv_n).
-sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_int *info, bool early_inv = false) {
+sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_int *info) {
     SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), ctx->stream));
     SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
     if (!ctx->aux_stream) {
         SBO_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_panel, hipEventDisableTiming));
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_trail, hipEventDisableTiming));
-    }
-    ctx->early_inv_n = 0;
-    const bool early = early_inv && n > kInvBase;
-    const int64_t h_inv = early ? inverse_split(n) : -1;
-    bool early_pending = false;
-    if (early) {
-        if (!ctx->inv_stream) {
-            SBO_HIP(hipStreamCreateWithFlags(&ctx->inv_stream, hipStreamNonBlocking));
-            SBO_HIP(hipEventCreateWithFlags(&ctx->ev_half, hipEventDisableTiming));
-            SBO_HIP(hipEventCreateWithFlags(&ctx->ev_inv, hipEventDisableTiming));
-        }
-        if (!ctx->blas_inv) {
-            SBO_BLAS(rocblas_create_handle(&ctx->blas_inv));
-            SBO_BLAS(rocblas_set_stream(ctx->blas_inv, ctx->inv_stream));
-        }
-        SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)ld * (size_t)ld));
-        SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max<int64_t>(inverse_scratch(n), 1)));
-        SBO_HIP(hipMemsetAsync(info + kInfoEarly, 0, sizeof(rocblas_int) * (kInfoSlots - kInfoEarly), ctx->stream));
     }
     const float one = 1.0f, minus_one = -1.0f;
     auto on = [&](hipStream_t st) { return rocblas_set_stream(ctx->blas, st); };
@@ -586,21 +509,6 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         if (rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
                           rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11, (rocblas_int)ld,
                           A21, (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
-        if (k + kb == h_inv) {
-            // the left h columns are final: the inverse's first half on inv_stream
-            if (hipEventRecord(ctx->ev_half, ctx->stream) != hipSuccess ||
-                hipStreamWaitEvent(ctx->inv_stream, ctx->ev_half, 0) != hipSuccess ||
-                sbo::launch_widen(ctx->inv_stream, L, ld, n, h_inv, true, ctx->Linv.as<double>(), ld) != hipSuccess) {
-                st = SBO_E_DEVICE;
-                break;
-            }
-            int slot = 0;
-            early_pending = true;
-            if ((st = inverse_first_half(ctx, ctx->blas_inv, ctx->Linv.as<double>(), n, ld, ctx->scratch.as<double>(),
-                                         kInfoEarly, slot)) != SBO_OK)
-                break;
-            if (hipEventRecord(ctx->ev_inv, ctx->inv_stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
-        }
         if (hipEventRecord(ctx->ev_panel, ctx->stream) != hipSuccess ||
             (trail_pending && hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0) != hipSuccess)) { st = SBO_E_DEVICE; break; }
         if (rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m2,
@@ -623,24 +531,17 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
     if (on(ctx->stream) != rocblas_status_success && st == SBO_OK) st = SBO_E_DEVICE;
     if (st != SBO_OK) {
         (void)hipStreamSynchronize(ctx->aux_stream);
-        if (early_pending) (void)hipStreamSynchronize(ctx->inv_stream);
         ctx->err = "blocked Cholesky: a rocBLAS or HIP call failed";
         return st;
     }
     if (trail_pending) SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
-    if (early_pending) {
-        SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_inv, 0));
-        ctx->early_inv_n = n;
-    }
     return SBO_OK;
 }
 
 sbo_status factor_and_refresh(sbo_ctx *ctx) {
     rocblas_int *info = ctx->info.as<rocblas_int>();
     if (ctx->chol_blocked) {
-        const bool early_inv = ctx->inverse_bits == 64 && ctx->inverse_rec;
-        if (sbo_status st = blocked_potrf(ctx, ctx->L.as<float>(), ctx->n, ctx->cap, info, early_inv); st != SBO_OK)
-            return st;
+        if (sbo_status st = blocked_potrf(ctx, ctx->L.as<float>(), ctx->n, ctx->cap, info); st != SBO_OK) return st;
     } else {
         SBO_BLAS(rocsolver_spotrf(ctx->blas, rocblas_fill_lower, (rocblas_int)ctx->n, ctx->L.as<float>(),
                                   (rocblas_int)ctx->cap, info));
@@ -865,10 +766,6 @@ SBO_API void sbo_destroy(sbo_ctx *ctx) {
     if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
     if (ctx->ev_trail) (void)hipEventDestroy(ctx->ev_trail);
     if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
-    if (ctx->blas_inv) rocblas_destroy_handle(ctx->blas_inv);
-    if (ctx->ev_half) (void)hipEventDestroy(ctx->ev_half);
-    if (ctx->ev_inv) (void)hipEventDestroy(ctx->ev_inv);
-    if (ctx->inv_stream) (void)hipStreamDestroy(ctx->inv_stream);
     if (ctx->blas) rocblas_destroy_handle(ctx->blas);
     if (ctx->host_key) (void)hipHostFree(ctx->host_key);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);

@@ -94,12 +94,6 @@ struct sbo_ctx {
     // (created on first use), ordered against `stream` by two events
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_panel = nullptr, ev_trail = nullptr;
-    // the fit's early inverse half (inv_stream, own rocBLAS handle): started
-    // once the Cholesky has finished the left half of the columns
-    hipStream_t inv_stream = nullptr;
-    rocblas_handle blas_inv = nullptr;
-    hipEvent_t ev_half = nullptr, ev_inv = nullptr;
-    int64_t early_inv_n = 0;     // n of the factor whose early half is done (0: none)
     std::string err;
 
     // fitted model
