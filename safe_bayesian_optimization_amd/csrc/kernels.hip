@@ -1583,8 +1583,18 @@ __global__ __launch_bounds__(kAcqThreads) void acquire_kernel(
     int64_t bi = -1;
     // (perm -1: a padded grid-patch position, no output)
     if (i < m && (!perm || perm[i] >= 0)) {
+        // the row blocks' partials, summed in f64 in ascending I; read eight
+        // at a time so their loads are in flight together (same sum order)
         double s = 0.0;
-        for (int I = 0; I < nI; ++I) s += (double)part[(int64_t)I * ldp + i];
+        int I = 0;
+        for (; I + 8 <= nI; I += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(I + u) * ldp + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += (double)v[u];
+        }
+        for (; I < nI; ++I) s += (double)part[(int64_t)I * ldp + i];
         double vd = (double)sf2 - s;
         float var = vd > 0.0 ? (float)vd : 0.0f;
         const float sd = __fsqrt_rn(var);
