@@ -1202,13 +1202,18 @@ __global__ void plan_perm_kernel(const unsigned long long *__restrict__ scan, in
     cnt2[p] = (unsigned long long)(desc[k].w & 0xffff);
 }
 
-// one wave per item: its tile list to the new offset, its descriptor to its new position
+__device__ __forceinline__ int4 step_record(int64_t ts, int I, int qb, int te, int i, int cnt);
+
+// one wave per item: its tile list to the new offset, its descriptor to its
+// new position, and (rec != nullptr) the split sweep's step records of the
+// moved list -- what plan_rec_kernel would write from desc2 / tl2
 __global__ __launch_bounds__(256) void plan_move_kernel(const unsigned long long *__restrict__ scan, int64_t n_items,
                                                         const int4 *__restrict__ desc,
                                                         const unsigned short *__restrict__ tl,
                                                         const int *__restrict__ pos_of,
                                                         const unsigned long long *__restrict__ off2,
-                                                        int4 *__restrict__ desc2, unsigned short *__restrict__ tl2) {
+                                                        int4 *__restrict__ desc2, unsigned short *__restrict__ tl2,
+                                                        int4 *__restrict__ rec) {
     const int64_t nne = (int64_t)(scan[n_items - 1] >> kPlanKeyShift);
     const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -1218,14 +1223,26 @@ __global__ __launch_bounds__(256) void plan_move_kernel(const unsigned long long
     const uint64_t off = (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
     const int p = pos_of[k];
     const uint64_t o2 = off2[p];
-    for (int i = lane; i < cnt; i += 64) tl2[o2 + i] = tl[off + i];
+    const int64_t ts = tile_start(d.x);
+    for (int i = lane; i < cnt; i += 64) {
+        const unsigned short te = tl[off + i];
+        tl2[o2 + i] = te;
+        if (rec) rec[o2 + i] = step_record(ts, d.x, d.y, te, i, cnt);
+    }
     if (lane == 0) desc2[p] = make_int4(d.x, d.y, (int)(uint32_t)o2, cnt | (int)((o2 >> 32) << 16));
 }
 
 // Step records of the split sweep (kRecFirst in sbo_internal.hpp), one
 // wave per non-empty item, in the order the sweep walks the list (after the
-// XCD permutation): the kernel then stages a tile from one record instead of
-// re-deriving offsets from the descriptor and tile list in every wave.
+// XCD permutation, where plan_move_kernel writes them): the kernel then
+// stages a tile from one record instead of re-deriving offsets from the
+// descriptor and tile list in every wave.
+__device__ __forceinline__ int4 step_record(int64_t ts, int I, int qb, int te, int i, int cnt) {
+    const int t = te & ((1 << kLevelShift) - 1);
+    const int w = I | ((te >> kLevelShift) << 16) | (i == 0 ? kRecFirst : 0) | (i == cnt - 1 ? kRecLast : 0);
+    return make_int4((int)(uint32_t)((ts + t) * 96), t * 256, qb, w);
+}
+
 __global__ __launch_bounds__(256) void plan_rec_kernel(const unsigned long long *__restrict__ scan, int64_t n_items,
                                                        const int4 *__restrict__ desc,
                                                        const unsigned short *__restrict__ tl, int4 *__restrict__ rec) {
@@ -1237,12 +1254,7 @@ __global__ __launch_bounds__(256) void plan_rec_kernel(const unsigned long long 
     const int cnt = d.w & 0xffff;
     const uint64_t off = (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
     const int64_t ts = tile_start(d.x);
-    for (int i = lane; i < cnt; i += 64) {
-        const int te = tl[off + i];
-        const int t = te & ((1 << kLevelShift) - 1);
-        const int w = d.x | ((te >> kLevelShift) << 16) | (i == 0 ? kRecFirst : 0) | (i == cnt - 1 ? kRecLast : 0);
-        rec[off + i] = make_int4((int)(uint32_t)((ts + t) * 96), t * 256, d.y, w);
-    }
+    for (int i = lane; i < cnt; i += 64) rec[off + i] = step_record(ts, d.x, d.y, tl[off + i], i, cnt);
 }
 
 __global__ void plan_seg2_kernel(const int *__restrict__ xseg, int G, int P, int *__restrict__ seg2) {
@@ -1923,11 +1935,8 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
                                 rocprim::plus<unsigned long long>(), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(plan_move_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, scan, items, desc, tl,
-                       pos_of, off2, desc2, tl2);
+                       pos_of, off2, desc2, tl2, skip.records ? rec : nullptr);
     hipLaunchKernelGGL(plan_seg2_kernel, dim3(1), dim3(256), 0, s, xseg, G, P, seg2);
-    if (skip.records)
-        hipLaunchKernelGGL(plan_rec_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, scan, items, desc2,
-                           tl2, rec);
     return hipGetLastError();
 }
 
