@@ -57,10 +57,12 @@ sbo_status finish(sbo_ctx *ctx, uint32_t flags) {
     return SBO_OK;
 }
 
-// rocSOLVER info slots: slot 0 for single calls, 1..kInfoSlots-1 for the
-// base cases of the recursive inverse (one each, so a later success cannot
-// overwrite an earlier singular block); refresh_operand reads them all.
-constexpr int kInfoSlots = 64;
+// rocSOLVER info slots: slot 0 for single calls, 1.. for the base cases of
+// the recursive inverse (one each, so a later success cannot overwrite an
+// earlier singular block); refresh_operand reads them all.  Base cases hold
+// more than 1024 columns each (a block of n > 2048 splits into halves of
+// >= n/2 - 64), so n/512 + 2 slots always suffice.
+int64_t info_slots(int64_t n) { return std::max<int64_t>(64, n / 512 + 2); }
 
 // X = L^-1 in place for the lower-triangular f64 matrix at Li (column-major,
 // lda ld; its strictly upper part is zero), by the block recursion
@@ -77,7 +79,7 @@ constexpr int kInfoSlots = 64;
 sbo_status inverse_lower_f64(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld, double *S, int &slot) {
     constexpr int64_t kBase = 2048;
     if (n <= kBase) {
-        rocblas_int *info = ctx->info.as<rocblas_int>() + 1 + (slot++ % (kInfoSlots - 1));
+        rocblas_int *info = ctx->info.as<rocblas_int>() + 1 + slot++;
         SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
                                   (rocblas_int)ld, info));
         return SBO_OK;
@@ -324,6 +326,8 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
     float *L = ctx->L.as<float>();
     float *alpha = ctx->alpha.as<float>();
+    const int64_t nslots = info_slots(n);
+    SBO_HIP(ctx->info.reserve(sizeof(rocblas_int) * (size_t)nslots));
     rocblas_int *info = ctx->info.as<rocblas_int>();
 
     // L^-1 (lower, non-unit).  Default: widen L to f64 and invert with dtrtri
@@ -339,7 +343,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                       sizeof(float) * old_tiles * sbo::kTileFloats));
     SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
     rocblas_int hinfo = 0;
-    SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int) * kInfoSlots, ctx->stream));
+    SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int) * (size_t)nslots, ctx->stream));
     if (ctx->inverse_bits == 64) {
         double *Li = ctx->Linv.as<double>();
         if (incr) {
@@ -459,8 +463,9 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     }
     SBO_HIP(ctx->kbox.reserve(sizeof(float4) * (size_t)(npad / sbo::kBK)));
     SBO_HIP(sbo::launch_tile_boxes(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, npad, ctx->kbox.as<float4>()));
-    rocblas_int hinfos[kInfoSlots];
-    SBO_HIP(hipMemcpyAsync(hinfos, info, sizeof(hinfos), hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<rocblas_int> hinfos((size_t)nslots);
+    SBO_HIP(hipMemcpyAsync(hinfos.data(), info, sizeof(rocblas_int) * (size_t)nslots, hipMemcpyDeviceToHost,
+                           ctx->stream));
     SBO_HIP(hipStreamSynchronize(ctx->stream));
     for (rocblas_int v : hinfos)
         if (hinfo == 0) hinfo = v;
@@ -493,8 +498,12 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_panel, hipEventDisableTiming));
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_trail, hipEventDisableTiming));
     }
+    if (!ctx->blas_aux) {
+        SBO_BLAS(rocblas_create_handle(&ctx->blas_aux));
+        SBO_BLAS(rocblas_set_stream(ctx->blas_aux, ctx->aux_stream));
+    }
+    SBO_BLAS(rocblas_set_pointer_mode(ctx->blas_aux, rocblas_pointer_mode_host));
     const float one = 1.0f, minus_one = -1.0f;
-    auto on = [&](hipStream_t st) { return rocblas_set_stream(ctx->blas, st); };
     SBO_HIP(sbo::launch_chol_diag(ctx->stream, L, ld, (int)std::min<int64_t>(sbo::kCholNB, n), 0, info));
     bool trail_pending = false;
     sbo_status st = SBO_OK;
@@ -505,7 +514,6 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         float *L11 = L + k + k * ld, *A21 = L11 + kb;
         const int64_t kb2 = std::min<int64_t>(sbo::kCholNB, m2);   // the next block column
         float *C1 = L11 + kb + kb * ld;                             // its rows k + kb ..
-        if (on(ctx->stream) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
         if (rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
                           rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11, (rocblas_int)ld,
                           A21, (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
@@ -518,17 +526,14 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         const int64_t m3 = m2 - kb2;
         trail_pending = false;
         if (m3 > 0) {
-            if (hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0) != hipSuccess ||
-                on(ctx->aux_stream) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
-            if (rocblas_ssyrk(ctx->blas, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)m3, (rocblas_int)kb,
+            if (hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0) != hipSuccess) { st = SBO_E_DEVICE; break; }
+            if (rocblas_ssyrk(ctx->blas_aux, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)m3, (rocblas_int)kb,
                               &minus_one, A21 + kb2, (rocblas_int)ld, &one, C1 + kb2 + kb2 * ld,
                               (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
             trail_pending = true;
             if (hipEventRecord(ctx->ev_trail, ctx->aux_stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
         }
     }
-    // everything after the factorization runs on `stream`
-    if (on(ctx->stream) != rocblas_status_success && st == SBO_OK) st = SBO_E_DEVICE;
     if (st != SBO_OK) {
         (void)hipStreamSynchronize(ctx->aux_stream);
         ctx->err = "blocked Cholesky: a rocBLAS or HIP call failed";
@@ -621,6 +626,15 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     SBO_HIP(ctx->keys.reserve(sizeof(sbo_key) * (size_t)(nb + 1)));
     sbo_key *bkeys = ctx->keys.as<sbo_key>();
     const int P = ctx->sweep_groups > 0 ? ctx->sweep_groups : std::max(1, ctx->num_cu);
+    {
+        // the plan's tile lists and step records are sized for the dense sweep
+        // (every tile of every item) and indexed by 32-bit list positions
+        // (predict_x3.hip reads an item's first entry from desc.z alone)
+        const int64_t nQ = (ms + sbo::kBN - 1) / sbo::kBN;
+        SBO_CHECK((double)2 * nI * (nI + 1) * (double)nQ < 4294967296.0, SBO_E_INVAL,
+                  "sbo_tick: N x M too large for one tick plan (2 nI (nI + 1) nQ >= 2^32 tile entries); "
+                  "split the queries into shards");
+    }
     SBO_HIP(ctx->plan_work.reserve(sbo::predict_work_bytes(ctx->npad, ms, P)));
     SBO_HIP(sbo::launch_plan(ctx->stream, ctx->kbox.as<float4>(), ctx->npad, qx, qy, ms, ldp,
                              (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan, ctx->part.as<float>(),
@@ -765,6 +779,7 @@ SBO_API void sbo_destroy(sbo_ctx *ctx) {
     if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
     if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
     if (ctx->ev_trail) (void)hipEventDestroy(ctx->ev_trail);
+    if (ctx->blas_aux) rocblas_destroy_handle(ctx->blas_aux);
     if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
     if (ctx->blas) rocblas_destroy_handle(ctx->blas);
     if (ctx->host_key) (void)hipHostFree(ctx->host_key);
@@ -1477,9 +1492,14 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
                   SBO_E_INVAL, "sbo_import_state: section offsets do not match the blob's (n, npad)");
         SBO_CHECK(h.total <= bytes, SBO_E_INVAL, "sbo_import_state: truncated blob");
         SBO_CHECK(h.spatial_order >= 0 && h.spatial_order <= 3 && std::isfinite(h.lg_tau_v) &&
-                      std::isfinite(h.hyper[0]) && h.hyper[0] > 0.0 && std::isfinite(h.hyper[1]) &&
-                      std::isfinite(h.hyper[3]) && h.bbox[0] <= h.bbox[1] && h.bbox[2] <= h.bbox[3],
+                      h.bbox[0] <= h.bbox[1] && h.bbox[2] <= h.bbox[3],
                   SBO_E_INVAL, "sbo_import_state: header fields out of range");
+        // the hyper-parameters (noise_level carries the exporter's jitter) pass the fit's own checks
+        const sbo_hyper hh{h.hyper[0], h.hyper[1], h.hyper[2], h.hyper[3]};
+        if (sbo_status st = check_hyper(ctx, hh)) {
+            ctx->err = "sbo_import_state: " + ctx->err;
+            return st;
+        }
     }
     ctx->fitted = false;
     ctx->has_factor = false;

@@ -91,8 +91,11 @@ struct sbo_ctx {
     hipStream_t stream = nullptr;
     rocblas_handle blas = nullptr;
     // the blocked Cholesky's look-ahead: trailing updates on a second stream
-    // (created on first use), ordered against `stream` by two events
+    // (created on first use), ordered against `stream` by two events, with a
+    // rocBLAS handle of its own (a handle's device workspace must not be
+    // shared by kernels in flight on two streams)
     hipStream_t aux_stream = nullptr;
+    rocblas_handle blas_aux = nullptr;
     hipEvent_t ev_panel = nullptr, ev_trail = nullptr;
     std::string err;
 

@@ -142,3 +142,24 @@ def test_c4_scale_frontier(ctx):
     fd, fh = _both(ctx, Dx, Dy, s, w, h)
     print(f"C4 frontier {fd.size} pts; subgoal device {1e3 * (t1 - t0):.2f} ms, host {1e3 * (t2 - t1):.2f} ms")
     assert np.array_equal(fd, fh) and gd == gh >= 0
+
+
+@pytest.mark.parametrize("w,h,sigma", [(1000, 1000, 12.0), (1000, 1000, 3.0), (300, 120, 4.0)])
+def test_device_frontier_topology(ctx, w, h, sigma):
+    """The device raster + border follow at C4 size (and the mapper's own
+    300 x 120 grid, config/lpsc.yaml:38) against the scipy.ndimage topology
+    of tests/frontier_props.py -- no border follower in the check: the
+    frontier's pixels are exactly the outer borders of the external safe
+    components, with at most #contours - 1 breaks in 8-adjacency."""
+    from tests.frontier_props import check_flat_frontier
+    from scipy.ndimage import gaussian_filter
+    rng = np.random.default_rng(int(sigma * 10) + w)
+    img = (gaussian_filter(rng.normal(size=(h, w)), sigma) > 0).astype(np.uint8)
+    cx, cy = _grid(w, h, 0.5, w - 0.5, 0.5, h - 0.5)
+    Dx = np.concatenate([[0.0], cx, [float(w)]])
+    Dy = np.concatenate([[0.0], cy, [float(h)]])
+    s = np.concatenate([[0], img.reshape(-1), [0]]).astype(np.uint8)
+    fd = ctx.frontier(_dev(Dx, np.float64), _dev(Dy, np.float64), _dev(s, np.uint8), w, h)
+    pix = np.stack([(fd - 1) % w, (fd - 1) // w], axis=1)
+    exp = check_flat_frontier(img, pix)
+    print(f"{w}x{h} sigma {sigma}: {len(exp)} external components, frontier {fd.size} px")

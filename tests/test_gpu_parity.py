@@ -957,6 +957,13 @@ def test_state_export_import(dev, mapper):
     bad[256:264] = bad[264:272]
     with pytest.raises(N.SboError):
         b.import_state(bad)
+    # hyper-parameters a fit would refuse: NaN / negative noise (hyper[2], byte
+    # 40: it carries the exporter's jitter) and sigma_f = 0 (hyper[1], byte 32)
+    for off, v in ((40, np.nan), (40, -0.5), (32, 0.0)):
+        bad = blob.clone()
+        bad[off:off + 8] = torch.tensor(np.array([v], np.float64).view(np.uint8), device=bad.device)
+        with pytest.raises(N.SboError):
+            b.import_state(bad)
     # the training bounds travel with the state (the service grid's default extent)
     b.import_state(blob)
     assert b.bounds() == a.bounds()
