@@ -67,6 +67,10 @@ def parse():
     p.add_argument("--grid", type=int, default=None, help="override grid side")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    p.add_argument("--force-pg", action="store_true",
+                   help="initialise the process group (and run every collective of the N > 1 path: key "
+                        "all-gather, cut broadcast, state broadcast + import, full-grid gather) even at one rank "
+                        "-- RCCL exercised on a one-GPU box")
     p.add_argument("--sharding", default="cost", choices=["cost", "equal"],
                    help="strong scaling: cost-balanced contiguous row blocks (default) or equal point counts")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
@@ -138,11 +142,17 @@ def main():
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
-    if world > 1:
+    pg = world > 1 or a.force_pg
+    if pg:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(a.backend)
+    a.pg = pg
     try:
         if a.config == "C5":
             line = run_streaming(a, dev, world, rank)
@@ -151,7 +161,7 @@ def main():
         if rank == 0:
             print(json.dumps(line), flush=True)
     finally:
-        if world > 1:
+        if pg:
             dist.barrier()
             dist.destroy_process_group()
     return 0
@@ -162,7 +172,8 @@ def dist_info(backend):
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
         return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
-                "collective": "all_gather_into_tensor of 16-byte (f64 score, i64 index) keys, one per tick"}
+                "collective": "all_gather_into_tensor of 16-byte (f64 score, i64 index) keys, one per tick",
+                "process_group": True}
     return {"world_size": 1, "backend": None, "collective": None}
 
 
@@ -206,7 +217,7 @@ def run_launch_check(a, world, rank):
 def _max_over_ranks(vals, dev, world, backend):
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if not dist.is_initialized():
         return vals
     t = torch.tensor(vals, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -257,7 +268,7 @@ def run_sweep(a, dev, world, rank):
     # SURVEY.md 8(e) alternative: rank 0 fits, the packed predictive state is
     # broadcast (RCCL) and imported elsewhere -- timed beside the replicated fit
     fit_bcast = None
-    if world > 1:
+    if a.pg:
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -276,12 +287,22 @@ def run_sweep(a, dev, world, rank):
             hb = blob.cpu()
             dist.broadcast(hb, 0)
             blob.copy_(hb)
-        if rank != 0:
-            gm.import_state(blob)
+        if rank != 0 or world == 1:
+            # (one rank: import the broadcast blob into a second context and
+            # check the sweep is bitwise the fitted one's -- the path a
+            # receiving rank takes)
+            tgt = gm if rank != 0 else TerrainMapper(dev.index, wl.hyper)
+            tgt.import_state(blob)
         torch.cuda.synchronize()
         dist.barrier()
         fit_bcast = {"ms": (time.perf_counter() - t0) * 1e3, "state_bytes": int(size.item()),
                      "how": "rank 0 sbo_fit + sbo_export_state, broadcast, sbo_import_state"}
+        if world == 1:
+            qs = f32(wl.qx[:65536]), f32(wl.qy[:65536])
+            ma, sa = gm.predict(*qs)
+            mb, sb = tgt.predict(*qs)
+            fit_bcast["import_bitwise_equal"] = bool(torch.equal(ma, mb) and torch.equal(sa, sb))
+            tgt.close()
         del blob
     # ---- this rank's contiguous block of grid rows (strong scaling): cut so
     # that every rank sweeps about the same number of k-tiles (rank 0 plans
@@ -289,7 +310,7 @@ def run_sweep(a, dev, world, rank):
     # point counts with --sharding equal
     if a.scaling == "weak":
         lo, hi = 0, m_total
-    elif world > 1 and a.sharding == "cost":
+    elif a.pg and a.sharding == "cost":
         lo, hi = cost_balanced_range(gm, f32(wl.qx), f32(wl.qy), rank, world)
     else:
         lo, hi = shard_range(m_total, rank, world)
@@ -300,6 +321,7 @@ def run_sweep(a, dev, world, rank):
         lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
         safe=torch.empty(m, dtype=torch.uint8, device=dev))
     cutoff, row_l1, alpha_l1 = gm.skip_info()
+    prec = gm.precision()
 
     # ---- RBF fill (a1) alone, warm (the fill inside fit also paid the code-object load)
     Kbuf = torch.empty(n * n, dtype=torch.float32, device=dev)
@@ -322,7 +344,7 @@ def run_sweep(a, dev, world, rank):
     for _ in range(a.warmup):
         step()
     prof.reset()   # time only the K measured launches
-    if world > 1:
+    if a.pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -330,7 +352,7 @@ def run_sweep(a, dev, world, rank):
     for _ in range(a.steps):
         best = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if a.pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     pr = prof.read()
@@ -339,9 +361,9 @@ def run_sweep(a, dev, world, rank):
     exec_flops_launch = pr["predict_flops"] / max(pr["predict_launches"], 1)
     mfma_flops_launch = pr["mfma_flops"] / max(pr["predict_launches"], 1)
     levels_launch = [x / max(pr["predict_launches"], 1) for x in pr["tiles_by_level"]]
-    elapsed, pred_ms_max = _max_over_ranks([elapsed, pred_ms], dev, world, a.backend)
+    elapsed, pred_ms_max, fit_ms_max = _max_over_ranks([elapsed, pred_ms, fit_ms], dev, world, a.backend)
     subgoal_sharded = None
-    if world > 1 and not a.no_outputs and a.scaling == "strong":
+    if a.pg and not a.no_outputs and a.scaling == "strong":
         # the node-parity frontier needs the whole grid: lo / hi / S of every
         # rank all-gathered (17 B per point, SURVEY.md 8(e) optional exchange),
         # then GetNextSubgoal on every rank -- timed apart from the tick
@@ -385,7 +407,7 @@ def run_sweep(a, dev, world, rank):
     # node-side selection on the tick's device outputs (8(f)1): frontier of S,
     # nearest quarter to the goal, widest interval -- GetNextSubgoal
     subgoal = None
-    if world == 1 and not a.no_outputs:
+    if world == 1 and not a.no_outputs and subgoal_sharded is None:
         Dx = torch.as_tensor(wl.qx, dtype=torch.float64, device=dev)
         Dy = torch.as_tensor(wl.qy, dtype=torch.float64, device=dev)
         goal = (float(wl.qx.mean()), float(wl.qy.mean()))
@@ -411,6 +433,9 @@ def run_sweep(a, dev, world, rank):
         if regimes:
             d = regimes["dense"]
             cpu["gpu_dense_over_cpu"] = d["value"] / cpu["value"]
+            for b in cpu["by_threads"]:
+                b["gpu_dense_over_cpu"] = d["value"] / b["value"]
+                b["gpu_over_cpu"] = value / b["value"]
             cpu["gpu_default_over_gpu_dense"] = value / d["value"]
             cpu["ratios"] = ("gpu_dense_over_cpu: hardware (the same dense algorithm on both); "
                              "gpu_default_over_gpu_dense: algorithmic (error-budgeted tile skipping and "
@@ -418,15 +443,19 @@ def run_sweep(a, dev, world, rank):
     return {
         "metric": METRIC, "value": value, "unit": "grid-points/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": a.scaling,
-        "vs_baseline": None, "dtype": dtype_of(a.variant), "data": DATA,
+        "vs_baseline": None, "dtype": "f64" if prec[0] else dtype_of(a.variant), "data": DATA,
         "world_size": winfo["world_size"], "backend": winfo["backend"], "collective": winfo["collective"],
         "config": {"workload": a.config, "n_train": n, "grid": [gw, gh], "M": m_total, "M_per_rank": m,
                    "beta": wl.beta, "f_min": round(wl.f_min, 6),
                    "hyper": [wl.hyper.length_scale, wl.hyper.sigma_f, wl.hyper.noise_level],
                    "kstar_cutoff_log2": cutoff, "parallelism": f"m-shard{world}" if world > 1 else "single",
                    "sharding": (a.sharding if world > 1 and a.scaling == "strong" else None),
-                   "outputs_written": not a.no_outputs},
-        "roofline": dict(predict_roofline(a.variant, exec_flops_launch, pred_ms, mfma_flops_launch, levels_launch),
+                   "outputs_written": not a.no_outputs,
+                   "precision": {"precise_sweep": prec[0], "probe_fast_sweep_variance_error": prec[1],
+                                 "probe_var_min": prec[2], "probe_var_max": prec[3],
+                                 "rule": "SBO_OPT_PRECISION -1: f64 sweep when the probe error > 7e-6"}},
+        "roofline": dict(predict_roofline(a.variant, exec_flops_launch, pred_ms, mfma_flops_launch, levels_launch,
+                                          prec[0]),
                          traffic=traffic,
                          traffic_source=traffic_src, avg_launch_ms=pred_ms, max_rank_launch_ms=pred_ms_max,
                          dense_flops_per_launch=dense_flops_launch,
@@ -436,11 +465,20 @@ def run_sweep(a, dev, world, rank):
                           "unit": "GB/s", "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None,
                           "avg_launch_ms": fill_ms, "algorithmic_bytes": fill_bytes},
         "fit_ms": fit_ms, "fit_first_ms": fit_first_ms, "fit_broadcast": fit_bcast,
+        "end_to_end": end_to_end(m_all, fit_ms_max, ms_per_step),
         "argmax": {"index": best[1], "score": best[0]},
         "subgoal": subgoal,
         "cpu_baseline": cpu,
         "regimes": regimes,
     }
+
+
+def end_to_end(m, fit_ms, tick_ms):
+    """the tick with a refit in front of it -- the reference's
+    trigger requests a new map on every spatial_data_size change
+    (node.cpp:552-566), so a fresh map costs the warm fit plus one tick."""
+    return {"value": m / ((fit_ms + tick_ms) * 1e-3), "unit": "grid-points/s", "fit_ms": fit_ms,
+            "tick_ms": tick_ms, "how": "M / (warm fit + one tick); fit replicated on every rank (max over ranks)"}
 
 
 def _timed_ticks(prof, step, steps):
@@ -460,10 +498,10 @@ def _timed_ticks(prof, step, steps):
     return wall, pr["predict_ms"] / k, pr["predict_flops"] / k, pr["mfma_flops"] / k, [x / k for x in pr["tiles_by_level"]]
 
 
-def _regime_line(a, name, how, m, n, wall, ms, flops, mflops, levels, extra=None):
+def _regime_line(a, name, how, m, n, wall, ms, flops, mflops, levels, extra=None, precise=False):
     dense = float(n) * float(n) * m
     r = {"what": how, "value": m / wall, "unit": "grid-points/s", "ms_per_step": wall * 1e3,
-         "roofline": dict(predict_roofline(a.variant, flops, ms, mflops, levels), avg_launch_ms=ms,
+         "roofline": dict(predict_roofline(a.variant, flops, ms, mflops, levels, precise), avg_launch_ms=ms,
                           dense_flops_per_launch=dense, executed_fraction_of_dense=flops / dense,
                           dense_equivalent_tflops=dense / (ms * 1e-3) / 1e12)}
     if extra:
@@ -510,17 +548,40 @@ def run_regime_stress(a, gm, prof, dev, n, gw, gh):
     def step():
         gm.tick(qx, qy, wl.beta, wl.f_min, score=N.SCORE_WIDTH, outputs=outs, key_out=key, async_=True)
 
+    precise, perr, vmin, vmax = gm.precision()
     res = _timed_ticks(prof, step, a.regime_steps)
+    sd_default = outs["sd"].clone()
+    # the fast split sweep on the same fit, and its variance error against the
+    # precise sweep over the whole grid (device against device; the tests
+    # measure both against the fp64 oracle: tests/test_gpu_headline.py)
+    gm.set_option(N.SBO_OPT_PRECISION, 0)
+    try:
+        fres = _timed_ticks(prof, step, 1)
+    finally:
+        gm.set_option(N.SBO_OPT_PRECISION, -1)
+    v_def = sd_default.double() ** 2
+    v_fast = outs["sd"].double() ** 2
+    fast_err = float((v_fast - v_def).abs().max() / v_def.abs().max())
+    fast = _regime_line(a, "lpsc_stress_box fast sweep", "SBO_OPT_PRECISION = 0 on the same fit", m, n, *fres)
+    fast["variance_error_vs_precise_sweep"] = fast_err
     return _regime_line(a, "lpsc_stress_box", "N points and the grid on x [0, 1] x y [0, 2.5] (config/lpsc.yaml:32-33), "
-                        "default plan (variant 3, auto cutoff, B = 20)", m, n, *res,
-                        extra={"fit_ms": fit_ms, "kstar_cutoff_log2": gm.skip_info()[0]})
+                        "default options (SBO_OPT_PRECISION = -1: the fit-time probe picks the sweep)", m, n, *res,
+                        extra={"fit_ms": fit_ms, "kstar_cutoff_log2": gm.skip_info()[0],
+                               "end_to_end": end_to_end(m, fit_ms, res[0] * 1e3),
+                               "precise_sweep": precise,
+                               "probe": {"fast_sweep_variance_error": perr, "var_min": vmin, "var_max": vmax,
+                                         "how": "32 x 32 grid over the training box, fast vs precise sweep"},
+                               "fast_sweep": fast}, precise=precise)
 
 
 def dtype_of(variant):
     return "f32 (bf16x3-split MFMA, f32 accumulation)" if variant in SPLIT_VARIANTS else "f32"
 
 
-def predict_roofline(variant, flops_f32, ms, mfma_flops, levels):
+PEAK_F64_MFMA_TFLOPS = 78.6    # MI355X spec: dense FP64 matrix (v_mfma_f64_16x16x4_f64)
+
+
+def predict_roofline(variant, flops_f32, ms, mfma_flops, levels, precise=False):
     """Roofline of the predictive kernel.  flops_f32 = the algorithmic work of
     one launch, 2*BM*BN*BK per multiplied k-tile (device counter); mfma_flops
     = the matrix-core work it issued (device counter: 2*BM*BN*BK per bf16
@@ -529,6 +590,10 @@ def predict_roofline(variant, flops_f32, ms, mfma_flops, levels):
     the dense bf16 (split sweeps) or f32 peak."""
     f32_tf = flops_f32 / (ms * 1e-3) / 1e12
     ach = mfma_flops / (ms * 1e-3) / 1e12
+    if precise:
+        return {"kernel": "predict_f64_kernel (V = sf2 L^-1 K*^T in f64: v_mfma_f64_16x16x4_f64, f64 K* and sums)",
+                "bound": "mfma", "achieved": f32_tf, "peak": PEAK_F64_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": f32_tf / PEAK_F64_MFMA_TFLOPS, "algorithmic_flops_per_launch": flops_f32}
     if variant in SPLIT_VARIANTS:
         return {"kernel": "predict_x3_kernel (V = sf2 L^-1 K*^T: bf16x3-split operands, up to six "
                           "v_mfma_f32_16x16x32_bf16 per f32 product, f32 accumulation)",
@@ -604,17 +669,78 @@ def run_streaming(a, dev, world, rank):
     mflops = pr["mfma_flops"] / max(pr["predict_launches"], 1)
     levels = [x / max(pr["predict_launches"], 1) for x in pr["tiles_by_level"]]
     (s, i), = key_tensor_to_pairs(last)
+    cpu = cpu_baseline_streaming(gm, wl, chunks, a.cpu_seconds) if not a.no_cpu else None
+    value = m * steps / elapsed
+    if cpu is not None:
+        cpu["gpu_over_cpu"] = value / cpu["value"]
+    traffic, traffic_src = pmc_traffic("C5", n_end, m, m)
     return {
-        "metric": METRIC, "value": m * steps / elapsed, "unit": "grid-points/s", "n_gpus": 1, "steps": steps,
+        "metric": METRIC, "value": value, "unit": "grid-points/s", "n_gpus": 1, "steps": steps,
         "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": dtype_of(a.variant), "data": DATA,
         "config": {"workload": "C5", "n_train": [n0, n_end], "iterations": iters, "grid": [g, g], "M": m,
                    "parallelism": "single", "step": "sbo_append (block Cholesky) + sbo_tick (includes one fit per loop)"},
-        "roofline": dict(predict_roofline(a.variant, flops, pred_ms, mflops, levels), traffic=None,
-                         avg_launch_ms=pred_ms),
+        "roofline": dict(predict_roofline(a.variant, flops, pred_ms, mflops, levels), traffic=traffic,
+                         traffic_source=traffic_src, avg_launch_ms=pred_ms),
         "append_ms_avg": t_app * 1e3 / steps, "tick_ms_avg": t_tick * 1e3 / steps,
-        "argmax": {"index": i, "score": s}, "cpu_baseline": None,
+        "argmax": {"index": i, "score": s}, "cpu_baseline": cpu,
     }
+
+
+def cpu_baseline_streaming(gm, wl, chunks, budget_s):
+    """C5's CPU comparator: the same Eigen-class dense path (cpu_baseline) on
+    the host's `nproc` cores, per iteration an append (block Cholesky update:
+    L21 by a triangular solve, K22 - L21 L21^T, its Cholesky; scipy/OpenBLAS)
+    and a tick over the 512 x 512 grid.  Both are timed at the loop's last
+    size (N 7857 -> 8000; the tick on a bounded sample of the grid,
+    extrapolated linearly in M) and scaled to the loop's average by the mean
+    of N^2 over the iterations (the tick's strsm and the append's solve are
+    O(N^2) per query / per new point)."""
+    import scipy.linalg as sla
+    from threadpoolctl import threadpool_limits
+
+    from oracle import oracle as O
+    threads, total = host_cores()
+    O.set_threads(threads)
+    L, alpha = gm.factor()
+    o = gm.order()
+    h = wl.hyper
+    n = L.shape[0]
+    b = int(chunks[-1] - chunks[-2])
+    n0 = n - b
+    xs, ys = wl.x.astype(np.float32)[o], wl.y.astype(np.float32)[o]
+    bp = O.BlasPredictor(L, alpha, xs, ys, h.length_scale, h.sf2, h.prior_mean)
+    with threadpool_limits(limits=threads, user_api="blas"):
+        # append of the last batch on the CPU (its inputs: the leading factor)
+        L11 = np.ascontiguousarray(L[:n0, :n0])
+        t0 = time.perf_counter()
+        K22 = O.rbf_fill_f32in(xs[n0:], ys[n0:], h.length_scale, h.sf2, h.noise_level).astype(np.float32)
+        Kx = np.empty((n0, b), np.float32, order="F")
+        O.lib().orc_cross_kernel_f32(xs[:n0], ys[:n0], n0, xs[n0:], ys[n0:], b, h.length_scale, h.sf2,
+                                     Kx.ctypes.data)
+        L21t = sla.solve_triangular(L11, Kx, lower=True, check_finite=False)
+        K22 -= L21t.T @ L21t
+        sla.cholesky(K22.astype(np.float64), lower=True, check_finite=False)
+        t_app = time.perf_counter() - t0
+        k = bp.block
+        bp.tick(wl.qx[:k], wl.qy[:k], wl.beta, wl.f_min)
+        t0 = time.perf_counter()
+        bp.tick(wl.qx[:k], wl.qy[:k], wl.beta, wl.f_min)
+        t = time.perf_counter() - t0
+        k2 = int(min(wl.qx.size, max(k, k * max(budget_s - 2 * t, 0.0) / max(t, 1e-6))))
+        k2 = max(k, (k2 // k) * k)
+        t0 = time.perf_counter()
+        bp.tick(wl.qx[:k2], wl.qy[:k2], wl.beta, wl.f_min)
+        t_tick = (time.perf_counter() - t0) * wl.qx.size / k2
+    ns = np.asarray(chunks[1:], np.float64)
+    scale = float(np.mean(ns ** 2) / float(n) ** 2)
+    step_s = (t_app + t_tick) * scale
+    return {"value": wl.qx.size / step_s, "unit": "grid-points/s", "cores": threads, "host_cpus": total,
+            "kind": "port", "append_s_last": t_app, "tick_s_last": t_tick, "n2_scale": scale,
+            "sample": f"last iteration (N {n0} -> {n}): CPU block append + a dense tick over {k2} of the "
+                      f"{wl.qx.size} grid points (oracle.BlasPredictor: OpenMP K*, sgemv, OpenBLAS strsm), "
+                      f"extrapolated to the grid and scaled by mean(N_i^2)/N_last^2 = {scale:.3f} over the 50 "
+                      f"iterations"}
 
 
 def pmc_traffic(config, n, m_total, m):
@@ -633,6 +759,9 @@ def pmc_traffic(config, n, m_total, m):
         return None, None
 
 
+GPUS_PER_NODE = 8   # an MI355X platform node: 8 OAM GPUs (the driver's SCALE node)
+
+
 def host_cores():
     """Cores the CPU comparator may use: `nproc` (the CPUs this process may
     run on, honouring OMP_NUM_THREADS as GNU nproc does), and the machine's
@@ -644,18 +773,51 @@ def host_cores():
     return max(1, n), os.cpu_count() or n
 
 
+def blas_max_threads(default=64):
+    """The largest thread count every loaded OpenBLAS was built for
+    (MAX_THREADS in its config string; asking threadpoolctl for more than
+    that crashes OpenBLAS)."""
+    import re
+    from threadpoolctl import threadpool_info
+    best = None
+    for i in threadpool_info():
+        if i.get("internal_api") != "openblas":
+            continue
+        mx = default
+        try:
+            lib = ctypes.CDLL(i["filepath"])
+            for nm in ("openblas_get_config", "scipy_openblas_get_config64_", "scipy_openblas_get_config",
+                       "openblas_get_config64_"):
+                f = getattr(lib, nm, None)
+                if f is not None:
+                    f.restype = ctypes.c_char_p
+                    m = re.search(rb"MAX_THREADS=(\d+)", f() or b"")
+                    if m:
+                        mx = int(m.group(1))
+                    break
+        except OSError:
+            pass
+        best = mx if best is None else min(best, mx)
+    return best or default
+
+
 def cpu_baseline(gm, wl, budget_s):
     """The Eigen-class dense CPU path on the host's cores: K*^T per query block
-    (numpy), mu by sgemv, V = L^-1 K*^T by OpenBLAS strsm (level-3, `nproc`
-    threads), var, ComputeSets + argmax (oracle C), given the device's own
-    factor; timed on a bounded contiguous sample of the grid and extrapolated
-    linearly (the M axis is embarrassingly parallel).  Dense: it does not skip
-    tiles -- the gpu_dense_over_cpu ratio compares like with like."""
+    (orc_cross_kernel_f32, OpenMP), mu by sgemv, V = L^-1 K*^T by OpenBLAS
+    strsm (level-3, multithreaded), var, ComputeSets + argmax (oracle C), given
+    the device's own factor; timed on a bounded contiguous sample of the grid
+    and extrapolated linearly (the M axis is embarrassingly parallel).  Dense:
+    it does not skip tiles -- the gpu_dense_over_cpu ratio compares like with
+    like.  Timed at three thread counts: `nproc` (the
+    box's OMP_NUM_THREADS share, the headline `value`), every CPU this process
+    may run on (sched_getaffinity), and the per-GPU share of an 8-GPU node
+    (host CPUs / 8) -- the ratio against the GPU depends on which share of
+    the node the CPU path is given."""
     from threadpoolctl import threadpool_info, threadpool_limits
 
     from oracle import oracle as O
     threads, total = host_cores()
-    O.set_threads(threads)
+    aff = len(os.sched_getaffinity(0))
     L, alpha = gm.factor()
     o = gm.order()                           # internal training order of the factor
     h = wl.hyper
@@ -668,20 +830,38 @@ def cpu_baseline(gm, wl, budget_s):
         bp.tick(wl.qx[:k], wl.qy[:k], wl.beta, wl.f_min)
         return time.perf_counter() - t0
 
-    with threadpool_limits(limits=threads, user_api="blas"):
-        blas = [f"{i.get('internal_api')} {i.get('version')} ({i.get('architecture')}, {i.get('num_threads')} threads)"
-                for i in threadpool_info() if i.get("user_api") == "blas"]
-        k = bp.block
-        run(k)                               # warm: thread pool, page-in of L
-        t = run(k)
-        k2 = int(min(wl.qx.size, max(k, k * max(budget_s - 2 * t, 0.0) / max(t, 1e-6))))
-        k2 = max(k, (k2 // k) * k)
-        t2 = run(k2)
-    return {"value": k2 / t2, "unit": "grid-points/s", "cores": threads, "host_cpus": total, "kind": "port",
-            "blas": blas[0] if blas else None,
-            "sample": f"{k2} contiguous grid points of {wl.name} (N={wl.x.size}): dense f32 K*^T + sgemv mean + "
-                      f"OpenBLAS strsm variance (oracle.BlasPredictor, the Eigen LLT-solve class) + ComputeSets + "
-                      f"argmax, given the device L/alpha; {t2:.1f} s wall, extrapolated linearly"}
+    bmax = blas_max_threads()
+
+    def measure(nt, budget):
+        O.set_threads(nt)
+        with threadpool_limits(limits=min(nt, bmax), user_api="blas"):
+            blas = [f"{i.get('internal_api')} {i.get('version')} ({i.get('architecture')}, "
+                    f"{i.get('num_threads')} threads)" for i in threadpool_info() if i.get("user_api") == "blas"]
+            k = bp.block
+            run(k)                           # warm: thread pool, page-in of L
+            t = run(k)
+            k2 = int(min(wl.qx.size, max(k, k * max(budget - 2 * t, 0.0) / max(t, 1e-6))))
+            k2 = max(k, (k2 // k) * k)
+            t2 = run(k2)
+        return {"threads": nt, "blas_threads": min(nt, bmax), "value": k2 / t2, "points": k2, "seconds": t2,
+                "blas": blas[0] if blas else None}
+
+    main = measure(threads, budget_s)
+    by = [dict(main, share="nproc (OMP_NUM_THREADS share of the box; the headline value)")]
+    for nt, share in ((aff, "sched_getaffinity: every CPU this process may run on"),
+                      (max(1, total // GPUS_PER_NODE), f"per-GPU share of an {GPUS_PER_NODE}-GPU node "
+                                                       f"({total} host CPUs / {GPUS_PER_NODE})")):
+        if nt != threads:
+            by.append(dict(measure(nt, budget_s / 2), share=share))
+        else:
+            by.append(dict(main, share=share))
+    O.set_threads(threads)
+    return {"value": main["value"], "unit": "grid-points/s", "cores": threads, "host_cpus": total,
+            "affinity_cpus": aff, "kind": "port", "blas": main["blas"], "by_threads": by,
+            "sample": f"{main['points']} contiguous grid points of {wl.name} (N={wl.x.size}): dense f32 K*^T "
+                      f"(OpenMP) + sgemv mean + OpenBLAS strsm variance (oracle.BlasPredictor, the Eigen LLT-solve "
+                      f"class) + ComputeSets + argmax, given the device L/alpha; {main['seconds']:.1f} s wall, "
+                      f"extrapolated linearly"}
 
 
 if __name__ == "__main__":

@@ -331,7 +331,29 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * exported state use it too) and sbo_get_jitter reports it; 0 keeps the
  * reference's behaviour of reporting the failure. */
 #define SBO_OPT_JITTER_RETRIES 10
+/* SBO_OPT_PRECISION (-1 auto default | 0 fast | 1 f64): the predictive
+ * sweep's arithmetic.  0: the split-operand bf16 sweep (f32-accurate products,
+ * f32 accumulation, A = sf2 L^-1 rounded to f32).  1: the precise sweep -- A
+ * in f64 from the fit's f64 inverse, K* in f64, f64 MFMA
+ * (v_mfma_f64_16x16x4_f64) and f64 sums; about 3-5x the fast sweep's time on
+ * the same tiles.  -1: every sbo_fit (and an sbo_append once N grew by a
+ * quarter since the last probe) sweeps a 32 x 32 grid over the training box
+ * both ways and ticks with the precise sweep when the fast sweep's variance
+ * error there, max |d var| / max var, exceeds 7e-6 (the 1e-5 contract less a margin):
+ * dense data, where the variance is orders below sf2 and sf2 - |V|^2 cancels
+ * (config/lpsc.yaml's own box at N = 16384).  The precise sweep's skip budget
+ * is 2^-B times the smallest probe variance (SBO_OPT_SKIP_BUDGET = B).  Needs
+ * SBO_OPT_INVERSE_BITS 64 and a fitted factor: an imported state always runs
+ * the fast sweep.  Setting it on a fitted context takes effect at once. */
+#define SBO_OPT_PRECISION 11
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
+
+/* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe
+ * (SBO_OPT_PRECISION): the fast sweep's normwise variance error against the
+ * precise one on the 32 x 32 probe grid and that grid's smallest and largest
+ * variance (-1 when no probe ran).  SBO_E_STATE before a fit. */
+SBO_API sbo_status sbo_get_precision(const sbo_ctx *ctx, int *precise, double *probe_err, double *probe_var_min,
+                                     double *probe_var_max);
 
 /* The K* tile cutoff in effect (auto or fixed) and the norms it was derived from. */
 SBO_API sbo_status sbo_get_skip(const sbo_ctx *ctx, int *cutoff_log2, double *max_row_l1, double *alpha_l1);

@@ -46,6 +46,8 @@ def lib():
         L.orc_rbf_fill_f32in.argtypes = [_f32p, _f32p, _i64, _dbl, _dbl, _dbl, _f64p]
         L.orc_rbf_fill_f32.argtypes = [_f32p, _f32p, _i64, ctypes.c_float, ctypes.c_float,
                                        ctypes.c_float, _f32p]
+        L.orc_cross_kernel_f32.argtypes = [_f32p, _f32p, _i64, _f32p, _f32p, _i64, ctypes.c_float,
+                                           ctypes.c_float, ctypes.c_void_p]
         L.orc_cholesky.argtypes = [_f64p, _i64]
         L.orc_cholesky.restype = _i64
         L.orc_chol_solve.argtypes = [_f64p, _i64, _f64p, _f64p]
@@ -304,7 +306,8 @@ class BlasPredictor:
     """The dense CPU predictive path a node would run on its host with Eigen
     (``LLT::matrixL().solve(K*^T)`` is a blocked TRSM, SURVEY.md 8(d) CPU
     comparator): given the lower factor L (f32) and alpha, for each block of
-    queries build K*^T (N x k, f32, numpy exp), mu = m0 + K*^T alpha (sgemv),
+    queries build K*^T (N x k, f32, orc_cross_kernel_f32 on every OpenMP
+    thread), mu = m0 + K*^T alpha (sgemv),
     V = L^-1 K*^T by OpenBLAS ``strsm`` (level-3, multithreaded), var = sf2 -
     colsum(V^2); then ComputeSets + argmax (orc_compute_sets / orc_argmax).
     Dense: no tile skipping.  TEST/BENCH INFRASTRUCTURE: only bench.py's
@@ -315,7 +318,7 @@ class BlasPredictor:
         self.alpha = np.ascontiguousarray(alpha, np.float32)
         self.x = np.ascontiguousarray(x, np.float32)[:, None]
         self.y = np.ascontiguousarray(y, np.float32)[:, None]
-        self.c = np.float32(-1.0 / (2.0 * ell * ell))
+        self.ell = float(ell)
         self.sf2, self.m0 = np.float32(sf2), np.float32(m0)
         self.block = int(block)
 
@@ -324,15 +327,18 @@ class BlasPredictor:
         qx = np.ascontiguousarray(qx, np.float32)
         qy = np.ascontiguousarray(qy, np.float32)
         m = qx.size
+        n = self.x.size
         mu = np.empty(m, np.float32)
         var = np.empty(m, np.float32)
+        K = np.empty((n, self.block), np.float32, order="F")
         for a in range(0, m, self.block):
             b = min(m, a + self.block)
-            dx = self.x - qx[None, a:b]
-            dy = self.y - qy[None, a:b]
-            K = np.asfortranarray(self.sf2 * np.exp((dx * dx + dy * dy) * self.c))   # N x k
-            mu[a:b] = self.m0 + self.alpha @ K
-            V = strsm(1.0, self.Lf, K, lower=1, overwrite_b=1)
+            Kb = K[:, : b - a]
+            # K*^T of the block on every thread (orc_cross_kernel_f32, OpenMP)
+            lib().orc_cross_kernel_f32(self.x.ravel(), self.y.ravel(), n, qx[a:b], qy[a:b], b - a, self.ell,
+                                       self.sf2, Kb.ctypes.data)
+            mu[a:b] = self.m0 + self.alpha @ Kb
+            V = strsm(1.0, self.Lf, Kb, lower=1, overwrite_b=1)
             var[a:b] = np.maximum(self.sf2 - np.einsum("ij,ij->j", V, V), 0.0)
         return mu, var
 

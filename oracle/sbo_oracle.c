@@ -124,6 +124,27 @@ ORC_EXPORT void orc_rbf_fill_f32(const float *x, const float *y, int64_t n,
     }
 }
 
+/* Cross kernel K*^T (n x m, column-major, f32) for the bench's dense CPU
+ * comparator (bench.py cpu_baseline, oracle.BlasPredictor): column q holds
+ * sf2 * exp(-|x_i - q|^2 / (2 l^2)) over the n training points, one OpenMP
+ * thread per block of query columns -- the Eigen-class path builds K* on
+ * every host core before its triangular solve.  Same f32 formulation as
+ * orc_rbf_fill_f32. */
+ORC_EXPORT void orc_cross_kernel_f32(const float *x, const float *y, int64_t n, const float *qx,
+                                     const float *qy, int64_t m, float ell, float sf2, float *Ks)
+{
+    const float c = -1.0f / (2.0f * ell * ell);
+#pragma omp parallel for schedule(static)
+    for (int64_t q = 0; q < m; ++q) {
+        float *col = Ks + q * n;
+        const float a = qx[q], b = qy[q];
+        for (int64_t i = 0; i < n; ++i) {
+            const float dx = x[i] - a, dy = y[i] - b;
+            col[i] = sf2 * expf(c * fmaf(dy, dy, dx * dx));
+        }
+    }
+}
+
 /* ------------------------------------------------------------------------ */
 /* a2: blocked right-looking Cholesky, lower, column-major, in place.        */
 /* Returns 0 on success, k+1 if the leading minor of order k+1 is not SPD.  */

@@ -32,7 +32,7 @@ EXPORTS = (
     "sbo_rbf_fill", "sbo_get_factor", "sbo_profile", "sbo_profile_read", "sbo_set_option", "sbo_get_inverse",
     "sbo_get_order", "sbo_profile_work", "sbo_profile_mfma", "sbo_debug_x3_stamps", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
     "sbo_get_bounds", "sbo_get_jitter", "sbo_get_tile_bounds", "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
-    "sbo_polygon_correct", "sbo_polydist", "sbo_point_within", "sbo_project_subgoal",
+    "sbo_polygon_correct", "sbo_polydist", "sbo_point_within", "sbo_project_subgoal", "sbo_get_precision",
 )
 SBO_OPT_INVERSE_BITS = 1
 SBO_OPT_SPATIAL_ORDER = 2
@@ -44,6 +44,7 @@ SBO_OPT_SKIP_BUDGET = 7
 SBO_OPT_CHOLESKY = 8
 SBO_OPT_INVERSE = 9
 SBO_OPT_JITTER_RETRIES = 10
+SBO_OPT_PRECISION = 11
 
 
 class SboError(RuntimeError):
@@ -148,6 +149,9 @@ def lib():
     L.sbo_set_option.restype = st
     L.sbo_get_skip.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(dbl), ctypes.POINTER(dbl)]
     L.sbo_get_skip.restype = st
+    L.sbo_get_precision.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(dbl), ctypes.POINTER(dbl),
+                                    ctypes.POINTER(dbl)]
+    L.sbo_get_precision.restype = st
     L.sbo_get_order.argtypes = [vp, vp]
     L.sbo_get_order.restype = st
     L.sbo_get_inverse.argtypes = [vp, vp]

@@ -967,7 +967,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, float m0, int64_t ldp, float *__restrict__ part, float *__restrict__ mean,
     unsigned long long *__restrict__ key, unsigned char *__restrict__ thr, unsigned long long *__restrict__ wkey,
-    unsigned long long *__restrict__ bits) {
+    unsigned long long *__restrict__ bits, int wide) {
     // dynamic LDS: the increment-bin cache [kPlanWaves][kPlanBinCache], then
     // the distance and |k|_2 caches of min(nkt, kPlanD2) tiles each
     extern __shared__ unsigned plan_dyn[];
@@ -1053,8 +1053,14 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
             for (int j = lane; j < kBN; j += 64) {
                 const int64_t q = qb * kBN + j;
                 if (q < m) {
-                    part[(int64_t)I * ldp + q] = 0.0f;
-                    if (I == nI - 1) mean[q] = m0;
+                    // (wide: the precise sweep's f64 partials and mean)
+                    if (wide) {
+                        reinterpret_cast<double *>(part)[(int64_t)I * ldp + q] = 0.0;
+                        if (I == nI - 1) reinterpret_cast<double *>(mean)[q] = (double)m0;
+                    } else {
+                        part[(int64_t)I * ldp + q] = 0.0f;
+                        if (I == nI - 1) mean[q] = m0;
+                    }
                 }
             }
     }
@@ -1584,9 +1590,10 @@ __device__ __forceinline__ void compute_sets_one(T mu, T sd, double beta, double
     safe = lo > f_min;
 }
 
+template <class PT>
 __global__ __launch_bounds__(kAcqThreads) void acquire_kernel(
-    const float *__restrict__ part, const float *__restrict__ mean, int nI, int64_t ldp, int64_t m,
-    float sf2, double beta, double f_min, int score_kind, int64_t index_offset,
+    const PT *__restrict__ part, const PT *__restrict__ mean, int nI, int64_t ldp, int64_t m,
+    double sf2, double beta, double f_min, int score_kind, int64_t index_offset,
     const int32_t *__restrict__ perm, float *__restrict__ mu_out, float *__restrict__ sd_out,
     double *__restrict__ lo_out, double *__restrict__ hi_out, uint8_t *__restrict__ safe_out,
     sbo_key *__restrict__ keys) {
@@ -1600,17 +1607,17 @@ __global__ __launch_bounds__(kAcqThreads) void acquire_kernel(
         double s = 0.0;
         int I = 0;
         for (; I + 8 <= nI; I += 8) {
-            float v[8];
+            PT v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(I + u) * ldp + i];
 #pragma unroll
             for (int u = 0; u < 8; ++u) s += (double)v[u];
         }
         for (; I < nI; ++I) s += (double)part[(int64_t)I * ldp + i];
-        double vd = (double)sf2 - s;
+        double vd = sf2 - s;
         float var = vd > 0.0 ? (float)vd : 0.0f;
         const float sd = __fsqrt_rn(var);
-        const float mu = mean[i];
+        const float mu = (float)mean[i];
         const int64_t o = perm ? (int64_t)perm[i] : i;  // caller's index of sweep position i
         if (mu_out) mu_out[o] = mu;
         if (sd_out) sd_out[o] = sd;
@@ -1889,7 +1896,8 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nQ), dim3(kPlanThreads), plan_lds, s, kbox, skip.kcoord, lgn,
                        levels, make_float2(skip.lvl_key[0], skip.lvl_key[1]), nI,
                        nQ, qx, qy,
-                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr, wkey, bits);
+                       m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr, wkey, bits,
+                       skip.wide ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t tb = L.temp_bytes;
@@ -1989,7 +1997,17 @@ hipError_t launch_acquire(hipStream_t s, const float *part, const float *mean, i
                           int64_t m, float sf2, double beta, double f_min, int score_kind,
                           int64_t index_offset, const int32_t *perm, float *mu, float *sd, double *lo,
                           double *hi, uint8_t *safe, sbo_key *block_keys) {
-    hipLaunchKernelGGL(acquire_kernel, dim3((unsigned)acq_blocks(m)), dim3(kAcqThreads), 0, s, part, mean,
+    hipLaunchKernelGGL(acquire_kernel<float>, dim3((unsigned)acq_blocks(m)), dim3(kAcqThreads), 0, s, part, mean,
+                       nI, ldp, m, (double)sf2, beta, f_min, score_kind, index_offset, perm, mu, sd, lo, hi, safe,
+                       block_keys);
+    return hipGetLastError();
+}
+
+hipError_t launch_acquire(hipStream_t s, const double *part, const double *mean, int nI, int64_t ldp,
+                          int64_t m, double sf2, double beta, double f_min, int score_kind,
+                          int64_t index_offset, const int32_t *perm, float *mu, float *sd, double *lo,
+                          double *hi, uint8_t *safe, sbo_key *block_keys) {
+    hipLaunchKernelGGL(acquire_kernel<double>, dim3((unsigned)acq_blocks(m)), dim3(kAcqThreads), 0, s, part, mean,
                        nI, ldp, m, sf2, beta, f_min, score_kind, index_offset, perm, mu, sd, lo, hi, safe,
                        block_keys);
     return hipGetLastError();

@@ -312,6 +312,15 @@ hipError_t grow_keep(sbo_ctx *ctx, DevBuf &buf, size_t bytes, size_t keep) {
     return hipSuccess;
 }
 
+// sweep selection of run_tick: -1 the context's (ctx->precise), 0 the fast
+// split sweep, 1 the precise f64 sweep under its budget, 2 the precise sweep
+// dense (only exact zeros dropped; the probe's reference)
+constexpr int kSweepCtx = -1, kSweepFast = 0, kSweepPrecise = 1, kSweepPreciseDense = 2;
+sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, double beta, double f_min,
+                    int score_kind, int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
+                    uint8_t *safe, sbo_key *key_dev, float *cost = nullptr, int sweep = kSweepCtx);
+sbo_status probe_precision(sbo_ctx *ctx);
+
 // Rebuild alpha, L^-1 and the packed predictive operand from the current L.
 // n_old > 0 (an append of rows n_old..n-1 to an unchanged leading factor):
 // with the f64 inverse of the leading block kept from the last refresh, only
@@ -401,6 +410,11 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         SBO_BLAS(rocblas_dtrmv(ctx->blas, rocblas_fill_lower, rocblas_operation_transpose, rocblas_diagonal_non_unit,
                                (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
         SBO_HIP(sbo::launch_narrow(ctx->stream, d, n, alpha));
+        // (the precise sweep's mean uses alpha in f64)
+        SBO_HIP(ctx->alpha64.reserve(sizeof(double) * (size_t)ld));
+        SBO_HIP(hipMemcpyAsync(ctx->alpha64.as<double>(), d, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice,
+                               ctx->stream));
+        ctx->a64_I0 = std::min(ctx->a64_I0, I0);
         SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, ld, n, npad, I0, sf2, ctx->x.as<float>(),
                                          ctx->y.as<float>(), alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
     } else {
@@ -473,7 +487,87 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     SBO_CHECK(hinfo == 0, SBO_E_NOT_SPD, "trtri: singular factor (info=" + std::to_string(hinfo) + ")");
     ctx->npad = npad;
     ctx->x3_I0 = std::min(ctx->x3_I0, I0);  // the split operand is derived lazily (run_tick)
+    if (!incr) ctx->a64_I0 = 0;
     ctx->fitted = true;
+    return probe_precision(ctx);
+}
+
+// The precise sweep's budget: the same construction as the automatic cutoff
+// (refresh_operand) with the tolerance 2^-B times the smallest variance the
+// probe saw inside the training box instead of 2^-B sf2 -- the 1e-5 contract
+// is relative to the largest variance of a query set, and in the dense
+// regime that is orders below sf2.
+void precise_budget(sbo_ctx *ctx) {
+    const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f, sf = std::sqrt(sf2);
+    const double floor_v = std::max(ctx->probe_vmin, 1e-12 * sf2);
+    const double tol = std::ldexp(1.0, -ctx->skip_budget) * std::min(floor_v, sf2);
+    const double tau2 = tol / (2.0 * sf) * 0.99;
+    const double need = ctx->max_row_l1 * std::sqrt((double)ctx->n) / tau2;
+    const double l2 = std::log2(std::max(need, 1.0));
+    ctx->p_skip_log2 = std::isfinite(l2) ? std::min(160, std::max(16, (int)std::ceil(l2))) : 160;
+    ctx->p_lg_tau_v = (float)std::log2(tau2 / std::sqrt((double)(ctx->npad / sbo::kBM)));
+}
+
+// SBO_OPT_PRECISION (-1 auto): which sweep the ticks run.  The probe sweeps a
+// 32 x 32 grid over the training box twice -- the fast split sweep and the
+// precise f64 sweep without skipping -- and measures the fast sweep's
+// normwise variance error against it, max |d var| / max var (the contract's
+// metric); above kPreciseTol the context's ticks use the precise sweep.
+// kPreciseTol = 7e-6: measured probe errors 1.8e-6 (C2), 4.3e-6 (C3), 4.9e-6
+// (C4), 4.7e-6 (C5's last fit), against 3.3e-4 on the lpsc.yaml box at
+// N = 16384; a full grid's error ran ~1.2x the probe's at C4 (5.96e-6 on a
+// 3072-point sample), so 7e-6 keeps the fast sweep only where it is inside
+// the 1e-5 contract with that margin (tools/r3_probe_values.py).
+// Re-probed at every fit, and on appends once N has grown by a quarter since
+// the last probe (the conditioning moves slowly with N).  Needs the f64
+// inverse (SBO_OPT_INVERSE_BITS 64) and a factor (not an imported state).
+constexpr double kPreciseTol = 7e-6;
+sbo_status probe_precision(sbo_ctx *ctx) {
+    const bool avail = ctx->inverse_bits == 64 && ctx->has_factor && ctx->linv_n == ctx->n;
+    if (!avail || ctx->precision_opt == 0) {
+        ctx->precise = false;
+        if (!avail) ctx->probe_n = 0;
+        return SBO_OK;
+    }
+    const bool fresh = ctx->probe_n == 0 || ctx->n >= ctx->probe_n + ctx->probe_n / 4 || ctx->n < ctx->probe_n;
+    if (fresh) {
+        constexpr int G = 32, M = G * G;
+        std::vector<float> h(2 * M);
+        for (int i = 0; i < G; ++i)
+            for (int j = 0; j < G; ++j) {
+                h[i * G + j] = ctx->bbox[0] + (ctx->bbox[1] - ctx->bbox[0]) * (float)j / (float)(G - 1);
+                h[M + i * G + j] = ctx->bbox[2] + (ctx->bbox[3] - ctx->bbox[2]) * (float)i / (float)(G - 1);
+            }
+        SBO_HIP(ctx->qprobe.reserve(sizeof(float) * 2 * M));
+        SBO_HIP(ctx->oprobe.reserve(sizeof(float) * 2 * M + sizeof(sbo_key)));
+        float *qx = ctx->qprobe.as<float>(), *qy = qx + M, *sdf = ctx->oprobe.as<float>(), *sdp = sdf + M;
+        sbo_key *key = reinterpret_cast<sbo_key *>(sdp + M);
+        SBO_HIP(hipMemcpyAsync(qx, h.data(), sizeof(float) * 2 * M, hipMemcpyHostToDevice, ctx->stream));
+        const bool prof = ctx->prof;
+        ctx->prof = false;  // (the probe is not a tick: no events, no counters)
+        sbo_status st = run_tick(ctx, qx, qy, M, 0.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, sdf, nullptr, nullptr,
+                                 nullptr, key, nullptr, kSweepFast);
+        if (st == SBO_OK)
+            st = run_tick(ctx, qx, qy, M, 0.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, sdp, nullptr, nullptr, nullptr, key,
+                          nullptr, kSweepPreciseDense);
+        ctx->prof = prof;
+        if (st != SBO_OK) return st;
+        SBO_HIP(hipMemcpyAsync(h.data(), sdf, sizeof(float) * 2 * M, hipMemcpyDeviceToHost, ctx->stream));
+        SBO_HIP(hipStreamSynchronize(ctx->stream));
+        double dmax = 0.0, vmax = 0.0, vmin = HUGE_VAL;
+        for (int i = 0; i < M; ++i) {
+            const double vf = (double)h[i] * h[i], vp = (double)h[M + i] * h[M + i];
+            dmax = std::max(dmax, std::fabs(vf - vp));
+            vmax = std::max(vmax, vp);
+            vmin = std::min(vmin, vp);
+        }
+        ctx->probe_err = vmax > 0.0 ? dmax / vmax : 0.0;
+        ctx->probe_vmin = vmin;
+        ctx->probe_vmax = vmax;
+        ctx->probe_n = ctx->n;
+    }
+    precise_budget(ctx);
+    ctx->precise = ctx->precision_opt == 1 || ctx->probe_err > kPreciseTol;
     return SBO_OK;
 }
 
@@ -566,25 +660,32 @@ sbo_status factor_and_refresh(sbo_ctx *ctx) {
 // Predictive sweep + acquisition over m queries already on the device.
 sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, double beta, double f_min,
                     int score_kind, int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
-                    uint8_t *safe, sbo_key *key_dev, float *cost = nullptr) {
+                    uint8_t *safe, sbo_key *key_dev, float *cost, int sweep) {
     const int64_t nI = ctx->npad / sbo::kBM;
+    if (sweep == kSweepCtx) sweep = ctx->precise ? kSweepPrecise : kSweepFast;
+    SBO_CHECK(sweep == kSweepFast || (ctx->has_factor && ctx->linv_n == ctx->n && ctx->inverse_bits == 64),
+              SBO_E_STATE, "precise sweep: needs the fit's f64 inverse (not an imported state, INVERSE_BITS 64)");
+    const bool precise = sweep != kSweepFast;
     // sweep the queries in grid patches or Morton order (compact 128-query
     // blocks skip more k-tiles); ms sweep positions (>= m: padded patches)
     const int32_t *perm = nullptr;
     int64_t ms = m;
     sbo::SkipPlan plan;
-    if (ctx->skip_log2 < 0) {
-        plan.L = ctx->auto_skip_log2;
+    if (sweep == kSweepPreciseDense) {
+        plan.L = 150;   // only exact zeros dropped (bitwise the dense sweep)
+    } else if (ctx->skip_log2 < 0) {
+        plan.L = precise ? ctx->p_skip_log2 : ctx->auto_skip_log2;
         plan.L_mean = ctx->auto_skip_mean_log2;
         plan.lgn = ctx->tile_lgn.as<float4>();
-        plan.levels = sbo::x3_levels(ctx->kernel_variant) ? 1 : 0;
+        plan.levels = !precise && sbo::x3_levels(ctx->kernel_variant) ? 1 : 0;
         plan.kcoord = ctx->kcoord.as<float>();
-        plan.lg_tau_v = ctx->lg_tau_v;
+        plan.lg_tau_v = precise ? ctx->p_lg_tau_v : ctx->lg_tau_v;
     } else {
         plan.L = ctx->skip_log2;
     }
-    plan.prod_full = ctx->kernel_variant >= 2 ? 6 : 1;
-    plan.records = ctx->kernel_variant >= 2;
+    plan.prod_full = !precise && ctx->kernel_variant >= 2 ? 6 : 1;
+    plan.records = !precise && ctx->kernel_variant >= 2;
+    plan.wide = precise;
 #ifdef SBO_DIAG
     // timing diagnostic (diagnostic build only): the drop-only plan
     // with every kept tile at level SBO_LVL_FORCE -- outside the error budget
@@ -620,8 +721,9 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         qy = sy;
     }
     const int64_t ldp = sbo::round_up(ms, 64);
-    SBO_HIP(ctx->part.reserve(sizeof(float) * (size_t)nI * (size_t)ldp));
-    SBO_HIP(ctx->mean.reserve(sizeof(float) * (size_t)ldp));
+    const size_t pw = precise ? sizeof(double) : sizeof(float);   // the precise sweep's partials are f64
+    SBO_HIP(ctx->part.reserve(pw * (size_t)nI * (size_t)ldp));
+    SBO_HIP(ctx->mean.reserve(pw * (size_t)ldp));
     const int64_t nb = sbo::acq_blocks(ms);
     SBO_HIP(ctx->keys.reserve(sizeof(sbo_key) * (size_t)(nb + 1)));
     sbo_key *bkeys = ctx->keys.as<sbo_key>();
@@ -647,7 +749,29 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
                                       ctx->qcost.as<float>(), cost));
         return SBO_OK;
     }
-    if (ctx->kernel_variant >= 2) {
+    if (precise) {
+        // f64 operand of any repacked row block, derived from the f64 inverse
+        const int64_t nIc = ctx->npad / sbo::kBM;
+        if (ctx->a64_I0 < nIc) {
+            const int64_t I0 = std::max<int64_t>(ctx->a64_I0, 0);
+            SBO_HIP(grow_keep(ctx, ctx->a64, sbo::f64_operand_bytes(ctx->npad), sbo::f64_operand_bytes(I0 * sbo::kBM)));
+            SBO_HIP(ctx->kc64.reserve(sbo::f64_coord_bytes(ctx->npad)));
+            SBO_HIP(sbo::launch_pack_f64(ctx->stream, ctx->Linv.as<double>(), ctx->cap, ctx->n, ctx->npad, I0,
+                                         ctx->hyper.sigma_f * ctx->hyper.sigma_f, ctx->x.as<float>(),
+                                         ctx->y.as<float>(), ctx->alpha64.as<double>(), ctx->a64.as<double>(),
+                                         ctx->kc64.as<double>()));
+            ctx->a64_I0 = INT64_MAX;
+        }
+        const int4 *desc = nullptr;
+        const unsigned short *tl = nullptr;
+        const int *seg = nullptr;
+        sbo::plan_views(ctx->npad, ms, P, ctx->plan_work.as<void>(), &desc, &tl, &seg);
+        Bracket br(ctx, ctx->ev_predict);
+        SBO_HIP(sbo::launch_predict_f64(ctx->stream, ctx->a64.as<double>(), ctx->kc64.as<double>(), desc, tl, seg, P,
+                                        (int)(nIc * ((ms + sbo::kBN - 1) / sbo::kBN)), (int)nIc, qx, qy, ms, ldp,
+                                        ctx->hyper.length_scale, ctx->hyper.prior_mean, ctx->part.as<double>(),
+                                        ctx->mean.as<double>()));
+    } else if (ctx->kernel_variant >= 2) {
         // split-operand sweep: derive the bf16 planes of any repacked row
         // block, and give the kernel whole 128-query blocks to read
         const int64_t nIc = ctx->npad / sbo::kBM;
@@ -690,9 +814,15 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
                                     ctx->part.as<float>(), ctx->mean.as<float>(), ctx->kernel_variant, P,
                                     ctx->plan_work.as<void>()));
     }
-    const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
-    SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<float>(), ctx->mean.as<float>(), (int)nI, ldp, ms, sf2,
-                                beta, f_min, score_kind, index_offset, perm, mu, sd, lo, hi, safe, bkeys));
+    if (precise) {
+        SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<double>(), ctx->mean.as<double>(), (int)nI, ldp, ms,
+                                    ctx->hyper.sigma_f * ctx->hyper.sigma_f, beta, f_min, score_kind, index_offset,
+                                    perm, mu, sd, lo, hi, safe, bkeys));
+    } else {
+        const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
+        SBO_HIP(sbo::launch_acquire(ctx->stream, ctx->part.as<float>(), ctx->mean.as<float>(), (int)nI, ldp, ms, sf2,
+                                    beta, f_min, score_kind, index_offset, perm, mu, sd, lo, hi, safe, bkeys));
+    }
     SBO_HIP(sbo::launch_reduce_keys(ctx->stream, bkeys, nb, key_dev ? key_dev : bkeys + nb));
     return SBO_OK;
 }
@@ -1224,6 +1354,24 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
                       "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22)");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
+        case SBO_OPT_PRECISION:
+            SBO_CHECK(value >= -1 && value <= 1, SBO_E_INVAL, "SBO_OPT_PRECISION must be -1 (auto), 0 or 1");
+            if (ctx->fitted) {
+                // takes effect at once: a first auto probe now, or the forced choice
+                const bool avail = ctx->has_factor && ctx->linv_n == ctx->n && ctx->inverse_bits == 64;
+                SBO_CHECK(value != 1 || avail, SBO_E_STATE,
+                          "SBO_OPT_PRECISION 1: needs the fit's f64 inverse (not an imported state)");
+                ctx->precision_opt = (int)value;
+                if (value != 0 && avail) {
+                    SBO_HIP(hipSetDevice(ctx->device));
+                    if (sbo_status st = probe_precision(ctx)) return st;
+                } else {
+                    ctx->precise = false;
+                }
+                return SBO_OK;
+            }
+            ctx->precision_opt = (int)value;
+            return SBO_OK;
         case SBO_OPT_TILE_SKIP:
             SBO_CHECK(value == -1 || value == 0 || (value >= 16 && value <= 1000), SBO_E_INVAL,
                       "SBO_OPT_TILE_SKIP must be -1 (auto), 0 (dense) or a cutoff exponent in [16, 1000]");
@@ -1232,6 +1380,17 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
     }
     ctx->err = "unknown option " + std::to_string(option);
     return SBO_E_INVAL;
+}
+
+SBO_API sbo_status sbo_get_precision(const sbo_ctx *ctx, int *precise, double *probe_err, double *probe_var_min,
+                                     double *probe_var_max) {
+    if (!ctx) return SBO_E_INVAL;
+    if (!ctx->fitted) return SBO_E_STATE;
+    if (precise) *precise = ctx->precise ? 1 : 0;
+    if (probe_err) *probe_err = ctx->probe_n ? ctx->probe_err : -1.0;
+    if (probe_var_min) *probe_var_min = ctx->probe_n ? ctx->probe_vmin : -1.0;
+    if (probe_var_max) *probe_var_max = ctx->probe_n ? ctx->probe_vmax : -1.0;
+    return SBO_OK;
 }
 
 SBO_API sbo_status sbo_get_skip(const sbo_ctx *ctx, int *cutoff_log2, double *max_row_l1, double *alpha_l1) {
@@ -1503,6 +1662,8 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
     }
     ctx->fitted = false;
     ctx->has_factor = false;
+    ctx->precise = false;   // no f64 inverse travels: an imported state ticks with the fast sweep
+    ctx->probe_n = 0;
     ctx->linv_n = 0;
     const int64_t nt = h.npad / sbo::kBK;
     const size_t aug_bytes = 4 * (size_t)sbo::total_tiles(h.npad / sbo::kBM) * sbo::kTileFloats;

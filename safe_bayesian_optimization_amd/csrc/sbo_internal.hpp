@@ -150,6 +150,17 @@ struct sbo_ctx {
     sbo::DevBuf info;            // rocSOLVER info
     sbo::DevBuf scratch;         // append workspace
     int64_t npad = 0;            // rows/cols of the packed operand (multiple of BM)
+    // precise sweep (SBO_OPT_PRECISION, predict_f64.hip)
+    int precision_opt = -1;      // -1 auto (fit-time probe), 0 the fast split sweep, 1 always f64
+    bool precise = false;        // the sweep ticks run in effect
+    sbo::DevBuf alpha64;         // alpha from the f64 solve (length cap)
+    sbo::DevBuf a64, kc64;       // f64 packed operand and coordinates, derived lazily
+    int64_t a64_I0 = 0;          // first row block whose f64 operand is stale
+    int64_t probe_n = 0;         // training points at the last probe (0: none)
+    double probe_err = -1.0, probe_vmin = 0.0, probe_vmax = 0.0;  // fast sweep's error on the probe, var range
+    int p_skip_log2 = 160;       // the precise plan's cutoffs and budget (2^-B of the probe's smallest variance)
+    float p_lg_tau_v = -1000.0f;
+    sbo::DevBuf qprobe, oprobe;  // probe grid and outputs
 
     // per-call staging
     sbo::DevBuf part, mean;      // predictive partial sums [nI][ldp], mean [ldp]
@@ -212,6 +223,7 @@ struct SkipPlan {
     int levels = 0;     // with lgn: tiles may run at the reduced precision levels (split sweep)
     int prod_full = 1;  // MFMA products per full-precision tile (6: split sweep), for the counter
     bool records = false;  // also write the split sweep's step records (plan_views' rec)
+    bool wide = false;     // empty items' outputs as f64 (the precise sweep's partials and mean)
     // rank of a tile's two level increments against drops: log2(time a drop
     // saves / time the level step saves), per-tile sweep time at C4 of six,
     // three, one product(s) 18.6, 12.9, 9.9 ns (variants 22, 20, 21)
@@ -302,6 +314,27 @@ hipError_t launch_acquire(hipStream_t s, const float *part, const float *mean, i
                           int64_t m, float sf2, double beta, double f_min, int score_kind,
                           int64_t index_offset, const int32_t *perm, float *mu, float *sd, double *lo,
                           double *hi, uint8_t *safe, sbo_key *block_keys);
+// the same over the precise sweep's f64 partials and mean (sf2 in f64)
+hipError_t launch_acquire(hipStream_t s, const double *part, const double *mean, int nI, int64_t ldp,
+                          int64_t m, double sf2, double beta, double f_min, int score_kind,
+                          int64_t index_offset, const int32_t *perm, float *mu, float *sd, double *lo,
+                          double *hi, uint8_t *safe, sbo_key *block_keys);
+// Precise sweep (predict_f64.hip, SBO_OPT_PRECISION): A = sf2 L^-1 packed in
+// f64 from the fit's f64 inverse for row blocks >= I0 (tile (I, t) at
+// tile_start(I) + t, two 64 KiB stages in MFMA fragment order), and per k-tile
+// half the f64 x, y, sf2 alpha (alpha from the f64 solve).
+size_t f64_operand_bytes(int64_t npad);
+size_t f64_coord_bytes(int64_t npad);
+hipError_t launch_pack_f64(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
+                           double sf2, const float *x, const float *y, const double *alpha, double *a64,
+                           double *kc64);
+// The sweep over the plan (descriptors and tile lists of plan_views; every
+// kept tile in f64): part[I][q] (f64) = sum over row block I of V^2, mean[q]
+// (f64) = m0 + sf2 alpha^T k_q.
+hipError_t launch_predict_f64(hipStream_t s, const double *a64, const double *kc64, const int4 *desc,
+                              const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
+                              const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
+                              double *mean);
 // Morton ordering of the queries (query_order.hip): workspace of
 // query_order_bytes(m); returns the permutation and the gathered coordinates
 // (all inside the workspace).

@@ -91,7 +91,7 @@ def cost_balanced_range(gm, qx, qy, rank: int, world: int, group=None) -> tuple[
         cost = gm.query_cost(qx, qy)
         cost = cost.cpu().numpy() if hasattr(cost, "cpu") else np.asarray(cost)
         cuts.copy_(torch.as_tensor(balanced_cuts(cost, world), dtype=torch.int64))
-    if world > 1:
+    if _group_size(group):
         if dist.get_backend(group) == "gloo" and cuts.is_cuda:
             h = cuts.cpu()
             dist.broadcast(h, 0, group=group)
@@ -101,6 +101,14 @@ def cost_balanced_range(gm, qx, qy, rank: int, world: int, group=None) -> tuple[
     c = [int(v) for v in cuts.cpu()]
     assert c[0] == 0 and c[-1] == m and all(a <= b for a, b in zip(c, c[1:])), c
     return c[rank], c[rank + 1]
+
+
+def _group_size(group=None) -> int:
+    """World size of an initialised process group, else 0 (no collectives).
+    A group of ONE rank still runs its collectives (RCCL exercised on a
+    one-GPU box, bench.py --force-pg)."""
+    import torch.distributed as dist
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 0
 
 
 def combine_keys(keys) -> tuple[float, int]:
@@ -126,8 +134,8 @@ def allreduce_key(key_dev, group=None) -> tuple[float, int]:
     CPU tensors) and combine."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
-    if world == 1:
+    world = _group_size(group)
+    if not world:
         return combine_keys(key_tensor_to_pairs(key_dev))
     out = torch.empty(world * 2, dtype=torch.int64, device=key_dev.device)
     dist.all_gather_into_tensor(out, key_dev.reshape(2), group=group)
@@ -139,8 +147,8 @@ def rank_cuts(lo: int, hi: int, device="cpu", group=None) -> list[int]:
     the blocks are contiguous and in rank order)."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
-    if world == 1:
+    world = _group_size(group)
+    if not world:
         return [lo, hi]
     mine = torch.tensor([lo, hi], dtype=torch.int64, device=device)
     out = torch.empty(2 * world, dtype=torch.int64, device=device)
@@ -161,7 +169,8 @@ def gather_rows(local, cuts, group=None):
     import torch
     import torch.distributed as dist
     world = len(cuts) - 1
-    if world == 1:
+    if not _group_size(group):
+        assert world == 1, cuts
         return local
     sizes = [b - a for a, b in zip(cuts, cuts[1:])]
     w = max(sizes)

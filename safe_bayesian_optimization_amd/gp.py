@@ -239,6 +239,14 @@ class TerrainMapper:
         self.ctx.check(self._lib.sbo_get_skip(self.ctx.handle, ctypes.byref(L), ctypes.byref(r), ctypes.byref(a)))
         return L.value, r.value, a.value
 
+    def precision(self):
+        """(precise sweep in effect, the probe's fast-sweep variance error,
+        smallest and largest probe variance) -- sbo_get_precision."""
+        p, e, vmin, vmax = ctypes.c_int(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        self.ctx.check(self._lib.sbo_get_precision(self.ctx.handle, ctypes.byref(p), ctypes.byref(e),
+                                                   ctypes.byref(vmin), ctypes.byref(vmax)))
+        return bool(p.value), e.value, vmin.value, vmax.value
+
     def set_option(self, option: int, value: int) -> None:
         self.ctx.check(self._lib.sbo_set_option(self.ctx.handle, int(option), int(value)))
 

@@ -182,3 +182,47 @@ def test_c5_streaming_loop(dev):
     print(f"C5 append vs refit: mu {dm:.2e} var {dv:.2e}")
     assert dm < 1e-4 and dv < 1e-4
     gm.close()
+
+
+@pytest.mark.parametrize("gw,gh", [(1000, 1000), (300, 120)])
+def test_lpsc_stress_box(dev, gw, gh):
+    """The mapping node's own domain (config/lpsc.yaml:32-37): N = 16384 on
+    x [0, 1] x y [0, 2.5], l = 0.4, sigma_f = 1, noise 0.1 -- the bench's
+    stress regime -- on the bench's 1000 x 1000 grid and on the mapper's own
+    resolution [300, 120] grid, default options.  The variance is 2e-4..3e-3
+    there (dense data), so sigma^2 = sf2 - |V|^2 cancels almost all of |V|^2:
+    the fast split sweep is 5e-4 off the oracle (an f32 strtrs on the same
+    factor 7e-5).  The fit-time probe must select the precise f64 sweep, and
+    mu and sigma^2 must meet the 1e-5 contract on a 3072-point sample against
+    the fp64 oracle given the device factor; lo/hi/S and the key bit-exact."""
+    from safe_bayesian_optimization_amd import _native as N
+    from safe_bayesian_optimization_amd.terrain import synthetic_box
+    wl = synthetic_box(16384, gw, gh, seed=0)
+    gm = TerrainMapper(0, wl.hyper)
+    t = lambda a: torch.tensor(f32(a), device=dev)  # noqa: E731
+    gm.fit(t(wl.x), t(wl.y), t(wl.obs))
+    precise, perr, vmin, vmax = gm.precision()
+    print(f"lpsc box {gw}x{gh}: precise={precise}, fast sweep's probe error {perr:.2e}, probe var {vmin:.2e}..{vmax:.2e}")
+    assert precise and perr > 1e-5
+    qx, qy = t(wl.qx), t(wl.qy)
+    m = qx.numel()
+    outs = full_outputs(m, dev)
+    k1 = gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs).clone()
+    torch.cuda.synchronize()
+    h = host(outs)
+    assert np.all(h["sd"] >= 0) and np.all(h["sd"] <= 1.0 + 1e-6)
+    check_sets_and_key(h, k1, wl.beta, wl.f_min)
+    sel = np.sort(np.random.default_rng(6).choice(m, min(3072, m), replace=False))
+    emu, evar, same = check_sample(gm, wl, h, sel, wl.beta, wl.f_min)
+    # the fast sweep on the same sample, for the record
+    gm.set_option(N.SBO_OPT_PRECISION, 0)
+    of = full_outputs(m, dev)
+    gm.tick(qx, qy, wl.beta, wl.f_min, outputs=of)
+    torch.cuda.synchronize()
+    omu, ovar = oracle_given_factor(gm, wl, wl.qx[sel], wl.qy[sel])
+    fvar = nrel(of["sd"].cpu().numpy()[sel].astype(np.float64) ** 2, ovar)
+    fmu = nrel(of["mu"].cpu().numpy()[sel], omu)
+    print(f"lpsc box {gw}x{gh}, sample of {sel.size}: precise mu {emu:.2e} var {evar:.2e} argmax same={same}; "
+          f"fast mu {fmu:.2e} var {fvar:.2e}")
+    assert emu < REL_TOL and evar < REL_TOL
+    gm.close()

@@ -763,6 +763,45 @@ def test_grid_query_blocks(mapper):
         gm.set_option(N.SBO_OPT_QUERY_ORDER, 3)
 
 
+def test_grid_patches_with_padding_band(mapper):
+    """A 300-wide raster shard of 17 rows (R % 16 == 1, W > 128) that starts
+    and ends mid-row: its last patch band is one row tall, so most of the
+    band's patch positions are padding.  Outputs and argmax equal the
+    caller-order sweep's, and sbo_query_cost on the patch layout is finite,
+    non-negative and sums to the level-weighted tiles the tick multiplies."""
+    W = 300
+    wl = synthetic(2500, W, 40, seed=61)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    a, b = W * 3 + 70, W * 19 + 150          # rows 3 (from x 70) .. 19 (to x 150): 17 rows
+    x, y = wl.qx[a:b], wl.qy[a:b]
+    try:
+        gm.set_option(N.SBO_OPT_QUERY_ORDER, 0)
+        ref, rkey = _grid_tick(gm, x, y, wl)
+        gm.set_option(N.SBO_OPT_QUERY_ORDER, 1)
+        out, key = _grid_tick(gm, x, y, wl)
+        assert nrel(out["mu"], ref["mu"].astype(np.float64)) < 1e-5
+        assert nrel(out["sd"].astype(np.float64) ** 2, ref["sd"].astype(np.float64) ** 2) < 1e-5
+        olo, ohi, osafe = O.compute_sets(out["mu"], out["sd"], wl.beta, wl.f_min)
+        assert np.array_equal(out["lo"], olo) and np.array_equal(out["safe"], osafe)
+        assert key[1] == O.argmax(ohi - olo, osafe)[0]
+        cost = gm.query_cost(x, y)
+        assert np.all(np.isfinite(cost)) and np.all(cost >= 0)
+        lib = N.lib()
+        lib.sbo_profile(gm.ctx.handle, 1)
+        gm.predict(x, y)
+        lv = (ctypes.c_int64 * 3)()
+        mf = ctypes.c_double()
+        lib.sbo_profile_mfma(gm.ctx.handle, ctypes.byref(mf), lv)
+        lib.sbo_profile(gm.ctx.handle, 0)
+        total = float(cost.astype(np.float64).sum())
+        assert sum(lv) > 0
+        assert (64 * lv[0] + 42 * lv[1] + 33 * lv[2]) / 64.0 * (1 - 1e-4) <= total <= \
+            (80 * lv[0] + 45 * lv[1] + 33 * lv[2]) / 64.0 * (1 + 1e-4)
+    finally:
+        gm.set_option(N.SBO_OPT_QUERY_ORDER, 1)
+
+
 def test_spatial_order_does_not_change_the_posterior(mapper):
     wl = synthetic(3000, 64, 48, seed=22)
     out = {}
@@ -1046,3 +1085,78 @@ def test_precision_levels(mapper):
     assert dvar <= 2 * 2.0 ** -20 + 4 * ulp
     assert dmu <= 2 * 2.0 ** -20 + 2 * ulp * np.abs(res[22][0]).max()
     assert res[3][2] == res[22][2]
+
+
+# ------------------------------------------- precise (f64) sweep, SBO_OPT_PRECISION
+@pytest.mark.parametrize("n,gw,gh,box", [(2048, 64, 48, False), (3000, 90, 70, True), (700, 40, 30, True)])
+def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box):
+    """SBO_OPT_PRECISION = 1: A = sf2 L^-1 in f64, K* in f64, f64 MFMA and sums
+    -- against the fp64 oracle given the same factor to f64-level agreement
+    (the budgeted skip at 2^-B of the smallest probe variance), on the
+    default domain and on the lpsc.yaml box (dense data, small variance)."""
+    from safe_bayesian_optimization_amd.terrain import synthetic_box
+    wl = synthetic_box(n, gw, gh, seed=n) if box else synthetic(n, gw, gh, seed=n + 1)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_PRECISION, 1)
+    try:
+        gm.fit(wl.x, wl.y, wl.obs)
+        precise, perr, vmin, vmax = gm.precision()
+        assert precise and 0.0 < vmin <= vmax
+        out = dict(mu=np.empty(wl.qx.size, np.float32), sd=np.empty(wl.qx.size, np.float32),
+                   lo=np.empty(wl.qx.size), hi=np.empty(wl.qx.size), safe=np.empty(wl.qx.size, np.uint8))
+        key = gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
+        omu, ovar = oracle_given_factor(gm, wl)
+        emu, evar = nrel(out["mu"], omu), nrel(out["sd"].astype(np.float64) ** 2, ovar)
+        print(f"precise N={n} box={box}: mu {emu:.2e} var {evar:.2e} (fast sweep on the probe: {perr:.2e}, "
+              f"probe var {vmin:.2e}..{vmax:.2e})")
+        # the outputs are f32: mu and sigma rounded once (sigma^2 within 2 ulp)
+        assert emu < 1e-6 and evar < 1e-6
+        olo, ohi, osafe = O.compute_sets(out["mu"], out["sd"], wl.beta, wl.f_min)
+        assert np.array_equal(out["lo"], olo) and np.array_equal(out["safe"], osafe)
+        assert key.idx == O.argmax(ohi - olo, osafe)[0]
+        # appends keep the f64 operand current (its new row blocks repacked)
+        gm.append(wl.x[:37] + 0.013, wl.y[:37], wl.obs[:37])
+        mu2, sd2 = gm.predict(wl.qx, wl.qy)
+        wl2 = type(wl)(wl.name, np.concatenate([wl.x, wl.x[:37] + 0.013]), np.concatenate([wl.y, wl.y[:37]]),
+                       np.concatenate([wl.obs, wl.obs[:37]]), wl.qx, wl.qy, gw, gh, wl.hyper, wl.f_min)
+        omu2, ovar2 = oracle_given_factor(gm, wl2)
+        assert nrel(mu2, omu2) < 1e-6 and nrel(sd2.astype(np.float64) ** 2, ovar2) < 1e-6
+    finally:
+        gm.set_option(N.SBO_OPT_PRECISION, -1)
+
+
+def test_precision_auto_probe(mapper):
+    """SBO_OPT_PRECISION = -1 (default): a well-conditioned fit keeps the fast
+    sweep (its probe error is inside half the contract), the lpsc.yaml box at
+    a density where sigma^2 << sf2 switches to the precise sweep; forcing 0
+    or 1 takes effect at once; an imported state runs the fast sweep."""
+    from safe_bayesian_optimization_amd.terrain import synthetic_box
+    wl = synthetic(2048, 64, 48, seed=5)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    precise, perr, vmin, vmax = gm.precision()
+    print(f"C2-like: precise={precise} probe err {perr:.2e} var {vmin:.2e}..{vmax:.2e}")
+    assert not precise and 0.0 <= perr < 7e-6
+    wb = synthetic_box(6000, 60, 150, seed=9)
+    gb = TerrainMapper(0, wb.hyper, ctx=mapper.ctx)
+    gb.fit(wb.x, wb.y, wb.obs)
+    precise, perr, vmin, vmax = gb.precision()
+    print(f"lpsc box N=6000: precise={precise} probe err {perr:.2e} var {vmin:.2e}..{vmax:.2e}")
+    assert precise and perr > 7e-6 and vmax < 0.1
+    mu_p, sd_p = gb.predict(wb.qx, wb.qy)
+    gb.set_option(N.SBO_OPT_PRECISION, 0)
+    assert not gb.precision()[0]
+    mu_f, sd_f = gb.predict(wb.qx, wb.qy)
+    omu, ovar = oracle_given_factor(gb, wb)
+    ep = nrel(sd_p.astype(np.float64) ** 2, ovar)
+    ef = nrel(sd_f.astype(np.float64) ** 2, ovar)
+    print(f"lpsc box N=6000 variance error: precise {ep:.2e}, fast {ef:.2e}")
+    assert ep < 1e-6 < ef
+    gb.set_option(N.SBO_OPT_PRECISION, -1)
+    assert gb.precision()[0]
+    b = TerrainMapper(0, wb.hyper)
+    b.import_state(gb.export_state())
+    with pytest.raises(N.SboError):
+        b.set_option(N.SBO_OPT_PRECISION, 1)      # no f64 inverse travels with a state
+    assert not b.precision()[0]
+    b.close()

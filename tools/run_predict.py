@@ -20,6 +20,8 @@ def main():
     import torch
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
     from safe_bayesian_optimization_amd.terrain import CONFIGS
+    if a.config == "C5":
+        return streaming(a)
     n, gw, gh = CONFIGS[a.config]
     n = a.n or n
     if a.grid:
@@ -46,6 +48,35 @@ def main():
         gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs)
     torch.cuda.synchronize()
     print("done", n, m)
+
+
+def streaming(a):
+    """C5 as bench.py runs it: fit 1000 points, 50 appends to 8000, a 512 x 512
+    tick after each (so per-kernel PMC averages match the bench's launches)."""
+    import torch
+    from safe_bayesian_optimization_amd import TerrainMapper, synthetic
+    from safe_bayesian_optimization_amd import _native as N
+    n_end, n0, iters, g = 8000, 1000, 50, a.grid or 512
+    wl = synthetic(n_end, g, g, seed=0, name="C5")
+    chunks = np.linspace(n0, n_end, iters + 1).round().astype(int)
+    dev = torch.device("cuda:0")
+    t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
+    X, Y, OBS = t(wl.x), t(wl.y), t(wl.obs)
+    qx, qy = t(wl.qx), t(wl.qy)
+    m = qx.numel()
+    gm = TerrainMapper(0, wl.hyper)
+    for kv in a.opt:
+        k, v = kv.split("=")
+        gm.set_option(getattr(N, k), int(v))
+    outs = dict(mu=torch.empty(m, device=dev), sd=torch.empty(m, device=dev),
+                lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
+                safe=torch.empty(m, dtype=torch.uint8, device=dev))
+    gm.fit(X[:n0], Y[:n0], OBS[:n0])
+    for i in range(iters):
+        gm.append(X[chunks[i]:chunks[i + 1]], Y[chunks[i]:chunks[i + 1]], OBS[chunks[i]:chunks[i + 1]])
+        gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs)
+    torch.cuda.synchronize()
+    print("done C5", gm.n, m)
 
 
 if __name__ == "__main__":
