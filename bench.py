@@ -7,8 +7,9 @@ accumulation, the mean alongside), ComputeSets in f64, the masked argmax of
 the confidence width over the safe set, and the cross-rank key exchange (one
 RCCL all-gather of 16-byte keys when N > 1).  Inputs (query coordinates) are
 resident in HBM before timing starts; mu/sd/lo/hi/S are written to HBM every
-step.  The fit (RBF fill + rocSOLVER potrf + dtrtri + operand pack) runs
-once, replicated on every rank, and is reported separately.
+step.  The fit (RBF fill, blocked Cholesky, f64 recursive L^-1, alpha,
+operand pack, precision probe) runs once, replicated on every rank, and is
+reported separately, with the end-to-end rate M / (fit + tick) beside it.
 
 Default workload = BASELINE.json configs[3] (C4: N=16384, 1000x1000 grid),
 the north-star target size, on 1 GPU; with --gpus P the same 10^6-point grid
@@ -75,12 +76,15 @@ def parse():
                    help="strong scaling: cost-balanced contiguous row blocks (default) or equal point counts")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--cpu-child", default=None, help=argparse.SUPPRESS)
     p.add_argument("--no-outputs", action="store_true", help="skip writing mu/sd/lo/hi/S (argmax only)")
     p.add_argument("--no-regimes", action="store_true",
                    help="N = 1: skip the dense (no tile skipping) and lpsc stress-box measurements")
     p.add_argument("--regime-steps", type=int, default=2, help="timed ticks per regime (after one warmup)")
     p.add_argument("--launch-check", action="store_true",
                    help="CPU rehearsal of the multi-rank path (gloo): launcher, shard cut broadcast, key all-gather")
+    p.add_argument("--resort", type=int, default=25,
+                   help="C5: SBO_OPT_RESORT, re-sort + refactor once appended points exceed this %% (0: never)")
     p.add_argument("--variant", type=int, default=3,
                    help="predictive kernel (SBO_OPT_KERNEL_VARIANT): 3 split-operand bf16 sweep (default), 0 f32 MFMA")
     return p.parse_args()
@@ -127,6 +131,8 @@ def launch(a):
 
 def main():
     a = parse()
+    if a.cpu_child:
+        return cpu_child(a.cpu_child, a.cpu_seconds)
     if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
         return launch(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -621,6 +627,7 @@ def run_streaming(a, dev, world, rank):
     stream = torch.cuda.current_stream(dev)
     gm = TerrainMapper(dev.index, wl.hyper)
     gm.set_option(N.SBO_OPT_KERNEL_VARIANT, a.variant)
+    gm.set_option(N.SBO_OPT_RESORT, a.resort)
     gm.ctx.set_stream(stream)
     prof = Prof(N.lib(), gm.ctx.handle)
     f32 = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
@@ -679,7 +686,9 @@ def run_streaming(a, dev, world, rank):
         "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": dtype_of(a.variant), "data": DATA,
         "config": {"workload": "C5", "n_train": [n0, n_end], "iterations": iters, "grid": [g, g], "M": m,
-                   "parallelism": "single", "step": "sbo_append (block Cholesky) + sbo_tick (includes one fit per loop)"},
+                   "parallelism": "single", "resort_pct": a.resort,
+                   "step": "sbo_append (block Cholesky update; a k-d re-sort + refactor when the points appended "
+                           "since the last sort exceed resort_pct %) + sbo_tick (includes one fit per loop)"},
         "roofline": dict(predict_roofline(a.variant, flops, pred_ms, mflops, levels), traffic=traffic,
                          traffic_source=traffic_src, avg_launch_ms=pred_ms),
         "append_ms_avg": t_app * 1e3 / steps, "tick_ms_avg": t_tick * 1e3 / steps,
@@ -773,34 +782,6 @@ def host_cores():
     return max(1, n), os.cpu_count() or n
 
 
-def blas_max_threads(default=64):
-    """The largest thread count every loaded OpenBLAS was built for
-    (MAX_THREADS in its config string; asking threadpoolctl for more than
-    that crashes OpenBLAS)."""
-    import re
-    from threadpoolctl import threadpool_info
-    best = None
-    for i in threadpool_info():
-        if i.get("internal_api") != "openblas":
-            continue
-        mx = default
-        try:
-            lib = ctypes.CDLL(i["filepath"])
-            for nm in ("openblas_get_config", "scipy_openblas_get_config64_", "scipy_openblas_get_config",
-                       "openblas_get_config64_"):
-                f = getattr(lib, nm, None)
-                if f is not None:
-                    f.restype = ctypes.c_char_p
-                    m = re.search(rb"MAX_THREADS=(\d+)", f() or b"")
-                    if m:
-                        mx = int(m.group(1))
-                    break
-        except OSError:
-            pass
-        best = mx if best is None else min(best, mx)
-    return best or default
-
-
 def cpu_baseline(gm, wl, budget_s):
     """The Eigen-class dense CPU path on the host's cores: K*^T per query block
     (orc_cross_kernel_f32, OpenMP), mu by sgemv, V = L^-1 K*^T by OpenBLAS
@@ -811,57 +792,84 @@ def cpu_baseline(gm, wl, budget_s):
     like.  Timed at three thread counts: `nproc` (the
     box's OMP_NUM_THREADS share, the headline `value`), every CPU this process
     may run on (sched_getaffinity), and the per-GPU share of an 8-GPU node
-    (host CPUs / 8) -- the ratio against the GPU depends on which share of
-    the node the CPU path is given."""
-    from threadpoolctl import threadpool_info, threadpool_limits
-
-    from oracle import oracle as O
+    (host CPUs / 8).  Each count runs in a child process started with
+    OMP_NUM_THREADS / OPENBLAS_NUM_THREADS set before numpy loads: OpenBLAS
+    sizes its per-thread buffers for the thread count it starts with and
+    crashes when raised past it at run time (measured: strsm with 10+ threads
+    in a process that started with 8)."""
+    import shutil
+    import tempfile
     threads, total = host_cores()
     aff = len(os.sched_getaffinity(0))
     L, alpha = gm.factor()
     o = gm.order()                           # internal training order of the factor
     h = wl.hyper
-    bp = O.BlasPredictor(L, alpha, wl.x.astype(np.float32)[o], wl.y.astype(np.float32)[o], h.length_scale, h.sf2,
-                         h.prior_mean)
-    del L
+    tmp = tempfile.mkdtemp(prefix="sbo_cpu_")
+    try:
+        np.save(os.path.join(tmp, "L.npy"), L)
+        del L
+        np.savez(os.path.join(tmp, "w.npz"), alpha=alpha, x=wl.x.astype(np.float32)[o], y=wl.y.astype(np.float32)[o],
+                 qx=wl.qx, qy=wl.qy, p=np.array([h.length_scale, h.sf2, h.prior_mean, wl.beta, wl.f_min]))
 
-    def run(k):
-        t0 = time.perf_counter()
-        bp.tick(wl.qx[:k], wl.qy[:k], wl.beta, wl.f_min)
-        return time.perf_counter() - t0
+        def child(nt, budget):
+            env = dict(os.environ, OMP_NUM_THREADS=str(nt), OPENBLAS_NUM_THREADS=str(nt))
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", tmp,
+                                "--cpu-seconds", str(budget)], env=env, capture_output=True, text=True,
+                               timeout=max(120.0, 20 * budget))
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if r.returncode != 0 or not lines:
+                return {"threads": nt, "error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+            return json.loads(lines[-1])
 
-    bmax = blas_max_threads()
-
-    def measure(nt, budget):
-        O.set_threads(nt)
-        with threadpool_limits(limits=min(nt, bmax), user_api="blas"):
-            blas = [f"{i.get('internal_api')} {i.get('version')} ({i.get('architecture')}, "
-                    f"{i.get('num_threads')} threads)" for i in threadpool_info() if i.get("user_api") == "blas"]
-            k = bp.block
-            run(k)                           # warm: thread pool, page-in of L
-            t = run(k)
-            k2 = int(min(wl.qx.size, max(k, k * max(budget - 2 * t, 0.0) / max(t, 1e-6))))
-            k2 = max(k, (k2 // k) * k)
-            t2 = run(k2)
-        return {"threads": nt, "blas_threads": min(nt, bmax), "value": k2 / t2, "points": k2, "seconds": t2,
-                "blas": blas[0] if blas else None}
-
-    main = measure(threads, budget_s)
-    by = [dict(main, share="nproc (OMP_NUM_THREADS share of the box; the headline value)")]
-    for nt, share in ((aff, "sched_getaffinity: every CPU this process may run on"),
-                      (max(1, total // GPUS_PER_NODE), f"per-GPU share of an {GPUS_PER_NODE}-GPU node "
-                                                       f"({total} host CPUs / {GPUS_PER_NODE})")):
-        if nt != threads:
-            by.append(dict(measure(nt, budget_s / 2), share=share))
-        else:
-            by.append(dict(main, share=share))
-    O.set_threads(threads)
+        main = child(threads, budget_s)
+        if "value" not in main:
+            return None
+        by = [dict(main, share="nproc (OMP_NUM_THREADS share of the box; the headline value)")]
+        for nt, share in ((aff, "sched_getaffinity: every CPU this process may run on"),
+                          (max(1, total // GPUS_PER_NODE), f"per-GPU share of an {GPUS_PER_NODE}-GPU node "
+                                                           f"({total} host CPUs / {GPUS_PER_NODE})")):
+            by.append(dict(child(nt, budget_s / 2) if nt != threads else main, share=share))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
     return {"value": main["value"], "unit": "grid-points/s", "cores": threads, "host_cpus": total,
-            "affinity_cpus": aff, "kind": "port", "blas": main["blas"], "by_threads": by,
+            "affinity_cpus": aff, "kind": "port", "blas": main.get("blas"), "by_threads": by,
             "sample": f"{main['points']} contiguous grid points of {wl.name} (N={wl.x.size}): dense f32 K*^T "
                       f"(OpenMP) + sgemv mean + OpenBLAS strsm variance (oracle.BlasPredictor, the Eigen LLT-solve "
                       f"class) + ComputeSets + argmax, given the device L/alpha; {main['seconds']:.1f} s wall, "
-                      f"extrapolated linearly"}
+                      f"extrapolated linearly; one child process per thread count"}
+
+
+def cpu_child(path, budget):
+    """bench.py --cpu-child DIR: one cpu_baseline measurement at the thread
+    count this process was started with (OMP_NUM_THREADS)."""
+    from threadpoolctl import threadpool_info
+
+    from oracle import oracle as O
+    nt = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    O.set_threads(nt)
+    L = np.load(os.path.join(path, "L.npy"), mmap_mode="r")
+    w = np.load(os.path.join(path, "w.npz"))
+    ell, sf2, m0, beta, f_min = (float(v) for v in w["p"])
+    bp = O.BlasPredictor(L, w["alpha"], w["x"], w["y"], ell, sf2, m0)
+    del L
+    qx, qy = w["qx"], w["qy"]
+
+    def run(k):
+        t0 = time.perf_counter()
+        bp.tick(qx[:k], qy[:k], beta, f_min)
+        return time.perf_counter() - t0
+
+    blas = [f"{i.get('internal_api')} {i.get('version')} ({i.get('architecture')}, {i.get('num_threads')} threads)"
+            for i in threadpool_info() if i.get("user_api") == "blas"]
+    k = bp.block
+    run(k)                                   # warm: thread pool, page-in of L
+    t = run(k)
+    k2 = int(min(qx.size, max(k, k * max(budget - 2 * t, 0.0) / max(t, 1e-6))))
+    k2 = max(k, (k2 // k) * k)
+    t2 = run(k2)
+    print(json.dumps({"threads": nt, "value": k2 / t2, "points": k2, "seconds": t2, "blas": blas[0] if blas else None}),
+          flush=True)
+    return 0
 
 
 if __name__ == "__main__":

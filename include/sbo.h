@@ -36,7 +36,7 @@ extern "C" {
 typedef enum sbo_status {
     SBO_OK = 0,
     SBO_E_INVAL = 1,    /* bad argument (null pointer, n <= 0, bad hyper-parameter) */
-    SBO_E_NOT_SPD = 2,  /* rocSOLVER potrf info > 0: K not positive definite */
+    SBO_E_NOT_SPD = 2,  /* the Cholesky's leading minor (rocSOLVER info convention): K not positive definite */
     SBO_E_DEVICE = 3,   /* HIP / rocBLAS / rocSOLVER runtime error */
     SBO_E_OOM = 4,      /* device allocation failed */
     SBO_E_EMPTY = 5,    /* nothing to operate on (no fit yet, empty input) */
@@ -85,8 +85,10 @@ SBO_API const char *sbo_last_error(const sbo_ctx *ctx);
 
 /* GP mapper (the external terrain_mapping_node, a1+a2) -------------------
  * Fit the posterior to n measurements (x, y, obs): RBF fill (HIP kernel),
- * rocSOLVER spotrf, alpha by spotrs, L^-1 by strtri, and packing of the
- * predictive operand.  Replaces the mapper's fit behind the service. */
+ * the library's blocked Cholesky (SBO_OPT_CHOLESKY), L^-1 in f64 by its block
+ * recursion (SBO_OPT_INVERSE), alpha = L^-T L^-1 (y - m0) from that inverse,
+ * the packed predictive operand and its tile bounds, and the precision probe
+ * (SBO_OPT_PRECISION).  Replaces the mapper's fit behind the service. */
 SBO_API sbo_status sbo_fit(sbo_ctx *ctx, const float *x, const float *y, const float *obs,
                            int64_t n, sbo_hyper hyper, uint32_t flags);
 
@@ -346,6 +348,15 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * SBO_OPT_INVERSE_BITS 64 and a fitted factor: an imported state always runs
  * the fast sweep.  Setting it on a fitted context takes effect at once. */
 #define SBO_OPT_PRECISION 11
+/* SBO_OPT_RESORT (percent, default 25; 0: never): sbo_append sorts each
+ * batch only among itself (k-d), so scattered batches leave k-tiles whose
+ * boxes span the domain and defeat the sweep's tile skipping.  Once the
+ * points appended since the last sort exceed this share of the sorted ones,
+ * the append re-sorts all points and refactors (a fit's cost, amortised over
+ * the appends in between); otherwise it is the block Cholesky update.  The
+ * posterior is the same either way (to f32 factorization rounding); caller
+ * indices (sbo_get_order) are kept. */
+#define SBO_OPT_RESORT 12
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe
@@ -386,9 +397,10 @@ SBO_API sbo_status sbo_profile_work(sbo_ctx *ctx, double *predict_flops);
 /* Matrix-core flops the predictive sweep issued since sbo_profile(ctx, 1):
  * 2*BM*BN*BK per MFMA product per multiplied tile -- six products per tile
  * for the split sweeps at full precision, three / one at the reduced
- * precision levels (variant 3), one for the f32 sweeps (variants 0, 1);
- * tiles_by_level (may be NULL): the multiplied tiles at six, three, one
- * product(s). */
+ * precision levels (variant 3), one for the f32 sweeps (variants 0, 1) and
+ * the precise f64 sweep; tiles_by_level (may be NULL): the multiplied tiles
+ * at six, three, one product(s). */
+SBO_API sbo_status sbo_profile_mfma(sbo_ctx *ctx, double *mfma_flops, int64_t *tiles_by_level /* [3] or NULL */);
 /* Diagnostic build only (libsbo_diag.so; the product returns zeros): with
  * SBO_OPT_KERNEL_VARIANT 39 (the default sweep with phase stamps,
  * s_memtime; never timed as the product) the summed cycles of every
@@ -396,7 +408,6 @@ SBO_API sbo_status sbo_profile_work(sbo_ctx *ctx, double *predict_flops);
  * item end, vmcnt wait, barrier, whole half-steps, body at six / three / one
  * product(s), half-steps at six / three / one product(s); then reset. */
 SBO_API sbo_status sbo_debug_x3_stamps(sbo_ctx *ctx, double *cycles, int n);
-SBO_API sbo_status sbo_profile_mfma(sbo_ctx *ctx, double *mfma_flops, int64_t *tiles_by_level /* [3] or NULL */);
 
 #ifdef __cplusplus
 }

@@ -45,6 +45,7 @@ SBO_OPT_CHOLESKY = 8
 SBO_OPT_INVERSE = 9
 SBO_OPT_JITTER_RETRIES = 10
 SBO_OPT_PRECISION = 11
+SBO_OPT_RESORT = 12
 
 
 class SboError(RuntimeError):

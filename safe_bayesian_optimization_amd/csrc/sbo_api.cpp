@@ -928,6 +928,83 @@ SBO_API const char *sbo_last_error(const sbo_ctx *ctx) { return ctx ? ctx->err.c
 
 SBO_API int64_t sbo_num_train(const sbo_ctx *ctx) { return ctx && ctx->fitted ? ctx->n : 0; }
 
+namespace {
+// Fill K of the ctx->n staged points (lda = ctx->cap) and factor it, with the
+// SBO_OPT_JITTER_RETRIES policy: a factorization that fails (NOT_SPD) is
+// retried up to R times with sf2 * 10^(r-7) added to the diagonal (r = 1..R);
+// the jitter that succeeded stays part of the noise term, so appends and
+// exported state use the same K (sbo_get_jitter).  base_noise: the noise
+// variance without jitter.
+sbo_status fill_and_factor(sbo_ctx *ctx, double base_noise) {
+    const int64_t n = ctx->n;
+    ctx->probe_n = 0;   // new data: the precision probe runs again (appends re-probe by growth)
+    const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
+    ctx->jitter = 0.0;
+    for (int r = 0;; ++r) {
+        const double jit = r == 0 ? 0.0 : sf2 * std::pow(10.0, r - 7);
+        {
+            Bracket br(ctx, ctx->ev_fill);
+            SBO_HIP(sbo::launch_rbf_fill(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, ctx->x.as<float>(),
+                                         ctx->y.as<float>(), n, ctx->cap, (float)ctx->hyper.length_scale, (float)sf2,
+                                         (float)(base_noise + jit), true, ctx->L.as<float>()));
+        }
+        ctx->hyper.noise_level = base_noise + jit;
+        const sbo_status st = factor_and_refresh(ctx);
+        if (st == SBO_OK) {
+            ctx->jitter = jit;
+            ctx->n_sorted = n;
+            return SBO_OK;
+        }
+        ctx->hyper.noise_level = base_noise;
+        if (st != SBO_E_NOT_SPD || r >= ctx->jitter_retries) return st;
+    }
+}
+
+// sbo_append's re-sort (SBO_OPT_RESORT): all n0 + b points staged again in
+// k-d order and factored from scratch, the caller's indices kept
+// (order[i] = the caller index of internal row i, appends numbered after
+// the fit).  Appended batches are k-d sorted only among themselves, so a
+// stream of scattered batches leaves k-tiles whose boxes span the domain and
+// defeat the sweep's tile skipping (C5: 50 batches of ~143 uniform points);
+// re-sorting once the unsorted tail exceeds a share of N restores compact
+// tiles for a fit amortised over that many appends.
+sbo_status resort_append(sbo_ctx *ctx, const float *x, const float *y, const float *obs, int64_t b, uint32_t flags) {
+    const int64_t n0 = ctx->n, n1 = n0 + b;
+    SBO_HIP(ctx->restage.reserve(sizeof(float) * 3 * (size_t)n1));
+    float *tx = ctx->restage.as<float>(), *ty = tx + n1, *to = ty + n1;
+    const hipMemcpyKind k = dev(flags) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    SBO_HIP(hipMemcpyAsync(tx, ctx->x.as<float>(), sizeof(float) * n0, hipMemcpyDeviceToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(ty, ctx->y.as<float>(), sizeof(float) * n0, hipMemcpyDeviceToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(to, ctx->obs.as<float>(), sizeof(float) * n0, hipMemcpyDeviceToDevice, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(tx + n0, x, sizeof(float) * b, k, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(ty + n0, y, sizeof(float) * b, k, ctx->stream));
+    SBO_HIP(hipMemcpyAsync(to + n0, obs, sizeof(float) * b, k, ctx->stream));
+    std::vector<int64_t> prev(ctx->order.begin(), ctx->order.begin() + n0);
+    for (int64_t i = n0; i < n1; ++i) prev.push_back(i);
+    if (n1 > ctx->cap) {  // geometric growth, as the block append does (contents are rebuilt)
+        const int64_t ncap = std::max<int64_t>(n1, sbo::round_up(ctx->cap + ctx->cap / 2, 256));
+        SBO_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->x.release();
+        ctx->y.release();
+        ctx->obs.release();
+        ctx->L.release();
+        ctx->Linv.release();
+        SBO_HIP(ctx->x.reserve(sizeof(float) * ncap));
+        SBO_HIP(ctx->y.reserve(sizeof(float) * ncap));
+        SBO_HIP(ctx->obs.reserve(sizeof(float) * ncap));
+        SBO_HIP(ctx->alpha.reserve(sizeof(float) * ncap));
+        SBO_HIP(ctx->L.reserve(sizeof(float) * (size_t)ncap * (size_t)ncap));
+        ctx->cap = ncap;
+    }
+    ctx->fitted = false;
+    ctx->n = n1;
+    ctx->linv_n = 0;
+    if (sbo_status st = stage_training(ctx, tx, ty, to, n1, 0, 0, SBO_DEVICE_PTRS)) return st;
+    for (int64_t i = 0; i < n1; ++i) ctx->order[(size_t)i] = prev[(size_t)ctx->order[(size_t)i]];
+    return fill_and_factor(ctx, ctx->hyper.noise_level - ctx->jitter);
+}
+}  // namespace
+
 SBO_API sbo_status sbo_fit(sbo_ctx *ctx, const float *x, const float *y, const float *obs, int64_t n,
                            sbo_hyper hyper, uint32_t flags) {
     if (!ctx) return SBO_E_INVAL;
@@ -947,28 +1024,7 @@ SBO_API sbo_status sbo_fit(sbo_ctx *ctx, const float *x, const float *y, const f
     SBO_HIP(ctx->alpha.reserve(sizeof(float) * n));
     SBO_HIP(ctx->L.reserve(sizeof(float) * (size_t)n * (size_t)n));
     if (sbo_status st = stage_training(ctx, x, y, obs, n, 0, 0, flags)) return st;
-    const double sf2 = hyper.sigma_f * hyper.sigma_f;
-    // SBO_OPT_JITTER_RETRIES = R > 0: a factorization that fails (NOT_SPD)
-    // is retried up to R times with sf2 * 10^(r-7) added to the diagonal
-    // (r = 1..R); the jitter that succeeded stays part of the noise term,
-    // so appends and exported state use the same K (sbo_get_jitter).
-    ctx->jitter = 0.0;
-    for (int r = 0;; ++r) {
-        const double jit = r == 0 ? 0.0 : sf2 * std::pow(10.0, r - 7);
-        {
-            Bracket br(ctx, ctx->ev_fill);
-            SBO_HIP(sbo::launch_rbf_fill(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), n, ctx->x.as<float>(),
-                                         ctx->y.as<float>(), n, n, (float)hyper.length_scale, (float)sf2,
-                                         (float)(hyper.noise_level + jit), true, ctx->L.as<float>()));
-        }
-        const sbo_status st = factor_and_refresh(ctx);
-        if (st == SBO_OK) {
-            ctx->jitter = jit;
-            ctx->hyper.noise_level = hyper.noise_level + jit;
-            break;
-        }
-        if (st != SBO_E_NOT_SPD || r >= ctx->jitter_retries) return st;
-    }
+    if (sbo_status st = fill_and_factor(ctx, hyper.noise_level)) return st;
     return finish(ctx, flags);
 }
 
@@ -991,6 +1047,12 @@ SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, cons
     const int64_t n0 = ctx->n, n1 = n0 + b;
     SBO_CHECK(n1 < (int64_t)1 << 30, SBO_E_INVAL, "sbo_append: n too large");
     const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
+    // SBO_OPT_RESORT: once the points appended since the last k-d sort exceed
+    // resort_pct % of the sorted ones, re-sort and refactor all of them
+    if (ctx->resort_pct > 0 && ctx->spatial_order != 0 && (n1 - ctx->n_sorted) * 100 > ctx->n_sorted * ctx->resort_pct) {
+        if (sbo_status st = resort_append(ctx, x, y, obs, b, flags)) return st;
+        return finish(ctx, flags);
+    }
 
     // grow storage (geometric) preserving the factor
     if (n1 > ctx->cap) {
@@ -1353,6 +1415,10 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             SBO_CHECK(sbo::variant_allowed((int)value), SBO_E_INVAL,
                       "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22)");
             ctx->kernel_variant = (int)value;
+            return SBO_OK;
+        case SBO_OPT_RESORT:
+            SBO_CHECK(value >= 0 && value <= 1000, SBO_E_INVAL, "SBO_OPT_RESORT must be in [0, 1000] (percent)");
+            ctx->resort_pct = (int)value;
             return SBO_OK;
         case SBO_OPT_PRECISION:
             SBO_CHECK(value >= -1 && value <= 1, SBO_E_INVAL, "SBO_OPT_PRECISION must be -1 (auto), 0 or 1");

@@ -152,6 +152,9 @@ struct sbo_ctx {
     int64_t npad = 0;            // rows/cols of the packed operand (multiple of BM)
     // precise sweep (SBO_OPT_PRECISION, predict_f64.hip)
     int precision_opt = -1;      // -1 auto (fit-time probe), 0 the fast split sweep, 1 always f64
+    int resort_pct = 25;         // SBO_OPT_RESORT: re-sort + refactor on append past this share of unsorted points
+    int64_t n_sorted = 0;        // points of the last k-d sort (fit / re-sort)
+    sbo::DevBuf restage;         // the re-sort's staging copy of all points
     bool precise = false;        // the sweep ticks run in effect
     sbo::DevBuf alpha64;         // alpha from the f64 solve (length cap)
     sbo::DevBuf a64, kc64;       // f64 packed operand and coordinates, derived lazily

@@ -143,6 +143,34 @@ def test_c4_headline(dev):
     gm.close()
 
 
+def test_c2_exact_workload(dev):
+    """C2 exactly as the bench runs it (BASELINE.json configs[1]): N = 2048,
+    the 256 x 256 grid, default options -- the whole grid against the fp64
+    oracle given the device factor (cheap at this N), lo/hi/S and the key
+    bit-exact, a second tick bitwise identical."""
+    n, gw, gh = CONFIGS["C2"]
+    wl = synthetic(n, gw, gh, seed=0, name="C2")
+    gm = TerrainMapper(0, wl.hyper)
+    t = lambda a: torch.tensor(f32(a), device=dev)  # noqa: E731
+    gm.fit(t(wl.x), t(wl.y), t(wl.obs))
+    assert not gm.precision()[0]          # the fast sweep, as in the bench line
+    qx, qy = t(wl.qx), t(wl.qy)
+    m = qx.numel()
+    outs = full_outputs(m, dev)
+    k1 = gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs).clone()
+    outs2 = full_outputs(m, dev)
+    k2 = gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs2).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(k1, k2) and all(torch.equal(outs[k], outs2[k]) for k in outs)
+    h = host(outs)
+    check_sets_and_key(h, k1, wl.beta, wl.f_min)
+    sel = np.arange(m)
+    emu, evar, same = check_sample(gm, wl, h, sel, wl.beta, wl.f_min)
+    print(f"C2 whole grid ({m}): mu {emu:.2e} var {evar:.2e} argmax same={same}")
+    assert emu < REL_TOL and evar < REL_TOL
+    gm.close()
+
+
 def test_c5_streaming_loop(dev):
     """C5: fit 1000 points, 50 appends to 8000, a 512 x 512 tick after each."""
     n_end, n0, iters, g = 8000, 1000, 50, 512

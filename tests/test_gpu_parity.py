@@ -827,6 +827,7 @@ def test_append_matches_refit(mapper):
     wl = synthetic(1200, 40, 40, seed=14)
     n0 = 700
     gm = TerrainMapper(0, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_RESORT, 0)      # the block Cholesky update itself (no re-sort)
     gm.fit(wl.x[:n0], wl.y[:n0], wl.obs[:n0])
     gm.append(wl.x[n0:1000], wl.y[n0:1000], wl.obs[n0:1000])
     gm.append(wl.x[1000:], wl.y[1000:], wl.obs[1000:])
@@ -838,6 +839,49 @@ def test_append_matches_refit(mapper):
     omu, ovar = oracle_given_factor(gm, wl)
     assert nrel(mu_a, omu) < REL_TOL and nrel(sd_a.astype(np.float64) ** 2, ovar) < REL_TOL
     assert nrel(mu_a, mu_r) < 1e-4 and nrel(sd_a.astype(np.float64) ** 2, sd_r.astype(np.float64) ** 2) < 1e-4
+    gm.set_option(N.SBO_OPT_RESORT, 25)
+
+
+def _tick_tiles(gm, wl):
+    lib = N.lib()
+    lib.sbo_profile(gm.ctx.handle, 1)
+    out = dict(mu=np.empty(wl.qx.size, np.float32), sd=np.empty(wl.qx.size, np.float32))
+    gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
+    w = ctypes.c_double()
+    lib.sbo_profile_work(gm.ctx.handle, ctypes.byref(w))
+    lib.sbo_profile(gm.ctx.handle, 0)
+    return out, w.value / (2.0 * 256 * 128 * 64)
+
+
+def test_append_resort(mapper):
+    """SBO_OPT_RESORT (default 25 %): scattered appended batches past a
+    quarter of the sorted points trigger a k-d re-sort + refactor inside
+    sbo_append.  The caller's indices survive (order is a permutation whose
+    rows carry the caller's points), the posterior equals the oracle given
+    the factor and the pure block-append stream to 1e-4, and the re-sorted
+    operand sweeps fewer k-tiles than the unsorted one."""
+    wl = synthetic(3000, 120, 100, seed=77)
+    res = {}
+    for pct in (0, 25):
+        gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+        gm.set_option(N.SBO_OPT_RESORT, pct)
+        gm.fit(wl.x[:1000], wl.y[:1000], wl.obs[:1000])
+        for a in range(1000, 3000, 143):
+            b = min(a + 143, 3000)
+            gm.append(wl.x[a:b], wl.y[a:b], wl.obs[a:b])
+        assert gm.n == 3000
+        o = gm.order()
+        assert np.array_equal(np.sort(o), np.arange(3000))
+        out, tiles = _tick_tiles(gm, wl)
+        omu, ovar = oracle_given_factor(gm, wl)
+        assert nrel(out["mu"], omu) < REL_TOL and nrel(out["sd"].astype(np.float64) ** 2, ovar) < REL_TOL
+        res[pct] = (out, tiles)
+    gm.set_option(N.SBO_OPT_RESORT, 25)
+    (o0, t0), (o25, t25) = res[0], res[25]
+    print(f"append stream to N=3000: k-tiles swept {t0:.0f} unsorted vs {t25:.0f} re-sorted")
+    assert t25 < 0.8 * t0
+    assert nrel(o25["mu"], o0["mu"].astype(np.float64)) < 1e-4
+    assert nrel(o25["sd"].astype(np.float64) ** 2, o0["sd"].astype(np.float64) ** 2) < 1e-4
 
 
 def test_append_incremental_inverse(mapper):
@@ -847,6 +891,7 @@ def test_append_incremental_inverse(mapper):
     one that grows the capacity."""
     wl = synthetic(900, 30, 30, seed=31)
     gm = TerrainMapper(0, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_RESORT, 0)      # every append incremental
     gm.fit(wl.x[:250], wl.y[:250], wl.obs[:250])
     for a, b in ((250, 251), (251, 252), (252, 300), (300, 512), (512, 513), (513, 900)):
         gm.append(wl.x[a:b], wl.y[a:b], wl.obs[a:b])
@@ -862,6 +907,7 @@ def test_append_incremental_inverse(mapper):
     mu, sd = gm.predict(wl.qx, wl.qy)
     omu, ovar = oracle_given_factor(gm, wl)
     assert nrel(mu, omu) < REL_TOL and nrel(sd.astype(np.float64) ** 2, ovar) < REL_TOL
+    gm.set_option(N.SBO_OPT_RESORT, 25)
 
 
 @pytest.mark.parametrize("n", [2049, 4100, 5000])
