@@ -311,11 +311,12 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * rounding of the sweep itself).  Takes effect at the next sbo_fit /
  * sbo_append. */
 #define SBO_OPT_SKIP_BUDGET 7
-/* SBO_OPT_CHOLESKY (1 default | 0): the fit's factorization -- 1 the
+/* SBO_OPT_CHOLESKY (1 default | 2 | 0): the fit's factorization -- 1 the
  * library's blocked right-looking Cholesky (a one-workgroup kernel per
- * 128-column diagonal block, rocBLAS strsm + ssyrk for the panel and the
- * trailing update), 0 rocSOLVER spotrf.  Same f32 algorithm class and the
- * same NOT_SPD reporting (leading minor). */
+ * 128-column diagonal block, its own panel triangular solve, rocBLAS sgemm +
+ * ssyrk for the trailing update with a look-ahead column), 2 the same with
+ * rocBLAS strsm for the panel, 0 rocSOLVER spotrf.  Same f32 algorithm class
+ * and the same NOT_SPD reporting (leading minor). */
 #define SBO_OPT_CHOLESKY 8
 /* SBO_OPT_INVERSE (1 default | 0): how the fit computes the f64 L^-1 of
  * SBO_OPT_INVERSE_BITS = 64 -- 1 the library's block recursion (rocSOLVER
@@ -357,6 +358,11 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * posterior is the same either way (to f32 factorization rounding); caller
  * indices (sbo_get_order) are kept. */
 #define SBO_OPT_RESORT 12
+/* SBO_OPT_CHOL_RESERVE (CUs, default 0): the blocked Cholesky's trailing
+ * updates (the look-ahead's second stream) run on a CU-masked stream that
+ * leaves this many CUs free for the latency-bound chain of diagonal blocks and
+ * panels.  Results do not depend on it (bitwise). */
+#define SBO_OPT_CHOL_RESERVE 13
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe

@@ -46,6 +46,7 @@ SBO_OPT_INVERSE = 9
 SBO_OPT_JITTER_RETRIES = 10
 SBO_OPT_PRECISION = 11
 SBO_OPT_RESORT = 12
+SBO_OPT_CHOL_RESERVE = 13
 
 
 class SboError(RuntimeError):

@@ -158,15 +158,26 @@ __global__ void pack_kcoord_kernel(const float *__restrict__ x, const float *__r
 // see info != 0 and leave their data alone.  Column-major, lda = ld; only
 // i >= j is written.
 constexpr int kCholPanel = 8;
+#ifdef SBO_CHOL_STAMPS
+// tools/chol_micro.hip only: s_memtime phase stamps of the fit's chain kernels
+__device__ unsigned long long g_chol_stamps[16];
+#define SBO_CSTAMP(i) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_chol_stamps[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#define SBO_CSTAMP_ADD(i, t0) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_chol_stamps[i] += __builtin_amdgcn_s_memtime() - (t0); } while (0)
+#else
+#define SBO_CSTAMP(i) do { } while (0)
+#define SBO_CSTAMP_ADD(i, t0) do { } while (0)
+#endif
 __device__ __forceinline__ float lane_value(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, int64_t ld, int kb, int64_t k0,
                                                         int *__restrict__ info) {
     static_assert(kCholNB <= 128, "two panel rows per lane of wave 0");
-    __shared__ float a[kCholNB][kCholNB + 1];
+    // row stride 132: a row's 8 panel columns are two aligned float4 reads
+    __shared__ __attribute__((aligned(16))) float a[kCholNB][kCholNB + 4];
     __shared__ int s_bad;
     if (*info != 0) return;
+    SBO_CSTAMP(0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // the block in, kCholLoad independent loads per thread in flight at a time
     // (one at a time, the reads' latency was most of this kernel)
@@ -188,8 +199,15 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, i
     }
     if (tid == 0) s_bad = 0;
     __syncthreads();
+    SBO_CSTAMP(1);
+#ifdef SBO_CHOL_STAMPS
+    if (threadIdx.x == 0) { g_chol_stamps[4] = 0; g_chol_stamps[5] = 0; }
+#endif
     for (int jb = 0; jb < kb; jb += kCholPanel) {
         const int w = min(kCholPanel, kb - jb);
+#ifdef SBO_CHOL_STAMPS
+        const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+#endif
         if (wave == 0) {
             const int r0 = jb + lane, r1 = jb + 64 + lane;
             float p0[kCholPanel], p1[kCholPanel];
@@ -208,10 +226,13 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, i
                     bad = j + 1;
                     continue;
                 }
-                const float d = __fsqrt_rn(djj);
-                if (r0 > j) p0[c] = __fdiv_rn(p0[c], d);
-                else if (r0 == j) p0[c] = d;
-                p1[c] = __fdiv_rn(p1[c], d);   // r1 > j always
+                // 1/sqrt(djj) once (v_rsq_f32), the column scaled by it and
+                // the pivot as djj * (1/sqrt(djj)): one transcendental on the
+                // serial chain instead of a sqrt and two divisions
+                const float rs = __builtin_amdgcn_rsqf(djj);
+                if (r0 > j) p0[c] = p0[c] * rs;
+                else if (r0 == j) p0[c] = djj * rs;
+                p1[c] = p1[c] * rs;   // r1 > j always
 #pragma unroll
                 for (int c2 = c + 1; c2 < kCholPanel; ++c2) {
                     if (c2 >= w) continue;
@@ -228,7 +249,11 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, i
             if (lane == 0 && bad) s_bad = bad;
         }
         __syncthreads();
+        SBO_CSTAMP_ADD(4, tp0);
         if (s_bad) break;
+#ifdef SBO_CHOL_STAMPS
+        const unsigned long long tu0 = __builtin_amdgcn_s_memtime();
+#endif
         // rank-w update of the trailing lower triangle [t0, kb) in 4 x 4 tiles
         const int t0 = jb + w, n2 = kb - t0;
         const int nt = (n2 + 3) >> 2, ntiles = nt * (nt + 1) / 2;
@@ -240,12 +265,20 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, i
             const int i0 = t0 + 4 * ti, l0 = t0 + 4 * tl;
             float li[4][kCholPanel], ll[4][kCholPanel];
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < 4; ++r) {
+                // rows past kb read (finite) padding rows of the array; columns
+                // past w are masked below
+                const float4 *pi = reinterpret_cast<const float4 *>(&a[min(i0 + r, kCholNB - 1)][jb]);
+                const float4 *pl = reinterpret_cast<const float4 *>(&a[min(l0 + r, kCholNB - 1)][jb]);
+                const float4 i0v = pi[0], i1v = pi[1], l0v = pl[0], l1v = pl[1];
+                const float iv[8] = {i0v.x, i0v.y, i0v.z, i0v.w, i1v.x, i1v.y, i1v.z, i1v.w};
+                const float lv[8] = {l0v.x, l0v.y, l0v.z, l0v.w, l1v.x, l1v.y, l1v.z, l1v.w};
 #pragma unroll
                 for (int c = 0; c < kCholPanel; ++c) {
-                    li[r][c] = (i0 + r < kb && c < w) ? a[i0 + r][jb + c] : 0.0f;
-                    ll[r][c] = (l0 + r < kb && c < w) ? a[l0 + r][jb + c] : 0.0f;
+                    li[r][c] = (i0 + r < kb && c < w) ? iv[c] : 0.0f;
+                    ll[r][c] = (l0 + r < kb && c < w) ? lv[c] : 0.0f;
                 }
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -261,7 +294,9 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, i
                 }
         }
         __syncthreads();
+        SBO_CSTAMP_ADD(5, tu0);
     }
+    SBO_CSTAMP(2);
     if (s_bad) {
         if (tid == 0) atomicCAS(info, 0, (int)(k0 + s_bad));
         return;
@@ -270,6 +305,134 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, i
         const int i = e % kb, j = e / kb;
         if (i >= j) A[i + (int64_t)j * ld] = a[i][j];
     }
+    SBO_CSTAMP(3);
+}
+
+// The blocked Cholesky's panel (a2): A21 := A21 L11^-T for the m2 x kb panel
+// below a factored kb x kb diagonal block (rocBLAS strsm right / lower /
+// transpose ran as ~10 launches, ~100 us per step, on the factorization's
+// critical path).  Forward substitution row by row, x L11^T = a: 128 panel
+// rows per workgroup, two threads per row (t and t + 128, one wave per SIMD);
+// L11 row-major in LDS (stride 132: a row's 16-column blocks are aligned
+// float4 reads, every lane reading the same address -- broadcast), the rows
+// being solved in LDS column-major (lane-linear, conflict-free).
+// Right-looking in 16-column blocks: both threads of a row solve the block's
+// 16 values in registers, x_j = (a_j - sum_{u<j} x_u L_ju) * (1 / L_jj)
+// (ascending u; the block of L read into registers first so that the chain
+// waits on no LDS read), then each takes every other later column and
+// subtracts the block's 16 terms.  Each x_j sees its terms in ascending
+// column order, as in the plain forward substitution; the reciprocal of the
+// pivot is the one extra rounding strsm's inverted diagonal has too.  kb <
+// 128 (the last step) pads L11 with the identity.
+constexpr int kTrsmLd = 132;
+__global__ __launch_bounds__(256) void chol_trsm_kernel(const float *__restrict__ L11, int64_t ld, int kb,
+                                                        float *__restrict__ A21, int64_t m2) {
+    __shared__ __attribute__((aligned(16))) float Ls[kCholNB * kTrsmLd];
+    __shared__ float X[kCholNB * kCholNB];
+    SBO_CSTAMP(8);
+    const int tid = threadIdx.x, t = tid & (kCholNB - 1), h = tid >> 7;
+    const int64_t row = (int64_t)blockIdx.x * kCholNB + t;
+    const bool in = row < m2;
+    // columns of L11 and of the panel rows (coalesced over t), 16 columns of
+    // loads in flight at a time, half the columns per thread of the pair;
+    // identity padding past kb
+    // (one predicate per thread for the loads, so all 16 of a batch are in
+    // flight together; the upper triangle and the padding are fixed up after)
+    const bool lin = t < kb;
+    for (int j0 = 8 * h; j0 < kCholNB; j0 += 16) {
+        float lv[8], xv[8];
+        if (j0 + 8 <= kb) {
+            if (lin) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) lv[u] = L11[t + (int64_t)(j0 + u) * ld];
+            }
+            if (in) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xv[u] = A21[row + (int64_t)(j0 + u) * ld];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                lv[u] = (lin && j0 + u < kb) ? L11[t + (int64_t)(j0 + u) * ld] : 0.0f;
+                xv[u] = (in && j0 + u < kb) ? A21[row + (int64_t)(j0 + u) * ld] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 + u;
+            Ls[t * kTrsmLd + j] = (j < kb && lin && t >= j) ? lv[u] : (t == j && j >= kb ? 1.0f : 0.0f);
+            X[j * kCholNB + t] = (in && j < kb) ? xv[u] : 0.0f;
+        }
+    }
+    __syncthreads();
+    SBO_CSTAMP(9);
+    for (int B = 0; B < kCholNB / 16; ++B) {
+        const int j0 = 16 * B;
+        // the 16 x 16 diagonal block of L (lower: row q needs q + 1 values)
+        float4 lb[16][4];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                if (4 * v <= q) lb[q][v] = reinterpret_cast<const float4 *>(Ls + (j0 + q) * kTrsmLd + j0)[v];
+        float xb[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) xb[u] = X[(j0 + u) * kCholNB + t];
+        float rinv[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const float4 d = lb[q][q >> 2];
+            rinv[q] = __fdiv_rn(1.0f, (q & 3) == 0 ? d.x : (q & 3) == 1 ? d.y : (q & 3) == 2 ? d.z : d.w);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            float s = xb[q];
+#pragma unroll
+            for (int u = 0; u < q; ++u) {
+                const float4 l4 = lb[q][u >> 2];
+                const float l = (u & 3) == 0 ? l4.x : (u & 3) == 1 ? l4.y : (u & 3) == 2 ? l4.z : l4.w;
+                s = fmaf(-xb[u], l, s);
+            }
+            xb[q] = s * rinv[q];
+        }
+        __syncthreads();   // every read of this block's columns is done
+        if (h == 0) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) X[(j0 + u) * kCholNB + t] = xb[u];
+        }
+        // later columns of this thread (every other one), four at a time:
+        // four independent FMA chains in flight instead of one
+        for (int c0 = j0 + 16 + h; c0 < kCholNB; c0 += 8) {
+            float v[4];
+            float lv[4][16];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int c = min(c0 + 2 * k, kCholNB - 1);
+                const float4 *lr = reinterpret_cast<const float4 *>(Ls + c * kTrsmLd + j0);
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const float4 l4 = lr[q4];
+                    lv[k][4 * q4] = l4.x;
+                    lv[k][4 * q4 + 1] = l4.y;
+                    lv[k][4 * q4 + 2] = l4.z;
+                    lv[k][4 * q4 + 3] = l4.w;
+                }
+                v[k] = X[c * kCholNB + t];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = fmaf(-xb[u], lv[k][u], v[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (c0 + 2 * k < kCholNB) X[(c0 + 2 * k) * kCholNB + t] = v[k];
+        }
+        __syncthreads();
+    }
+    SBO_CSTAMP(10);
+    if (in)
+        for (int j = h; j < kb; j += 2) A21[row + (int64_t)j * ld] = X[j * kCholNB + t];
+    SBO_CSTAMP(11);
 }
 
 // Row 1-norms of the packed operand: block I, thread r sums |A[I*BM + r][:]|.
@@ -1757,6 +1920,14 @@ hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t 
 hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info) {
     if (kb <= 0 || kb > kCholNB) return hipErrorInvalidValue;
     hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, s, A, ld, kb, k0, info);
+    return hipGetLastError();
+}
+
+hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb, float *A21, int64_t m2) {
+    if (kb <= 0 || kb > kCholNB || m2 < 0) return hipErrorInvalidValue;
+    if (m2 == 0) return hipSuccess;
+    hipLaunchKernelGGL(chol_trsm_kernel, dim3((unsigned)((m2 + kCholNB - 1) / kCholNB)), dim3(2 * kCholNB), 0, s,
+                       L11, ld, kb, A21, m2);
     return hipGetLastError();
 }
 

@@ -314,7 +314,7 @@ hipError_t grow_keep(sbo_ctx *ctx, DevBuf &buf, size_t bytes, size_t keep) {
 
 // sweep selection of run_tick: -1 the context's (ctx->precise), 0 the fast
 // split sweep, 1 the precise f64 sweep under its budget, 2 the precise sweep
-// dense (only exact zeros dropped; the probe's reference)
+// under a 2^-44 sf2 budget (the probe's reference)
 constexpr int kSweepCtx = -1, kSweepFast = 0, kSweepPrecise = 1, kSweepPreciseDense = 2;
 sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, double beta, double f_min,
                     int score_kind, int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
@@ -497,20 +497,26 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
 // probe saw inside the training box instead of 2^-B sf2 -- the 1e-5 contract
 // is relative to the largest variance of a query set, and in the dense
 // regime that is orders below sf2.
-void precise_budget(sbo_ctx *ctx) {
+// (cutoff exponent, log2 of the row blocks' |dV_I|_2 share) keeping the
+// dropped tiles' effect on any variance below tol (absolute)
+void skip_budget_for(const sbo_ctx *ctx, double tol, int &L, float &lg_tau) {
     const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f, sf = std::sqrt(sf2);
-    const double floor_v = std::max(ctx->probe_vmin, 1e-12 * sf2);
-    const double tol = std::ldexp(1.0, -ctx->skip_budget) * std::min(floor_v, sf2);
     const double tau2 = tol / (2.0 * sf) * 0.99;
     const double need = ctx->max_row_l1 * std::sqrt((double)ctx->n) / tau2;
     const double l2 = std::log2(std::max(need, 1.0));
-    ctx->p_skip_log2 = std::isfinite(l2) ? std::min(160, std::max(16, (int)std::ceil(l2))) : 160;
-    ctx->p_lg_tau_v = (float)std::log2(tau2 / std::sqrt((double)(ctx->npad / sbo::kBM)));
+    L = std::isfinite(l2) ? std::min(160, std::max(16, (int)std::ceil(l2))) : 160;
+    lg_tau = (float)std::log2(tau2 / std::sqrt((double)(ctx->npad / sbo::kBM)));
+}
+void precise_budget(sbo_ctx *ctx) {
+    const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
+    const double floor_v = std::max(ctx->probe_vmin, 1e-12 * sf2);
+    skip_budget_for(ctx, std::ldexp(1.0, -ctx->skip_budget) * std::min(floor_v, sf2), ctx->p_skip_log2,
+                    ctx->p_lg_tau_v);
 }
 
 // SBO_OPT_PRECISION (-1 auto): which sweep the ticks run.  The probe sweeps a
 // 32 x 32 grid over the training box twice -- the fast split sweep and the
-// precise f64 sweep without skipping -- and measures the fast sweep's
+// precise f64 sweep at a 2^-44 sf2 skip budget -- and measures the fast sweep's
 // normwise variance error against it, max |d var| / max var (the contract's
 // metric); above kPreciseTol the context's ticks use the precise sweep.
 // kPreciseTol = 7e-6: measured probe errors 1.8e-6 (C2), 4.3e-6 (C3), 4.9e-6
@@ -587,8 +593,25 @@ sbo_status probe_precision(sbo_ctx *ctx) {
 sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_int *info) {
     SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), ctx->stream));
     SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
+    if (ctx->aux_stream && ctx->aux_reserved != ctx->chol_reserve) {  // another CU mask: a new aux stream
+        SBO_HIP(hipStreamSynchronize(ctx->aux_stream));
+        SBO_HIP(hipStreamDestroy(ctx->aux_stream));
+        ctx->aux_stream = nullptr;
+    }
     if (!ctx->aux_stream) {
-        SBO_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+        if (ctx->chol_reserve > 0) {
+            // the trailing updates stay off the first chol_reserve CUs, so the
+            // latency-bound chain (diagonal block, panel) finds them free
+            std::vector<uint32_t> mask((size_t)(ctx->num_cu + 31) / 32, 0u);
+            for (int c = ctx->chol_reserve; c < ctx->num_cu; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+            SBO_HIP(hipExtStreamCreateWithCUMask(&ctx->aux_stream, (uint32_t)mask.size(), mask.data()));
+        } else {
+            SBO_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+        }
+        ctx->aux_reserved = ctx->chol_reserve;
+        if (ctx->blas_aux) SBO_BLAS(rocblas_set_stream(ctx->blas_aux, ctx->aux_stream));
+    }
+    if (!ctx->ev_panel) {
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_panel, hipEventDisableTiming));
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_trail, hipEventDisableTiming));
     }
@@ -608,9 +631,14 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         float *L11 = L + k + k * ld, *A21 = L11 + kb;
         const int64_t kb2 = std::min<int64_t>(sbo::kCholNB, m2);   // the next block column
         float *C1 = L11 + kb + kb * ld;                             // its rows k + kb ..
-        if (rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
-                          rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11, (rocblas_int)ld,
-                          A21, (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
+        if (ctx->chol_trsm_own) {
+            if (sbo::launch_chol_trsm(ctx->stream, L11, ld, (int)kb, A21, m2) != hipSuccess) { st = SBO_E_DEVICE; break; }
+        } else if (rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                                 rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11,
+                                 (rocblas_int)ld, A21, (rocblas_int)ld) != rocblas_status_success) {
+            st = SBO_E_DEVICE;
+            break;
+        }
         if (hipEventRecord(ctx->ev_panel, ctx->stream) != hipSuccess ||
             (trail_pending && hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0) != hipSuccess)) { st = SBO_E_DEVICE; break; }
         if (rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m2,
@@ -672,7 +700,13 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     int64_t ms = m;
     sbo::SkipPlan plan;
     if (sweep == kSweepPreciseDense) {
-        plan.L = 150;   // only exact zeros dropped (bitwise the dense sweep)
+        // the probe's reference: the precise sweep under a budget of 2^-44 sf2
+        // on any variance (5.7e-14 sf2: far below the probe's resolution of
+        // the fast sweep's error for any variance above ~1e-8 sf2)
+        skip_budget_for(ctx, std::ldexp(ctx->hyper.sigma_f * ctx->hyper.sigma_f, -44), plan.L, plan.lg_tau_v);
+        plan.L_mean = ctx->auto_skip_mean_log2;
+        plan.lgn = ctx->tile_lgn.as<float4>();
+        plan.kcoord = ctx->kcoord.as<float>();
     } else if (ctx->skip_log2 < 0) {
         plan.L = precise ? ctx->p_skip_log2 : ctx->auto_skip_log2;
         plan.L_mean = ctx->auto_skip_mean_log2;
@@ -1380,8 +1414,9 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
     if (!ctx) return SBO_E_INVAL;
     switch (option) {
         case SBO_OPT_CHOLESKY:
-            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_CHOLESKY must be 0 or 1");
+            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_CHOLESKY must be 0, 1 or 2");
             ctx->chol_blocked = value != 0;
+            ctx->chol_trsm_own = value == 1;
             return SBO_OK;
         case SBO_OPT_JITTER_RETRIES:
             SBO_CHECK(value >= 0 && value <= 8, SBO_E_INVAL, "SBO_OPT_JITTER_RETRIES must be in [0, 8]");
@@ -1415,6 +1450,11 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             SBO_CHECK(sbo::variant_allowed((int)value), SBO_E_INVAL,
                       "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22)");
             ctx->kernel_variant = (int)value;
+            return SBO_OK;
+        case SBO_OPT_CHOL_RESERVE:
+            SBO_CHECK(value >= 0 && value < ctx->num_cu, SBO_E_INVAL,
+                      "SBO_OPT_CHOL_RESERVE must be in [0, compute units)");
+            ctx->chol_reserve = (int)value;
             return SBO_OK;
         case SBO_OPT_RESORT:
             SBO_CHECK(value >= 0 && value <= 1000, SBO_E_INVAL, "SBO_OPT_RESORT must be in [0, 1000] (percent)");

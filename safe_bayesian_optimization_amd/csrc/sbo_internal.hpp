@@ -96,6 +96,8 @@ struct sbo_ctx {
     // shared by kernels in flight on two streams)
     hipStream_t aux_stream = nullptr;
     rocblas_handle blas_aux = nullptr;
+    int chol_reserve = 0;        // SBO_OPT_CHOL_RESERVE: CUs the trailing updates leave free (CU-masked aux stream)
+    int aux_reserved = 0;        // the mask the current aux stream was created with
     hipEvent_t ev_panel = nullptr, ev_trail = nullptr;
     std::string err;
 
@@ -115,6 +117,7 @@ struct sbo_ctx {
     double jitter = 0.0;         // the diagonal jitter of the current fit (0 unless a retry succeeded)
     bool inverse_rec = true;     // SBO_OPT_INVERSE: 1 own recursive f64 inverse (panelled dgemms), 0 rocSOLVER dtrtri
     bool chol_blocked = true;    // SBO_OPT_CHOLESKY: 1 own blocked factorization, 0 rocSOLVER spotrf
+    bool chol_trsm_own = true;   //   1: its panels by chol_trsm_kernel, 2: by rocBLAS strsm
     int spatial_order = 3;       // SBO_OPT_SPATIAL_ORDER: 0 caller order, 1 Hilbert, 2 Morton, 3 k-d
     int skip_log2 = -1;          // SBO_OPT_TILE_SKIP: skip K* tiles with every entry < 2^-L (-1: auto)
     int auto_skip_log2 = 160;    // auto K* cutoff for V (half the budget), computed at fit (refresh_operand)
@@ -302,6 +305,8 @@ hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int6
 // lda = ld) of step k0 in place (kb <= kCholNB); info as rocSOLVER's.
 constexpr int kCholNB = 128;
 hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info);
+// The panel below it: A21 (m2 x kb, lda ld) := A21 L11^-T (forward substitution, f32).
+hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb, float *A21, int64_t m2);
 // d = (double)in - v;  out = (float)d
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out);

@@ -1,0 +1,51 @@
+// Micro-benchmark of the blocked Cholesky's chain kernels in isolation
+// (chol_diag_kernel, chol_trsm_kernel) at C4's leading dimension, with
+// s_memtime phase stamps (-DSBO_CHOL_STAMPS).  GPU diagnostic:
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DSBO_CHOL_STAMPS -I/opt/rocm/include \
+//         tools/chol_micro.hip -o /tmp/chol_micro && /tmp/chol_micro
+#include "../safe_bayesian_optimization_amd/csrc/kernels.hip"
+
+#include <cstdio>
+#include <vector>
+
+int main() {
+    const int64_t n = 16384, ld = n, kb = 128, m2 = n - kb;
+    std::vector<float> h((size_t)kb * ld * 2, 0.0f);
+    // an SPD 128 x 128 block (diagonally dominant) and a panel below it
+    for (int j = 0; j < kb; ++j)
+        for (int64_t i = 0; i < n; ++i) h[i + (size_t)j * ld] = (i == j) ? 200.0f : 0.5f / (1.0f + (float)((i * 7 + j * 3) % 13));
+    float *dA = nullptr;
+    int *info = nullptr;
+    (void)hipMalloc(&dA, sizeof(float) * (size_t)kb * ld);
+    (void)hipMalloc(&info, sizeof(int));
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    unsigned long long st[16];
+    for (int rep = 0; rep < 3; ++rep) {
+        (void)hipMemcpy(dA, h.data(), sizeof(float) * (size_t)kb * ld, hipMemcpyHostToDevice);
+        (void)hipMemset(info, 0, sizeof(int));
+        (void)hipEventRecord(e0, 0);
+        (void)sbo::launch_chol_diag(0, dA, ld, (int)kb, 0, info);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms_d = 0.f;
+        (void)hipEventElapsedTime(&ms_d, e0, e1);
+        (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(sbo::g_chol_stamps), sizeof(st));
+        printf("diag: %.1f us  | memtime ticks: load %llu, panels %llu, updates %llu, factor total %llu, store %llu\n",
+               ms_d * 1e3, st[1] - st[0], st[4], st[5], st[2] - st[1], st[3] - st[2]);
+        (void)hipEventRecord(e0, 0);
+        (void)sbo::launch_chol_trsm(0, dA, ld, (int)kb, dA + kb, m2);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms_t = 0.f;
+        (void)hipEventElapsedTime(&ms_t, e0, e1);
+        (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(sbo::g_chol_stamps), sizeof(st));
+        printf("trsm (m2 %lld): %.1f us | block 0 ticks: load %llu, solve %llu, store %llu\n", (long long)m2,
+               ms_t * 1e3, st[9] - st[8], st[10] - st[9], st[11] - st[10]);
+    }
+    int hinfo = 0;
+    (void)hipMemcpy(&hinfo, info, sizeof(int), hipMemcpyDeviceToHost);
+    printf("info %d (s_memtime ticks at 100 MHz)\n", hinfo);
+    return 0;
+}
