@@ -342,7 +342,8 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * the same tiles.  -1: every sbo_fit (and an sbo_append once N grew by a
  * quarter since the last probe) sweeps a 32 x 32 grid over the training box
  * both ways and ticks with the precise sweep when the fast sweep's variance
- * error there, max |d var| / max var, exceeds 7e-6 (the 1e-5 contract less a margin):
+ * error there, max |d var| / max var, exceeds 7e-6 (the 1e-5 contract less a margin;
+ * 7e-6 * 2^(20 - B) for a looser SBO_OPT_SKIP_BUDGET B < 20):
  * dense data, where the variance is orders below sf2 and sf2 - |V|^2 cancels
  * (config/lpsc.yaml's own box at N = 16384).  The precise sweep's skip budget
  * is 2^-B times the smallest probe variance (SBO_OPT_SKIP_BUDGET = B).  Needs

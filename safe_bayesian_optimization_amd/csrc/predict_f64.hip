@@ -51,27 +51,47 @@ __device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
 // One stage: acc[rb] += A[16 rb + (l & 15)][4 s + (l >> 4)] * K*[4 s + (l >> 4)][q]
 // over the stage's eight k steps, and mu += K* sf2 alpha * wmean (1 on the
 // last row block, whose items carry the mean; one code path, so the
-// accumulators keep their registers).  The A operands of step s + 1 are read
-// from LDS while step s's sixteen MFMAs run.
+// accumulators keep their registers).  Software pipeline, pinned with
+// scheduling fences: step s issues the LDS reads of step s + 1's sixteen A
+// operands and evaluates step s + 1's K* (f64 exp2) beside its own sixteen
+// MFMAs, so no MFMA waits on a read or an exp issued in its own step.
 __device__ __forceinline__ void stage_steps(const double *__restrict__ pa, const double *__restrict__ pc, double xq,
                                             double yq, double cexp, double wmean, f64x4 (&acc)[kDRB], double &mu) {
     double a[kDRB], an[kDRB];
 #pragma unroll
     for (int rb = 0; rb < kDRB; ++rb) a[rb] = pa[rb * 64];
+    auto kstar = [&](double xk, double yk) {
+        const double dx = xk - xq, dy = yk - yq;
+        return exp2(cexp * fma(dy, dy, dx * dx));
+    };
+    double e = kstar(pc[0], pc[kDH]);
+    mu = fma(e, pc[2 * kDH] * wmean, mu);
 #pragma unroll
     for (int s = 0; s < kDSteps; ++s) {
-        const double dx = pc[4 * s] - xq, dy = pc[kDH + 4 * s] - yq;
-        const double e = exp2(cexp * fma(dy, dy, dx * dx));
-        mu = fma(e, pc[2 * kDH + 4 * s] * wmean, mu);
+        double en = 0.0;
         if (s + 1 < kDSteps) {
+            // the next step's coordinates first, then its A operands: the K*
+            // below waits only for the coordinates (LDS reads retire in order)
+            const double xk = pc[4 * (s + 1)], yk = pc[kDH + 4 * (s + 1)], ak = pc[2 * kDH + 4 * (s + 1)];
 #pragma unroll
             for (int rb = 0; rb < kDRB; ++rb) an[rb] = pa[((s + 1) * kDRB + rb) * 64];
+            en = kstar(xk, yk);
+            mu = fma(en, ak * wmean, mu);
         }
 #pragma unroll
         for (int rb = 0; rb < kDRB; ++rb) acc[rb] = mfma_f64(a[rb], e, acc[rb]);
+        // one MFMA, then up to two VALU and one LDS read, in turn
+#pragma unroll
+        for (int j = 0; j < kDRB; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        }
+        __builtin_amdgcn_sched_barrier(0);
         if (s + 1 < kDSteps) {
 #pragma unroll
             for (int rb = 0; rb < kDRB; ++rb) a[rb] = an[rb];
+            e = en;
         }
     }
 }

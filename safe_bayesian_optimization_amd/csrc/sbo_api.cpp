@@ -573,7 +573,10 @@ sbo_status probe_precision(sbo_ctx *ctx) {
         ctx->probe_n = ctx->n;
     }
     precise_budget(ctx);
-    ctx->precise = ctx->precision_opt == 1 || ctx->probe_err > kPreciseTol;
+    // a looser skip budget than the default (B < 20: the caller trades
+    // accuracy for speed) loosens the threshold by the same factor
+    const double tol = kPreciseTol * std::ldexp(1.0, std::max(0, 20 - ctx->skip_budget));
+    ctx->precise = ctx->precision_opt == 1 || ctx->probe_err > tol;
     return SBO_OK;
 }
 
