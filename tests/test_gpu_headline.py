@@ -254,3 +254,38 @@ def test_lpsc_stress_box(dev, gw, gh):
           f"fast mu {fmu:.2e} var {fvar:.2e}")
     assert emu < REL_TOL and evar < REL_TOL
     gm.close()
+
+
+def test_c4_bitwise_across_sweep_groups(dev):
+    """The split sweep's staging (LDS-DMA stages, the step-record windows and
+    their refills) at C4 size: the default tick with the persistent sweep cut
+    into 256 (one per CU), 200, 97 and 31 workgroup ranges -- every range
+    starts and ends at other items, so window boundaries fall at other steps
+    -- must give bitwise the same mu, sigma and key (a reverted
+    one-step variant once differed in 20 of 10^6 sigma; this pins the shared
+    staging code at the bench's own size)."""
+    from safe_bayesian_optimization_amd import _native as N
+    n, gw, gh = CONFIGS["C4"]
+    wl = synthetic(n, gw, gh, seed=0, name="C4")
+    gm = TerrainMapper(0, wl.hyper)
+    t = lambda a: torch.tensor(f32(a), device=dev)  # noqa: E731
+    gm.fit(t(wl.x), t(wl.y), t(wl.obs))
+    qx, qy = t(wl.qx), t(wl.qy)
+    m = qx.numel()
+    ref = None
+    try:
+        for groups in (0, 200, 97, 31):
+            gm.set_option(N.SBO_OPT_SWEEP_GROUPS, groups)
+            outs = full_outputs(m, dev)
+            k = gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs).clone()
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = (k, outs)
+                continue
+            assert torch.equal(k, ref[0]), groups
+            for name in ("mu", "sd"):
+                diff = int((outs[name] != ref[1][name]).sum())
+                assert diff == 0, (groups, name, diff)
+    finally:
+        gm.set_option(N.SBO_OPT_SWEEP_GROUPS, 0)
+    gm.close()

@@ -107,12 +107,13 @@ def test_cholesky_backward_error(mapper, n):
 
 @pytest.mark.parametrize("n", [129, 300, 2048, 4100])
 def test_blocked_cholesky_matches_spotrf(mapper, n):
-    """The library's blocked Cholesky (SBO_OPT_CHOLESKY = 1, default) and
-    rocSOLVER spotrf (0): both within the backward-error bound, factors equal
+    """The library's blocked Cholesky with its own panel solve
+    (SBO_OPT_CHOLESKY = 1, default), with rocBLAS strsm panels (2), and
+    rocSOLVER spotrf (0): all within the backward-error bound, factors equal
     to f32 rounding, the same posterior to the contract."""
     wl = synthetic(n, 24, 20, seed=n + 3)
     res = {}
-    for ch in (0, 1):
+    for ch in (0, 2, 1):
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
         gm.set_option(N.SBO_OPT_CHOLESKY, ch)
         gm.fit(wl.x, wl.y, wl.obs)
@@ -124,9 +125,10 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
         assert be <= 10 * n * EPS32, (ch, be)
         res[ch] = (L64, gm.predict(wl.qx, wl.qy))
     gm.set_option(N.SBO_OPT_CHOLESKY, 1)
-    assert np.abs(res[0][0] - res[1][0]).max() <= 1e-4 * np.abs(res[0][0]).max()
-    assert nrel(res[1][1][0], res[0][1][0].astype(np.float64)) < REL_TOL
-    assert nrel(res[1][1][1].astype(np.float64) ** 2, res[0][1][1].astype(np.float64) ** 2) < REL_TOL
+    for ch in (1, 2):   # own panel solve (default) and rocBLAS strsm panels, against spotrf
+        assert np.abs(res[0][0] - res[ch][0]).max() <= 1e-4 * np.abs(res[0][0]).max()
+        assert nrel(res[ch][1][0], res[0][1][0].astype(np.float64)) < REL_TOL
+        assert nrel(res[ch][1][1].astype(np.float64) ** 2, res[0][1][1].astype(np.float64) ** 2) < REL_TOL
 
 
 def test_blocked_cholesky_not_spd_past_first_block(mapper):
