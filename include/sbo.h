@@ -364,6 +364,13 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * leaves this many CUs free for the latency-bound chain of diagonal blocks and
  * panels.  Results do not depend on it (bitwise). */
 #define SBO_OPT_CHOL_RESERVE 13
+/* SBO_OPT_INV_OVERLAP (CUs, default 0: off): with the recursive f64 inverse,
+ * its first half (the inverse of the factor's leading half and the product
+ * below it: half the inverse's flops) starts as soon as the factor's left
+ * half is final and runs beside the Cholesky's last steps, on a CU-masked
+ * stream that leaves this many CUs to the factorization's latency-bound
+ * chain.  Results do not depend on it (bitwise). */
+#define SBO_OPT_INV_OVERLAP 14
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe

@@ -47,6 +47,7 @@ SBO_OPT_JITTER_RETRIES = 10
 SBO_OPT_PRECISION = 11
 SBO_OPT_RESORT = 12
 SBO_OPT_CHOL_RESERVE = 13
+SBO_OPT_INV_OVERLAP = 14
 
 
 class SboError(RuntimeError):

@@ -150,7 +150,10 @@ __device__ __forceinline__ float kstar1(float xk, float yk, float xq, float yq, 
 //   this body then): its K* pieces are kh alone, the split is skipped (a
 //   one-product step reads no other piece, so the results are bitwise those
 //   of the full split).
-template <int NC, bool FRESH, int DIAG, int PIECES, int LV = 0, bool KHN = false>
+//   MEAN: 1 the next step is the mean's row block, 0 it is not (compile
+//   time: a uniform branch inside the MFMA region splits it into separately
+//   scheduled pieces, four per half-step), -1 the runtime test of msc.
+template <int NC, bool FRESH, long long DIAG, int PIECES, int LV = 0, bool KHN = false, int MEAN = -1>
 __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn, const float (&xq)[NC],
                                         const float (&yq)[NC], int g, float cexp, float msc, const KPieces<NC> &kb,
                                         f32x4 (&acc)[NC][16], f32x4 (&outer)[NC][16], KPieces<NC> &nx,
@@ -192,7 +195,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
     // DIAG & 67108864: sf2 alpha read only before the mean's row block (msc != 0)
     constexpr bool AK_MEAN = (DIAG & 67108864) != 0;
     f32x2v xk = lds_f2(pcn + g * 32), yk = lds_f2(pcn + 128 + g * 32), ak = {0.f, 0.f};
-    if (!AK_MEAN || msc != 0.0f) ak = lds_f2(pcn + 256 + g * 32);
+    if (!AK_MEAN || (MEAN < 0 ? msc != 0.0f : MEAN == 1)) ak = lds_f2(pcn + 256 + g * 32);
     f32x2v e[NC];
 #pragma unroll
     for (int rb = 0; rb < 16; ++rb) {
@@ -247,7 +250,17 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                 nx.l[c][i] = w2;
             }
         } else {
-            if (msc != 0.0f) {  // the next step is the mean's row block (uniform branch)
+            // (DIAG & 2^32: the mean terms by a select, every step, instead of a branch)
+            constexpr bool BLM = (DIAG & 4294967296LL) != 0;
+            if constexpr (BLM) {
+                const bool mn = msc != 0.0f;
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    const double t = (double)fmaf(ak.x, e[c].x, ak.y * e[c].y);
+                    mu[c] = mn ? mu[c] + t : mu[c];
+                    SBO_PIN(mu[c]);
+                }
+            } else if (MEAN < 0 ? msc != 0.0f : MEAN == 1) {  // the next step is the mean's row block
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
                     // the pair's terms in f32 (one rounding of a two-term sum,
@@ -261,7 +274,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                     xk = lds_f2(pcn + g * 32 + (i + 1) * 8);
                     yk = lds_f2(pcn + 128 + g * 32 + (i + 1) * 8);
                 }
-                if (!AK_MEAN || msc != 0.0f) ak = lds_f2(pcn + 256 + g * 32 + (i + 1) * 8);
+                if (!AK_MEAN || (MEAN < 0 ? msc != 0.0f : MEAN == 1)) ak = lds_f2(pcn + 256 + g * 32 + (i + 1) * 8);
             }
         }
         if (SPREAD && rb >= 1 && rb <= PIECES && loader) {
@@ -389,7 +402,7 @@ __device__ __forceinline__ f32x16 mfma32(u32x4 a, u32x4 b, f32x16 c) {
 // sub-step p>>2) is evaluated at even u and split (+ mean terms, + the next
 // pair's coordinates) at odd u; the finished chains of row block rb-1 are
 // added into `outer` over sub-steps 2rb, 2rb+1.
-template <bool FRESH, int DIAG>
+template <bool FRESH, long long DIAG>
 __device__ __forceinline__ void x3w_half(const lds_char *pa, const lds_char *pcn, float xq, float yq, int h,
                                          float cexp, float msc, const KPieces<2> &kb, f32x16 (&acc)[8],
                                          f32x16 (&outer)[8], KPieces<2> &nx, double &mu, uint32_t voff,
@@ -508,7 +521,7 @@ constexpr int kFirst = 2, kLast = 4, kValid = 8;
 // 16 (not a diagnostic): A pieces spread over the row blocks; 32: A fragments
 // read one row block ahead instead of two; 8192 (not a diagnostic): every
 // tile at the precision level its plan entry names (code << kLevelShift).
-template <int NC, int DIAG>
+template <int NC, long long DIAG>
 __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     const char *__restrict__ ax3, const float *__restrict__ kc3, const int4 *__restrict__ desc,
     const int4 *__restrict__ rec, const int *__restrict__ seg, int P, int n_items, int nI, uint32_t a_max, int rot,
@@ -748,21 +761,38 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         if constexpr (WIDE)
             x3w_half<FRESH, DIAG>(pa, pcn, xq[0], yq[0], lane >> 5, cexp, msc, kb, acc[0], outer[0], nx, mu[0],
                                   voff, a_src, a_dst);
-        else if (LEVELS && s0.lv == 2 && (DIAG & 1073741824) && nvalid && s1.lv == 2)
-            x3_half<NC, FRESH, DIAG, kPieces, 2, true>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff,
-                                                       a_src, a_dst, is_loader, np2);
-        else if (LEVELS && s0.lv == 2)
-            x3_half<NC, FRESH, DIAG, kPieces, 2>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
-                                                 a_dst, is_loader, np2);
-        else if (LEVELS && s0.lv == 1 && (DIAG & 1073741824) && (DIAG & 524288) && nvalid && s1.lv == 2)
-            x3_half<NC, FRESH, DIAG, kPieces, 1, true>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff,
-                                                       a_src, a_dst, is_loader, np2);
-        else if (LEVELS && s0.lv == 1)
-            x3_half<NC, FRESH, DIAG, kPieces, 1>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
-                                                 a_dst, is_loader, np2);
-        else
-            x3_half<NC, FRESH, DIAG, kPieces>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
-                                              a_dst, is_loader, np2);
+        else {
+            // the body by the tile's level, the next step's, and whether the
+            // next step is the mean's row block (all uniform: one branch here,
+            // none inside the body's MFMA region)
+            // (DIAG & 2^31: the one-product bodies by the mean test, at compile time)
+            constexpr bool MSPLIT = (DIAG & 2147483648LL) != 0;
+            if (LEVELS && s0.lv == 2 && (DIAG & 1073741824) && nvalid && s1.lv == 2) {
+                if (MSPLIT && msc == 0.0f)
+                    x3_half<NC, FRESH, DIAG, kPieces, 2, true, 0>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx,
+                                                                  mu, voff, a_src, a_dst, is_loader, np2);
+                else
+                    x3_half<NC, FRESH, DIAG, kPieces, 2, true, MSPLIT ? 1 : -1>(pa, pcn, xq, yq, g, cexp, msc, kb, acc,
+                                                                               outer, nx, mu, voff, a_src, a_dst,
+                                                                               is_loader, np2);
+            } else if (LEVELS && s0.lv == 2) {
+                if (MSPLIT && msc == 0.0f)
+                    x3_half<NC, FRESH, DIAG, kPieces, 2, false, 0>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx,
+                                                                   mu, voff, a_src, a_dst, is_loader, np2);
+                else
+                    x3_half<NC, FRESH, DIAG, kPieces, 2, false, MSPLIT ? 1 : -1>(pa, pcn, xq, yq, g, cexp, msc, kb,
+                                                                                acc, outer, nx, mu, voff, a_src,
+                                                                                a_dst, is_loader, np2);
+            } else if (LEVELS && s0.lv == 1 && (DIAG & 1073741824) && (DIAG & 524288) && nvalid && s1.lv == 2)
+                x3_half<NC, FRESH, DIAG, kPieces, 1, true>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff,
+                                                           a_src, a_dst, is_loader, np2);
+            else if (LEVELS && s0.lv == 1)
+                x3_half<NC, FRESH, DIAG, kPieces, 1>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff,
+                                                     a_src, a_dst, is_loader, np2);
+            else
+                x3_half<NC, FRESH, DIAG, kPieces>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
+                                                  a_dst, is_loader, np2);
+        }
         if constexpr (STAMP) SBO_STAMP(t2);
         if (!FRESH && (s0.flags & kLast)) {
             // item done: column sums of V^2 over its rows (lanes l, l+16, l+32,
@@ -1017,6 +1047,10 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 55: SBO_X3_LAUNCH(1, 73776 + 33554432); break;  // variant 3 without the kh-only split (the default before it)
         case 56: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 524288); break;  // variant 3, kh-only split from three-product steps too (slower)
         case 57: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824); break;  // variant 3 reading sf2 alpha before every step (the default before)
+        case 60: SBO_X3_LAUNCH(2, 73776 + 33554432 + 1073741824 + 67108864); break;  // variant 3's options, four waves of 32 queries (one per SIMD)
+        case 61: SBO_X3_LAUNCH(2, 73776 + 33554432 + 67108864); break;  //   without the kh-only split bodies
+        case 59: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 4294967296LL); break;  // variant 3, mean terms by a select (no branch)
+        case 58: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 67108864 + 2147483648LL); break;  // variant 3, one-product bodies split by the mean test at compile time
 #endif
         default: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 67108864); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead, next coordinates at ph 1, kh-only split between one-product steps, sf2 alpha read only before the mean's row block
     }

@@ -75,35 +75,67 @@ int64_t info_slots(int64_t n) { return std::max<int64_t>(64, n / 512 + 2); }
 //     X21[p, :] = -Cinv[p, 0:p1] S[0:p1, :]       (row panels p of C^-1)
 // Each panel's diagonal block is multiplied in full; its strictly upper part
 // is zero (widen() writes it, neither rocSOLVER nor this recursion touches
-// it).  S: (n - h) x h doubles of scratch at the top level, reused below.
-sbo_status inverse_lower_f64(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld, double *S, int &slot) {
-    constexpr int64_t kBase = 2048;
-    if (n <= kBase) {
-        rocblas_int *info = ctx->info.as<rocblas_int>() + 1 + slot++;
-        SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
-                                  (rocblas_int)ld, info));
-        return SBO_OK;
-    }
-    const int64_t h = sbo::round_up(n / 2, 128), m = n - h;
-    double *B = Li + h, *C = Li + h + h * ld;
-    if (sbo_status st = inverse_lower_f64(ctx, Li, h, ld, S, slot); st != SBO_OK) return st;
-    if (sbo_status st = inverse_lower_f64(ctx, C, m, ld, S, slot); st != SBO_OK) return st;
-    SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
-    const double one = 1.0, minus_one = -1.0, zero = 0.0;
+// it).  The first half (A^-1, then S) reads only the factor's left h
+// columns, so the fit can run it beside the Cholesky's last steps
+// (blocked_potrf, SBO_OPT_INV_OVERLAP); the second half (C^-1, X21) follows
+// the factor.  S: (n - h) x h doubles of scratch, C^-1's own scratch after
+// it (inverse_scratch).  hb: the rocBLAS handle (and so the stream) to run on;
+// slot: the next free info slot (one per dtrtri base case).
+constexpr int64_t kInvBase = 2048;
+int64_t inverse_split(int64_t n) { return sbo::round_up(n / 2, 128); }
+
+int64_t inverse_scratch(int64_t n) {
+    if (n <= kInvBase) return 0;
+    const int64_t h = inverse_split(n), m = n - h;
+    return h * m + std::max(inverse_scratch(h), inverse_scratch(m));
+}
+
+sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
+                             int &slot);
+
+sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
+                              int &slot) {
+    const int64_t h = inverse_split(n), m = n - h;
+    if (sbo_status st = inverse_lower_f64(ctx, hb, Li, h, ld, S + h * m, slot); st != SBO_OK) return st;
+    SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
+    const double one = 1.0, zero = 0.0;
     const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / 8, 128));
     for (int64_t p0 = 0; p0 < h; p0 += nb) {
         const int64_t w = std::min(nb, h - p0);
-        SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)m,
-                               (rocblas_int)w, (rocblas_int)(h - p0), &one, B + p0 * ld, (rocblas_int)ld,
-                               Li + p0 + p0 * ld, (rocblas_int)ld, &zero, S + p0 * m, (rocblas_int)m));
-    }
-    for (int64_t p0 = 0; p0 < m; p0 += nb) {
-        const int64_t w = std::min(nb, m - p0);
-        SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)w,
-                               (rocblas_int)h, (rocblas_int)(p0 + w), &minus_one, C + p0, (rocblas_int)ld, S,
-                               (rocblas_int)m, &zero, B + p0, (rocblas_int)ld));
+        SBO_BLAS(rocblas_dgemm(hb, rocblas_operation_none, rocblas_operation_none, (rocblas_int)m, (rocblas_int)w,
+                               (rocblas_int)(h - p0), &one, Li + h + p0 * ld, (rocblas_int)ld, Li + p0 + p0 * ld,
+                               (rocblas_int)ld, &zero, S + p0 * m, (rocblas_int)m));
     }
     return SBO_OK;
+}
+
+sbo_status inverse_second_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
+                               int &slot) {
+    const int64_t h = inverse_split(n), m = n - h;
+    double *B = Li + h, *C = Li + h + h * ld;
+    if (sbo_status st = inverse_lower_f64(ctx, hb, C, m, ld, S + h * m, slot); st != SBO_OK) return st;
+    SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
+    const double minus_one = -1.0, zero = 0.0;
+    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / 8, 128));
+    for (int64_t p0 = 0; p0 < m; p0 += nb) {
+        const int64_t w = std::min(nb, m - p0);
+        SBO_BLAS(rocblas_dgemm(hb, rocblas_operation_none, rocblas_operation_none, (rocblas_int)w, (rocblas_int)h,
+                               (rocblas_int)(p0 + w), &minus_one, C + p0, (rocblas_int)ld, S, (rocblas_int)m, &zero,
+                               B + p0, (rocblas_int)ld));
+    }
+    return SBO_OK;
+}
+
+sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
+                             int &slot) {
+    if (n <= kInvBase) {
+        rocblas_int *info = ctx->info.as<rocblas_int>() + 1 + slot++;
+        SBO_BLAS(rocsolver_dtrtri(hb, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
+                                  (rocblas_int)ld, info));
+        return SBO_OK;
+    }
+    if (sbo_status st = inverse_first_half(ctx, hb, Li, n, ld, S, slot); st != SBO_OK) return st;
+    return inverse_second_half(ctx, hb, Li, n, ld, S, slot);
 }
 
 sbo_status check_hyper(sbo_ctx *ctx, const sbo_hyper &h) {
@@ -352,7 +384,17 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                       sizeof(float) * old_tiles * sbo::kTileFloats));
     SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
     rocblas_int hinfo = 0;
-    SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int) * (size_t)nslots, ctx->stream));
+    // the inverse's first half ran beside the Cholesky (blocked_potrf): its
+    // info slots 1 .. inv_slot stay, the rest are cleared
+    const bool early = ctx->inverse_bits == 64 && ctx->inverse_rec && !incr && ctx->early_inv_n == n;
+    ctx->early_inv_n = 0;
+    if (early) {
+        SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), ctx->stream));
+        SBO_HIP(hipMemsetAsync(info + 1 + ctx->inv_slot, 0, sizeof(rocblas_int) * (size_t)(nslots - 1 - ctx->inv_slot),
+                               ctx->stream));
+    } else {
+        SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int) * (size_t)nslots, ctx->stream));
+    }
     if (ctx->inverse_bits == 64) {
         double *Li = ctx->Linv.as<double>();
         if (incr) {
@@ -386,14 +428,26 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         } else {
             SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)ld * (size_t)ld));
             Li = ctx->Linv.as<double>();
-            SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
-            if (ctx->inverse_rec) {
-                const int64_t h = sbo::round_up(n / 2, 128);
-                SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max<int64_t>(h * (n - h), 1)));
+            if (early) {
+                // A^-1 and S = B A^-1 are done: widen the right columns (their
+                // rows 0..h-1 zero), then C^-1 and X21 = -C^-1 S
+                const int64_t h = inverse_split(n);
+                SBO_HIP(sbo::launch_widen(ctx->stream, L + h + h * ld, ld, n - h, n - h, true, Li + h + h * ld, ld));
+                SBO_HIP(hipMemset2DAsync(Li + h * ld, sizeof(double) * (size_t)ld, 0, sizeof(double) * (size_t)h,
+                                         (size_t)(n - h), ctx->stream));
+                int slot = ctx->inv_slot;
+                if (sbo_status st = inverse_second_half(ctx, ctx->blas, Li, n, ld, ctx->scratch.as<double>(), slot);
+                    st != SBO_OK)
+                    return st;
+            } else if (ctx->inverse_rec) {
+                SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
+                SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max<int64_t>(inverse_scratch(n), 1)));
                 int slot = 0;
-                if (sbo_status st = inverse_lower_f64(ctx, Li, n, ld, ctx->scratch.as<double>(), slot); st != SBO_OK)
+                if (sbo_status st = inverse_lower_f64(ctx, ctx->blas, Li, n, ld, ctx->scratch.as<double>(), slot);
+                    st != SBO_OK)
                     return st;
             } else {
+                SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
                 SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n,
                                           Li, (rocblas_int)ld, info));
             }
@@ -593,8 +647,52 @@ sbo_status probe_precision(sbo_ctx *ctx) {
 // of step k waits for step k's panel; the next block column of step k + 1
 // waits for the rest of step k (which also wrote that column).  info:
 // rocSOLVER's.
-sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_int *info) {
+//
+// early_inv (a fit with the recursive f64 inverse and SBO_OPT_INV_OVERLAP =
+// R > 0): once the panel of the block column that ends at h =
+// inverse_split(n) is done, the factor's left h columns are final, and the
+// inverse's first half (widen them, A^-1, S = B A^-1: half its flops) runs on
+// inv_stream with its own rocBLAS handle beside the Cholesky's last steps,
+// which leave most CUs idle (one-workgroup diagonal blocks, small trailing
+// updates).  inv_stream is CU-masked to leave R CUs to the chain, whose
+// kernels would otherwise queue behind the long dgemm workgroups.
+// refresh_operand finishes the inverse (early_inv_n).
+sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_int *info, bool early_inv = false) {
     SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), ctx->stream));
+    ctx->early_inv_n = 0;
+    const bool early = early_inv && ctx->inv_overlap > 0 && n > kInvBase;
+    const int64_t h_inv = early ? inverse_split(n) : -1;
+    bool early_pending = false;
+    if (early) {
+        if (ctx->inv_stream && ctx->inv_reserved != ctx->inv_overlap) {
+            SBO_HIP(hipStreamSynchronize(ctx->inv_stream));
+            SBO_HIP(hipStreamDestroy(ctx->inv_stream));
+            ctx->inv_stream = nullptr;
+        }
+        if (!ctx->inv_stream) {
+            std::vector<uint32_t> mask((size_t)(ctx->num_cu + 31) / 32, 0u);
+            for (int c = ctx->inv_overlap; c < ctx->num_cu; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+            SBO_HIP(hipExtStreamCreateWithCUMask(&ctx->inv_stream, (uint32_t)mask.size(), mask.data()));
+            ctx->inv_reserved = ctx->inv_overlap;
+            if (ctx->blas_inv) SBO_BLAS(rocblas_set_stream(ctx->blas_inv, ctx->inv_stream));
+        }
+        if (!ctx->ev_half) {
+            SBO_HIP(hipEventCreateWithFlags(&ctx->ev_half, hipEventDisableTiming));
+            SBO_HIP(hipEventCreateWithFlags(&ctx->ev_inv, hipEventDisableTiming));
+        }
+        if (!ctx->blas_inv) {
+            SBO_BLAS(rocblas_create_handle(&ctx->blas_inv));
+            SBO_BLAS(rocblas_set_stream(ctx->blas_inv, ctx->inv_stream));
+        }
+        // every buffer the first half touches, sized before it starts (a
+        // reserve that reallocates later would free memory in use)
+        SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)ld * (size_t)ld));
+        SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max<int64_t>(inverse_scratch(n), 1)));
+        const int64_t nslots = info_slots(n);
+        SBO_HIP(ctx->info.reserve(sizeof(rocblas_int) * (size_t)nslots));
+        info = ctx->info.as<rocblas_int>();
+        SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int) * (size_t)nslots, ctx->stream));
+    }
     SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
     if (ctx->aux_stream && ctx->aux_reserved != ctx->chol_reserve) {  // another CU mask: a new aux stream
         SBO_HIP(hipStreamSynchronize(ctx->aux_stream));
@@ -642,6 +740,22 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
             st = SBO_E_DEVICE;
             break;
         }
+        if (k + kb == h_inv) {
+            // the left h columns are final: the inverse's first half on inv_stream
+            if (hipEventRecord(ctx->ev_half, ctx->stream) != hipSuccess ||
+                hipStreamWaitEvent(ctx->inv_stream, ctx->ev_half, 0) != hipSuccess ||
+                sbo::launch_widen(ctx->inv_stream, L, ld, n, h_inv, true, ctx->Linv.as<double>(), ld) != hipSuccess) {
+                st = SBO_E_DEVICE;
+                break;
+            }
+            early_pending = true;
+            int slot = 0;
+            if ((st = inverse_first_half(ctx, ctx->blas_inv, ctx->Linv.as<double>(), n, ld, ctx->scratch.as<double>(),
+                                         slot)) != SBO_OK)
+                break;
+            ctx->inv_slot = slot;
+            if (hipEventRecord(ctx->ev_inv, ctx->inv_stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
+        }
         if (hipEventRecord(ctx->ev_panel, ctx->stream) != hipSuccess ||
             (trail_pending && hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0) != hipSuccess)) { st = SBO_E_DEVICE; break; }
         if (rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m2,
@@ -661,17 +775,25 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
     }
     if (st != SBO_OK) {
         (void)hipStreamSynchronize(ctx->aux_stream);
+        if (early_pending) (void)hipStreamSynchronize(ctx->inv_stream);
         ctx->err = "blocked Cholesky: a rocBLAS or HIP call failed";
         return st;
     }
     if (trail_pending) SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
+    if (early_pending) {
+        SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_inv, 0));
+        ctx->early_inv_n = n;
+    }
     return SBO_OK;
 }
 
 sbo_status factor_and_refresh(sbo_ctx *ctx) {
     rocblas_int *info = ctx->info.as<rocblas_int>();
     if (ctx->chol_blocked) {
-        if (sbo_status st = blocked_potrf(ctx, ctx->L.as<float>(), ctx->n, ctx->cap, info); st != SBO_OK) return st;
+        const bool early_inv = ctx->inverse_bits == 64 && ctx->inverse_rec;
+        if (sbo_status st = blocked_potrf(ctx, ctx->L.as<float>(), ctx->n, ctx->cap, info, early_inv); st != SBO_OK)
+            return st;
+        info = ctx->info.as<rocblas_int>();   // (blocked_potrf may have grown it)
     } else {
         SBO_BLAS(rocsolver_spotrf(ctx->blas, rocblas_fill_lower, (rocblas_int)ctx->n, ctx->L.as<float>(),
                                   (rocblas_int)ctx->cap, info));
@@ -948,6 +1070,11 @@ SBO_API void sbo_destroy(sbo_ctx *ctx) {
     if (ctx->ev_trail) (void)hipEventDestroy(ctx->ev_trail);
     if (ctx->blas_aux) rocblas_destroy_handle(ctx->blas_aux);
     if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
+    if (ctx->inv_stream) (void)hipStreamSynchronize(ctx->inv_stream);
+    if (ctx->ev_half) (void)hipEventDestroy(ctx->ev_half);
+    if (ctx->ev_inv) (void)hipEventDestroy(ctx->ev_inv);
+    if (ctx->blas_inv) rocblas_destroy_handle(ctx->blas_inv);
+    if (ctx->inv_stream) (void)hipStreamDestroy(ctx->inv_stream);
     if (ctx->blas) rocblas_destroy_handle(ctx->blas);
     if (ctx->host_key) (void)hipHostFree(ctx->host_key);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
@@ -1453,6 +1580,11 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             SBO_CHECK(sbo::variant_allowed((int)value), SBO_E_INVAL,
                       "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22)");
             ctx->kernel_variant = (int)value;
+            return SBO_OK;
+        case SBO_OPT_INV_OVERLAP:
+            SBO_CHECK(value >= 0 && value < ctx->num_cu, SBO_E_INVAL,
+                      "SBO_OPT_INV_OVERLAP must be in [0, compute units)");
+            ctx->inv_overlap = (int)value;
             return SBO_OK;
         case SBO_OPT_CHOL_RESERVE:
             SBO_CHECK(value >= 0 && value < ctx->num_cu, SBO_E_INVAL,

@@ -99,6 +99,14 @@ struct sbo_ctx {
     int chol_reserve = 0;        // SBO_OPT_CHOL_RESERVE: CUs the trailing updates leave free (CU-masked aux stream)
     int aux_reserved = 0;        // the mask the current aux stream was created with
     hipEvent_t ev_panel = nullptr, ev_trail = nullptr;
+    // the recursive inverse's first half beside the Cholesky's last steps
+    // (SBO_OPT_INV_OVERLAP = R > 0: on inv_stream, CU-masked to leave R CUs free)
+    hipStream_t inv_stream = nullptr;
+    rocblas_handle blas_inv = nullptr;
+    int inv_overlap = 0, inv_reserved = 0;
+    hipEvent_t ev_half = nullptr, ev_inv = nullptr;
+    int64_t early_inv_n = 0;     // n of a factor whose inverse's first half is done (refresh_operand finishes it)
+    int inv_slot = 0;            // info slots the first half used (1 .. inv_slot)
     std::string err;
 
     // fitted model
@@ -274,14 +282,14 @@ constexpr int kLevelShift = 14;
 // its item (kRecFirst, kRecLast).
 constexpr int kRecFirst = 1 << 20, kRecLast = 1 << 21;
 // the split sweeps that honour the plan's precision levels
-inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39 || variant == 41 || variant == 42 || variant == 43 || variant == 46 || variant == 47 || variant == 48 || variant == 49 || variant == 51 || variant == 52 || variant == 53 || variant == 54 || variant == 55 || variant == 56 || variant == 57; }
+inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39 || variant == 41 || variant == 42 || variant == 43 || variant == 46 || variant == 47 || variant == 48 || variant == 49 || variant == 51 || variant == 52 || variant == 53 || variant == 54 || variant == 55 || variant == 56 || variant == 57 || (variant >= 58 && variant <= 61); }
 // Sweeps the product library accepts (all compute the full result; 3 is the
 // default).  The timing diagnostics (parts of the work left out, forced
 // precision levels, phase stamps) exist only in the diagnostic build
 // (-DSBO_DIAG, lib/libsbo_diag.so, selected by SBO_LIB for tools/).
 inline bool variant_allowed(int v) {
 #ifdef SBO_DIAG
-    return v >= 0 && v <= 57;
+    return v >= 0 && v <= 61;
 #else
     return v == 0 || v == 1 || v == 2 || v == 3 || v == 9 || v == 10 || v == 13 || v == 22;
 #endif

@@ -942,6 +942,45 @@ def test_recursive_inverse_matches_dtrtri(mapper, n):
     assert np.abs(got[0] - got[1]).max() <= 2e-6 * np.abs(got[0]).max()
 
 
+@pytest.mark.parametrize("n", [4100, 5000])
+def test_inverse_overlap_is_bitwise(mapper, n):
+    """SBO_OPT_INV_OVERLAP = R: the recursive inverse's first half runs beside
+    the Cholesky's last steps on a CU-masked stream.  The inverse, alpha and
+    the posterior are bitwise those of the serial fit for every R; a NOT_SPD
+    fit with the overlap on reports the error and leaves the context usable."""
+    wl = synthetic(n, 24, 20, seed=n + 11)
+    got = {}
+    for ov in (0, 32, 128, 0):
+        gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+        gm.set_option(N.SBO_OPT_INV_OVERLAP, ov)
+        gm.fit(wl.x, wl.y, wl.obs)
+        A = np.zeros((n, n), np.float32)
+        gm.ctx.check(N.lib().sbo_get_inverse(gm.ctx.handle, A.ctypes.data))
+        L, alpha = gm.factor()
+        mu, sd = gm.predict(wl.qx, wl.qy)
+        if ov in got:
+            assert np.array_equal(got[ov][0], A)
+        got[ov] = (A, alpha, mu, sd)
+    for ov in (32, 128):
+        for a, b in zip(got[0], got[ov]):
+            assert np.array_equal(a, b), ov
+    omu, ovar = oracle_given_factor(gm, wl)
+    assert nrel(mu, omu) < REL_TOL and nrel(sd.astype(np.float64) ** 2, ovar) < REL_TOL
+    # a singular K (duplicated point, no noise) with the overlap on
+    x, y = f32(wl.x).copy(), f32(wl.y).copy()
+    x[n - 7], y[n - 7] = x[5], y[5]
+    bad = TerrainMapper(0, Hyper(noise_level=0.0), ctx=mapper.ctx)
+    bad.set_option(N.SBO_OPT_INV_OVERLAP, 64)
+    with pytest.raises(N.NotSPDError):
+        bad.fit(x, y, wl.obs)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_INV_OVERLAP, 64)
+    gm.fit(wl.x, wl.y, wl.obs)
+    mu2, sd2 = gm.predict(wl.qx, wl.qy)
+    assert np.array_equal(mu2, got[0][2]) and np.array_equal(sd2, got[0][3])
+    gm.set_option(N.SBO_OPT_INV_OVERLAP, 0)
+
+
 # ------------------------------------------------------ full-size properties
 def test_c3_properties(dev):
     """N=8192 with a 1024x1024 grid (C3): properties that hold at any size --

@@ -17,12 +17,14 @@ def main():
     p.add_argument("--chol", type=int, nargs="+", default=[1], help="SBO_OPT_CHOLESKY values to time (1 own, 0 rocSOLVER)")
     p.add_argument("--inv", type=int, nargs="+", default=[1], help="SBO_OPT_INVERSE values to time (1 own recursion, 0 rocSOLVER dtrtri)")
     p.add_argument("--reserve", type=int, nargs="+", default=[0], help="SBO_OPT_CHOL_RESERVE values to time")
+    p.add_argument("--overlap", type=int, nargs="+", default=[0], help="SBO_OPT_INV_OVERLAP values to time")
     a = p.parse_args()
     import torch
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
     dev = torch.device("cuda:0")
     from safe_bayesian_optimization_amd import _native as N
-    for n, ch, inv, rsv in [(n, c, i, r) for n in a.n for c in a.chol for i in a.inv for r in a.reserve]:
+    for n, ch, inv, rsv, ov in [(n, c, i, r, o) for n in a.n for c in a.chol for i in a.inv for r in a.reserve
+                                for o in a.overlap]:
         wl = synthetic(n, 64, 64, seed=0)
         t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
         X, Y, O = t(wl.x), t(wl.y), t(wl.obs)
@@ -30,6 +32,7 @@ def main():
         gm.set_option(N.SBO_OPT_CHOLESKY, ch)
         gm.set_option(N.SBO_OPT_INVERSE, inv)
         gm.set_option(N.SBO_OPT_CHOL_RESERVE, rsv)
+        gm.set_option(N.SBO_OPT_INV_OVERLAP, ov)
         ts = []
         for _ in range(a.reps + 1):
             torch.cuda.synchronize()
@@ -37,7 +40,7 @@ def main():
             gm.fit(X, Y, O)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
-        print(f"N={n} cholesky={ch} inverse={'own recursion' if inv else 'rocSOLVER dtrtri'} reserve={rsv}: first fit {ts[0]:.1f} ms, warm refits {', '.join(f'{v:.1f}' for v in ts[1:])} ms", flush=True)
+        print(f"N={n} cholesky={ch} inverse={'own recursion' if inv else 'rocSOLVER dtrtri'} reserve={rsv} overlap={ov}: first fit {ts[0]:.1f} ms, warm refits {', '.join(f'{v:.1f}' for v in ts[1:])} ms", flush=True)
         gm.close()
 
 
