@@ -371,6 +371,16 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * stream that leaves this many CUs to the factorization's latency-bound
  * chain.  Results do not depend on it (bitwise). */
 #define SBO_OPT_INV_OVERLAP 14
+/* SBO_OPT_CHOL_OUTER (columns, default 512; a multiple of 128 in [128, 4096]):
+ * the blocked Cholesky's outer panel.  Each outer panel is factored by the
+ * 128-column chain with its updates kept inside the panel, and the rest of
+ * the trailing matrix takes one rank-512 update per outer panel; 128 is the
+ * one-level factorization (a rank-128 update per 128 columns). */
+#define SBO_OPT_CHOL_OUTER 15
+/* SBO_OPT_CHOL_DIAG (default 1): the blocked Cholesky's 128 x 128 diagonal
+ * blocks by 16-column panels with matrix-core trailing updates (1) or by the
+ * 8-column VALU kernel (0); the factor is bitwise the same. */
+#define SBO_OPT_CHOL_DIAG 16
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe

@@ -48,6 +48,8 @@ SBO_OPT_PRECISION = 11
 SBO_OPT_RESORT = 12
 SBO_OPT_CHOL_RESERVE = 13
 SBO_OPT_INV_OVERLAP = 14
+SBO_OPT_CHOL_OUTER = 15
+SBO_OPT_CHOL_DIAG = 16
 
 
 class SboError(RuntimeError):

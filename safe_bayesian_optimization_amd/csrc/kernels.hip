@@ -308,6 +308,146 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, i
     SBO_CSTAMP(3);
 }
 
+// The same diagonal block in 16-column panels with the trailing updates on
+// the matrix cores (chol_diag_kernel's default replacement).  The block is
+// padded to 128 x 128 with the identity (pivots 1, zero coupling: the real
+// part sees exactly the arithmetic of the kb x kb factorization).  Panel:
+// wave 0 in registers, as above (16 columns).  Trailing update: the lower
+// triangle of 16 x 16 blocks behind the panel, spread over the four waves,
+// each block C -= L_i L_l^T as four v_mfma_f32_16x16x4_f32 over the panel's
+// 16 columns -- an MFMA is bit for bit a k-ordered fmaf chain
+// (cdna_hip_programming.md section 3), so every element still sees
+// fmaf(-L[i][j], L[l][j], a) with j ascending and the factor is bitwise that
+// of chol_diag_kernel.  The block in: all 64 loads per thread in flight;
+// out: 64 stores per thread issued back to back.
+constexpr int kCholPW = 16;
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void chol_diag_mfma_kernel(float *__restrict__ A, int64_t ld, int kb, int64_t k0,
+                                                             int *__restrict__ info) {
+    static_assert(kCholNB == 128, "two panel rows per lane of wave 0, 8 x 16 blocks");
+    __shared__ __attribute__((aligned(16))) float a[kCholNB][kCholNB + 4];
+    __shared__ int s_bad;
+    if (*info != 0) return;
+    SBO_CSTAMP(0);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // thread (i, h): row i = tid & 127 of columns h, h + 2, h + 4, ... (coalesced
+    // over i), 16 loads in flight per batch
+    // (every load unconditional, from inside the kb x kb block: the rows and
+    // columns past kb read its last row / column and are replaced after)
+    const int li = tid & (kCholNB - 1), lh = tid >> 7;
+    const float *colp = A + min(li, kb - 1);
+    for (int j0 = 0; j0 < kCholNB; j0 += 32) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = colp[(int64_t)min(j0 + 2 * u + lh, kb - 1) * ld];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int j = j0 + 2 * u + lh;
+            a[li][j] = (li < kb && j < kb && li >= j) ? v[u] : (li == j ? 1.0f : 0.0f);
+        }
+    }
+    if (tid == 0) s_bad = 0;
+    __syncthreads();
+    SBO_CSTAMP(1);
+#ifdef SBO_CHOL_STAMPS
+    if (threadIdx.x == 0) { g_chol_stamps[4] = 0; g_chol_stamps[5] = 0; }
+#endif
+    for (int jb = 0; jb < kCholNB; jb += kCholPW) {
+#ifdef SBO_CHOL_STAMPS
+        const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+#endif
+        if (wave == 0) {
+            const int r0 = jb + lane, r1 = jb + 64 + lane;
+            const int q0 = min(r0, kCholNB - 1), q1 = min(r1, kCholNB - 1);
+            float p0[kCholPW], p1[kCholPW];
+#pragma unroll
+            for (int c4 = 0; c4 < kCholPW / 4; ++c4) {
+                const float4 u0 = reinterpret_cast<const float4 *>(&a[q0][jb])[c4];
+                const float4 u1 = reinterpret_cast<const float4 *>(&a[q1][jb])[c4];
+                p0[4 * c4] = u0.x; p0[4 * c4 + 1] = u0.y; p0[4 * c4 + 2] = u0.z; p0[4 * c4 + 3] = u0.w;
+                p1[4 * c4] = u1.x; p1[4 * c4 + 1] = u1.y; p1[4 * c4 + 2] = u1.z; p1[4 * c4 + 3] = u1.w;
+            }
+            int bad = 0;
+#pragma unroll
+            for (int c = 0; c < kCholPW; ++c) {
+                // (no early exit inside the unrolled panel: a failed pivot is
+                // recorded and the rest of the panel computes garbage that the
+                // block never stores)
+                const int j = jb + c;
+                const float djj = lane_value(p0[c], c);   // row j is lane c's first row
+                if (bad == 0 && (!(djj > 0.0f) || !(djj < __builtin_huge_valf()))) bad = j + 1;
+                // every lane, no row tests: the lanes above the diagonal
+                // (row < column) compute values of the upper triangle that
+                // nothing reads (the lane-mask per column and row would be
+                // 136 live SGPR pairs); the diagonal lane's p0[c] is djj, so
+                // L_jj = djj * rs there
+                const float rs = __builtin_amdgcn_rsqf(djj);
+                p0[c] = p0[c] * rs;
+                p1[c] = p1[c] * rs;
+#pragma unroll
+                for (int c2 = c + 1; c2 < kCholPW; ++c2) {
+                    const float lc2 = lane_value(p0[c], c2);   // L[jb + c2][j], lane c2's (already scaled)
+                    p0[c2] = fmaf(-p0[c], lc2, p0[c2]);
+                    p1[c2] = fmaf(-p1[c], lc2, p1[c2]);
+                }
+            }
+            if (r0 < kCholNB) {
+#pragma unroll
+                for (int c = 0; c < kCholPW; ++c) a[r0][jb + c] = p0[c];
+            }
+            if (r1 < kCholNB) {
+#pragma unroll
+                for (int c = 0; c < kCholPW; ++c) a[r1][jb + c] = p1[c];
+            }
+            if (lane == 0 && bad) s_bad = bad;
+        }
+        __syncthreads();
+        SBO_CSTAMP_ADD(4, tp0);
+        if (s_bad) break;
+#ifdef SBO_CHOL_STAMPS
+        const unsigned long long tu0 = __builtin_amdgcn_s_memtime();
+#endif
+        // rank-16 update of the trailing lower triangle, 16 x 16 blocks
+        const int t0 = jb + kCholPW, nbt = (kCholNB - t0) / 16, nblk = nbt * (nbt + 1) / 2;
+        const int fi = lane & 15, fk = lane >> 4;   // operand lane map: A[fi][fk], B[fk][fi]; C row 4 fk + v, col fi
+        for (int q = wave; q < nblk; q += 4) {
+            int bi = 0, r = q;
+            while (r > bi) { r -= bi + 1; ++bi; }
+            const int i0 = t0 + 16 * bi, l0 = t0 + 16 * r;
+            f32x4_t acc;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[v] = a[i0 + 4 * fk + v][l0 + fi];
+#pragma unroll
+            for (int kk = 0; kk < kCholPW / 4; ++kk) {
+                const float av = -a[i0 + fi][jb + 4 * kk + fk];
+                const float bv = a[l0 + fi][jb + 4 * kk + fk];
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) a[i0 + 4 * fk + v][l0 + fi] = acc[v];
+        }
+        __syncthreads();
+        SBO_CSTAMP_ADD(5, tu0);
+    }
+    SBO_CSTAMP(2);
+    if (s_bad) {
+        if (tid == 0) atomicCAS(info, 0, (int)(k0 + s_bad));
+        return;
+    }
+    float *colw = A + li + (int64_t)lh * ld;
+    for (int j0 = 0; j0 < kCholNB; j0 += 32) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = a[li][j0 + 2 * u + lh];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int j = j0 + 2 * u + lh;
+            if (li < kb && j < kb && li >= j) colw[(int64_t)(j0 + 2 * u) * ld] = v[u];
+        }
+    }
+    SBO_CSTAMP(3);
+}
+
 // The blocked Cholesky's panel (a2): A21 := A21 L11^-T for the m2 x kb panel
 // below a factored kb x kb diagonal block (rocBLAS strsm right / lower /
 // transpose ran as ~10 launches, ~100 us per step, on the factorization's
@@ -1917,9 +2057,12 @@ hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t 
     return hipGetLastError();
 }
 
-hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info) {
+hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info, int version) {
     if (kb <= 0 || kb > kCholNB) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, s, A, ld, kb, k0, info);
+    if (version == 1)
+        hipLaunchKernelGGL(chol_diag_mfma_kernel, dim3(1), dim3(256), 0, s, A, ld, kb, k0, info);
+    else
+        hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, s, A, ld, kb, k0, info);
     return hipGetLastError();
 }
 

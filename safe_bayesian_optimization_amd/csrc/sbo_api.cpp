@@ -722,53 +722,91 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
     }
     SBO_BLAS(rocblas_set_pointer_mode(ctx->blas_aux, rocblas_pointer_mode_host));
     const float one = 1.0f, minus_one = -1.0f;
-    SBO_HIP(sbo::launch_chol_diag(ctx->stream, L, ld, (int)std::min<int64_t>(sbo::kCholNB, n), 0, info));
+    // Two levels (SBO_OPT_CHOL_OUTER = NB2 > kCholNB): outer panels of NB2
+    // columns, each factored by the kCholNB chain above with its updates kept
+    // inside the panel (one sgemm per inner step over the panel's remaining
+    // columns); the rest of the trailing matrix takes one rank-NB2 update per
+    // outer panel (k = 512: rocBLAS ssyrk at ~1.5x its k = 128 rate, and a
+    // quarter of the trailing matrix's HBM passes).  The look-ahead is the
+    // outer panel's: the next outer panel's columns first (sgemm on `stream`),
+    // the rest on aux_stream.  NB2 = kCholNB is the one-level factorization.
+    const int64_t NB = sbo::kCholNB;
+    const int64_t NB2 = std::max<int64_t>(NB, (int64_t)ctx->chol_outer / NB * NB);
+    // below this size the trailing update is one sgemm over the full square
+    // (rocBLAS ssyrk: 82 vs 49 us at m = 4000, 67 vs 20 at 2000, k = 128;
+    // tools/r3_gemm_probe.cpp); the upper triangle it also writes is never read
+    constexpr int64_t kSmallTrail = 6144;
     bool trail_pending = false;
     sbo_status st = SBO_OK;
-    for (int64_t k = 0; k < n; k += sbo::kCholNB) {
-        const int64_t kb = std::min<int64_t>(sbo::kCholNB, n - k);
-        const int64_t m2 = n - k - kb;
-        if (m2 <= 0) break;
-        float *L11 = L + k + k * ld, *A21 = L11 + kb;
-        const int64_t kb2 = std::min<int64_t>(sbo::kCholNB, m2);   // the next block column
-        float *C1 = L11 + kb + kb * ld;                             // its rows k + kb ..
-        if (ctx->chol_trsm_own) {
-            if (sbo::launch_chol_trsm(ctx->stream, L11, ld, (int)kb, A21, m2) != hipSuccess) { st = SBO_E_DEVICE; break; }
-        } else if (rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
-                                 rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11,
-                                 (rocblas_int)ld, A21, (rocblas_int)ld) != rocblas_status_success) {
-            st = SBO_E_DEVICE;
-            break;
-        }
-        if (k + kb == h_inv) {
-            // the left h columns are final: the inverse's first half on inv_stream
-            if (hipEventRecord(ctx->ev_half, ctx->stream) != hipSuccess ||
-                hipStreamWaitEvent(ctx->inv_stream, ctx->ev_half, 0) != hipSuccess ||
-                sbo::launch_widen(ctx->inv_stream, L, ld, n, h_inv, true, ctx->Linv.as<double>(), ld) != hipSuccess) {
+    for (int64_t K = 0; K < n && st == SBO_OK; K += NB2) {
+        const int64_t W = std::min(NB2, n - K);
+        for (int64_t k = K; k < K + W; k += NB) {
+            const int64_t kb = std::min<int64_t>(NB, n - k);
+            const int64_t m2 = n - k - kb;
+            float *L11 = L + k + k * ld, *A21 = L11 + kb;
+            if (sbo::launch_chol_diag(ctx->stream, L11, ld, (int)kb, k, info, ctx->chol_diag) != hipSuccess) {
                 st = SBO_E_DEVICE;
                 break;
             }
-            early_pending = true;
-            int slot = 0;
-            if ((st = inverse_first_half(ctx, ctx->blas_inv, ctx->Linv.as<double>(), n, ld, ctx->scratch.as<double>(),
-                                         slot)) != SBO_OK)
+            if (m2 <= 0) break;
+            if (ctx->chol_trsm_own) {
+                if (sbo::launch_chol_trsm(ctx->stream, L11, ld, (int)kb, A21, m2) != hipSuccess) { st = SBO_E_DEVICE; break; }
+            } else if (rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                                     rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11,
+                                     (rocblas_int)ld, A21, (rocblas_int)ld) != rocblas_status_success) {
+                st = SBO_E_DEVICE;
                 break;
-            ctx->inv_slot = slot;
-            if (hipEventRecord(ctx->ev_inv, ctx->inv_stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
+            }
+            if (k + kb == h_inv) {
+                // the left h columns are final: the inverse's first half on inv_stream
+                if (hipEventRecord(ctx->ev_half, ctx->stream) != hipSuccess ||
+                    hipStreamWaitEvent(ctx->inv_stream, ctx->ev_half, 0) != hipSuccess ||
+                    sbo::launch_widen(ctx->inv_stream, L, ld, n, h_inv, true, ctx->Linv.as<double>(), ld) != hipSuccess) {
+                    st = SBO_E_DEVICE;
+                    break;
+                }
+                early_pending = true;
+                int slot = 0;
+                if ((st = inverse_first_half(ctx, ctx->blas_inv, ctx->Linv.as<double>(), n, ld,
+                                             ctx->scratch.as<double>(), slot)) != SBO_OK)
+                    break;
+                ctx->inv_slot = slot;
+                if (hipEventRecord(ctx->ev_inv, ctx->inv_stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
+            }
+            // the outer panel's remaining columns (rows below this block)
+            const int64_t rem = K + W - (k + kb);
+            if (rem > 0 &&
+                rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m2,
+                              (rocblas_int)rem, (rocblas_int)kb, &minus_one, A21, (rocblas_int)ld, A21,
+                              (rocblas_int)ld, &one, L11 + kb + kb * ld, (rocblas_int)ld) != rocblas_status_success) {
+                st = SBO_E_DEVICE;
+                break;
+            }
         }
+        if (st != SBO_OK) break;
+        const int64_t m3 = n - K - W;
+        if (m3 <= 0) break;
+        const float *P = L + (K + W) + K * ld;   // the panel's rows below it: m3 x W
+        float *C1 = L + (K + W) + (K + W) * ld;
+        const int64_t W2 = std::min(NB2, m3);    // the next outer panel
         if (hipEventRecord(ctx->ev_panel, ctx->stream) != hipSuccess ||
             (trail_pending && hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0) != hipSuccess)) { st = SBO_E_DEVICE; break; }
-        if (rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m2,
-                          (rocblas_int)kb2, (rocblas_int)kb, &minus_one, A21, (rocblas_int)ld, A21, (rocblas_int)ld,
-                          &one, C1, (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
-        if (sbo::launch_chol_diag(ctx->stream, C1, ld, (int)kb2, k + kb, info) != hipSuccess) { st = SBO_E_DEVICE; break; }
-        const int64_t m3 = m2 - kb2;
+        if (rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m3,
+                          (rocblas_int)W2, (rocblas_int)W, &minus_one, P, (rocblas_int)ld, P, (rocblas_int)ld, &one, C1,
+                          (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
+        const int64_t m4 = m3 - W2;
         trail_pending = false;
-        if (m3 > 0) {
+        if (m4 > 0) {
             if (hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0) != hipSuccess) { st = SBO_E_DEVICE; break; }
-            if (rocblas_ssyrk(ctx->blas_aux, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)m3, (rocblas_int)kb,
-                              &minus_one, A21 + kb2, (rocblas_int)ld, &one, C1 + kb2 + kb2 * ld,
-                              (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
+            const rocblas_status bs =
+                m4 <= kSmallTrail
+                    ? rocblas_sgemm(ctx->blas_aux, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m4,
+                                    (rocblas_int)m4, (rocblas_int)W, &minus_one, P + W2, (rocblas_int)ld, P + W2,
+                                    (rocblas_int)ld, &one, C1 + W2 + W2 * ld, (rocblas_int)ld)
+                    : rocblas_ssyrk(ctx->blas_aux, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)m4,
+                                    (rocblas_int)W, &minus_one, P + W2, (rocblas_int)ld, &one, C1 + W2 + W2 * ld,
+                                    (rocblas_int)ld);
+            if (bs != rocblas_status_success) { st = SBO_E_DEVICE; break; }
             trail_pending = true;
             if (hipEventRecord(ctx->ev_trail, ctx->aux_stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
         }
@@ -1580,6 +1618,15 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             SBO_CHECK(sbo::variant_allowed((int)value), SBO_E_INVAL,
                       "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22)");
             ctx->kernel_variant = (int)value;
+            return SBO_OK;
+        case SBO_OPT_CHOL_DIAG:
+            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_CHOL_DIAG must be 0 or 1");
+            ctx->chol_diag = (int)value;
+            return SBO_OK;
+        case SBO_OPT_CHOL_OUTER:
+            SBO_CHECK(value >= sbo::kCholNB && value <= 4096 && value % sbo::kCholNB == 0, SBO_E_INVAL,
+                      "SBO_OPT_CHOL_OUTER must be a multiple of 128 in [128, 4096]");
+            ctx->chol_outer = (int)value;
             return SBO_OK;
         case SBO_OPT_INV_OVERLAP:
             SBO_CHECK(value >= 0 && value < ctx->num_cu, SBO_E_INVAL,

@@ -99,6 +99,8 @@ struct sbo_ctx {
     int chol_reserve = 0;        // SBO_OPT_CHOL_RESERVE: CUs the trailing updates leave free (CU-masked aux stream)
     int aux_reserved = 0;        // the mask the current aux stream was created with
     hipEvent_t ev_panel = nullptr, ev_trail = nullptr;
+    int chol_diag = 1;           // SBO_OPT_CHOL_DIAG: 1 the MFMA diagonal-block kernel, 0 the VALU one (bitwise equal)
+    int chol_outer = 512;        // SBO_OPT_CHOL_OUTER: outer panel width of the two-level Cholesky (128: one level)
     // the recursive inverse's first half beside the Cholesky's last steps
     // (SBO_OPT_INV_OVERLAP = R > 0: on inv_stream, CU-masked to leave R CUs free)
     hipStream_t inv_stream = nullptr;
@@ -312,7 +314,8 @@ hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int6
 // Blocked Cholesky: factor the kb x kb diagonal block at A (column-major,
 // lda = ld) of step k0 in place (kb <= kCholNB); info as rocSOLVER's.
 constexpr int kCholNB = 128;
-hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info);
+// version 1: chol_diag_mfma_kernel (16-column panels, MFMA trailing updates; default), 0: chol_diag_kernel
+hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info, int version = 1);
 // The panel below it: A21 (m2 x kb, lda ld) := A21 L11^-T (forward substitution, f32).
 hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb, float *A21, int64_t m2);
 // d = (double)in - v;  out = (float)d

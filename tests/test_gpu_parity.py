@@ -110,12 +110,16 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
     """The library's blocked Cholesky with its own panel solve
     (SBO_OPT_CHOLESKY = 1, default), with rocBLAS strsm panels (2), and
     rocSOLVER spotrf (0): all within the backward-error bound, factors equal
-    to f32 rounding, the same posterior to the contract."""
+    to f32 rounding, the same posterior to the contract.  The own
+    factorization in one level (SBO_OPT_CHOL_OUTER = 128) and in two (256,
+    1024; 512 default) too."""
     wl = synthetic(n, 24, 20, seed=n + 3)
     res = {}
-    for ch in (0, 2, 1):
+    for ch in (0, 2, (1, 128), (1, 256), (1, 1024), 1):
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
-        gm.set_option(N.SBO_OPT_CHOLESKY, ch)
+        outer = ch[1] if isinstance(ch, tuple) else 512
+        gm.set_option(N.SBO_OPT_CHOL_OUTER, outer)
+        gm.set_option(N.SBO_OPT_CHOLESKY, ch[0] if isinstance(ch, tuple) else ch)
         gm.fit(wl.x, wl.y, wl.obs)
         L, alpha = gm.factor()
         o = gm.order()
@@ -125,10 +129,29 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
         assert be <= 10 * n * EPS32, (ch, be)
         res[ch] = (L64, gm.predict(wl.qx, wl.qy))
     gm.set_option(N.SBO_OPT_CHOLESKY, 1)
-    for ch in (1, 2):   # own panel solve (default) and rocBLAS strsm panels, against spotrf
+    gm.set_option(N.SBO_OPT_CHOL_OUTER, 512)
+    for ch in (1, 2, (1, 128), (1, 256), (1, 1024)):   # own panel solve (default), rocBLAS strsm panels, one / two levels, against spotrf
         assert np.abs(res[0][0] - res[ch][0]).max() <= 1e-4 * np.abs(res[0][0]).max()
         assert nrel(res[ch][1][0], res[0][1][0].astype(np.float64)) < REL_TOL
         assert nrel(res[ch][1][1].astype(np.float64) ** 2, res[0][1][1].astype(np.float64) ** 2) < REL_TOL
+
+
+@pytest.mark.parametrize("n", [77, 300, 4100])
+def test_chol_diag_kernels_bitwise(mapper, n):
+    """The diagonal-block kernels (SBO_OPT_CHOL_DIAG 1: 16-column panels with
+    matrix-core trailing updates, 0: 8-column VALU panels) give the same
+    factor bit for bit: every element sees fmaf(-L[i][j], L[l][j], a) with j
+    ascending either way (an f32 MFMA is a k-ordered fmaf chain).  n = 77 and
+    300 end in a partial block (the identity padding)."""
+    wl = synthetic(n, 16, 12, seed=n + 5)
+    got = []
+    for dv in (0, 1):
+        gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+        gm.set_option(N.SBO_OPT_CHOL_DIAG, dv)
+        gm.fit(wl.x, wl.y, wl.obs)
+        got.append(gm.factor()[0])
+    gm.set_option(N.SBO_OPT_CHOL_DIAG, 1)
+    assert np.array_equal(got[0], got[1])
 
 
 def test_blocked_cholesky_not_spd_past_first_block(mapper):
@@ -137,10 +160,16 @@ def test_blocked_cholesky_not_spd_past_first_block(mapper):
     wl = synthetic(300, 8, seed=4)
     x, y = f32(wl.x), f32(wl.y)
     x[200], y[200] = x[10], y[10]          # a duplicated point with no noise: K singular
-    gm = TerrainMapper(0, Hyper(noise_level=0.0), ctx=mapper.ctx)
-    gm.set_option(N.SBO_OPT_CHOLESKY, 1)
-    with pytest.raises(N.NotSPDError):
-        gm.fit(x, y, wl.obs)
+    msgs = []
+    for dv in (0, 1):   # both diagonal-block kernels report the same leading minor
+        gm = TerrainMapper(0, Hyper(noise_level=0.0), ctx=mapper.ctx)
+        gm.set_option(N.SBO_OPT_CHOLESKY, 1)
+        gm.set_option(N.SBO_OPT_CHOL_DIAG, dv)
+        with pytest.raises(N.NotSPDError) as ei:
+            gm.fit(x, y, wl.obs)
+        msgs.append(str(ei.value))
+    gm.set_option(N.SBO_OPT_CHOL_DIAG, 1)
+    assert msgs[0] == msgs[1] and "leading minor" in msgs[0], msgs
 
 
 def test_jitter_retry_recovers_not_spd(mapper):

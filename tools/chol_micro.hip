@@ -1,5 +1,5 @@
 // Micro-benchmark of the blocked Cholesky's chain kernels in isolation
-// (chol_diag_kernel, chol_trsm_kernel) at C4's leading dimension, with
+// (chol_diag_kernel, chol_diag_mfma_kernel, chol_trsm_kernel) at C4's leading dimension, with
 // s_memtime phase stamps (-DSBO_CHOL_STAMPS).  GPU diagnostic:
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DSBO_CHOL_STAMPS -I/opt/rocm/include \
 //         tools/chol_micro.hip -o /tmp/chol_micro && /tmp/chol_micro
@@ -22,18 +22,23 @@ int main() {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     unsigned long long st[16];
-    for (int rep = 0; rep < 3; ++rep) {
+    std::vector<float> out[2];
+    for (int rep = 0; rep < 6; ++rep) {
+        const int ver = rep % 2;   // 0: chol_diag_kernel, 1: chol_diag_mfma_kernel
         (void)hipMemcpy(dA, h.data(), sizeof(float) * (size_t)kb * ld, hipMemcpyHostToDevice);
         (void)hipMemset(info, 0, sizeof(int));
         (void)hipEventRecord(e0, 0);
-        (void)sbo::launch_chol_diag(0, dA, ld, (int)kb, 0, info);
+        (void)sbo::launch_chol_diag(0, dA, ld, (int)kb, 0, info, ver);
         (void)hipEventRecord(e1, 0);
         (void)hipEventSynchronize(e1);
         float ms_d = 0.f;
         (void)hipEventElapsedTime(&ms_d, e0, e1);
         (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(sbo::g_chol_stamps), sizeof(st));
-        printf("diag: %.1f us  | memtime ticks: load %llu, panels %llu, updates %llu, factor total %llu, store %llu\n",
-               ms_d * 1e3, st[1] - st[0], st[4], st[5], st[2] - st[1], st[3] - st[2]);
+        printf("diag v%d: %.1f us  | memtime ticks: load %llu, panels %llu, updates %llu, factor total %llu, store %llu\n",
+               ver, ms_d * 1e3, st[1] - st[0], st[4], st[5], st[2] - st[1], st[3] - st[2]);
+        out[ver].resize((size_t)kb * kb);
+        for (int j = 0; j < kb; ++j)
+            (void)hipMemcpy(out[ver].data() + (size_t)j * kb, dA + (size_t)j * ld, sizeof(float) * kb, hipMemcpyDeviceToHost);
         (void)hipEventRecord(e0, 0);
         (void)sbo::launch_chol_trsm(0, dA, ld, (int)kb, dA + kb, m2);
         (void)hipEventRecord(e1, 0);
@@ -46,6 +51,10 @@ int main() {
     }
     int hinfo = 0;
     (void)hipMemcpy(&hinfo, info, sizeof(int), hipMemcpyDeviceToHost);
-    printf("info %d (s_memtime ticks at 100 MHz)\n", hinfo);
+    size_t diff = 0;
+    for (int j = 0; j < kb; ++j)
+        for (int i = j; i < kb; ++i) diff += out[0][i + (size_t)j * kb] != out[1][i + (size_t)j * kb];
+    printf("info %d; diagonal block factors v0 vs v1: %zu of %lld lower entries differ (s_memtime ticks = shader cycles)\n",
+           hinfo, diff, (long long)kb * (kb + 1) / 2);
     return 0;
 }
