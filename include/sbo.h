@@ -377,10 +377,17 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * the trailing matrix takes one rank-512 update per outer panel; 128 is the
  * one-level factorization (a rank-128 update per 128 columns). */
 #define SBO_OPT_CHOL_OUTER 15
-/* SBO_OPT_CHOL_DIAG (default 1): the blocked Cholesky's 128 x 128 diagonal
- * blocks by 16-column panels with matrix-core trailing updates (1) or by the
- * 8-column VALU kernel (0); the factor is bitwise the same. */
+/* SBO_OPT_CHOL_DIAG (default 1): the blocked Cholesky's chain kernels -- the
+ * 128 x 128 diagonal blocks (16-column panels) and the panel solves below
+ * them -- with their inner updates on the matrix cores (1) or on the VALU (0);
+ * the factor is bitwise the same. */
 #define SBO_OPT_CHOL_DIAG 16
+/* SBO_OPT_CHOL_GEMM (default 0): the blocked Cholesky's updates by rocBLAS
+ * sgemm / ssyrk (0) or by the library's f32 matrix-core kernel -- 2 all of
+ * them, 1 the trailing updates of at most 8192 rows, where it measured faster
+ * than ssyrk (the fit's time is the same: those run beside the chain).  All
+ * compute in f32 with exact f32 products; the factors agree to f32 rounding. */
+#define SBO_OPT_CHOL_GEMM 17
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe

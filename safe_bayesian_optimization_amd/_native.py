@@ -50,6 +50,7 @@ SBO_OPT_CHOL_RESERVE = 13
 SBO_OPT_INV_OVERLAP = 14
 SBO_OPT_CHOL_OUTER = 15
 SBO_OPT_CHOL_DIAG = 16
+SBO_OPT_CHOL_GEMM = 17
 
 
 class SboError(RuntimeError):

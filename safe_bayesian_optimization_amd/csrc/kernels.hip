@@ -448,6 +448,134 @@ __global__ __launch_bounds__(256) void chol_diag_mfma_kernel(float *__restrict__
     SBO_CSTAMP(3);
 }
 
+// The blocked Cholesky's trailing updates (a2): C[r][c] -= sum_k P[r][k] Q[c][k]
+// over 128 x 128 tiles of C (all tiles of an m x nc block, or, lower != 0,
+// the tiles on and below the diagonal of an m x m block), f32 in and out,
+// column-major with leading dimension ld, K columns of P and Q.  The products
+// on the matrix cores (v_mfma_f32_16x16x4_f32: exact f32 products, bit for
+// bit a k-ordered fmaf chain) with C itself as the accumulator's start, so
+// every element sees fmaf(-P[r][k], Q[c][k], C) in k order, as in a
+// right-looking factorization.  rocBLAS ssyrk / sgemm ran these at 55-75 TF
+// (tools/r3_gemm_probe.cpp).  Workgroup: 4 waves as 2 x 2 of 64 x 64; the
+// MFMA's A side takes Q (the tile's columns) and its B side P (rows), so a
+// lane's result column is a row of C: the stores run down C's columns.
+// K in chunks of 32 staged through LDS as [k][row] (row stride 144 floats:
+// the 16 rows x 4 k of one fragment read hit 64 distinct banks), double
+// buffered, the next chunk's global loads in flight during the MFMAs.
+constexpr int kUpBM = 128, kUpBK = 32, kUpLd = kUpBM + 16;
+__global__ __launch_bounds__(256, 2) void chol_update_kernel(const float *__restrict__ P, const float *__restrict__ Q,
+                                                             int64_t ld, int m, int nc, int K, int lower,
+                                                             float *__restrict__ C) {
+    __shared__ float Ps[2][kUpBK][kUpLd], Qs[2][kUpBK][kUpLd];
+    int ti, tj;
+    if (lower) {
+        const int q = blockIdx.x;
+        ti = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+        while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
+        while (ti * (ti + 1) / 2 > q) --ti;
+        tj = q - ti * (ti + 1) / 2;
+    } else {
+        const int ntj = (nc + kUpBM - 1) / kUpBM;
+        ti = blockIdx.x / ntj;
+        tj = blockIdx.x % ntj;
+    }
+    const int r0 = ti * kUpBM, c0 = tj * kUpBM;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+    // loader: row (tid & 127) of the chunk's k = (tid >> 7) + 2 u, u < 16, for P and Q
+    const int lrow = tid & (kUpBM - 1), lk = tid >> 7;
+    const bool prow = r0 + lrow < m, qrow = c0 + lrow < nc;
+    const float *pp = P + (prow ? r0 + lrow : 0), *qp = Q + (qrow ? c0 + lrow : 0);
+    float vp[16], vq[16];
+    auto gload = [&](int k0) {
+        // (K is a multiple of kUpBK: every k in range; rows past m / nc read
+        // row 0 and are zeroed)
+        const float *p0 = pp + (int64_t)(k0 + lk) * ld, *q0 = qp + (int64_t)(k0 + lk) * ld;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const float a = p0[(int64_t)(2 * u) * ld], c = q0[(int64_t)(2 * u) * ld];
+            vp[u] = prow ? a : 0.0f;
+            vq[u] = qrow ? c : 0.0f;
+        }
+    };
+    auto lstore = [&](int b) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            Ps[b][lk + 2 * u][lrow] = vp[u];
+            Qs[b][lk + 2 * u][lrow] = vq[u];
+        }
+    };
+    // accumulators from C: acc[cb][rb] holds C[r0 + 64 wr + 16 rb + (lane & 15)][c0 + 64 wc + 16 cb + 4 (lane >> 4) + v]
+    const int fr = lane & 15, fg = lane >> 4;
+    // a tile inside the block (uniform) needs no per-element tests
+    const bool interior = r0 + kUpBM <= m && c0 + kUpBM <= nc;
+    float *cw = C + (int64_t)(r0 + 64 * wr + fr) + (int64_t)(c0 + 64 * wc + 4 * fg) * ld;
+    f32x4_t acc[4][4];
+    if (interior) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[cb][rb][v] = cw[16 * rb + (int64_t)(16 * cb + v) * ld];
+    } else {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb) {
+                const int r = r0 + 64 * wr + 16 * rb + fr;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int c = c0 + 64 * wc + 16 * cb + 4 * fg + v;
+                    acc[cb][rb][v] = (r < m && c < nc) ? cw[16 * rb + (int64_t)(16 * cb + v) * ld] : 0.0f;
+                }
+            }
+    }
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    const int nchunk = K / kUpBK;
+    for (int ch = 0; ch < nchunk; ++ch) {
+        const int b = ch & 1;
+        if (ch + 1 < nchunk) gload((ch + 1) * kUpBK);
+#pragma unroll
+        for (int kk = 0; kk < kUpBK / 4; ++kk) {
+            const int k = 4 * kk + fg;
+            float qa[4], pb[4];
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) qa[cb] = Qs[b][k][64 * wc + 16 * cb + fr];
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb) pb[rb] = -Ps[b][k][64 * wr + 16 * rb + fr];
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int rb = 0; rb < 4; ++rb)
+                    acc[cb][rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[cb], pb[rb], acc[cb][rb], 0, 0, 0);
+        }
+        if (ch + 1 < nchunk) lstore(b ^ 1);
+        __syncthreads();
+    }
+    if (interior) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) cw[16 * rb + (int64_t)(16 * cb + v) * ld] = acc[cb][rb][v];
+    } else {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb) {
+                const int r = r0 + 64 * wr + 16 * rb + fr;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int c = c0 + 64 * wc + 16 * cb + 4 * fg + v;
+                    if (r < m && c < nc) cw[16 * rb + (int64_t)(16 * cb + v) * ld] = acc[cb][rb][v];
+                }
+            }
+    }
+}
+
 // The blocked Cholesky's panel (a2): A21 := A21 L11^-T for the m2 x kb panel
 // below a factored kb x kb diagonal block (rocBLAS strsm right / lower /
 // transpose ran as ~10 launches, ~100 us per step, on the factorization's
@@ -572,6 +700,109 @@ __global__ __launch_bounds__(256) void chol_trsm_kernel(const float *__restrict_
     SBO_CSTAMP(10);
     if (in)
         for (int j = h; j < kb; j += 2) A21[row + (int64_t)j * ld] = X[j * kCholNB + t];
+    SBO_CSTAMP(11);
+}
+
+// The same panel solve with the later columns' updates on the matrix cores
+// (chol_trsm_kernel's default replacement).  Per 16-column block: the rows
+// solve the block in registers, right-looking -- after x_q, every later s_q'
+// of the block takes fmaf(-x_q, L[q'][q], s_q'), so each s still sees its
+// terms in ascending column order, as in the forward substitution -- with the
+// pivots' reciprocals computed once per workgroup; then the block's rank-16
+// update of the later columns, X[c][t] -= sum_u L[c][u] x_u(t), as
+// v_mfma_f32_16x16x4_f32 (a k-ordered fmaf chain from X itself: the same
+// terms in the same order as chol_trsm_kernel's VALU loop, so the panel is
+// bitwise the same).  The MFMA's A side takes L (result rows = columns c of
+// X), its B side the solved x (result columns = panel rows t, contiguous in
+// X's [c][t] layout, row stride 132: conflict-free result reads and writes).
+// The block of L11 and the 128 panel rows in: two batches of 64 loads per
+// thread in flight.
+constexpr int kTrX = kCholNB + 4;
+__global__ __launch_bounds__(256) void chol_trsm_mfma_kernel(const float *__restrict__ L11, int64_t ld, int kb,
+                                                             float *__restrict__ A21, int64_t m2) {
+    __shared__ __attribute__((aligned(16))) float Ls[kCholNB * kTrsmLd];
+    __shared__ float X[kCholNB * kTrX];
+    __shared__ float rinv[kCholNB];
+    SBO_CSTAMP(8);
+    const int tid = threadIdx.x, t = tid & (kCholNB - 1), h = tid >> 7;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int64_t row = (int64_t)blockIdx.x * kCholNB + t;
+    const bool in = row < m2, lin = t < kb;
+    // loads: thread (t, h) takes columns h, h + 2, ... of L11's row t and of panel row t
+    // (every load unconditional, clamped into the block; padding replaced below)
+    const float *lp = L11 + min(t, kb - 1);
+    const float *xp = A21 + (in ? row : 0);
+    for (int jb = 0; jb < kCholNB; jb += 64) {
+        float lv[32], xv[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            const int64_t off = (int64_t)min(jb + 2 * u + h, kb - 1) * ld;
+            lv[u] = lp[off];
+            xv[u] = xp[off];
+        }
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            const int j = jb + 2 * u + h;
+            Ls[t * kTrsmLd + j] = (j < kb && lin && t >= j) ? lv[u] : (t == j && j >= kb ? 1.0f : 0.0f);
+            X[j * kTrX + t] = (in && j < kb) ? xv[u] : 0.0f;
+        }
+    }
+    __syncthreads();
+    if (tid < kCholNB) rinv[tid] = __fdiv_rn(1.0f, Ls[tid * kTrsmLd + tid]);
+    __syncthreads();
+    SBO_CSTAMP(9);
+    const int fr = lane & 15, fg = lane >> 4;
+    for (int B = 0; B < kCholNB / 16; ++B) {
+        const int j0 = 16 * B;
+        if (h == 0) {
+            // the block's 16 x 16 lower triangle of L (broadcast reads)
+            float4 lb[16][4];
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    if (4 * v <= q) lb[q][v] = reinterpret_cast<const float4 *>(Ls + (j0 + q) * kTrsmLd + j0)[v];
+            float sb[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) sb[q] = X[(j0 + q) * kTrX + t];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                sb[q] = sb[q] * rinv[j0 + q];
+#pragma unroll
+                for (int q2 = q + 1; q2 < 16; ++q2) {
+                    const float4 l4 = lb[q2][q >> 2];
+                    const float l = (q & 3) == 0 ? l4.x : (q & 3) == 1 ? l4.y : (q & 3) == 2 ? l4.z : l4.w;
+                    sb[q2] = fmaf(-sb[q], l, sb[q2]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) X[(j0 + q) * kTrX + t] = sb[q];
+        }
+        __syncthreads();
+        // rank-16 update of the later columns: 16 x 16 result blocks (column
+        // block ci, row block ri), spread over the four waves
+        const int c1 = j0 + 16, nci = (kCholNB - c1) / 16, nblk = nci * (kCholNB / 16);
+        for (int qb = wave; qb < nblk; qb += 4) {
+            const int ci = qb / (kCholNB / 16), ri = qb % (kCholNB / 16);
+            const int cb0 = c1 + 16 * ci, rb0 = 16 * ri;
+            f32x4_t acc;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[v] = X[(cb0 + 4 * fg + v) * kTrX + rb0 + fr];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const int u = 4 * kk + fg;
+                const float av = -Ls[(cb0 + fr) * kTrsmLd + j0 + u];
+                const float bv = X[(j0 + u) * kTrX + rb0 + fr];
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) X[(cb0 + 4 * fg + v) * kTrX + rb0 + fr] = acc[v];
+        }
+        __syncthreads();
+    }
+    SBO_CSTAMP(10);
+    if (in)
+        for (int j = h; j < kb; j += 2) A21[row + (int64_t)j * ld] = X[j * kTrX + t];
     SBO_CSTAMP(11);
 }
 
@@ -2066,11 +2297,29 @@ hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t
     return hipGetLastError();
 }
 
-hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb, float *A21, int64_t m2) {
+hipError_t launch_chol_update(hipStream_t s, const float *P, const float *Q, int64_t ld, int64_t m, int64_t nc,
+                              int64_t K, bool lower, float *C) {
+    if (m < 0 || nc < 0 || K < 0 || m > INT32_MAX / 2 || nc > INT32_MAX / 2 || K > INT32_MAX / 2 || (lower && nc != m) ||
+        K % kUpBK != 0)
+        return hipErrorInvalidValue;
+    if (m == 0 || nc == 0 || K == 0) return hipSuccess;
+    const int64_t nti = (m + kUpBM - 1) / kUpBM, ntj = (nc + kUpBM - 1) / kUpBM;
+    const int64_t tiles = lower ? nti * (nti + 1) / 2 : nti * ntj;
+    if (tiles > INT32_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(chol_update_kernel, dim3((unsigned)tiles), dim3(256), 0, s, P, Q, ld, (int)m, (int)nc, (int)K,
+                       lower ? 1 : 0, C);
+    return hipGetLastError();
+}
+
+hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb, float *A21, int64_t m2, int version) {
     if (kb <= 0 || kb > kCholNB || m2 < 0) return hipErrorInvalidValue;
     if (m2 == 0) return hipSuccess;
-    hipLaunchKernelGGL(chol_trsm_kernel, dim3((unsigned)((m2 + kCholNB - 1) / kCholNB)), dim3(2 * kCholNB), 0, s,
-                       L11, ld, kb, A21, m2);
+    if (version == 1)
+        hipLaunchKernelGGL(chol_trsm_mfma_kernel, dim3((unsigned)((m2 + kCholNB - 1) / kCholNB)), dim3(2 * kCholNB), 0,
+                           s, L11, ld, kb, A21, m2);
+    else
+        hipLaunchKernelGGL(chol_trsm_kernel, dim3((unsigned)((m2 + kCholNB - 1) / kCholNB)), dim3(2 * kCholNB), 0, s,
+                           L11, ld, kb, A21, m2);
     return hipGetLastError();
 }
 

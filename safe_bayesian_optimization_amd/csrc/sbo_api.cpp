@@ -750,7 +750,10 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
             }
             if (m2 <= 0) break;
             if (ctx->chol_trsm_own) {
-                if (sbo::launch_chol_trsm(ctx->stream, L11, ld, (int)kb, A21, m2) != hipSuccess) { st = SBO_E_DEVICE; break; }
+                if (sbo::launch_chol_trsm(ctx->stream, L11, ld, (int)kb, A21, m2, ctx->chol_diag) != hipSuccess) {
+                    st = SBO_E_DEVICE;
+                    break;
+                }
             } else if (rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
                                      rocblas_diagonal_non_unit, (rocblas_int)m2, (rocblas_int)kb, &one, L11,
                                      (rocblas_int)ld, A21, (rocblas_int)ld) != rocblas_status_success) {
@@ -775,12 +778,16 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
             }
             // the outer panel's remaining columns (rows below this block)
             const int64_t rem = K + W - (k + kb);
-            if (rem > 0 &&
-                rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m2,
-                              (rocblas_int)rem, (rocblas_int)kb, &minus_one, A21, (rocblas_int)ld, A21,
-                              (rocblas_int)ld, &one, L11 + kb + kb * ld, (rocblas_int)ld) != rocblas_status_success) {
-                st = SBO_E_DEVICE;
-                break;
+            if (rem > 0) {
+                const bool ok =
+                    ctx->chol_gemm_own == 2
+                        ? sbo::launch_chol_update(ctx->stream, A21, A21, ld, m2, rem, kb, false, L11 + kb + kb * ld) ==
+                              hipSuccess
+                        : rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m2,
+                                        (rocblas_int)rem, (rocblas_int)kb, &minus_one, A21, (rocblas_int)ld, A21,
+                                        (rocblas_int)ld, &one, L11 + kb + kb * ld,
+                                        (rocblas_int)ld) == rocblas_status_success;
+                if (!ok) { st = SBO_E_DEVICE; break; }
             }
         }
         if (st != SBO_OK) break;
@@ -791,22 +798,33 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         const int64_t W2 = std::min(NB2, m3);    // the next outer panel
         if (hipEventRecord(ctx->ev_panel, ctx->stream) != hipSuccess ||
             (trail_pending && hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0) != hipSuccess)) { st = SBO_E_DEVICE; break; }
-        if (rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m3,
-                          (rocblas_int)W2, (rocblas_int)W, &minus_one, P, (rocblas_int)ld, P, (rocblas_int)ld, &one, C1,
-                          (rocblas_int)ld) != rocblas_status_success) { st = SBO_E_DEVICE; break; }
+        const bool la_ok =
+            ctx->chol_gemm_own == 2
+                ? sbo::launch_chol_update(ctx->stream, P, P, ld, m3, W2, W, false, C1) == hipSuccess
+                : rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m3,
+                                (rocblas_int)W2, (rocblas_int)W, &minus_one, P, (rocblas_int)ld, P, (rocblas_int)ld,
+                                &one, C1, (rocblas_int)ld) == rocblas_status_success;
+        if (!la_ok) { st = SBO_E_DEVICE; break; }
         const int64_t m4 = m3 - W2;
         trail_pending = false;
         if (m4 > 0) {
             if (hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0) != hipSuccess) { st = SBO_E_DEVICE; break; }
-            const rocblas_status bs =
-                m4 <= kSmallTrail
-                    ? rocblas_sgemm(ctx->blas_aux, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m4,
-                                    (rocblas_int)m4, (rocblas_int)W, &minus_one, P + W2, (rocblas_int)ld, P + W2,
-                                    (rocblas_int)ld, &one, C1 + W2 + W2 * ld, (rocblas_int)ld)
-                    : rocblas_ssyrk(ctx->blas_aux, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)m4,
-                                    (rocblas_int)W, &minus_one, P + W2, (rocblas_int)ld, &one, C1 + W2 + W2 * ld,
-                                    (rocblas_int)ld);
-            if (bs != rocblas_status_success) { st = SBO_E_DEVICE; break; }
+            // (1: the own kernel only where it measured faster than rocBLAS,
+            // the lower update of m4 <= 8192; 2: every update)
+            bool ok;
+            if (ctx->chol_gemm_own == 2 || (ctx->chol_gemm_own == 1 && m4 <= 8192))
+                ok = sbo::launch_chol_update(ctx->aux_stream, P + W2, P + W2, ld, m4, m4, W, true,
+                                             C1 + W2 + W2 * ld) == hipSuccess;
+            else
+                ok = (m4 <= kSmallTrail
+                          ? rocblas_sgemm(ctx->blas_aux, rocblas_operation_none, rocblas_operation_transpose,
+                                          (rocblas_int)m4, (rocblas_int)m4, (rocblas_int)W, &minus_one, P + W2,
+                                          (rocblas_int)ld, P + W2, (rocblas_int)ld, &one, C1 + W2 + W2 * ld,
+                                          (rocblas_int)ld)
+                          : rocblas_ssyrk(ctx->blas_aux, rocblas_fill_lower, rocblas_operation_none, (rocblas_int)m4,
+                                          (rocblas_int)W, &minus_one, P + W2, (rocblas_int)ld, &one,
+                                          C1 + W2 + W2 * ld, (rocblas_int)ld)) == rocblas_status_success;
+            if (!ok) { st = SBO_E_DEVICE; break; }
             trail_pending = true;
             if (hipEventRecord(ctx->ev_trail, ctx->aux_stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
         }
@@ -1618,6 +1636,10 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             SBO_CHECK(sbo::variant_allowed((int)value), SBO_E_INVAL,
                       "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22)");
             ctx->kernel_variant = (int)value;
+            return SBO_OK;
+        case SBO_OPT_CHOL_GEMM:
+            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_CHOL_GEMM must be 0, 1 or 2");
+            ctx->chol_gemm_own = (int)value;
             return SBO_OK;
         case SBO_OPT_CHOL_DIAG:
             SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_CHOL_DIAG must be 0 or 1");

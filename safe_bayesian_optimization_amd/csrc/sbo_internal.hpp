@@ -99,7 +99,8 @@ struct sbo_ctx {
     int chol_reserve = 0;        // SBO_OPT_CHOL_RESERVE: CUs the trailing updates leave free (CU-masked aux stream)
     int aux_reserved = 0;        // the mask the current aux stream was created with
     hipEvent_t ev_panel = nullptr, ev_trail = nullptr;
-    int chol_diag = 1;           // SBO_OPT_CHOL_DIAG: 1 the MFMA diagonal-block kernel, 0 the VALU one (bitwise equal)
+    int chol_gemm_own = 0;       // SBO_OPT_CHOL_GEMM: 2 every factorization update by chol_update_kernel, 1 the small trailing ones, 0 rocBLAS
+    int chol_diag = 1;           // SBO_OPT_CHOL_DIAG: 1 the MFMA chain kernels (diagonal block, panel), 0 the VALU ones (bitwise equal)
     int chol_outer = 512;        // SBO_OPT_CHOL_OUTER: outer panel width of the two-level Cholesky (128: one level)
     // the recursive inverse's first half beside the Cholesky's last steps
     // (SBO_OPT_INV_OVERLAP = R > 0: on inv_stream, CU-masked to leave R CUs free)
@@ -316,8 +317,12 @@ hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int6
 constexpr int kCholNB = 128;
 // version 1: chol_diag_mfma_kernel (16-column panels, MFMA trailing updates; default), 0: chol_diag_kernel
 hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info, int version = 1);
+// C -= P Q^T over 128 x 128 tiles (lower: the tiles on and below the diagonal of an m x m C), f32, lda ld, K columns
+hipError_t launch_chol_update(hipStream_t s, const float *P, const float *Q, int64_t ld, int64_t m, int64_t nc,
+                              int64_t K, bool lower, float *C);
 // The panel below it: A21 (m2 x kb, lda ld) := A21 L11^-T (forward substitution, f32).
-hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb, float *A21, int64_t m2);
+// version 1: chol_trsm_mfma_kernel (MFMA updates of the later columns; default), 0: chol_trsm_kernel (bitwise equal)
+hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb, float *A21, int64_t m2, int version = 1);
 // d = (double)in - v;  out = (float)d
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out);

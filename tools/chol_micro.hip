@@ -22,7 +22,7 @@ int main() {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     unsigned long long st[16];
-    std::vector<float> out[2];
+    std::vector<float> out[2], pan[2];
     for (int rep = 0; rep < 6; ++rep) {
         const int ver = rep % 2;   // 0: chol_diag_kernel, 1: chol_diag_mfma_kernel
         (void)hipMemcpy(dA, h.data(), sizeof(float) * (size_t)kb * ld, hipMemcpyHostToDevice);
@@ -40,21 +40,28 @@ int main() {
         for (int j = 0; j < kb; ++j)
             (void)hipMemcpy(out[ver].data() + (size_t)j * kb, dA + (size_t)j * ld, sizeof(float) * kb, hipMemcpyDeviceToHost);
         (void)hipEventRecord(e0, 0);
-        (void)sbo::launch_chol_trsm(0, dA, ld, (int)kb, dA + kb, m2);
+        (void)sbo::launch_chol_trsm(0, dA, ld, (int)kb, dA + kb, m2, ver);
         (void)hipEventRecord(e1, 0);
         (void)hipEventSynchronize(e1);
         float ms_t = 0.f;
         (void)hipEventElapsedTime(&ms_t, e0, e1);
         (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(sbo::g_chol_stamps), sizeof(st));
-        printf("trsm (m2 %lld): %.1f us | block 0 ticks: load %llu, solve %llu, store %llu\n", (long long)m2,
+        printf("trsm v%d (m2 %lld): %.1f us | block 0 ticks: load %llu, solve %llu, store %llu\n", ver, (long long)m2,
                ms_t * 1e3, st[9] - st[8], st[10] - st[9], st[11] - st[10]);
+        pan[ver].resize((size_t)m2 * kb);
+        for (int j = 0; j < kb; ++j)
+            (void)hipMemcpy(pan[ver].data() + (size_t)j * m2, dA + kb + (size_t)j * ld, sizeof(float) * m2,
+                            hipMemcpyDeviceToHost);
     }
     int hinfo = 0;
     (void)hipMemcpy(&hinfo, info, sizeof(int), hipMemcpyDeviceToHost);
     size_t diff = 0;
     for (int j = 0; j < kb; ++j)
         for (int i = j; i < kb; ++i) diff += out[0][i + (size_t)j * kb] != out[1][i + (size_t)j * kb];
-    printf("info %d; diagonal block factors v0 vs v1: %zu of %lld lower entries differ (s_memtime ticks = shader cycles)\n",
-           hinfo, diff, (long long)kb * (kb + 1) / 2);
+    size_t pdiff = 0;
+    for (size_t i = 0; i < pan[0].size(); ++i) pdiff += pan[0][i] != pan[1][i];
+    printf("info %d; diagonal block factors v0 vs v1: %zu of %lld lower entries differ; panels: %zu of %zu differ "
+           "(s_memtime ticks = shader cycles)\n",
+           hinfo, diff, (long long)kb * (kb + 1) / 2, pdiff, pan[0].size());
     return 0;
 }
