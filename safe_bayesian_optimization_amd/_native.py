@@ -51,6 +51,8 @@ SBO_OPT_INV_OVERLAP = 14
 SBO_OPT_CHOL_OUTER = 15
 SBO_OPT_CHOL_DIAG = 16
 SBO_OPT_CHOL_GEMM = 17
+SBO_OPT_INV_BASE = 18
+SBO_OPT_INV_PANELS = 19
 
 
 class SboError(RuntimeError):

@@ -867,48 +867,58 @@ typedef double f64x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f64x4_t mfma_f64(double a, double b, f64x4_t c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
-__global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
-                                                        float4 *__restrict__ lgn) {
-    __shared__ float at[kBM * kBK];            // the tile (or one of its pieces), [row][k]  (64 KiB)
+__global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
+                                                           float4 *__restrict__ lgn) {
+    // 66 KiB of LDS, two workgroups per CU: the tile (or one of its pieces)
+    // staged 128 rows at a time, the Gram matrix and its powers in place (a
+    // product is held in registers until every read of its factor is done)
+    __shared__ float at[(kBM / 2) * kBK];      // half the tile, [row][k]  (32 KiB)
     __shared__ double gm[kBK * kBK];           // G, then its powers (32 KiB)
-    __shared__ double hm[kBK * kBK];           // squaring scratch  (32 KiB)
+    __shared__ double rsum[kBM];               // row 1-norms
     __shared__ double red[2][kBM / 64];
     const int64_t tile = t0 + blockIdx.x;
     const float *t = aug + tile * kTileFloats;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lrow = tid & (kBM / 2 - 1), kh = tid >> 7;   // staging: row lrow of the half, k in [32 kh, 32 kh + 32)
     float out[6];                                // (rows, spectral) of A; of A1; of A2
     double lg_fro_a = -1000.0;
-#pragma unroll
+#pragma unroll 1
     for (int pi = 0; pi < 3; ++pi) {
         const int plane = pi == 0 ? -1 : pi;     // -1: A itself, then A1, A2
-        double s = 0.0;
-        for (int k = 0; k < kBK; ++k) {
-            const float a0 = t[tile_offset(k, tid)];
-            const float a = plane < 0 ? a0 : split_piece(a0, plane);
-            at[tid * kBK + k] = a;
-            s += fabs((double)a);
+        // G = A^T A: lane l of wave w feeds A^T[i = 16w + (l&15)][r] and
+        // A[r][j = 16 bj + (l&15)] at r = r0 + (l>>4)
+        f64x4_t acc[4];
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) acc[bj] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 1
+        for (int half = 0; half < 2; ++half) {
+            const int r = half * (kBM / 2) + lrow;
+            double sp = 0.0;
+            for (int k = 32 * kh; k < 32 * kh + 32; ++k) {
+                const float a0 = t[tile_offset(k, r)];
+                const float a = plane < 0 ? a0 : split_piece(a0, plane);
+                at[lrow * kBK + k] = a;
+                sp += fabs((double)a);
+            }
+            if (kh == 1) rsum[r] = sp;
+            __syncthreads();
+            if (kh == 0) rsum[r] += sp;
+            for (int r0 = 0; r0 < kBM / 2; r0 += 4) {
+                const float *row = at + (r0 + (lane >> 4)) * kBK + (lane & 15);
+                const double av = (double)row[16 * wave];
+#pragma unroll
+                for (int bj = 0; bj < 4; ++bj) acc[bj] = mfma_f64(av, (double)row[16 * bj], acc[bj]);
+            }
+            __syncthreads();   // at is restaged for the next half
         }
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) gm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = acc[bj][v];
+        double s = rsum[tid];
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) s = fmax(s, __shfl_xor(s, o));
         if ((tid & 63) == 0) red[0][tid >> 6] = s;
-        __syncthreads();
-        {
-            // G = A^T A: lane l of wave w feeds A^T[i = 16w + (l&15)][r] and
-            // A[r][j = 16 bj + (l&15)] at r = r0 + (l>>4)
-            f64x4_t acc[4];
-#pragma unroll
-            for (int bj = 0; bj < 4; ++bj) acc[bj] = f64x4_t{0.0, 0.0, 0.0, 0.0};
-            for (int r0 = 0; r0 < kBM; r0 += 4) {
-                const float *row = at + (r0 + (lane >> 4)) * kBK + (lane & 15);
-                const double a = (double)row[16 * wave];
-#pragma unroll
-                for (int bj = 0; bj < 4; ++bj) acc[bj] = mfma_f64(a, (double)row[16 * bj], acc[bj]);
-            }
-#pragma unroll
-            for (int bj = 0; bj < 4; ++bj)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) gm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = acc[bj][v];
-        }
         __syncthreads();
         const double fro2 = [&] {  // trace G = |A|_F^2 (every thread reads it)
             double tr = 0.0;
@@ -930,25 +940,25 @@ __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict_
             __syncthreads();
             if (!(mx > 0.0)) break;
             const int ex = ilogb(mx);
-            // G' = 2^-ex G in place (exact), then hm = G'^2 by MFMA
+            // G' = 2^-ex G in place (exact), then G'^2 by MFMA into registers,
+            // written over G once every read of it is done
             for (int i = tid; i < kBK * kBK; i += kBM) gm[i] = ldexp(gm[i], -ex);
             __syncthreads();
-            f64x4_t acc[4];
+            f64x4_t sq[4];
 #pragma unroll
-            for (int bj = 0; bj < 4; ++bj) acc[bj] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+            for (int bj = 0; bj < 4; ++bj) sq[bj] = f64x4_t{0.0, 0.0, 0.0, 0.0};
             for (int k0 = 0; k0 < kBK; k0 += 4) {
-                const double a = gm[(16 * wave + (lane & 15)) * kBK + k0 + (lane >> 4)];
+                const double av = gm[(16 * wave + (lane & 15)) * kBK + k0 + (lane >> 4)];
                 const double *brow = gm + (k0 + (lane >> 4)) * kBK + (lane & 15);
 #pragma unroll
-                for (int bj = 0; bj < 4; ++bj) acc[bj] = mfma_f64(a, brow[16 * bj], acc[bj]);
+                for (int bj = 0; bj < 4; ++bj) sq[bj] = mfma_f64(av, brow[16 * bj], sq[bj]);
             }
+            e8 = 2.0 * (e8 + (double)ex);  // (2^e G')^2 = 2^(2e) G'^2
+            __syncthreads();
 #pragma unroll
             for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
-                for (int v = 0; v < 4; ++v) hm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = acc[bj][v];
-            e8 = 2.0 * (e8 + (double)ex);  // (2^e G')^2 = 2^(2e) G'^2
-            __syncthreads();
-            for (int i = tid; i < kBK * kBK; i += kBM) gm[i] = hm[i];
+                for (int v = 0; v < 4; ++v) gm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = sq[bj][v];
             __syncthreads();
         }
         // ||G^(2^k)||_inf: largest absolute row sum
@@ -965,7 +975,7 @@ __global__ __launch_bounds__(kBM) void tile_norm_kernel(const float *__restrict_
         out[o] = s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f;
         out[o + 1] = (float)fmin(lg_spec, lg_fro) + 1e-5f;
         if (plane < 0) lg_fro_a = lg_fro;
-        __syncthreads();   // gm / red / at are rewritten for the next matrix
+        __syncthreads();   // gm / red / rsum / at are rewritten for the next matrix
     }
     if (tid == 0) {
         lgn[2 * tile] = make_float4(out[0], out[1], (float)lg_fro_a + 1e-5f, 0.0f);

@@ -81,25 +81,41 @@ int64_t info_slots(int64_t n) { return std::max<int64_t>(64, n / 512 + 2); }
 // the factor.  S: (n - h) x h doubles of scratch, C^-1's own scratch after
 // it (inverse_scratch).  hb: the rocBLAS handle (and so the stream) to run on;
 // slot: the next free info slot (one per dtrtri base case).
-constexpr int64_t kInvBase = 2048;
+// (SBO_OPT_INV_BASE: the dtrtri base-case size, default 2048, >= 1024 so
+// that info_slots holds; SBO_OPT_INV_PANELS: the products' panels per half,
+// default 16, at least 512 columns each: C4 warm fit 58.0 ms at 8 panels,
+// 56.0 at 16; a 256-column floor: 59.8 at 16, 68 at 32, profiles/r3_fit_invtune*.log)
 int64_t inverse_split(int64_t n) { return sbo::round_up(n / 2, 128); }
 
-int64_t inverse_scratch(int64_t n) {
-    if (n <= kInvBase) return 0;
+int64_t inverse_scratch(int64_t n, int64_t base) {
+    if (n <= base) return 0;
     const int64_t h = inverse_split(n), m = n - h;
-    return h * m + std::max(inverse_scratch(h), inverse_scratch(m));
+    return h * m + std::max(inverse_scratch(h, base), inverse_scratch(m, base));
+}
+// with the two halves' inverses side by side (inverse_lower_f64_par)
+int64_t inverse_scratch_par(int64_t n, int64_t base) {
+    if (n <= base) return 0;
+    const int64_t h = inverse_split(n), m = n - h;
+    return h * m + inverse_scratch(h, base) + inverse_scratch(m, base);
+}
+// dtrtri base cases of an n-column recursion (one info slot each)
+int inverse_base_cases(int64_t n, int64_t base) {
+    if (n <= base) return 1;
+    const int64_t h = inverse_split(n);
+    return inverse_base_cases(h, base) + inverse_base_cases(n - h, base);
 }
 
 sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
                              int &slot);
 
+// A^-1 (recursion scratch scr), then S = B A^-1
 sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                              int &slot) {
+                              double *scr, int &slot) {
     const int64_t h = inverse_split(n), m = n - h;
-    if (sbo_status st = inverse_lower_f64(ctx, hb, Li, h, ld, S + h * m, slot); st != SBO_OK) return st;
+    if (sbo_status st = inverse_lower_f64(ctx, hb, Li, h, ld, scr, slot); st != SBO_OK) return st;
     SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
     const double one = 1.0, zero = 0.0;
-    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / 8, 128));
+    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / ctx->inv_panels, 128));
     for (int64_t p0 = 0; p0 < h; p0 += nb) {
         const int64_t w = std::min(nb, h - p0);
         SBO_BLAS(rocblas_dgemm(hb, rocblas_operation_none, rocblas_operation_none, (rocblas_int)m, (rocblas_int)w,
@@ -109,14 +125,16 @@ sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64
     return SBO_OK;
 }
 
+// C^-1 (recursion scratch scr; skipped when c_done), then X21 = -C^-1 S
 sbo_status inverse_second_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                               int &slot) {
+                               double *scr, int &slot, bool c_done = false) {
     const int64_t h = inverse_split(n), m = n - h;
     double *B = Li + h, *C = Li + h + h * ld;
-    if (sbo_status st = inverse_lower_f64(ctx, hb, C, m, ld, S + h * m, slot); st != SBO_OK) return st;
+    if (!c_done)
+        if (sbo_status st = inverse_lower_f64(ctx, hb, C, m, ld, scr, slot); st != SBO_OK) return st;
     SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
     const double minus_one = -1.0, zero = 0.0;
-    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / 8, 128));
+    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / ctx->inv_panels, 128));
     for (int64_t p0 = 0; p0 < m; p0 += nb) {
         const int64_t w = std::min(nb, m - p0);
         SBO_BLAS(rocblas_dgemm(hb, rocblas_operation_none, rocblas_operation_none, (rocblas_int)w, (rocblas_int)h,
@@ -128,14 +146,44 @@ sbo_status inverse_second_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int6
 
 sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
                              int &slot) {
-    if (n <= kInvBase) {
+    if (n <= ctx->inv_base) {
         rocblas_int *info = ctx->info.as<rocblas_int>() + 1 + slot++;
         SBO_BLAS(rocsolver_dtrtri(hb, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
                                   (rocblas_int)ld, info));
         return SBO_OK;
     }
-    if (sbo_status st = inverse_first_half(ctx, hb, Li, n, ld, S, slot); st != SBO_OK) return st;
-    return inverse_second_half(ctx, hb, Li, n, ld, S, slot);
+    const int64_t h = inverse_split(n), m = n - h;
+    if (sbo_status st = inverse_first_half(ctx, hb, Li, n, ld, S, S + h * m, slot); st != SBO_OK) return st;
+    return inverse_second_half(ctx, hb, Li, n, ld, S, S + h * m, slot);
+}
+
+// The top of the recursion with its two independent halves side by side:
+// C^-1 on aux_stream (the Cholesky's look-ahead stream and rocBLAS handle,
+// idle by now) while `stream` computes A^-1 and S = B A^-1, then X21 once
+// both are done.  The lower levels' GEMMs are too small to fill the chip on
+// their own.  Scratch: inverse_scratch_par(n); info slots as the sequential
+// recursion's (C's base cases after A's).
+sbo_status inverse_lower_f64_par(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld, double *S) {
+    int slot = 0;
+    if (n <= ctx->inv_base || !ctx->blas_aux || !ctx->aux_stream || !ctx->ev_panel)
+        return inverse_lower_f64(ctx, ctx->blas, Li, n, ld, S, slot);
+    const int64_t h = inverse_split(n), m = n - h;
+    double *scrA = S + h * m, *scrC = scrA + inverse_scratch(h, ctx->inv_base);
+    int slotC = inverse_base_cases(h, ctx->inv_base);
+    SBO_HIP(hipEventRecord(ctx->ev_panel, ctx->stream));            // Li widened
+    SBO_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0));
+    SBO_BLAS(rocblas_set_pointer_mode(ctx->blas_aux, rocblas_pointer_mode_host));
+    if (sbo_status st = inverse_lower_f64(ctx, ctx->blas_aux, Li + h + h * ld, m, ld, scrC, slotC); st != SBO_OK) {
+        (void)hipStreamSynchronize(ctx->aux_stream);
+        return st;
+    }
+    SBO_HIP(hipEventRecord(ctx->ev_trail, ctx->aux_stream));
+    if (sbo_status st = inverse_first_half(ctx, ctx->blas, Li, n, ld, S, scrA, slot); st != SBO_OK) {
+        (void)hipStreamSynchronize(ctx->aux_stream);
+        return st;
+    }
+    SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
+    return inverse_second_half(ctx, ctx->blas, Li, n, ld, S, nullptr, slot, true);
 }
 
 sbo_status check_hyper(sbo_ctx *ctx, const sbo_hyper &h) {
@@ -436,15 +484,15 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                 SBO_HIP(hipMemset2DAsync(Li + h * ld, sizeof(double) * (size_t)ld, 0, sizeof(double) * (size_t)h,
                                          (size_t)(n - h), ctx->stream));
                 int slot = ctx->inv_slot;
-                if (sbo_status st = inverse_second_half(ctx, ctx->blas, Li, n, ld, ctx->scratch.as<double>(), slot);
+                if (sbo_status st = inverse_second_half(ctx, ctx->blas, Li, n, ld, ctx->scratch.as<double>(),
+                                                        ctx->scratch.as<double>() + h * (n - h), slot);
                     st != SBO_OK)
                     return st;
             } else if (ctx->inverse_rec) {
                 SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
-                SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max<int64_t>(inverse_scratch(n), 1)));
-                int slot = 0;
-                if (sbo_status st = inverse_lower_f64(ctx, ctx->blas, Li, n, ld, ctx->scratch.as<double>(), slot);
-                    st != SBO_OK)
+                SBO_HIP(ctx->scratch.reserve(sizeof(double) *
+                                             (size_t)std::max<int64_t>(inverse_scratch_par(n, ctx->inv_base), 1)));
+                if (sbo_status st = inverse_lower_f64_par(ctx, Li, n, ld, ctx->scratch.as<double>()); st != SBO_OK)
                     return st;
             } else {
                 SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
@@ -660,7 +708,7 @@ sbo_status probe_precision(sbo_ctx *ctx) {
 sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_int *info, bool early_inv = false) {
     SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), ctx->stream));
     ctx->early_inv_n = 0;
-    const bool early = early_inv && ctx->inv_overlap > 0 && n > kInvBase;
+    const bool early = early_inv && ctx->inv_overlap > 0 && n > ctx->inv_base;
     const int64_t h_inv = early ? inverse_split(n) : -1;
     bool early_pending = false;
     if (early) {
@@ -687,7 +735,7 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         // every buffer the first half touches, sized before it starts (a
         // reserve that reallocates later would free memory in use)
         SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)ld * (size_t)ld));
-        SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max<int64_t>(inverse_scratch(n), 1)));
+        SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max<int64_t>(inverse_scratch(n, ctx->inv_base), 1)));
         const int64_t nslots = info_slots(n);
         SBO_HIP(ctx->info.reserve(sizeof(rocblas_int) * (size_t)nslots));
         info = ctx->info.as<rocblas_int>();
@@ -770,8 +818,10 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
                 }
                 early_pending = true;
                 int slot = 0;
+                const int64_t hq = inverse_split(n);
                 if ((st = inverse_first_half(ctx, ctx->blas_inv, ctx->Linv.as<double>(), n, ld,
-                                             ctx->scratch.as<double>(), slot)) != SBO_OK)
+                                             ctx->scratch.as<double>(),
+                                             ctx->scratch.as<double>() + hq * (n - hq), slot)) != SBO_OK)
                     break;
                 ctx->inv_slot = slot;
                 if (hipEventRecord(ctx->ev_inv, ctx->inv_stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
@@ -890,7 +940,11 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         plan.kcoord = ctx->kcoord.as<float>();
     } else if (ctx->skip_log2 < 0) {
         plan.L = precise ? ctx->p_skip_log2 : ctx->auto_skip_log2;
-        plan.L_mean = ctx->auto_skip_mean_log2;
+        // the precise sweep's mean 2^8 tighter than the budget's 2^-B sf
+        // (absolute): its tiles are the last row block's only, and the mean
+        // of an ill-conditioned fit (large |alpha|_1) otherwise sits right at
+        // its budget
+        plan.L_mean = precise ? std::min(160, ctx->auto_skip_mean_log2 + 8) : ctx->auto_skip_mean_log2;
         plan.lgn = ctx->tile_lgn.as<float4>();
         plan.levels = !precise && sbo::x3_levels(ctx->kernel_variant) ? 1 : 0;
         plan.kcoord = ctx->kcoord.as<float>();
@@ -1636,6 +1690,14 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             SBO_CHECK(sbo::variant_allowed((int)value), SBO_E_INVAL,
                       "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22)");
             ctx->kernel_variant = (int)value;
+            return SBO_OK;
+        case SBO_OPT_INV_BASE:
+            SBO_CHECK(value >= 1024 && value <= 8192, SBO_E_INVAL, "SBO_OPT_INV_BASE must be in [1024, 8192]");
+            ctx->inv_base = value;
+            return SBO_OK;
+        case SBO_OPT_INV_PANELS:
+            SBO_CHECK(value >= 1 && value <= 64, SBO_E_INVAL, "SBO_OPT_INV_PANELS must be in [1, 64]");
+            ctx->inv_panels = value;
             return SBO_OK;
         case SBO_OPT_CHOL_GEMM:
             SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_CHOL_GEMM must be 0, 1 or 2");

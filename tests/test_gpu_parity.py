@@ -68,6 +68,24 @@ def oracle_given_factor(gm, wl, qx=None, qy=None):
                      h.length_scale, h.sf2, h.prior_mean)
 
 
+def oracle_given_factor64(gm, wl, qx=None, qy=None):
+    """The same with alpha solved in f64 from the device's factor, L L^T alpha
+    = y - m0: the posterior of the device factor that the precise sweep
+    targets (its mean uses the f64 alpha from the f64 inverse; the device's
+    f32 alpha differs from it by its own rounding times |K*|)."""
+    from scipy.linalg import solve_triangular
+    L, _ = gm.factor()
+    o = gm.order()
+    L64 = L.astype(np.float64)
+    h = wl.hyper
+    r = f32(wl.obs)[o].astype(np.float64) - h.prior_mean
+    alpha = solve_triangular(L64.T, solve_triangular(L64, r, lower=True), lower=False)
+    Lcm = O.colmajor_from_lower(L64)
+    qx = wl.qx if qx is None else qx
+    qy = wl.qy if qy is None else qy
+    return O.predict(Lcm, alpha, f32(wl.x)[o], f32(wl.y)[o], f32(qx), f32(qy), h.length_scale, h.sf2, h.prior_mean)
+
+
 # ------------------------------------------------------------------ (1) fill
 @pytest.mark.parametrize("n", [1, 3, 129, 1000, 2048])
 def test_fill_ulp(mapper, n):
@@ -973,6 +991,17 @@ def test_recursive_inverse_matches_dtrtri(mapper, n):
         got[rec] = np.tril(A)
     gm.set_option(N.SBO_OPT_INVERSE, 1)
     assert np.abs(got[0] - got[1]).max() <= 2e-6 * np.abs(got[0]).max()
+    # the recursion's tuning (base-case size, panels per product) changes f64 rounding only
+    for base, panels in ((1024, 4), (4096, 16)):
+        gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+        gm.set_option(N.SBO_OPT_INV_BASE, base)
+        gm.set_option(N.SBO_OPT_INV_PANELS, panels)
+        gm.fit(wl.x, wl.y, wl.obs)
+        A = np.zeros((n, n), np.float32)
+        gm.ctx.check(N.lib().sbo_get_inverse(gm.ctx.handle, A.ctypes.data))
+        assert np.abs(np.tril(A) - got[1]).max() <= 2e-6 * np.abs(got[1]).max(), (base, panels)
+    gm.set_option(N.SBO_OPT_INV_BASE, 2048)
+    gm.set_option(N.SBO_OPT_INV_PANELS, 16)
 
 
 @pytest.mark.parametrize("n", [4100, 5000])
@@ -1211,9 +1240,12 @@ def test_precision_levels(mapper):
 @pytest.mark.parametrize("n,gw,gh,box", [(2048, 64, 48, False), (3000, 90, 70, True), (700, 40, 30, True)])
 def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box):
     """SBO_OPT_PRECISION = 1: A = sf2 L^-1 in f64, K* in f64, f64 MFMA and sums
-    -- against the fp64 oracle given the same factor to f64-level agreement
-    (the budgeted skip at 2^-B of the smallest probe variance), on the
-    default domain and on the lpsc.yaml box (dense data, small variance)."""
+    -- against the fp64 oracle given the same factor, alpha solved from it in
+    f64 (the f32 alpha the fast sweep uses would add its own rounding times
+    |K*| to the mean: 1.5e-6 after the N = 700 box's append), to f64-level
+    agreement (the budgeted skip at 2^-B of the smallest probe variance), on
+    the default domain and on the lpsc.yaml box (dense data, small
+    variance)."""
     from safe_bayesian_optimization_amd.terrain import synthetic_box
     wl = synthetic_box(n, gw, gh, seed=n) if box else synthetic(n, gw, gh, seed=n + 1)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
@@ -1225,7 +1257,7 @@ def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box):
         out = dict(mu=np.empty(wl.qx.size, np.float32), sd=np.empty(wl.qx.size, np.float32),
                    lo=np.empty(wl.qx.size), hi=np.empty(wl.qx.size), safe=np.empty(wl.qx.size, np.uint8))
         key = gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
-        omu, ovar = oracle_given_factor(gm, wl)
+        omu, ovar = oracle_given_factor64(gm, wl)
         emu, evar = nrel(out["mu"], omu), nrel(out["sd"].astype(np.float64) ** 2, ovar)
         print(f"precise N={n} box={box}: mu {emu:.2e} var {evar:.2e} (fast sweep on the probe: {perr:.2e}, "
               f"probe var {vmin:.2e}..{vmax:.2e})")
@@ -1239,7 +1271,7 @@ def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box):
         mu2, sd2 = gm.predict(wl.qx, wl.qy)
         wl2 = type(wl)(wl.name, np.concatenate([wl.x, wl.x[:37] + 0.013]), np.concatenate([wl.y, wl.y[:37]]),
                        np.concatenate([wl.obs, wl.obs[:37]]), wl.qx, wl.qy, gw, gh, wl.hyper, wl.f_min)
-        omu2, ovar2 = oracle_given_factor(gm, wl2)
+        omu2, ovar2 = oracle_given_factor64(gm, wl2)
         assert nrel(mu2, omu2) < 1e-6 and nrel(sd2.astype(np.float64) ** 2, ovar2) < 1e-6
     finally:
         gm.set_option(N.SBO_OPT_PRECISION, -1)
