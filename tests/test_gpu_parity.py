@@ -895,6 +895,30 @@ def test_append_matches_refit(mapper):
     gm.set_option(N.SBO_OPT_RESORT, 25)
 
 
+def test_append_large_batch(mapper):
+    """A batch wider than the Cholesky's 512-column outer panel (b = 700):
+    the appended block is factored in two levels too (its own look-ahead and
+    rank-512 trailing update); the posterior equals the oracle's given the
+    factor and a refit's."""
+    wl = synthetic(1200, 32, 32, seed=21)
+    n0 = 500
+    gm = TerrainMapper(0, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_RESORT, 0)
+    try:
+        gm.fit(wl.x[:n0], wl.y[:n0], wl.obs[:n0])
+        gm.append(wl.x[n0:], wl.y[n0:], wl.obs[n0:])
+        assert gm.n == 1200
+        mu_a, sd_a = gm.predict(wl.qx, wl.qy)
+        omu, ovar = oracle_given_factor(gm, wl)
+        assert nrel(mu_a, omu) < REL_TOL and nrel(sd_a.astype(np.float64) ** 2, ovar) < REL_TOL
+        ref = TerrainMapper(0, ctx=mapper.ctx)
+        ref.fit(wl.x, wl.y, wl.obs)
+        mu_r, sd_r = ref.predict(wl.qx, wl.qy)
+        assert nrel(mu_a, mu_r) < 1e-4 and nrel(sd_a.astype(np.float64) ** 2, sd_r.astype(np.float64) ** 2) < 1e-4
+    finally:
+        gm.set_option(N.SBO_OPT_RESORT, 25)
+
+
 def _tick_tiles(gm, wl):
     lib = N.lib()
     lib.sbo_profile(gm.ctx.handle, 1)
