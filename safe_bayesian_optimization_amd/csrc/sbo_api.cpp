@@ -109,13 +109,24 @@ sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_
                              int &slot);
 
 // A^-1 (recursion scratch scr), then S = B A^-1
+// dgemm panel width of a product of the recursion at split h: h / panels,
+// at least 512 columns -- and at least 1024 for 2048 < h <= 6144, where
+// rocBLAS dgemm with ~4096 rows and fewer than 1024 columns at K > 2048 ran
+// at half speed (38.5 vs 76.5 TF at 4096 x 512 x 4096 against 4096 x 1024 x
+// 4096, tools/r3_dgemm_probe.cpp, profiles/r3_dgemm_probe.log)
+int64_t inverse_panel(const sbo_ctx *ctx, int64_t h) {
+    int64_t nb = std::max<int64_t>(512, sbo::round_up(h / ctx->inv_panels, 128));
+    if (h > 2048 && h <= 6144) nb = std::max<int64_t>(nb, 1024);
+    return nb;
+}
+
 sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
                               double *scr, int &slot) {
     const int64_t h = inverse_split(n), m = n - h;
     if (sbo_status st = inverse_lower_f64(ctx, hb, Li, h, ld, scr, slot); st != SBO_OK) return st;
     SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
     const double one = 1.0, zero = 0.0;
-    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / ctx->inv_panels, 128));
+    const int64_t nb = inverse_panel(ctx, h);
     for (int64_t p0 = 0; p0 < h; p0 += nb) {
         const int64_t w = std::min(nb, h - p0);
         SBO_BLAS(rocblas_dgemm(hb, rocblas_operation_none, rocblas_operation_none, (rocblas_int)m, (rocblas_int)w,
@@ -134,7 +145,7 @@ sbo_status inverse_second_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int6
         if (sbo_status st = inverse_lower_f64(ctx, hb, C, m, ld, scr, slot); st != SBO_OK) return st;
     SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
     const double minus_one = -1.0, zero = 0.0;
-    const int64_t nb = std::max<int64_t>(512, sbo::round_up(h / ctx->inv_panels, 128));
+    const int64_t nb = inverse_panel(ctx, h);
     for (int64_t p0 = 0; p0 < m; p0 += nb) {
         const int64_t w = std::min(nb, m - p0);
         SBO_BLAS(rocblas_dgemm(hb, rocblas_operation_none, rocblas_operation_none, (rocblas_int)w, (rocblas_int)h,
