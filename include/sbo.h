@@ -388,13 +388,17 @@ SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t
  * than ssyrk (the fit's time is the same: those run beside the chain).  All
  * compute in f32 with exact f32 products; the factors agree to f32 rounding. */
 #define SBO_OPT_CHOL_GEMM 17
-/* SBO_OPT_INV_BASE (default 2048, in [1024, 8192]) and SBO_OPT_INV_PANELS
- * (default 16, in [1, 64]): the recursive f64 inverse's base-case size (rocSOLVER
- * dtrtri) and the number of dgemm panels each of its products is cut into
- * (fewer panels: larger GEMMs, more multiplied zeros).  Tuning only; the
- * inverse agrees to f64 rounding. */
+/* SBO_OPT_INV_BASE (default 2048, in [1024, 8192], rounded down to a multiple
+ * of 128) and SBO_OPT_INV_PANELS (default 16, in [1, 64]): the recursive f64
+ * inverse's base-case size (rocSOLVER dtrtri on the diagonal blocks at
+ * multiples of it) and the number of dgemm panels each of its products is cut
+ * into (fewer panels: larger GEMMs, more multiplied zeros).  SBO_OPT_INV_LEAVES
+ * (default 1): every base case up front in one strided-batched dtrtri (0: one
+ * call per base case inside the recursion).  Tuning only; the inverse agrees
+ * to f64 rounding. */
 #define SBO_OPT_INV_BASE 18
 #define SBO_OPT_INV_PANELS 19
+#define SBO_OPT_INV_LEAVES 20
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe

@@ -53,6 +53,7 @@ SBO_OPT_CHOL_DIAG = 16
 SBO_OPT_CHOL_GEMM = 17
 SBO_OPT_INV_BASE = 18
 SBO_OPT_INV_PANELS = 19
+SBO_OPT_INV_LEAVES = 20
 
 
 class SboError(RuntimeError):

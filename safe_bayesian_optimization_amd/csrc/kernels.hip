@@ -2252,6 +2252,22 @@ hipError_t launch_copy_lower(hipStream_t s, const float *src, int64_t ld_src, in
     return hipGetLastError();
 }
 
+hipError_t launch_pack_tiles(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
+                             double sf2, float *aug) {
+    const int64_t nI = npad / kBM;
+    if (I0 >= nI) return hipSuccess;
+    hipLaunchKernelGGL(pack_operand_kernel<double>, dim3((unsigned)(nI * kTilesPerRowBlockStep), (unsigned)(nI - I0)),
+                       dim3(256), 0, s, Linv, ld, n, sf2, I0, aug);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_kcoord(hipStream_t s, const float *x, const float *y, const float *alpha, int64_t n,
+                              int64_t npad, double sf2, float *kcoord) {
+    hipLaunchKernelGGL(pack_kcoord_kernel, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, s, x, y, alpha, n, npad,
+                       (float)sf2, kcoord);
+    return hipGetLastError();
+}
+
 template <class T>
 hipError_t launch_pack_operand_t(hipStream_t s, const T *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
                                  double sf2, const float *x, const float *y, const float *alpha, float *aug,

@@ -85,23 +85,27 @@ int64_t info_slots(int64_t n) { return std::max<int64_t>(64, n / 512 + 2); }
 // that info_slots holds; SBO_OPT_INV_PANELS: the products' panels per half,
 // default 16, at least 512 columns each: C4 warm fit 58.0 ms at 8 panels,
 // 56.0 at 16; a 256-column floor: 59.8 at 16, 68 at 32, profiles/r3_fit_invtune*.log)
-int64_t inverse_split(int64_t n) { return sbo::round_up(n / 2, 128); }
+// The split lands on a multiple of the base size b (SBO_OPT_INV_BASE, a
+// multiple of 128): every base case is then a b x b diagonal block at a
+// multiple of b (the last one partial), so all of them can be inverted up
+// front in one batched rocSOLVER call (inverse_leaves).
+int64_t inverse_split(int64_t n, int64_t b) { return ((n + b - 1) / b + 1) / 2 * b; }
 
 int64_t inverse_scratch(int64_t n, int64_t base) {
     if (n <= base) return 0;
-    const int64_t h = inverse_split(n), m = n - h;
+    const int64_t h = inverse_split(n, base), m = n - h;
     return h * m + std::max(inverse_scratch(h, base), inverse_scratch(m, base));
 }
 // with the two halves' inverses side by side (inverse_lower_f64_par)
 int64_t inverse_scratch_par(int64_t n, int64_t base) {
     if (n <= base) return 0;
-    const int64_t h = inverse_split(n), m = n - h;
+    const int64_t h = inverse_split(n, base), m = n - h;
     return h * m + inverse_scratch(h, base) + inverse_scratch(m, base);
 }
 // dtrtri base cases of an n-column recursion (one info slot each)
 int inverse_base_cases(int64_t n, int64_t base) {
     if (n <= base) return 1;
-    const int64_t h = inverse_split(n);
+    const int64_t h = inverse_split(n, base);
     return inverse_base_cases(h, base) + inverse_base_cases(n - h, base);
 }
 
@@ -121,9 +125,10 @@ int64_t inverse_panel(const sbo_ctx *ctx, int64_t h) {
 }
 
 sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                              double *scr, int &slot) {
-    const int64_t h = inverse_split(n), m = n - h;
-    if (sbo_status st = inverse_lower_f64(ctx, hb, Li, h, ld, scr, slot); st != SBO_OK) return st;
+                              double *scr, int &slot, bool a_done = false) {
+    const int64_t h = inverse_split(n, ctx->inv_base), m = n - h;
+    if (!a_done)
+        if (sbo_status st = inverse_lower_f64(ctx, hb, Li, h, ld, scr, slot); st != SBO_OK) return st;
     SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
     const double one = 1.0, zero = 0.0;
     const int64_t nb = inverse_panel(ctx, h);
@@ -139,7 +144,7 @@ sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64
 // C^-1 (recursion scratch scr; skipped when c_done), then X21 = -C^-1 S
 sbo_status inverse_second_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
                                double *scr, int &slot, bool c_done = false) {
-    const int64_t h = inverse_split(n), m = n - h;
+    const int64_t h = inverse_split(n, ctx->inv_base), m = n - h;
     double *B = Li + h, *C = Li + h + h * ld;
     if (!c_done)
         if (sbo_status st = inverse_lower_f64(ctx, hb, C, m, ld, scr, slot); st != SBO_OK) return st;
@@ -159,29 +164,54 @@ sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_
                              int &slot) {
     if (n <= ctx->inv_base) {
         rocblas_int *info = ctx->info.as<rocblas_int>() + 1 + slot++;
-        SBO_BLAS(rocsolver_dtrtri(hb, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
-                                  (rocblas_int)ld, info));
+        if (!ctx->inv_leaves_done)
+            SBO_BLAS(rocsolver_dtrtri(hb, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n, Li,
+                                      (rocblas_int)ld, info));
         return SBO_OK;
     }
-    const int64_t h = inverse_split(n), m = n - h;
+    const int64_t h = inverse_split(n, ctx->inv_base), m = n - h;
     if (sbo_status st = inverse_first_half(ctx, hb, Li, n, ld, S, S + h * m, slot); st != SBO_OK) return st;
     return inverse_second_half(ctx, hb, Li, n, ld, S, S + h * m, slot);
+}
+
+// Every base case of the recursion over the n columns at Li -- the b x b
+// diagonal blocks at multiples of b = inv_base, the last one partial -- in
+// one strided-batched rocSOLVER dtrtri (+ one call for the partial block),
+// info slots in the recursion's order (block k: slot k).  One at a time
+// inside the recursion each 2048 block took ~0.46 ms of mostly idle chip
+// (C4: eight of them; profiles/r3_fit_timeline_leaves.txt).
+sbo_status inverse_leaves(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld) {
+    const int64_t b = ctx->inv_base, nf = n / b, r = n - nf * b;
+    rocblas_int *info = ctx->info.as<rocblas_int>() + 1;
+    if (nf > 0)
+        SBO_BLAS(rocsolver_dtrtri_strided_batched(hb, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)b,
+                                                  Li, (rocblas_int)ld, (rocblas_stride)(b * (ld + 1)), info,
+                                                  (rocblas_int)nf));
+    if (r > 0)
+        SBO_BLAS(rocsolver_dtrtri(hb, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)r,
+                                  Li + nf * b * (ld + 1), (rocblas_int)ld, info + nf));
+    return SBO_OK;
 }
 
 // The top of the recursion with its two independent halves side by side:
 // C^-1 on aux_stream (the Cholesky's look-ahead stream and rocBLAS handle,
 // idle by now) while `stream` computes A^-1 and S = B A^-1, then X21 once
 // both are done.  The lower levels' GEMMs are too small to fill the chip on
-// their own.  Scratch: inverse_scratch_par(n); info slots as the sequential
-// recursion's (C's base cases after A's).
+// their own.  Enqueue order: A^-1 first, then C^-1, then S -- the host spends
+// ~3 ms issuing a half's ~90 rocSOLVER/rocBLAS launches, and C^-1 is needed
+// only after S (C4 trace: with C^-1 issued first, `stream` sat idle for
+// those 3 ms; profiles/r3_fit_timeline_invorder.txt).  Scratch:
+// inverse_scratch_par(n); info slots as the sequential recursion's (C's base
+// cases after A's).
 sbo_status inverse_lower_f64_par(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld, double *S) {
     int slot = 0;
     if (n <= ctx->inv_base || !ctx->blas_aux || !ctx->aux_stream || !ctx->ev_panel)
         return inverse_lower_f64(ctx, ctx->blas, Li, n, ld, S, slot);
-    const int64_t h = inverse_split(n), m = n - h;
+    const int64_t h = inverse_split(n, ctx->inv_base), m = n - h;
     double *scrA = S + h * m, *scrC = scrA + inverse_scratch(h, ctx->inv_base);
     int slotC = inverse_base_cases(h, ctx->inv_base);
     SBO_HIP(hipEventRecord(ctx->ev_panel, ctx->stream));            // Li widened
+    if (sbo_status st = inverse_lower_f64(ctx, ctx->blas, Li, h, ld, scrA, slot); st != SBO_OK) return st;
     SBO_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0));
     SBO_BLAS(rocblas_set_pointer_mode(ctx->blas_aux, rocblas_pointer_mode_host));
     if (sbo_status st = inverse_lower_f64(ctx, ctx->blas_aux, Li + h + h * ld, m, ld, scrC, slotC); st != SBO_OK) {
@@ -189,7 +219,7 @@ sbo_status inverse_lower_f64_par(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld
         return st;
     }
     SBO_HIP(hipEventRecord(ctx->ev_trail, ctx->aux_stream));
-    if (sbo_status st = inverse_first_half(ctx, ctx->blas, Li, n, ld, S, scrA, slot); st != SBO_OK) {
+    if (sbo_status st = inverse_first_half(ctx, ctx->blas, Li, n, ld, S, scrA, slot, true); st != SBO_OK) {
         (void)hipStreamSynchronize(ctx->aux_stream);
         return st;
     }
@@ -443,6 +473,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                       sizeof(float) * old_tiles * sbo::kTileFloats));
     SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
     rocblas_int hinfo = 0;
+    bool alpha_aux = false, kcoord_pending = false;
     // the inverse's first half ran beside the Cholesky (blocked_potrf): its
     // info slots 1 .. inv_slot stay, the rest are cleared
     const bool early = ctx->inverse_bits == 64 && ctx->inverse_rec && !incr && ctx->early_inv_n == n;
@@ -490,7 +521,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             if (early) {
                 // A^-1 and S = B A^-1 are done: widen the right columns (their
                 // rows 0..h-1 zero), then C^-1 and X21 = -C^-1 S
-                const int64_t h = inverse_split(n);
+                const int64_t h = inverse_split(n, ctx->inv_base);
                 SBO_HIP(sbo::launch_widen(ctx->stream, L + h + h * ld, ld, n - h, n - h, true, Li + h + h * ld, ld));
                 SBO_HIP(hipMemset2DAsync(Li + h * ld, sizeof(double) * (size_t)ld, 0, sizeof(double) * (size_t)h,
                                          (size_t)(n - h), ctx->stream));
@@ -500,11 +531,17 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                     st != SBO_OK)
                     return st;
             } else if (ctx->inverse_rec) {
-                SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
+                if (ctx->widened_n != n) SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
+                ctx->widened_n = 0;
+                if (ctx->inv_batched) {
+                    if (sbo_status st = inverse_leaves(ctx, ctx->blas, Li, n, ld); st != SBO_OK) return st;
+                }
+                ctx->inv_leaves_done = ctx->inv_batched;
                 SBO_HIP(ctx->scratch.reserve(sizeof(double) *
                                              (size_t)std::max<int64_t>(inverse_scratch_par(n, ctx->inv_base), 1)));
-                if (sbo_status st = inverse_lower_f64_par(ctx, Li, n, ld, ctx->scratch.as<double>()); st != SBO_OK)
-                    return st;
+                const sbo_status st = inverse_lower_f64_par(ctx, Li, n, ld, ctx->scratch.as<double>());
+                ctx->inv_leaves_done = false;
+                if (st != SBO_OK) return st;
             } else {
                 SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
                 SBO_BLAS(rocsolver_dtrtri(ctx->blas, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)n,
@@ -514,22 +551,30 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         ctx->linv_n = n;
         // alpha = K^-1 (y - m0) = L^-T L^-1 (y - m0), in f64 from the f64
         // inverse: two triangular matrix-vector products (bandwidth-bound and
-        // parallel, unlike the two sequential triangular solves of spotrs)
-        SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)std::max(npad, n)));
-        double *d = ctx->scratch.as<double>();
-        SBO_HIP(sbo::launch_widen_sub(ctx->stream, ctx->obs.as<float>(), ctx->hyper.prior_mean, n, d));
-        SBO_BLAS(rocblas_dtrmv(ctx->blas, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit,
+        // parallel, unlike the two sequential triangular solves of spotrs),
+        // into alpha64 (the precise sweep's mean uses alpha in f64).  They
+        // only feed the coordinate pack: on aux_stream (blas_aux) beside the
+        // operand pack, row sums and tile norms, which read only L^-1 (C4:
+        // 0.75 ms off the fit's critical path).
+        SBO_HIP(ctx->alpha64.reserve(sizeof(double) * (size_t)std::max(npad, ld)));
+        double *d = ctx->alpha64.as<double>();
+        alpha_aux = ctx->blas_aux && ctx->aux_stream && ctx->ev_panel;
+        hipStream_t sa = alpha_aux ? ctx->aux_stream : ctx->stream;
+        rocblas_handle ha = alpha_aux ? ctx->blas_aux : ctx->blas;
+        if (alpha_aux) {
+            SBO_HIP(hipEventRecord(ctx->ev_panel, ctx->stream));
+            SBO_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0));
+        }
+        SBO_HIP(sbo::launch_widen_sub(sa, ctx->obs.as<float>(), ctx->hyper.prior_mean, n, d));
+        SBO_BLAS(rocblas_dtrmv(ha, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit,
                                (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
-        SBO_BLAS(rocblas_dtrmv(ctx->blas, rocblas_fill_lower, rocblas_operation_transpose, rocblas_diagonal_non_unit,
+        SBO_BLAS(rocblas_dtrmv(ha, rocblas_fill_lower, rocblas_operation_transpose, rocblas_diagonal_non_unit,
                                (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
-        SBO_HIP(sbo::launch_narrow(ctx->stream, d, n, alpha));
-        // (the precise sweep's mean uses alpha in f64)
-        SBO_HIP(ctx->alpha64.reserve(sizeof(double) * (size_t)ld));
-        SBO_HIP(hipMemcpyAsync(ctx->alpha64.as<double>(), d, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice,
-                               ctx->stream));
+        SBO_HIP(sbo::launch_narrow(sa, d, n, alpha));
+        if (alpha_aux) SBO_HIP(hipEventRecord(ctx->ev_trail, ctx->aux_stream));
         ctx->a64_I0 = std::min(ctx->a64_I0, I0);
-        SBO_HIP(sbo::launch_pack_operand(ctx->stream, Li, ld, n, npad, I0, sf2, ctx->x.as<float>(),
-                                         ctx->y.as<float>(), alpha, ctx->aug.as<float>(), ctx->kcoord.as<float>()));
+        SBO_HIP(sbo::launch_pack_tiles(ctx->stream, Li, ld, n, npad, I0, sf2, ctx->aug.as<float>()));
+        kcoord_pending = true;
     } else {
         ctx->linv_n = 0;
         // alpha = K^-1 (y - m0) by the f32 triangular solves
@@ -565,6 +610,11 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         SBO_HIP(grow_keep(ctx, ctx->tile_lgn, 2 * sizeof(float4) * (size_t)sbo::total_tiles(nI),
                           2 * sizeof(float4) * old_tiles));
         SBO_HIP(sbo::launch_tile_norms(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->tile_lgn.as<float4>()));
+        if (kcoord_pending) {
+            if (alpha_aux) SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
+            SBO_HIP(sbo::launch_pack_kcoord(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), alpha, n, npad, sf2,
+                                            ctx->kcoord.as<float>()));
+        }
         const int64_t r0 = I0 * sbo::kBM;
         std::vector<double> rl1((size_t)(npad - r0));
         std::vector<float> ha((size_t)n);
@@ -666,6 +716,21 @@ sbo_status probe_precision(sbo_ctx *ctx) {
         ctx->prof = false;  // (the probe is not a tick: no events, no counters)
         sbo_status st = run_tick(ctx, qx, qy, M, 0.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, sdf, nullptr, nullptr,
                                  nullptr, key, nullptr, kSweepFast);
+        if (st == SBO_OK) {
+            // the reference's budget: 2^-30 of the largest variance the fast
+            // sweep sees (its own error is orders below that: any estimate
+            // within 2x serves), so the reference moves the measured error by
+            // < 1e-9 of max var against the 7e-6 threshold; at most 2^-30 sf2,
+            // at least 2^-60 sf2 (was a fixed 2^-44 sf2: C4 probe 4.8 -> see
+            // DESIGN.md section 5a)
+            const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
+            if (hipMemcpyAsync(h.data(), sdf, sizeof(float) * M, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                hipStreamSynchronize(ctx->stream) != hipSuccess)
+                st = SBO_E_DEVICE;
+            double vf = 0.0;
+            for (int i = 0; i < M; ++i) vf = std::max(vf, (double)h[i] * h[i]);
+            ctx->probe_ref_tol = std::ldexp(std::clamp(std::isfinite(vf) ? vf : sf2, std::ldexp(sf2, -30), sf2), -30);
+        }
         if (st == SBO_OK)
             st = run_tick(ctx, qx, qy, M, 0.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, sdp, nullptr, nullptr, nullptr, key,
                           nullptr, kSweepPreciseDense);
@@ -709,7 +774,7 @@ sbo_status probe_precision(sbo_ctx *ctx) {
 //
 // early_inv (a fit with the recursive f64 inverse and SBO_OPT_INV_OVERLAP =
 // R > 0): once the panel of the block column that ends at h =
-// inverse_split(n) is done, the factor's left h columns are final, and the
+// inverse_split(n, inv_base) is done, the factor's left h columns are final, and the
 // inverse's first half (widen them, A^-1, S = B A^-1: half its flops) runs on
 // inv_stream with its own rocBLAS handle beside the Cholesky's last steps,
 // which leave most CUs idle (one-workgroup diagonal blocks, small trailing
@@ -720,7 +785,7 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
     SBO_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), ctx->stream));
     ctx->early_inv_n = 0;
     const bool early = early_inv && ctx->inv_overlap > 0 && n > ctx->inv_base;
-    const int64_t h_inv = early ? inverse_split(n) : -1;
+    const int64_t h_inv = early ? inverse_split(n, ctx->inv_base) : -1;
     bool early_pending = false;
     if (early) {
         if (ctx->inv_stream && ctx->inv_reserved != ctx->inv_overlap) {
@@ -780,6 +845,19 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         SBO_BLAS(rocblas_set_stream(ctx->blas_aux, ctx->aux_stream));
     }
     SBO_BLAS(rocblas_set_pointer_mode(ctx->blas_aux, rocblas_pointer_mode_host));
+    // The f64 copy of the factor the inverse starts from (refresh_operand),
+    // widened panel by panel as outer panels become final: on aux_stream
+    // after each trailing update, beside the chain's latency-bound second
+    // half, instead of one 0.7 ms pass between the factorization and the
+    // inverse (C4).  The strictly upper part is zeroed with it.
+    const bool wid = early_inv && !early;
+    double *Lw = nullptr;
+    int64_t Kw = 0;   // columns [0, Kw) widened (enqueued)
+    if (wid) {
+        SBO_HIP(ctx->Linv.reserve(sizeof(double) * (size_t)ld * (size_t)ld));
+        Lw = ctx->Linv.as<double>();
+    }
+    ctx->widened_n = 0;
     const float one = 1.0f, minus_one = -1.0f;
     // Two levels (SBO_OPT_CHOL_OUTER = NB2 > kCholNB): outer panels of NB2
     // columns, each factored by the kCholNB chain above with its updates kept
@@ -829,7 +907,7 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
                 }
                 early_pending = true;
                 int slot = 0;
-                const int64_t hq = inverse_split(n);
+                const int64_t hq = inverse_split(n, ctx->inv_base);
                 if ((st = inverse_first_half(ctx, ctx->blas_inv, ctx->Linv.as<double>(), n, ld,
                                              ctx->scratch.as<double>(),
                                              ctx->scratch.as<double>() + hq * (n - hq), slot)) != SBO_OK)
@@ -889,6 +967,19 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
             trail_pending = true;
             if (hipEventRecord(ctx->ev_trail, ctx->aux_stream) != hipSuccess) { st = SBO_E_DEVICE; break; }
         }
+        if (wid) {
+            // this outer panel's columns are final (ev_panel); ev_trail above
+            // leaves the widen off the look-ahead's dependency chain
+            if ((m4 <= 0 && hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0) != hipSuccess) ||
+                sbo::launch_widen(ctx->aux_stream, L + K + K * ld, ld, n - K, W, true, Lw + K + K * ld, ld) !=
+                    hipSuccess ||
+                (K > 0 && hipMemset2DAsync(Lw + K * ld, sizeof(double) * (size_t)ld, 0, sizeof(double) * (size_t)K,
+                                           (size_t)W, ctx->aux_stream) != hipSuccess)) {
+                st = SBO_E_DEVICE;
+                break;
+            }
+            Kw = K + W;
+        }
     }
     if (st != SBO_OK) {
         (void)hipStreamSynchronize(ctx->aux_stream);
@@ -897,6 +988,16 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         return st;
     }
     if (trail_pending) SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
+    if (wid) {
+        // the last outer panel here; the aux_stream widens before it
+        SBO_HIP(sbo::launch_widen(ctx->stream, L + Kw + Kw * ld, ld, n - Kw, n - Kw, true, Lw + Kw + Kw * ld, ld));
+        if (Kw > 0)
+            SBO_HIP(hipMemset2DAsync(Lw + Kw * ld, sizeof(double) * (size_t)ld, 0, sizeof(double) * (size_t)Kw,
+                                     (size_t)(n - Kw), ctx->stream));
+        SBO_HIP(hipEventRecord(ctx->ev_trail, ctx->aux_stream));
+        SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
+        ctx->widened_n = n;
+    }
     if (early_pending) {
         SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_inv, 0));
         ctx->early_inv_n = n;
@@ -906,6 +1007,7 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
 
 sbo_status factor_and_refresh(sbo_ctx *ctx) {
     rocblas_int *info = ctx->info.as<rocblas_int>();
+    ctx->widened_n = 0;
     if (ctx->chol_blocked) {
         const bool early_inv = ctx->inverse_bits == 64 && ctx->inverse_rec;
         if (sbo_status st = blocked_potrf(ctx, ctx->L.as<float>(), ctx->n, ctx->cap, info, early_inv); st != SBO_OK)
@@ -942,10 +1044,9 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     int64_t ms = m;
     sbo::SkipPlan plan;
     if (sweep == kSweepPreciseDense) {
-        // the probe's reference: the precise sweep under a budget of 2^-44 sf2
-        // on any variance (5.7e-14 sf2: far below the probe's resolution of
-        // the fast sweep's error for any variance above ~1e-8 sf2)
-        skip_budget_for(ctx, std::ldexp(ctx->hyper.sigma_f * ctx->hyper.sigma_f, -44), plan.L, plan.lg_tau_v);
+        // the probe's reference: the precise sweep under a budget of 2^-30 of
+        // the largest variance the probe's fast sweep saw (probe_precision)
+        skip_budget_for(ctx, ctx->probe_ref_tol, plan.L, plan.lg_tau_v);
         plan.L_mean = ctx->auto_skip_mean_log2;
         plan.lgn = ctx->tile_lgn.as<float4>();
         plan.kcoord = ctx->kcoord.as<float>();
@@ -1704,7 +1805,11 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             return SBO_OK;
         case SBO_OPT_INV_BASE:
             SBO_CHECK(value >= 1024 && value <= 8192, SBO_E_INVAL, "SBO_OPT_INV_BASE must be in [1024, 8192]");
-            ctx->inv_base = value;
+            ctx->inv_base = value / 128 * 128;   // (the split lands on multiples of it: Cholesky block columns)
+            return SBO_OK;
+        case SBO_OPT_INV_LEAVES:
+            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_INV_LEAVES must be 0 or 1");
+            ctx->inv_batched = value == 1;
             return SBO_OK;
         case SBO_OPT_INV_PANELS:
             SBO_CHECK(value >= 1 && value <= 64, SBO_E_INVAL, "SBO_OPT_INV_PANELS must be in [1, 64]");

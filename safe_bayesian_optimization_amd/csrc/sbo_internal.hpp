@@ -177,6 +177,10 @@ struct sbo_ctx {
     int64_t a64_I0 = 0;          // first row block whose f64 operand is stale
     int64_t probe_n = 0;         // training points at the last probe (0: none)
     double probe_err = -1.0, probe_vmin = 0.0, probe_vmax = 0.0;  // fast sweep's error on the probe, var range
+    bool inv_batched = true;      // SBO_OPT_INV_LEAVES: the recursion's base cases in one batched dtrtri
+    bool inv_leaves_done = false; // (set while a recursion runs whose base cases are already inverted)
+    int64_t widened_n = 0;       // blocked_potrf widened the factor into Linv (n) for refresh_operand
+    double probe_ref_tol = 0.0;  // the probe reference sweep's skip budget (absolute variance)
     int p_skip_log2 = 160;       // the precise plan's cutoffs and budget (2^-B of the probe's smallest variance)
     float p_lg_tau_v = -1000.0f;
     sbo::DevBuf qprobe, oprobe;  // probe grid and outputs
@@ -211,6 +215,12 @@ hipError_t launch_copy_lower(hipStream_t s, const float *src, int64_t ld_src, in
 // Pack A = sf2 * L^-1 (from an f32 or f64 inverse, lower, column-major) into
 // [BK][BM] tiles for row blocks I >= I0 (earlier row blocks are left as they
 // are), plus per-k coordinates and sf2 * alpha for all k.
+// the two halves of launch_pack_operand (f64 inverse): the operand tiles, and the
+// per-k-tile coordinates + sf2 alpha (which waits for alpha)
+hipError_t launch_pack_tiles(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
+                             double sf2, float *aug);
+hipError_t launch_pack_kcoord(hipStream_t s, const float *x, const float *y, const float *alpha, int64_t n,
+                              int64_t npad, double sf2, float *kcoord);
 hipError_t launch_pack_operand(hipStream_t s, const float *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
                                double sf2, const float *x, const float *y, const float *alpha, float *aug,
                                float *kcoord);

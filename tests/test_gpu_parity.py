@@ -991,7 +991,7 @@ def test_append_incremental_inverse(mapper):
 def test_recursive_inverse_matches_dtrtri(mapper, n):
     """The fit's f64 L^-1 by the library's block recursion (SBO_OPT_INVERSE =
     1, default: panelled dgemms over the triangles' nonzero parts, rocSOLVER
-    dtrtri on <= 2048 diagonal blocks) and by rocsolver_dtrtri on the whole
+    dtrtri on the 2048 diagonal blocks, batched) and by rocsolver_dtrtri on the whole
     factor (0): both equal sf2 * inv(L) of the device factor to f32 rounding
     of the packed operand, and the posterior agrees with the oracle."""
     from scipy.linalg import solve_triangular
@@ -1015,17 +1015,22 @@ def test_recursive_inverse_matches_dtrtri(mapper, n):
         got[rec] = np.tril(A)
     gm.set_option(N.SBO_OPT_INVERSE, 1)
     assert np.abs(got[0] - got[1]).max() <= 2e-6 * np.abs(got[0]).max()
-    # the recursion's tuning (base-case size, panels per product) changes f64 rounding only
-    for base, panels in ((1024, 4), (4096, 16)):
+    # the recursion's tuning (base-case size -- 1100 rounds down to 1024 --,
+    # panels per product, base cases batched up front or one by one) changes
+    # f64 rounding only
+    for base, panels, leaves in ((1024, 4, 1), (1100, 16, 0), (4096, 16, 1), (2048, 16, 0)):
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
         gm.set_option(N.SBO_OPT_INV_BASE, base)
         gm.set_option(N.SBO_OPT_INV_PANELS, panels)
+        gm.set_option(N.SBO_OPT_INV_LEAVES, leaves)
         gm.fit(wl.x, wl.y, wl.obs)
         A = np.zeros((n, n), np.float32)
         gm.ctx.check(N.lib().sbo_get_inverse(gm.ctx.handle, A.ctypes.data))
-        assert np.abs(np.tril(A) - got[1]).max() <= 2e-6 * np.abs(got[1]).max(), (base, panels)
+        assert np.abs(np.tril(A) - got[1]).max() <= 2e-6 * np.abs(got[1]).max(), (base, panels, leaves)
+        assert not np.triu(A, 1).any()
     gm.set_option(N.SBO_OPT_INV_BASE, 2048)
     gm.set_option(N.SBO_OPT_INV_PANELS, 16)
+    gm.set_option(N.SBO_OPT_INV_LEAVES, 1)
 
 
 @pytest.mark.parametrize("n", [4100, 5000])
