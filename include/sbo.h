@@ -245,6 +245,12 @@ SBO_API sbo_status sbo_rbf_fill(sbo_ctx *ctx, const float *x, const float *y, in
  * zeroed) and alpha (n), both in the internal training order (sbo_get_order). */
 SBO_API sbo_status sbo_get_factor(sbo_ctx *ctx, float *L, float *alpha, uint32_t flags);
 
+/* The k-d order sbo_fit stores host points in (SBO_OPT_SPATIAL_ORDER 3):
+ * perm[j] = the caller's index of stored row j, for n points whose first lands
+ * at position first_offset of a 64-point k-tile (0 for a fit; sbo_append's
+ * batch starts at the current N).  Host pointers, no context, no device. */
+SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64_t first_offset, int64_t *perm);
+
 /* Options.  SBO_OPT_INVERSE_BITS (32 | 64, default 64): precision in which
  * L^-1 is computed before sf2 * L^-1 is rounded to f32 for the predictive
  * sweep (64 = widen L, rocsolver_dtrtri; 32 = rocsolver_strtri).  Takes

@@ -312,14 +312,16 @@ void kd_rec(KdPoint *p, int64_t cnt, int64_t off, int par) {
         std::nth_element(p, p + left, p + cnt,
                          [](const KdPoint &a, const KdPoint &b) { return a.y < b.y || (a.y == b.y && a.i < b.i); });
     const int64_t off2 = (off + left) % sbo::kBK;
+    std::thread t;
     if (par > 0 && cnt >= 4096) {
-        std::thread t([=] { kd_rec(p, left, off, par - 1); });
-        kd_rec(p + left, cnt - left, off2, par - 1);
-        t.join();
-    } else {
-        kd_rec(p, left, off, 0);
-        kd_rec(p + left, cnt - left, off2, 0);
+        try {
+            t = std::thread([=] { kd_rec(p, left, off, par - 1); });
+        } catch (...) {  // no thread to be had: this one does both halves (same order)
+        }
     }
+    if (!t.joinable()) kd_rec(p, left, off, 0);
+    kd_rec(p + left, cnt - left, off2, t.joinable() ? par - 1 : 0);
+    if (t.joinable()) t.join();
 }
 void kd_order(const std::vector<float> &hx, const std::vector<float> &hy, int64_t *perm, int64_t cnt, int64_t off) {
     auto key = [](float v) { return std::isfinite(v) ? v : -std::numeric_limits<float>::max(); };
@@ -1914,6 +1916,19 @@ SBO_API sbo_status sbo_get_order(const sbo_ctx *ctx, int64_t *order) {
     if (!ctx || !order) return SBO_E_INVAL;
     if (!ctx->fitted) return SBO_E_STATE;
     std::copy(ctx->order.begin(), ctx->order.begin() + ctx->n, order);
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64_t first_offset, int64_t *perm) {
+    if (n < 0 || (n > 0 && (!x || !y || !perm)) || first_offset < 0) return SBO_E_INVAL;
+    if (n == 0) return SBO_OK;
+    try {
+        std::vector<float> hx(x, x + n), hy(y, y + n);
+        for (int64_t i = 0; i < n; ++i) perm[i] = i;
+        kd_order(hx, hy, perm, n, first_offset % sbo::kBK);
+    } catch (...) {
+        return SBO_E_OOM;
+    }
     return SBO_OK;
 }
 
