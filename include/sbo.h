@@ -296,11 +296,6 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * eight waves per CU; with the automatic cutoff the tile plan runs tiles
  * whose share of the variance is small at three or one product(s), charged
  * to the same error budget as the skipped tiles (SBO_OPT_SKIP_BUDGET);
- * on raster-grid queries (SBO_OPT_QUERY_ORDER 1) it builds K* from
- * per-patch tables of exp2(c dx^2) and exp2(c dy^2) (the separable RBF
- * kernel: 1.5 exps per lane per half-step instead of 8), falling back to the
- * direct K* when the points are not the grid the cached layout was made
- * for; 63 = variant 3 with the direct K* everywhere (A/B);
  * 22 = variant 3 with every kept tile at six products (f32-accurate:
  * variance error vs a host f64 sweep 5.07e-6 at N = 16384 against 5.00e-6
  * for variant 0); 2 = variant 22 with four waves of 32 queries; 0 = f32

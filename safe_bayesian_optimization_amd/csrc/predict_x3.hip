@@ -124,49 +124,6 @@ __device__ __forceinline__ float kstar1(float xk, float yk, float xq, float yq, 
     return fast_exp2(fmaf(dy, dy, dx * dx) * cexp);
 }
 
-// ---- the separable K* of grid patches (DIAG & kSep).  A query block of the
-// patch layout (query_order.hip) is a wl x (128 / wl) piece of a raster grid:
-// query l sits at column xs = l % wl and row ys = l / wl, and every query of
-// a column shares its x, every query of a row its y (the gather checks this
-// and pads separably), so
-//     K*(k, q) = exp2(c dx^2) exp2(c dy^2) = Ex[xs][k] Ey[ys][k]
-// and a half-step's 32 x 128 K* block needs only 32 (wl + 128 / wl) exps --
-// 768 for the 8 x 16 patches, 1.5 per lane instead of 8.  The workgroup builds
-// the two tables for the next step in LDS (each entry by one lane, from its
-// own query's coordinates) at row block 1 of a half-step, a barrier later
-// every lane reads its pairs back and multiplies.  Both factors are rounded
-// to f32 before the product (|dK*| <= 2 ulp more than the fused form); the
-// kernel's first step builds its K* directly with the same two factors, so
-// the result does not depend on where a workgroup's range starts.
-constexpr long long kSep = 8589934592LL;  // DIAG bit
-constexpr int kSepRow = 34 * 4;            // table row: 32 k + 2 pad (bytes)
-constexpr int kSepEy = 32 * kSepRow;       // Ey rows after 32 Ex rows
-constexpr int kSepDummy = kSepEy + 16 * kSepRow;  // the write target of a lane without an entry
-constexpr int kSepBytes = kSepDummy + 16;
-__device__ __forceinline__ float kfac(float d, float cexp) { return fast_exp2((d * d) * cexp); }
-
-// A lane's part in the tables of one query block (wl = 2^lgw columns):
-// its K* reads (rx, ry: bytes into the table), and the entries it builds:
-// Ex[xs][k] for k = kx0, kx1 and Ey[ys][ky] (wx0, wx1, wy: bytes into the
-// table, kSepDummy when it has none; cx0, cx1, cy: the k's coordinate bytes)
-struct SepLane {
-    uint32_t rx, ry, wx0, wx1, wy, cx0, cx1, cy;
-};
-__device__ __forceinline__ SepLane sep_lane(int q, int g, int lgw) {
-    const int xs = q & ((1 << lgw) - 1), ys = q >> lgw;
-    const int kx0 = ys * 4 + g, kx1 = kx0 + (512 >> lgw), ky = xs * 4 + g;
-    SepLane s;
-    s.rx = (uint32_t)(xs * kSepRow + g * 32);
-    s.ry = (uint32_t)(kSepEy + ys * kSepRow + g * 32);
-    s.wx0 = kx0 < 32 ? (uint32_t)(xs * kSepRow + kx0 * 4) : (uint32_t)kSepDummy;
-    s.wx1 = kx1 < 32 ? (uint32_t)(xs * kSepRow + kx1 * 4) : (uint32_t)kSepDummy;
-    s.wy = ky < 32 ? (uint32_t)(kSepEy + ys * kSepRow + ky * 4) : (uint32_t)kSepDummy;
-    s.cx0 = (uint32_t)(min(kx0, 31) * 4);
-    s.cx1 = (uint32_t)(min(kx1, 31) * 4);
-    s.cy = (uint32_t)(128 + min(ky, 31) * 4);
-    return s;
-}
-
 // Pin a value's computation to this point of the instruction stream (the
 // IR-level sinking passes ignore sched_barrier and would otherwise bunch the
 // next step's K* work after the last MFMA), in an arch VGPR.
@@ -201,11 +158,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
                                         const float (&yq)[NC], int g, float cexp, float msc, const KPieces<NC> &kb,
                                         f32x4 (&acc)[NC][16], f32x4 (&outer)[NC][16], KPieces<NC> &nx,
                                         double (&mu)[NC], uint32_t voff, const char *asrc, uint32_t adst,
-                                        bool loader, int npieces, lds_char *ptab = nullptr,
-                                        const SepLane &sl = SepLane{}) {
-    // SEP: the next step's K* from the separable tables (kSep, above)
-    constexpr bool SEP = (DIAG & kSep) != 0;
-    static_assert(!SEP || NC == 1, "the separable K* is built for one 16-query column block per wave");
+                                        bool loader, int npieces) {
     // SPREAD (DIAG & 16): this wave's A pieces of stage i+2 are issued one
     // per row block between the MFMAs instead of in a burst at the top
     constexpr bool SPREAD = (DIAG & 16) != 0;
@@ -241,22 +194,8 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
     // coordinates of pair 0; pair i+1's are read while pair i is built
     // DIAG & 67108864: sf2 alpha read only before the mean's row block (msc != 0)
     constexpr bool AK_MEAN = (DIAG & 67108864) != 0;
-    constexpr bool MEAN_STATIC = MEAN >= 0;
-    const bool has_mean = MEAN_STATIC ? MEAN == 1 : msc != 0.0f;
-    f32x2v xk = {0.f, 0.f}, yk = {0.f, 0.f}, ak = {0.f, 0.f};
-    // SEP: the coordinates of this lane's table entries, the pairs' factors
-    // (two in flight: read two row blocks before their product)
-    float cxa = 0.f, cxb = 0.f, cyv = 0.f;
-    f32x2v sx[2] = {}, sy[2] = {}, sa[2] = {};
-    if constexpr (SEP) {
-        cxa = lds_f(pcn + sl.cx0);
-        cxb = lds_f(pcn + sl.cx1);
-        cyv = lds_f(pcn + sl.cy);
-    } else {
-        xk = lds_f2(pcn + g * 32);
-        yk = lds_f2(pcn + 128 + g * 32);
-        if (!AK_MEAN || has_mean) ak = lds_f2(pcn + 256 + g * 32);
-    }
+    f32x2v xk = lds_f2(pcn + g * 32), yk = lds_f2(pcn + 128 + g * 32), ak = {0.f, 0.f};
+    if (!AK_MEAN || (MEAN < 0 ? msc != 0.0f : MEAN == 1)) ak = lds_f2(pcn + 256 + g * 32);
     f32x2v e[NC];
 #pragma unroll
     for (int rb = 0; rb < 16; ++rb) {
@@ -273,51 +212,6 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
         // evaluate (two slots), split, mean terms + the next pair's coordinates
         const int i = rb >> 2, ph = rb & 3;
         if (DIAG & 1) {
-        } else if constexpr (SEP) {
-            // row block 1: this lane's table entries (the barrier follows the
-            // row block); pair p: its factors read at row block 2 + 2p, their
-            // product at 4 + 2p, split and mean terms at 5 + 2p
-            if (rb == 1) {
-                const float v0 = kfac(cxa - xq[0], cexp), v1 = kfac(cxb - xq[0], cexp), v2 = kfac(cyv - yq[0], cexp);
-                *reinterpret_cast<__attribute__((address_space(3))) float *>(ptab + sl.wx0) = v0;
-                *reinterpret_cast<__attribute__((address_space(3))) float *>(ptab + sl.wx1) = v1;
-                *reinterpret_cast<__attribute__((address_space(3))) float *>(ptab + sl.wy) = v2;
-            }
-            if (rb >= 2 && rb <= 8 && (rb & 1) == 0) {
-                const int p = (rb - 2) >> 1;
-                sx[p & 1] = lds_f2(ptab + sl.rx + p * 8);
-                sy[p & 1] = lds_f2(ptab + sl.ry + p * 8);
-                if (!AK_MEAN || has_mean) sa[p & 1] = lds_f2(pcn + 256 + g * 32 + p * 8);
-            }
-            if (rb >= 4 && rb <= 10 && (rb & 1) == 0) {
-                const int p = (rb - 4) >> 1;
-                float e0 = sx[p & 1].x * sy[p & 1].x, e1 = sx[p & 1].y * sy[p & 1].y;
-                SBO_PIN(e0);
-                SBO_PIN(e1);
-                e[0].x = e0;
-                e[0].y = e1;
-            }
-            if (rb >= 5 && rb <= 11 && (rb & 1) == 1) {
-                const int p = (rb - 5) >> 1;
-                uint32_t w0, w1, w2;
-                if constexpr (KHN) {
-                    w0 = pk_bf16(e[0].x, e[0].y);
-                    SBO_PIN(w0);
-                    nx.h[0][p] = w0;
-                } else {
-                    split3(e[0].x, e[0].y, w0, w1, w2);
-                    SBO_PIN(w0);
-                    SBO_PIN(w1);
-                    SBO_PIN(w2);
-                    nx.h[0][p] = w0;
-                    nx.m[0][p] = w1;
-                    nx.l[0][p] = w2;
-                }
-                if (has_mean) {
-                    mu[0] += (double)fmaf(sa[p & 1].x, e[0].x, sa[p & 1].y * e[0].y);
-                    SBO_PIN(mu[0]);
-                }
-            }
         } else if (ph <= 1) {
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
@@ -441,11 +335,6 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        // SEP: every lane's table entries are in before any lane reads its pairs
-        // (DIAG & 2^34: without it -- timing only, the reads race the writes)
-        if constexpr (SEP && !(DIAG & 17179869184LL)) {
-            if (rb == 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        }
         // DIAG & 16384: piece rb of stage i+2 after row block rb, and only the
         // planes its level reads (a uniform branch at the scheduling-region
         // boundary; the step's vmcnt wait counts npieces)
@@ -475,8 +364,7 @@ __device__ __forceinline__ void x3_half(const lds_char *pa, const lds_char *pcn,
 }
 
 // K* pieces of one step directly (the prologue's first step)
-// (SEP: as the product of the separable tables' two factors)
-template <int NC, bool SEP = false>
+template <int NC>
 __device__ __forceinline__ void x3_kstar(const lds_char *pc, const float (&xq)[NC], const float (&yq)[NC], int g,
                                          float cexp, bool mean, KPieces<NC> &kb, double (&mu)[NC]) {
 #pragma unroll
@@ -485,10 +373,7 @@ __device__ __forceinline__ void x3_kstar(const lds_char *pc, const float (&xq)[N
         const f32x2v ak = lds_f2(pc + 256 + g * 32 + i * 8);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            const float e0 = SEP ? kfac(xk.x - xq[c], cexp) * kfac(yk.x - yq[c], cexp)
-                                 : kstar1(xk.x, yk.x, xq[c], yq[c], cexp);
-            const float e1 = SEP ? kfac(xk.y - xq[c], cexp) * kfac(yk.y - yq[c], cexp)
-                                 : kstar1(xk.y, yk.y, xq[c], yq[c], cexp);
+            const float e0 = kstar1(xk.x, yk.x, xq[c], yq[c], cexp), e1 = kstar1(xk.y, yk.y, xq[c], yq[c], cexp);
             uint32_t w0, w1, w2;
             split3(e0, e1, w0, w1, w2);
             kb.h[c][i] = w0;
@@ -641,18 +526,8 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
     const char *__restrict__ ax3, const float *__restrict__ kc3, const int4 *__restrict__ desc,
     const int4 *__restrict__ rec, const int *__restrict__ seg, int P, int n_items, int nI, uint32_t a_max, int rot,
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp, float cexp, float m0,
-    float *__restrict__ part, float *__restrict__ mean, const int *__restrict__ sep_flag, int sep_mode, int sep_nfp,
-    int sep_lgwl) {
-    constexpr bool SEP = (DIAG & kSep) != 0;
-    __shared__ __attribute__((aligned(16))) char smem[kXSmem + (SEP ? kSepBytes : 0)];
-    // a grid tick launches the separable sweep and this one, each with the
-    // gather's verdict (sep_flag != 0: the points are not the grid the cached
-    // layout was made for): sep_mode 1 runs only on a separable tick, 2 only
-    // on the others, 0 always
-    if (sep_mode != 0) {
-        const int nonsep = __builtin_amdgcn_readfirstlane(*sep_flag);
-        if ((sep_mode == 1) == (nonsep != 0)) return;
-    }
+    float *__restrict__ part, float *__restrict__ mean) {
+    __shared__ __attribute__((aligned(16))) char smem[kXSmem];
     // NC = 1, 2: 16x16x32 MFMA, NC 16-query column blocks per wave; NC = 3:
     // the wide shape (32x32x16, 32 queries per wave)
     constexpr bool WIDE = NC == 3;
@@ -807,13 +682,8 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
         if constexpr (WIDE)
             x3w_kstar(lds + kXA, xq[0], yq[0], lane >> 5, cexp, s0.I == nI - 1, kb, mu[0]);
         else
-            x3_kstar<NC, SEP>(lds + kXA, xq, yq, g, cexp, s0.I == nI - 1, kb, mu);
+            x3_kstar<NC>(lds + kXA, xq, yq, g, cexp, s0.I == nI - 1, kb, mu);
     }
-    // SEP: the separable tables and this lane's part in them for the item
-    // whose K* is being built (the next step's)
-    lds_char *ptab = (lds_char *)smem + kXSmem;
-    SepLane sl{};
-    if constexpr (SEP) sl = sep_lane(qo, g, s0.qb < sep_nfp ? 3 : sep_lgwl);
     // deferred outputs of the item finished in the previous step (stored at
     // the top of the next step, before its stage DMA, so that the vmcnt count
     // at the end of every step is the A pieces of one stage)
@@ -886,7 +756,6 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
                 xq[c] = lds_f(pqn + (qo + 16 * c) * 4);
                 yq[c] = lds_f(pqn + (kBN + qo + 16 * c) * 4);
             }
-            if constexpr (SEP) sl = sep_lane(qo, g, s1.qb < sep_nfp ? 3 : sep_lgwl);
         }
         if constexpr (STAMP) SBO_STAMP(t1);
         if constexpr (WIDE)
@@ -901,28 +770,28 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void predict_x3_kernel(
             if (LEVELS && s0.lv == 2 && (DIAG & 1073741824) && nvalid && s1.lv == 2) {
                 if (MSPLIT && msc == 0.0f)
                     x3_half<NC, FRESH, DIAG, kPieces, 2, true, 0>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx,
-                                                                  mu, voff, a_src, a_dst, is_loader, np2, ptab, sl);
+                                                                  mu, voff, a_src, a_dst, is_loader, np2);
                 else
                     x3_half<NC, FRESH, DIAG, kPieces, 2, true, MSPLIT ? 1 : -1>(pa, pcn, xq, yq, g, cexp, msc, kb, acc,
                                                                                outer, nx, mu, voff, a_src, a_dst,
-                                                                               is_loader, np2, ptab, sl);
+                                                                               is_loader, np2);
             } else if (LEVELS && s0.lv == 2) {
                 if (MSPLIT && msc == 0.0f)
                     x3_half<NC, FRESH, DIAG, kPieces, 2, false, 0>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx,
-                                                                   mu, voff, a_src, a_dst, is_loader, np2, ptab, sl);
+                                                                   mu, voff, a_src, a_dst, is_loader, np2);
                 else
                     x3_half<NC, FRESH, DIAG, kPieces, 2, false, MSPLIT ? 1 : -1>(pa, pcn, xq, yq, g, cexp, msc, kb,
                                                                                 acc, outer, nx, mu, voff, a_src,
-                                                                                a_dst, is_loader, np2, ptab, sl);
+                                                                                a_dst, is_loader, np2);
             } else if (LEVELS && s0.lv == 1 && (DIAG & 1073741824) && (DIAG & 524288) && nvalid && s1.lv == 2)
                 x3_half<NC, FRESH, DIAG, kPieces, 1, true>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff,
-                                                           a_src, a_dst, is_loader, np2, ptab, sl);
+                                                           a_src, a_dst, is_loader, np2);
             else if (LEVELS && s0.lv == 1)
                 x3_half<NC, FRESH, DIAG, kPieces, 1>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff,
-                                                     a_src, a_dst, is_loader, np2, ptab, sl);
+                                                     a_src, a_dst, is_loader, np2);
             else
                 x3_half<NC, FRESH, DIAG, kPieces>(pa, pcn, xq, yq, g, cexp, msc, kb, acc, outer, nx, mu, voff, a_src,
-                                                  a_dst, is_loader, np2, ptab, sl);
+                                                  a_dst, is_loader, np2);
         }
         if constexpr (STAMP) SBO_STAMP(t2);
         if (!FRESH && (s0.flags & kLast)) {
@@ -1112,8 +981,7 @@ hipError_t read_x3_stamps(double *out, int n) {
 
 hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, const int4 *desc, const int4 *rec,
                              const int *seg, int P, int n_items, int nI, const float *qx, const float *qy, int64_t m,
-                             int64_t ldp, float cexp, float m0, float *part, float *mean, int variant,
-                             const int *sep_flag, int sep_nfp, int sep_lgwl) {
+                             int64_t ldp, float cexp, float m0, float *part, float *mean, int variant) {
     // the largest tile offset a record may name (KiB): keeps every staged address inside ax3
     const int64_t amax = (total_tiles(nI) - 1) * (2 * kXA / 1024);
     if (nI <= 0 || amax > 0xffffffffll) return hipErrorInvalidValue;
@@ -1122,22 +990,9 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
 #ifdef SBO_DIAG
     if (const char *e = getenv("SBO_XCD_ROT")) rot = std::clamp(atoi(e), 0, 7);
 #endif
-    // sep_flag: a grid-patch tick (query_order.hip) whose gather checks
-    // separability -- the default sweep runs as the separable one and the
-    // plain one, each leaving at once when the check says it is not its tick
-    int sep_mode = 0;
 #define SBO_X3_LAUNCH(NC, D) \
     hipLaunchKernelGGL((predict_x3_kernel<NC, D>), dim3((unsigned)P), dim3(NC == 1 ? 512 : 256), 0, s, ax3, kc3, desc, rec, \
-                       seg, P, n_items, nI, a_max, rot, qx, qy, m, ldp, cexp, m0, part, mean, sep_flag, sep_mode, \
-                       sep_nfp, sep_lgwl)
-    constexpr long long kDefault = 73776 + 33554432 + 1073741824 + 67108864;
-    if (variant == 3 && sep_flag) {
-        sep_mode = 1;
-        SBO_X3_LAUNCH(1, kDefault + kSep);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        sep_mode = 2;
-    }
+                       seg, P, n_items, nI, a_max, rot, qx, qy, m, ldp, cexp, m0, part, mean)
     switch (variant) {
         case 2: SBO_X3_LAUNCH(2, 16); break;   // four waves of 32 queries
         case 9: SBO_X3_LAUNCH(1, 0); break;    // A pieces in a burst at the top of the step
@@ -1196,11 +1051,8 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
         case 61: SBO_X3_LAUNCH(2, 73776 + 33554432 + 67108864); break;  //   without the kh-only split bodies
         case 59: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 4294967296LL); break;  // variant 3, mean terms by a select (no branch)
         case 58: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 67108864 + 2147483648LL); break;  // variant 3, one-product bodies split by the mean test at compile time
-        case 64: SBO_X3_LAUNCH(1, kDefault + kSep + 17179869184LL); break;  // diagnostics: the separable K* without its barrier (wrong results)
-        case 65: SBO_X3_LAUNCH(1, kDefault + kSep); break;  // the separable K* on every tick (no check: grid ticks only)
 #endif
-        case 63: SBO_X3_LAUNCH(1, kDefault); break;  // variant 3 without the separable K* of grid ticks (A/B)
-        default: SBO_X3_LAUNCH(1, kDefault); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead, next coordinates at ph 1, kh-only split between one-product steps, sf2 alpha read only before the mean's row block
+        default: SBO_X3_LAUNCH(1, 73776 + 33554432 + 1073741824 + 67108864); break;  // 3: eight waves of 16 queries, A pieces spread, tile levels, A 1 / 2 / 4 blocks ahead, next coordinates at ph 1, kh-only split between one-product steps, sf2 alpha read only before the mean's row block
     }
 #undef SBO_X3_LAUNCH
     return hipGetLastError();

@@ -100,49 +100,30 @@ __global__ void grid_check_kernel(const float *__restrict__ qx, const float *__r
 }
 
 // Sweep position p of the patch layout (see launch_query_grid) -> caller index (or -1) and coordinates.
-// The layout is separable: a patch's queries in one column share its x, in
-// one row its y -- a grid point's own coordinates, and for a padded position
-// the x of its column (clamped to the grid, taken from row 1, which is whole)
-// and the y of its patch row (its row, clamped; a row without a point in the
-// patch's columns -- row 0 before the first row's start c0, row R-1 past the
-// last point -- takes its neighbour's), so the patch's box stays the
-// patch's.  A grid point whose coordinates are not its row's y and its
-// column's x (a cached layout over a buffer that no longer holds that grid)
-// sets *nonsep: the sweep then runs its plain K* (predict_x3.hip, kSep).
 __global__ void grid_gather_kernel(const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, QueryGrid q,
-                                   int32_t *__restrict__ perm, float *__restrict__ sx, float *__restrict__ sy,
-                                   int *__restrict__ nonsep) {
+                                   int32_t *__restrict__ perm, float *__restrict__ sx, float *__restrict__ sy) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= q.ms) return;
     const int64_t W = q.W, c0 = q.c0, R = q.R;
     const int64_t patch = p / kBN, l = p % kBN, nfp = q.nfull * q.npf;
     // whole patch rows, then the last rows (R % kGridPatchSlow of them) in
     // patches q.wl wide and kBN / q.wl tall
-    const bool full = patch < nfp;
-    const int64_t pc0 = full ? (patch % q.npf) * kGridPatchFast : (patch - nfp) * q.wl;
-    const int64_t pw = full ? kGridPatchFast : q.wl;
-    const int64_t cf = pc0 + l % pw;
-    const int64_t rs = full ? (patch / q.npf) * kGridPatchSlow + l / kGridPatchFast : q.nfull * kGridPatchSlow + l / q.wl;
+    const int64_t cf = patch < nfp ? (patch % q.npf) * kGridPatchFast + l % kGridPatchFast
+                                   : (patch - nfp) * q.wl + l % q.wl;
+    const int64_t rs = patch < nfp ? (patch / q.npf) * kGridPatchSlow + l / kGridPatchFast
+                                   : q.nfull * kGridPatchSlow + l / q.wl;
     const int64_t i = rs * W + cf - c0;
     const bool valid = cf < W && rs < R && i >= 0 && i < m;
-    // (R >= 3: the detection needs a whole second row and a third)
-    const int64_t ix = (W - c0) + (cf < W ? cf : W - 1);   // row 1, column cf
-    const int64_t e = c0 + m - (R - 1) * W;                 // row R-1 ends before column e
-    int64_t rr = rs < R ? rs : R - 1;
-    if (rr == 0 && pc0 + pw <= c0) rr = 1;
-    else if (rr == R - 1 && pc0 >= e) rr = R - 2;
-    const int64_t iy = rr == 0 ? 0 : rr * W - c0;         // row rr's first point
+    // a padded position repeats the nearest grid point of its own column
+    // (the next row before the first row's start c0, the previous row past
+    // the last row's end), so the patch's box stays the patch's
+    int64_t src = (rs < R ? rs : R - 1) * W + (cf < W ? cf : W - 1) - c0;
+    if (src < 0) src += W;
+    if (src >= m) src -= W;
+    src = src < 0 ? 0 : (src >= m ? m - 1 : src);
     perm[p] = valid ? (int32_t)i : -1;
-    const float gx = qx[ix], gy = qy[iy];
-    if (valid) {
-        const float vx = qx[i], vy = qy[i];
-        sx[p] = vx;
-        sy[p] = vy;
-        if (vx != gx || vy != gy) *nonsep = 1;
-    } else {
-        sx[p] = gx;
-        sy[p] = gy;
-    }
+    sx[p] = qx[src];
+    sy[p] = qy[src];
 }
 
 }  // namespace
@@ -190,19 +171,15 @@ bool grid_layout(const unsigned long long g[6], int64_t m, QueryGrid &q) {
 }
 
 hipError_t launch_query_grid(hipStream_t s, const float *qx, const float *qy, int64_t m, const QueryGrid &q,
-                             void *work, int32_t **perm_out, float **sqx, float **sqy, int **nonsep_out) {
+                             void *work, int32_t **perm_out, float **sqx, float **sqy) {
     char *p = static_cast<char *>(work) + 256;
     const size_t a = (size_t)grid_max_positions(m);
     int32_t *perm = reinterpret_cast<int32_t *>(p);
     float *xs = reinterpret_cast<float *>(perm + a);
     float *ys = xs + a;
-    int *nonsep = reinterpret_cast<int *>(static_cast<char *>(work) + 64);  // after g[6]
-    hipError_t e = hipMemsetAsync(nonsep, 0, sizeof(int), s);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(grid_gather_kernel, dim3((unsigned)((q.ms + 255) / 256)), dim3(256), 0, s, qx, qy, m, q, perm,
-                       xs, ys, nonsep);
+                       xs, ys);
     *perm_out = perm;
-    if (nonsep_out) *nonsep_out = nonsep;
     *sqx = xs;
     *sqy = ys;
     return hipGetLastError();

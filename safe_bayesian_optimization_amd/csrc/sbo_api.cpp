@@ -1095,8 +1095,6 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     // with every kept tile at level SBO_LVL_FORCE -- outside the error budget
     if (const char *e = getenv("SBO_LVL_FORCE"); e && plan.levels) plan.levels = 2 + std::clamp(atoi(e), 0, 2);
 #endif
-    int *sep_flag = nullptr;   // a grid tick's separability verdict (device; launch_predict_x3)
-    int sep_nfp = 0, sep_lgwl = 3;
     if (ctx->query_order && plan.L > 0 && m > sbo::kBN) {
         int32_t *p = nullptr;
         float *sx = nullptr, *sy = nullptr;
@@ -1115,16 +1113,8 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
             }
         }
         if (ctx->query_order == 1 && ctx->qgrid.ok) {
-            SBO_HIP(sbo::launch_query_grid(ctx->stream, qx, qy, m, ctx->qgrid, ctx->qgwork.as<void>(), &p, &sx, &sy,
-                                           &sep_flag));
+            SBO_HIP(sbo::launch_query_grid(ctx->stream, qx, qy, m, ctx->qgrid, ctx->qgwork.as<void>(), &p, &sx, &sy));
             ms = ctx->qgrid.ms;
-            // the separable K* tables hold patches up to 32 columns wide (the
-            // last rows' patches are kBN / 2^ceil(log2(R % 16)) wide)
-            const sbo::QueryGrid &g = ctx->qgrid;
-            if (g.R % sbo::kGridPatchSlow != 0 && g.wl > 32) sep_flag = nullptr;
-            sep_nfp = (int)(g.nfull * g.npf);
-            sep_lgwl = 3;
-            while (g.R % sbo::kGridPatchSlow != 0 && (1 << sep_lgwl) < g.wl) ++sep_lgwl;
         } else {
             const size_t wb = sbo::query_order_bytes(m);
             SBO_HIP(ctx->qwork.reserve(wb));
@@ -1220,7 +1210,7 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
                                        (int)(nIc * ((ms + sbo::kBN - 1) / sbo::kBN)), (int)nIc, qx, qy, ms, ldp,
                                        sbo::exp2_coef_f((float)ctx->hyper.length_scale),
                                        (float)ctx->hyper.prior_mean, ctx->part.as<float>(), ctx->mean.as<float>(),
-                                       ctx->kernel_variant, sep_flag, sep_nfp, sep_lgwl));
+                                       ctx->kernel_variant));
     } else {
         Bracket br(ctx, ctx->ev_predict);
         SBO_HIP(sbo::launch_predict(ctx->stream, ctx->aug.as<float>(), ctx->kcoord.as<float>(), ctx->npad, qx, qy,
@@ -1833,7 +1823,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
             SBO_CHECK(sbo::variant_allowed((int)value), SBO_E_INVAL,
-                      "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22, 63)");
+                      "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22)");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
         case SBO_OPT_INV_BASE:

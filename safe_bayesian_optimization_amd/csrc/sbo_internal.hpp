@@ -297,16 +297,16 @@ constexpr int kLevelShift = 14;
 // its item (kRecFirst, kRecLast).
 constexpr int kRecFirst = 1 << 20, kRecLast = 1 << 21;
 // the split sweeps that honour the plan's precision levels
-inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39 || variant == 41 || variant == 42 || variant == 43 || variant == 46 || variant == 47 || variant == 48 || variant == 49 || variant == 51 || variant == 52 || variant == 53 || variant == 54 || variant == 55 || variant == 56 || variant == 57 || (variant >= 58 && variant <= 61) || (variant >= 63 && variant <= 65); }
+inline bool x3_levels(int variant) { return variant == 3 || variant == 23 || variant == 24 || variant == 30 || variant == 32 || variant == 33 || variant == 39 || variant == 41 || variant == 42 || variant == 43 || variant == 46 || variant == 47 || variant == 48 || variant == 49 || variant == 51 || variant == 52 || variant == 53 || variant == 54 || variant == 55 || variant == 56 || variant == 57 || (variant >= 58 && variant <= 61); }
 // Sweeps the product library accepts (all compute the full result; 3 is the
 // default).  The timing diagnostics (parts of the work left out, forced
 // precision levels, phase stamps) exist only in the diagnostic build
 // (-DSBO_DIAG, lib/libsbo_diag.so, selected by SBO_LIB for tools/).
 inline bool variant_allowed(int v) {
 #ifdef SBO_DIAG
-    return (v >= 0 && v <= 61) || (v >= 63 && v <= 65);
+    return v >= 0 && v <= 61;
 #else
-    return v == 0 || v == 1 || v == 2 || v == 3 || v == 9 || v == 10 || v == 13 || v == 22 || v == 63;
+    return v == 0 || v == 1 || v == 2 || v == 3 || v == 9 || v == 10 || v == 13 || v == 22;
 #endif
 }
 inline int x3_layout(int variant) { return (variant == 13 || variant == 14) ? 1 : 0; }
@@ -318,8 +318,7 @@ inline int x3_layout(int variant) { return (variant == 13 || variant == 14) ? 1 
 hipError_t read_x3_stamps(double *out, int n);
 hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, const int4 *desc, const int4 *rec,
                              const int *seg, int P, int n_items, int nI, const float *qx, const float *qy, int64_t m,
-                             int64_t ldp, float cexp, float m0, float *part, float *mean, int variant,
-                             const int *sep_flag = nullptr, int sep_nfp = 0, int sep_lgwl = 3);
+                             int64_t ldp, float cexp, float m0, float *part, float *mean, int variant);
 // lgn[2 (tile_start(I) + t)] = log2 bounds (16 max row 1-norm, spectral,
 // Frobenius) of A_It, lgn[2 (..) + 1] = (16 max row 1-norm, spectral) of its
 // bf16 pieces A1 and A2 (f64 sums, rounded up) for row blocks I >= I0 (-1000
@@ -389,10 +388,8 @@ size_t query_grid_bytes(int64_t m);
 hipError_t launch_grid_detect(hipStream_t s, const float *qx, const float *qy, int64_t m, void *work,
                               unsigned long long host_g[6]);
 bool grid_layout(const unsigned long long g[6], int64_t m, QueryGrid &q);
-// (*nonsep: a device int, nonzero when the points are not the grid the
-// layout was made for, so the patches are not separable -- predict_x3.hip)
 hipError_t launch_query_grid(hipStream_t s, const float *qx, const float *qy, int64_t m, const QueryGrid &q,
-                             void *work, int32_t **perm, float **sqx, float **sqy, int **nonsep = nullptr);
+                             void *work, int32_t **perm, float **sqx, float **sqy);
 // ComputeSets from given mu/sd (staged API).
 hipError_t launch_sets(hipStream_t s, const float *mu, const float *sd, int64_t m, double beta,
                        double f_min, double *lo, double *hi, uint8_t *safe);

@@ -431,7 +431,7 @@ def test_product_rejects_diagnostic_variants(mapper):
     for v in (4, 5, 6, 7, 8, 11, 12, 14, 15, 16, 17, 18, 19, 20, 21, 23, 25, 29, 30, 35, 37, 39, 40):
         with pytest.raises(N.SboError):
             gm.set_option(N.SBO_OPT_KERNEL_VARIANT, v)
-    for v in (0, 1, 2, 9, 10, 13, 22, 63, 3):
+    for v in (0, 1, 2, 9, 10, 13, 22, 3):
         gm.set_option(N.SBO_OPT_KERNEL_VARIANT, v)
 
 
@@ -814,54 +814,6 @@ def test_grid_query_blocks(mapper):
         gm.set_option(N.SBO_OPT_QUERY_ORDER, 1)
     with pytest.raises(N.SboError):
         gm.set_option(N.SBO_OPT_QUERY_ORDER, 3)
-
-
-def test_separable_grid_kstar(mapper):
-    """The default sweep builds a grid tick's K* from the per-patch tables
-    (predict_x3.hip, kSep): against the direct K* (variant 63) and the fp64
-    oracle given the device factor it stays within f32 rounding, its mean and
-    variance differ from the direct form (the tables ran), the padded last
-    patch rows (R % 16 = 8 -> 16 x 8 patches, R % 16 = 13 -> 8 x 16) and a shard
-    cut mid-row included; on points that are not the grid the cached layout
-    was made for, the sweep falls back to the direct K*, bitwise."""
-    wl = synthetic(3000, 203, 157, seed=31)
-    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
-    gm.fit(wl.x, wl.y, wl.obs)
-    W = 203
-    rng = np.random.default_rng(8)
-    cases = {
-        "grid 203 x 157 (R % 16 = 13)": (wl.qx, wl.qy, True),
-        # (the same size right after the grid: the staged copy's cached patch
-        # layout is reused over points that are not that grid any more)
-        "scattered points": (rng.permutation(wl.qx), rng.permutation(wl.qy), False),
-        "rows 2 .. 145 cut mid-row (R % 16 = 8)": (wl.qx[W * 2 + 11: W * 145 + 90], wl.qy[W * 2 + 11: W * 145 + 90],
-                                                   True),
-    }
-    try:
-        for name, (x, y, sep) in cases.items():
-            gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 63)
-            ref, rkey = _grid_tick(gm, x, y, wl)
-            gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 3)
-            out, key = _grid_tick(gm, x, y, wl)
-            e_mu = nrel(out["mu"], ref["mu"].astype(np.float64))
-            e_var = nrel(out["sd"].astype(np.float64) ** 2, ref["sd"].astype(np.float64) ** 2)
-            print(f"{name}: mu {e_mu:.2e}  var {e_var:.2e}  key {key} vs {rkey}")
-            if sep:
-                # (K* differs by f32 rounding; sigma^2 = sf2 - |V|^2 amplifies it
-                # like any other f32 rounding of the sweep)
-                assert e_mu < 1e-5 and e_var < 1e-5, name
-                assert not np.array_equal(out["sd"], ref["sd"]), name
-                s = rng.choice(x.size, 2048, replace=False)
-                omu, ovar = oracle_given_factor(gm, wl, x[s], y[s])
-                errs = [(nrel(o["mu"][s], omu), nrel(o["sd"][s].astype(np.float64) ** 2, ovar)) for o in (out, ref)]
-                print(f"   vs the fp64 oracle: separable mu {errs[0][0]:.2e} var {errs[0][1]:.2e}; "
-                      f"direct mu {errs[1][0]:.2e} var {errs[1][1]:.2e}")
-                assert errs[0][0] < 1e-5 and errs[0][1] < 1e-5, name
-            else:
-                assert np.array_equal(out["mu"], ref["mu"]) and np.array_equal(out["sd"], ref["sd"]), name
-                assert key == rkey, name
-    finally:
-        gm.set_option(N.SBO_OPT_KERNEL_VARIANT, 3)
 
 
 def test_grid_patches_with_padding_band(mapper):
