@@ -911,14 +911,26 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
             }
             __syncthreads();   // at is restaged for the next half
         }
+        // G into LDS, and its largest entry (for the first squaring's rescale)
+        // from the registers
+        double gmx = 0.0;
 #pragma unroll
         for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
-            for (int v = 0; v < 4; ++v) gm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = acc[bj][v];
+            for (int v = 0; v < 4; ++v) {
+                gm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = acc[bj][v];
+                gmx = fmax(gmx, fabs(acc[bj][v]));
+            }
         double s = rsum[tid];
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) s = fmax(s, __shfl_xor(s, o));
-        if ((tid & 63) == 0) red[0][tid >> 6] = s;
+        for (int o = 32; o >= 1; o >>= 1) {
+            s = fmax(s, __shfl_xor(s, o));
+            gmx = fmax(gmx, __shfl_xor(gmx, o));
+        }
+        if ((tid & 63) == 0) {
+            red[0][tid >> 6] = s;
+            red[1][tid >> 6] = gmx;
+        }
         __syncthreads();
         const double fro2 = [&] {  // trace G = |A|_F^2 (every thread reads it)
             double tr = 0.0;
@@ -926,39 +938,39 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
             return tr;
         }();
         // k squarings, G <- (G/c)^2 with c = the largest entry (exact power-of-two
-        // rescale), tracking log2 of the scale: G^(2^k) = 2^e8 * gm
+        // rescale), tracking log2 of the scale: G^(2^k) = 2^e8 * gm.  The
+        // rescale rides on the MFMA's A operand, (2^-2ex a) b = (2^-ex a)(2^-ex b)
+        // exactly, and each power's largest entry comes from the registers
+        // that hold it (no LDS pass for either; the same powers bit for bit)
         constexpr int kGramSquarings = 4;
         double e8 = 0.0;
         for (int it = 0; it < kGramSquarings; ++it) {
-            double mx = 0.0;
-            for (int i = tid; i < kBK * kBK; i += kBM) mx = fmax(mx, fabs(gm[i]));
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-            if ((tid & 63) == 0) red[1][tid >> 6] = mx;
-            __syncthreads();
-            mx = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
-            __syncthreads();
+            const double mx = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
             if (!(mx > 0.0)) break;
             const int ex = ilogb(mx);
-            // G' = 2^-ex G in place (exact), then G'^2 by MFMA into registers,
-            // written over G once every read of it is done
-            for (int i = tid; i < kBK * kBK; i += kBM) gm[i] = ldexp(gm[i], -ex);
-            __syncthreads();
             f64x4_t sq[4];
 #pragma unroll
             for (int bj = 0; bj < 4; ++bj) sq[bj] = f64x4_t{0.0, 0.0, 0.0, 0.0};
             for (int k0 = 0; k0 < kBK; k0 += 4) {
-                const double av = gm[(16 * wave + (lane & 15)) * kBK + k0 + (lane >> 4)];
+                const double av = ldexp(gm[(16 * wave + (lane & 15)) * kBK + k0 + (lane >> 4)], -2 * ex);
                 const double *brow = gm + (k0 + (lane >> 4)) * kBK + (lane & 15);
 #pragma unroll
                 for (int bj = 0; bj < 4; ++bj) sq[bj] = mfma_f64(av, brow[16 * bj], sq[bj]);
             }
             e8 = 2.0 * (e8 + (double)ex);  // (2^e G')^2 = 2^(2e) G'^2
-            __syncthreads();
+            double qmx = 0.0;
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) qmx = fmax(qmx, fabs(sq[bj][v]));
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) qmx = fmax(qmx, __shfl_xor(qmx, o));
+            __syncthreads();   // every read of G and of red[1] is done
 #pragma unroll
             for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
                 for (int v = 0; v < 4; ++v) gm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = sq[bj][v];
+            if (lane == 0) red[1][wave] = qmx;
             __syncthreads();
         }
         // ||G^(2^k)||_inf: largest absolute row sum

@@ -946,13 +946,14 @@ hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, 
                           char *ax3, float *kc3) {
     const int64_t nI = npad / kBM;
     const int64_t T0 = tile_start(I0), T1 = tile_start(nI);
-    if (T1 > T0) {
+    if (ax3 && T1 > T0) {
         const int64_t th = (T1 - T0) * 2048;
         hipLaunchKernelGGL(pack_x3_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, aug, T0, T1 - T0, wide,
                            ax3);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
+    if (!kc3) return hipSuccess;
     const int64_t nkt = npad / kBK;
     hipLaunchKernelGGL(pack_kc3_kernel, dim3((unsigned)((nkt * 256 + 255) / 256)), dim3(256), 0, s, kcoord, nkt, kc3);
     return hipGetLastError();

@@ -464,6 +464,11 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
                     int score_kind, int64_t index_offset, float *mu, float *sd, double *lo, double *hi,
                     uint8_t *safe, sbo_key *key_dev, float *cost = nullptr, int sweep = kSweepCtx);
 sbo_status probe_precision(sbo_ctx *ctx);
+// the precision probe runs on this refresh (probe_precision): on a fresh fit,
+// and on appends once N has grown by a quarter since the last probe
+bool probe_due(const sbo_ctx *ctx) {
+    return ctx->probe_n == 0 || ctx->n >= ctx->probe_n + ctx->probe_n / 4 || ctx->n < ctx->probe_n;
+}
 
 // Rebuild alpha, L^-1 and the packed predictive operand from the current L.
 // n_old > 0 (an append of rows n_old..n-1 to an unchanged leading factor):
@@ -496,7 +501,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                       sizeof(float) * old_tiles * sbo::kTileFloats));
     SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
     rocblas_int hinfo = 0;
-    bool alpha_aux = false, kcoord_pending = false;
+    bool alpha_aux = false, kcoord_pending = false, x3_planes_aux = false, packs_aux = false;
     // the inverse's first half ran beside the Cholesky (blocked_potrf): its
     // info slots 1 .. inv_slot stay, the rest are cleared
     const bool early = ctx->inverse_bits == 64 && ctx->inverse_rec && !incr && ctx->early_inv_n == n;
@@ -581,7 +586,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         // 0.75 ms off the fit's critical path).
         SBO_HIP(ctx->alpha64.reserve(sizeof(double) * (size_t)std::max(npad, ld)));
         double *d = ctx->alpha64.as<double>();
-        alpha_aux = ctx->blas_aux && ctx->aux_stream && ctx->ev_panel;
+        alpha_aux = ctx->blas_aux && ctx->aux_stream && ctx->ev_panel && ctx->ev_pack;
         hipStream_t sa = alpha_aux ? ctx->aux_stream : ctx->stream;
         rocblas_handle ha = alpha_aux ? ctx->blas_aux : ctx->blas;
         if (alpha_aux) {
@@ -596,7 +601,49 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         SBO_HIP(sbo::launch_narrow(sa, d, n, alpha));
         if (alpha_aux) SBO_HIP(hipEventRecord(ctx->ev_trail, ctx->aux_stream));
         ctx->a64_I0 = std::min(ctx->a64_I0, I0);
+        if (!incr) ctx->a64_I0 = 0;
+        // the sweeps' operands, derived from the packed f32 tiles (the split
+        // bf16 planes) and from L^-1 (the f64 operand, when the precision probe
+        // or the precise sweep will read it), on aux_stream beside the row sums
+        // and tile norms below, instead of lazily at the first tick (HBM-bound
+        // beside MFMA-bound; C4: 0.22 + 0.41 ms off the fit's critical path)
+        const int layout = sbo::x3_layout(ctx->kernel_variant);
+        const bool eager_x3 = alpha_aux && ctx->kernel_variant >= 2;
+        const bool eager_f64 = alpha_aux && ctx->precision_opt != 0 && (probe_due(ctx) || ctx->precise);
+        if (eager_x3) {
+            if (layout != ctx->x3_layout) ctx->x3_I0 = 0;
+            const int64_t xI0 = std::max<int64_t>(std::min(ctx->x3_I0, I0), 0);
+            SBO_HIP(grow_keep(ctx, ctx->ax3, sbo::x3_operand_bytes(npad), sbo::x3_operand_bytes(xI0 * sbo::kBM)));
+            SBO_HIP(ctx->kc3.reserve(sbo::x3_coord_bytes(npad)));
+            ctx->x3_I0 = xI0;
+        }
+        if (eager_f64) {
+            const int64_t fI0 = std::max<int64_t>(ctx->a64_I0, 0);
+            SBO_HIP(grow_keep(ctx, ctx->a64, sbo::f64_operand_bytes(npad), sbo::f64_operand_bytes(fI0 * sbo::kBM)));
+            SBO_HIP(ctx->kc64.reserve(sbo::f64_coord_bytes(npad)));
+        }
         SBO_HIP(sbo::launch_pack_tiles(ctx->stream, Li, ld, n, npad, I0, sf2, ctx->aug.as<float>()));
+        if (eager_x3 || eager_f64) {
+            SBO_HIP(hipEventRecord(ctx->ev_panel, ctx->stream));
+            SBO_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0));
+            if (eager_x3) {
+                SBO_HIP(sbo::launch_pack_x3(ctx->aux_stream, ctx->aug.as<float>(), nullptr, npad, ctx->x3_I0, layout,
+                                            ctx->ax3.as<char>(), nullptr));
+                x3_planes_aux = true;
+            }
+            // the row sums too (the skip budget's, read by the host after the
+            // tile norms): the tile norms start right after the pack
+            SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)npad));
+            SBO_HIP(sbo::launch_row_l1(ctx->aux_stream, ctx->aug.as<float>(), npad, I0, ctx->scratch.as<double>()));
+            if (eager_f64) {
+                SBO_HIP(sbo::launch_pack_f64(ctx->aux_stream, Li, ld, n, npad, std::max<int64_t>(ctx->a64_I0, 0), sf2,
+                                             ctx->x.as<float>(), ctx->y.as<float>(), d, ctx->a64.as<double>(),
+                                             ctx->kc64.as<double>()));
+                ctx->a64_I0 = INT64_MAX;
+            }
+            SBO_HIP(hipEventRecord(ctx->ev_pack, ctx->aux_stream));
+            packs_aux = true;
+        }
         kcoord_pending = true;
     } else {
         ctx->linv_n = 0;
@@ -628,8 +675,10 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     // 2^-L_mean |sf2 alpha|_1 <= 2^-B sf2^(1/2).  Rows of earlier row blocks
     // are unchanged by an append: only the repacked row blocks are measured.
     {
-        SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)npad));
-        SBO_HIP(sbo::launch_row_l1(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->scratch.as<double>()));
+        if (!packs_aux) {
+            SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)npad));
+            SBO_HIP(sbo::launch_row_l1(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->scratch.as<double>()));
+        }
         SBO_HIP(grow_keep(ctx, ctx->tile_lgn, 2 * sizeof(float4) * (size_t)sbo::total_tiles(nI),
                           2 * sizeof(float4) * old_tiles));
         SBO_HIP(sbo::launch_tile_norms(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->tile_lgn.as<float4>()));
@@ -637,7 +686,11 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             if (alpha_aux) SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
             SBO_HIP(sbo::launch_pack_kcoord(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), alpha, n, npad, sf2,
                                             ctx->kcoord.as<float>()));
+            if (x3_planes_aux)  // the split sweep's coordinates (its planes are on aux_stream)
+                SBO_HIP(sbo::launch_pack_x3(ctx->stream, nullptr, ctx->kcoord.as<float>(), npad, 0, 0, nullptr,
+                                            ctx->kc3.as<float>()));
         }
+        if (packs_aux) SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_pack, 0));  // row sums and packs
         const int64_t r0 = I0 * sbo::kBM;
         std::vector<double> rl1((size_t)(npad - r0));
         std::vector<float> ha((size_t)n);
@@ -672,8 +725,13 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     if (hinfo != 0) ctx->linv_n = 0;
     SBO_CHECK(hinfo == 0, SBO_E_NOT_SPD, "trtri: singular factor (info=" + std::to_string(hinfo) + ")");
     ctx->npad = npad;
-    ctx->x3_I0 = std::min(ctx->x3_I0, I0);  // the split operand is derived lazily (run_tick)
-    if (!incr) ctx->a64_I0 = 0;
+    if (x3_planes_aux) {
+        ctx->x3_I0 = INT64_MAX;
+        ctx->x3_layout = sbo::x3_layout(ctx->kernel_variant);
+    } else {
+        ctx->x3_I0 = std::min(ctx->x3_I0, I0);  // the split operand is derived lazily (run_tick)
+        if (!incr && ctx->a64_I0 != INT64_MAX) ctx->a64_I0 = 0;
+    }
     ctx->fitted = true;
     return probe_precision(ctx);
 }
@@ -721,7 +779,7 @@ sbo_status probe_precision(sbo_ctx *ctx) {
         if (!avail) ctx->probe_n = 0;
         return SBO_OK;
     }
-    const bool fresh = ctx->probe_n == 0 || ctx->n >= ctx->probe_n + ctx->probe_n / 4 || ctx->n < ctx->probe_n;
+    const bool fresh = probe_due(ctx);
     if (fresh) {
         constexpr int G = 32, M = G * G;
         std::vector<float> h(2 * M);
@@ -862,6 +920,7 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
     if (!ctx->ev_panel) {
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_panel, hipEventDisableTiming));
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_trail, hipEventDisableTiming));
+        SBO_HIP(hipEventCreateWithFlags(&ctx->ev_pack, hipEventDisableTiming));
     }
     if (!ctx->blas_aux) {
         SBO_BLAS(rocblas_create_handle(&ctx->blas_aux));
@@ -1313,6 +1372,7 @@ SBO_API void sbo_destroy(sbo_ctx *ctx) {
     if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
     if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
     if (ctx->ev_trail) (void)hipEventDestroy(ctx->ev_trail);
+    if (ctx->ev_pack) (void)hipEventDestroy(ctx->ev_pack);
     if (ctx->blas_aux) rocblas_destroy_handle(ctx->blas_aux);
     if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
     if (ctx->inv_stream) (void)hipStreamSynchronize(ctx->inv_stream);

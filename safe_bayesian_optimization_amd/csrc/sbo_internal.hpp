@@ -99,6 +99,7 @@ struct sbo_ctx {
     int chol_reserve = 0;        // SBO_OPT_CHOL_RESERVE: CUs the trailing updates leave free (CU-masked aux stream)
     int aux_reserved = 0;        // the mask the current aux stream was created with
     hipEvent_t ev_panel = nullptr, ev_trail = nullptr;
+    hipEvent_t ev_pack = nullptr;  // the fit's operand packs on aux_stream (refresh_operand)
     int chol_gemm_own = 0;       // SBO_OPT_CHOL_GEMM: 2 every factorization update by chol_update_kernel, 1 the small trailing ones, 0 rocBLAS
     int chol_diag = 1;           // SBO_OPT_CHOL_DIAG: 1 the MFMA chain kernels (diagonal block, panel), 0 the VALU ones (bitwise equal)
     int chol_outer = 512;        // SBO_OPT_CHOL_OUTER: outer panel width of the two-level Cholesky (128: one level)
@@ -285,6 +286,7 @@ void plan_views(int64_t npad, int64_t m, int P, const void *work, const int4 **d
 // coordinates in natural order, for row blocks >= I0 (coordinates: all).
 size_t x3_operand_bytes(int64_t npad);
 size_t x3_coord_bytes(int64_t npad);
+// (ax3 null: the coordinates only; kc3 null: the planes only)
 hipError_t launch_pack_x3(hipStream_t s, const float *aug, const float *kcoord, int64_t npad, int64_t I0, int wide,
                           char *ax3, float *kc3);
 // the split operand's layout a kernel variant reads (1: the wide 32x32x16 shape)

@@ -1,5 +1,5 @@
 """Bitwise A/B of two libsbo builds on the same ticks (GPU): each library runs
-in its own process (SBO_LIB), writes mu/sd/lo/hi/S and the key of a few
+in its own process (SBO_LIB), writes the fit's tile bounds, mu/sd/lo/hi/S and the key of a few
 workloads, and the outputs are compared element by element.
 
   python tools/compare_libs.py LIB_A LIB_B [--configs C4 C2 box]"""
@@ -29,6 +29,10 @@ for name in {configs!r}:
     t = lambda a: torch.tensor(np.ascontiguousarray(a, np.float32), device=dev)
     gm = TerrainMapper(0, wl.hyper)
     gm.fit(t(wl.x), t(wl.y), t(wl.obs))
+    nI = (gm.n + 255) // 256
+    b = np.empty(8 * sum(4 * (I + 1) for I in range(nI)), np.float32)   # the plan's tile bounds
+    gm.ctx.check(N.lib().sbo_get_tile_bounds(gm.ctx.handle, b.ctypes.data, b.size))
+    out[name + "_tile_bounds"] = b
     m = wl.qx.size
     o = dict(mu=torch.empty(m, device=dev), sd=torch.empty(m, device=dev),
              lo=torch.empty(m, dtype=torch.float64, device=dev), hi=torch.empty(m, dtype=torch.float64, device=dev),
