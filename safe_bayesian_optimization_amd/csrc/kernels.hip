@@ -835,13 +835,6 @@ __device__ __forceinline__ float bf16_rn(float a) {
     const uint32_t w = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
     return __uint_as_float(w << 16);
 }
-__device__ __forceinline__ float split_piece(float a, int plane) {
-    const float a0 = bf16_rn(a);
-    if (plane == 0) return a0;
-    const float r1 = a - a0, a1 = bf16_rn(r1);
-    if (plane == 1) return a1;
-    return bf16_rn(r1 - a1);
-}
 
 // Per packed tile, gain bounds (log2, rounded up), two float4 per tile:
 // lgn[2T]   .x = log2(16 max_r |A_r|_1)  (|A k|_2 <= sqrt(256) |A k|_inf <= 16 max_r |A_r|_1 max|k|)
@@ -867,6 +860,16 @@ typedef double f64x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f64x4_t mfma_f64(double a, double b, f64x4_t c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
+// a 16 x 16 block (bi, bj) of a symmetric 64 x 64 matrix from its MFMA
+// accumulator (lane l, element v: row 16 bi + (l>>4) + 4v, column 16 bj + (l&15)),
+// and its transpose at (bj, bi)
+__device__ __forceinline__ void store_sym(double *g, int bi, int bj, int lane, f64x4_t a) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        g[(16 * bi + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = a[v];
+        if (bi != bj) g[(16 * bj + (lane & 15)) * kBK + 16 * bi + (lane >> 4) + 4 * v] = a[v];
+    }
+}
 __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
                                                            float4 *__restrict__ lgn) {
     // 66 KiB of LDS, two workgroups per CU: the tile (or one of its pieces)
@@ -882,22 +885,38 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
     const int lrow = tid & (kBM / 2 - 1), kh = tid >> 7;   // staging: row lrow of the half, k in [32 kh, 32 kh + 32)
     float out[6];                                // (rows, spectral) of A; of A1; of A2
     double lg_fro_a = -1000.0;
+    // this wave's lower blocks of the 4 x 4 block grid of G: (0,0) (1,0) (1,1) |
+    // (2,0) (2,1) (2,2) | (3,0) (3,1) | (3,2) (3,3)
+    const int nb = wave < 2 ? 3 : 2;
+    const int tbi[3] = {wave < 2 ? 2 * wave : 3, wave < 2 ? 2 * wave + (wave == 0 ? 1 : 0) : 3, wave == 0 ? 1 : 2};
+    const int tbj[3] = {wave < 3 ? 0 : 2, wave == 0 ? 0 : (wave == 1 ? 1 : (wave == 2 ? 1 : 3)), wave == 0 ? 1 : 2};
 #pragma unroll 1
     for (int pi = 0; pi < 3; ++pi) {
         const int plane = pi == 0 ? -1 : pi;     // -1: A itself, then A1, A2
-        // G = A^T A: lane l of wave w feeds A^T[i = 16w + (l&15)][r] and
-        // A[r][j = 16 bj + (l&15)] at r = r0 + (l>>4)
-        f64x4_t acc[4];
+        // G = A^T A, its lower 16 x 16 blocks (bi >= bj; G and its powers are
+        // symmetric bit for bit -- the same products summed in the same order
+        // -- so the upper blocks are written as their transposes): wave w
+        // owns blocks nb, two or three; lane l feeds A^T[i = 16 bi + (l&15)][r]
+        // and A[r][j = 16 bj + (l&15)] at r = r0 + (l>>4)
+        f64x4_t acc[3];
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj) acc[bj] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+        for (int b = 0; b < 3; ++b) acc[b] = f64x4_t{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 1
         for (int half = 0; half < 2; ++half) {
             const int r = half * (kBM / 2) + lrow;
+            // the thread's 32 values in flight at once (a load-use chain per
+            // value was the kernel's critical path), then the piece by
+            // selects (plane is uniform, but a branch per value kept the
+            // compiler from batching the loads); the same sums in the same order
+            float v[32];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) v[j] = t[tile_offset(32 * kh + j, r)];
             double sp = 0.0;
-            for (int k = 32 * kh; k < 32 * kh + 32; ++k) {
-                const float a0 = t[tile_offset(k, r)];
-                const float a = plane < 0 ? a0 : split_piece(a0, plane);
-                at[lrow * kBK + k] = a;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                const float a0 = bf16_rn(v[j]), r1 = v[j] - a0, a1 = bf16_rn(r1), a2 = bf16_rn(r1 - a1);
+                const float a = plane < 0 ? v[j] : (plane == 1 ? a1 : a2);
+                at[lrow * kBK + 32 * kh + j] = a;
                 sp += fabs((double)a);
             }
             if (kh == 1) rsum[r] = sp;
@@ -905,9 +924,9 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
             if (kh == 0) rsum[r] += sp;
             for (int r0 = 0; r0 < kBM / 2; r0 += 4) {
                 const float *row = at + (r0 + (lane >> 4)) * kBK + (lane & 15);
-                const double av = (double)row[16 * wave];
 #pragma unroll
-                for (int bj = 0; bj < 4; ++bj) acc[bj] = mfma_f64(av, (double)row[16 * bj], acc[bj]);
+                for (int b = 0; b < 3; ++b)
+                    if (b < nb) acc[b] = mfma_f64((double)row[16 * tbi[b]], (double)row[16 * tbj[b]], acc[b]);
             }
             __syncthreads();   // at is restaged for the next half
         }
@@ -915,11 +934,11 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
         // from the registers
         double gmx = 0.0;
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj)
+        for (int b = 0; b < 3; ++b)
+            if (b < nb) {
+                store_sym(gm, tbi[b], tbj[b], lane, acc[b]);
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                gm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = acc[bj][v];
-                gmx = fmax(gmx, fabs(acc[bj][v]));
+                for (int v = 0; v < 4; ++v) gmx = fmax(gmx, fabs(acc[b][v]));
             }
         double s = rsum[tid];
 #pragma unroll
@@ -948,28 +967,29 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
             const double mx = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
             if (!(mx > 0.0)) break;
             const int ex = ilogb(mx);
-            f64x4_t sq[4];
+            f64x4_t sq[3];
 #pragma unroll
-            for (int bj = 0; bj < 4; ++bj) sq[bj] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+            for (int b = 0; b < 3; ++b) sq[b] = f64x4_t{0.0, 0.0, 0.0, 0.0};
             for (int k0 = 0; k0 < kBK; k0 += 4) {
-                const double av = ldexp(gm[(16 * wave + (lane & 15)) * kBK + k0 + (lane >> 4)], -2 * ex);
+                const double *arow = gm + (lane & 15) * kBK + k0 + (lane >> 4);
                 const double *brow = gm + (k0 + (lane >> 4)) * kBK + (lane & 15);
 #pragma unroll
-                for (int bj = 0; bj < 4; ++bj) sq[bj] = mfma_f64(av, brow[16 * bj], sq[bj]);
+                for (int b = 0; b < 3; ++b)
+                    if (b < nb) sq[b] = mfma_f64(ldexp(arow[16 * kBK * tbi[b]], -2 * ex), brow[16 * tbj[b]], sq[b]);
             }
             e8 = 2.0 * (e8 + (double)ex);  // (2^e G')^2 = 2^(2e) G'^2
             double qmx = 0.0;
 #pragma unroll
-            for (int bj = 0; bj < 4; ++bj)
+            for (int b = 0; b < 3; ++b)
+                if (b < nb)
 #pragma unroll
-                for (int v = 0; v < 4; ++v) qmx = fmax(qmx, fabs(sq[bj][v]));
+                    for (int v = 0; v < 4; ++v) qmx = fmax(qmx, fabs(sq[b][v]));
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) qmx = fmax(qmx, __shfl_xor(qmx, o));
             __syncthreads();   // every read of G and of red[1] is done
 #pragma unroll
-            for (int bj = 0; bj < 4; ++bj)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) gm[(16 * wave + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = sq[bj][v];
+            for (int b = 0; b < 3; ++b)
+                if (b < nb) store_sym(gm, tbi[b], tbj[b], lane, sq[b]);
             if (lane == 0) red[1][wave] = qmx;
             __syncthreads();
         }
