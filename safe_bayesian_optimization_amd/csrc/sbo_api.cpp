@@ -772,6 +772,7 @@ void precise_budget(sbo_ctx *ctx) {
 // the last probe (the conditioning moves slowly with N).  Needs the f64
 // inverse (SBO_OPT_INVERSE_BITS 64) and a factor (not an imported state).
 constexpr double kPreciseTol = 7e-6;
+constexpr int kProbeRefBits = 24;
 sbo_status probe_precision(sbo_ctx *ctx) {
     const bool avail = ctx->inverse_bits == 64 && ctx->has_factor && ctx->linv_n == ctx->n;
     if (!avail || ctx->precision_opt == 0) {
@@ -798,19 +799,20 @@ sbo_status probe_precision(sbo_ctx *ctx) {
         sbo_status st = run_tick(ctx, qx, qy, M, 0.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, sdf, nullptr, nullptr,
                                  nullptr, key, nullptr, kSweepFast);
         if (st == SBO_OK) {
-            // the reference's budget: 2^-30 of the largest variance the fast
-            // sweep sees (its own error is orders below that: any estimate
-            // within 2x serves), so the reference moves the measured error by
-            // < 1e-9 of max var against the 7e-6 threshold; at most 2^-30 sf2,
-            // at least 2^-60 sf2 (was a fixed 2^-44 sf2: C4 probe 4.8 -> see
-            // DESIGN.md section 5a)
+            // the reference's budget: 2^-kProbeRefBits of the largest variance
+            // the fast sweep sees (its own error is orders below that: any
+            // estimate within 2x serves), so the reference moves the measured
+            // error by < 2^-23 of max var (1.7 % of the 7e-6 threshold); at
+            // most 2^-kProbeRefBits sf2, at least 2^-(2 kProbeRefBits) sf2 (was
+            // a fixed 2^-44 sf2, then 2^-30 of max var: DESIGN.md section 5a)
             const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
             if (hipMemcpyAsync(h.data(), sdf, sizeof(float) * M, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
                 hipStreamSynchronize(ctx->stream) != hipSuccess)
                 st = SBO_E_DEVICE;
             double vf = 0.0;
             for (int i = 0; i < M; ++i) vf = std::max(vf, (double)h[i] * h[i]);
-            ctx->probe_ref_tol = std::ldexp(std::clamp(std::isfinite(vf) ? vf : sf2, std::ldexp(sf2, -30), sf2), -30);
+            ctx->probe_ref_tol = std::ldexp(
+                std::clamp(std::isfinite(vf) ? vf : sf2, std::ldexp(sf2, -kProbeRefBits), sf2), -kProbeRefBits);
         }
         if (st == SBO_OK)
             st = run_tick(ctx, qx, qy, M, 0.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, sdp, nullptr, nullptr, nullptr, key,
