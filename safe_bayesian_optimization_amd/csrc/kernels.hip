@@ -857,6 +857,11 @@ __device__ __forceinline__ float bf16_rn(float a) {
 // (v_mfma_f64_16x16x4_f64; wave w owns rows 16w .. 16w+15 of G, four 16 x 16
 // accumulators).
 typedef double f64x4_t __attribute__((ext_vector_type(4)));
+// LDS row strides of the tile-norm kernel's staged tile (floats) and Gram
+// matrix (doubles), padded off the 64-bank period: with 64 the staging
+// writes (one row per lane) were 64-way bank conflicts, the squarings'
+// column reads 16-way and the final row sums 64-way (measured: DESIGN.md)
+constexpr int kTnAtLd = kBK + 1, kTnGmLd = kBK + 4;
 __device__ __forceinline__ f64x4_t mfma_f64(double a, double b, f64x4_t c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -866,8 +871,8 @@ __device__ __forceinline__ f64x4_t mfma_f64(double a, double b, f64x4_t c) {
 __device__ __forceinline__ void store_sym(double *g, int bi, int bj, int lane, f64x4_t a) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-        g[(16 * bi + (lane >> 4) + 4 * v) * kBK + 16 * bj + (lane & 15)] = a[v];
-        if (bi != bj) g[(16 * bj + (lane & 15)) * kBK + 16 * bi + (lane >> 4) + 4 * v] = a[v];
+        g[(16 * bi + (lane >> 4) + 4 * v) * kTnGmLd + 16 * bj + (lane & 15)] = a[v];
+        if (bi != bj) g[(16 * bj + (lane & 15)) * kTnGmLd + 16 * bi + (lane >> 4) + 4 * v] = a[v];
     }
 }
 __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
@@ -875,8 +880,8 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
     // 66 KiB of LDS, two workgroups per CU: the tile (or one of its pieces)
     // staged 128 rows at a time, the Gram matrix and its powers in place (a
     // product is held in registers until every read of its factor is done)
-    __shared__ float at[(kBM / 2) * kBK];      // half the tile, [row][k]  (32 KiB)
-    __shared__ double gm[kBK * kBK];           // G, then its powers (32 KiB)
+    __shared__ float at[(kBM / 2) * kTnAtLd];  // half the tile, [row][k]  (32.5 KiB)
+    __shared__ double gm[kBK * kTnGmLd];       // G, then its powers (34 KiB)
     __shared__ double rsum[kBM];               // row 1-norms
     __shared__ double red[2][kBM / 64];
     const int64_t tile = t0 + blockIdx.x;
@@ -916,14 +921,14 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
             for (int j = 0; j < 32; ++j) {
                 const float a0 = bf16_rn(v[j]), r1 = v[j] - a0, a1 = bf16_rn(r1), a2 = bf16_rn(r1 - a1);
                 const float a = plane < 0 ? v[j] : (plane == 1 ? a1 : a2);
-                at[lrow * kBK + 32 * kh + j] = a;
+                at[lrow * kTnAtLd + 32 * kh + j] = a;
                 sp += fabs((double)a);
             }
             if (kh == 1) rsum[r] = sp;
             __syncthreads();
             if (kh == 0) rsum[r] += sp;
             for (int r0 = 0; r0 < kBM / 2; r0 += 4) {
-                const float *row = at + (r0 + (lane >> 4)) * kBK + (lane & 15);
+                const float *row = at + (r0 + (lane >> 4)) * kTnAtLd + (lane & 15);
 #pragma unroll
                 for (int b = 0; b < 3; ++b)
                     if (b < nb) acc[b] = mfma_f64((double)row[16 * tbi[b]], (double)row[16 * tbj[b]], acc[b]);
@@ -953,7 +958,7 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
         __syncthreads();
         const double fro2 = [&] {  // trace G = |A|_F^2 (every thread reads it)
             double tr = 0.0;
-            for (int i = 0; i < kBK; ++i) tr += gm[i * kBK + i];
+            for (int i = 0; i < kBK; ++i) tr += gm[i * kTnGmLd + i];
             return tr;
         }();
         // k squarings, G <- (G/c)^2 with c = the largest entry (exact power-of-two
@@ -971,11 +976,11 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
 #pragma unroll
             for (int b = 0; b < 3; ++b) sq[b] = f64x4_t{0.0, 0.0, 0.0, 0.0};
             for (int k0 = 0; k0 < kBK; k0 += 4) {
-                const double *arow = gm + (lane & 15) * kBK + k0 + (lane >> 4);
-                const double *brow = gm + (k0 + (lane >> 4)) * kBK + (lane & 15);
+                const double *arow = gm + (lane & 15) * kTnGmLd + k0 + (lane >> 4);
+                const double *brow = gm + (k0 + (lane >> 4)) * kTnGmLd + (lane & 15);
 #pragma unroll
                 for (int b = 0; b < 3; ++b)
-                    if (b < nb) sq[b] = mfma_f64(ldexp(arow[16 * kBK * tbi[b]], -2 * ex), brow[16 * tbj[b]], sq[b]);
+                    if (b < nb) sq[b] = mfma_f64(ldexp(arow[16 * kTnGmLd * tbi[b]], -2 * ex), brow[16 * tbj[b]], sq[b]);
             }
             e8 = 2.0 * (e8 + (double)ex);  // (2^e G')^2 = 2^(2e) G'^2
             double qmx = 0.0;
@@ -996,7 +1001,7 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
         // ||G^(2^k)||_inf: largest absolute row sum
         double rs = 0.0;
         if (tid < kBK)
-            for (int j = 0; j < kBK; ++j) rs += fabs(gm[tid * kBK + j]);
+            for (int j = 0; j < kBK; ++j) rs += fabs(gm[tid * kTnGmLd + j]);
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) rs = fmax(rs, __shfl_xor(rs, o));
         s = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
