@@ -857,11 +857,13 @@ __device__ __forceinline__ float bf16_rn(float a) {
 // (v_mfma_f64_16x16x4_f64; wave w owns rows 16w .. 16w+15 of G, four 16 x 16
 // accumulators).
 typedef double f64x4_t __attribute__((ext_vector_type(4)));
-// LDS row strides of the tile-norm kernel's staged tile (floats) and Gram
-// matrix (doubles), padded off the 64-bank period: with 64 the staging
-// writes (one row per lane) were 64-way bank conflicts, the squarings'
-// column reads 16-way and the final row sums 64-way (measured: DESIGN.md)
-constexpr int kTnAtLd = kBK + 1, kTnGmLd = kBK + 4;
+// LDS strides of the tile-norm kernel: the Gram matrix (doubles, row
+// stride padded off the 64-bank period: with 64 the squarings' column
+// reads were 16-way bank conflicts and the final row sums 64-way) and the
+// staged half-tile, held k-major ([k][row], 128 rows + 4 padding) so that
+// the staging writes (one row per lane) and the Gram's reads (four rows x 16
+// columns per MFMA operand) both fall on distinct banks
+constexpr int kTnAtLd = kBM / 2 + 4, kTnGmLd = kBK + 4;
 __device__ __forceinline__ f64x4_t mfma_f64(double a, double b, f64x4_t c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -880,7 +882,7 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
     // 66 KiB of LDS, two workgroups per CU: the tile (or one of its pieces)
     // staged 128 rows at a time, the Gram matrix and its powers in place (a
     // product is held in registers until every read of its factor is done)
-    __shared__ float at[(kBM / 2) * kTnAtLd];  // half the tile, [row][k]  (32.5 KiB)
+    __shared__ float at[kBK * kTnAtLd];        // half the tile, [k][row]  (33 KiB)
     __shared__ double gm[kBK * kTnGmLd];       // G, then its powers (34 KiB)
     __shared__ double rsum[kBM];               // row 1-norms
     __shared__ double red[2][kBM / 64];
@@ -921,17 +923,18 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
             for (int j = 0; j < 32; ++j) {
                 const float a0 = bf16_rn(v[j]), r1 = v[j] - a0, a1 = bf16_rn(r1), a2 = bf16_rn(r1 - a1);
                 const float a = plane < 0 ? v[j] : (plane == 1 ? a1 : a2);
-                at[lrow * kTnAtLd + 32 * kh + j] = a;
+                at[(32 * kh + j) * kTnAtLd + lrow] = a;
                 sp += fabs((double)a);
             }
             if (kh == 1) rsum[r] = sp;
             __syncthreads();
             if (kh == 0) rsum[r] += sp;
             for (int r0 = 0; r0 < kBM / 2; r0 += 4) {
-                const float *row = at + (r0 + (lane >> 4)) * kTnAtLd + (lane & 15);
+                const float *col = at + (lane & 15) * kTnAtLd + r0 + (lane >> 4);
 #pragma unroll
                 for (int b = 0; b < 3; ++b)
-                    if (b < nb) acc[b] = mfma_f64((double)row[16 * tbi[b]], (double)row[16 * tbj[b]], acc[b]);
+                    if (b < nb)
+                        acc[b] = mfma_f64((double)col[16 * kTnAtLd * tbi[b]], (double)col[16 * kTnAtLd * tbj[b]], acc[b]);
             }
             __syncthreads();   // at is restaged for the next half
         }
