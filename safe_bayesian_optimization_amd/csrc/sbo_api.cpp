@@ -609,7 +609,8 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         // beside MFMA-bound; C4: 0.22 + 0.41 ms off the fit's critical path)
         const int layout = sbo::x3_layout(ctx->kernel_variant);
         const bool eager_x3 = alpha_aux && ctx->kernel_variant >= 2;
-        const bool eager_f64 = alpha_aux && ctx->precision_opt != 0 && (probe_due(ctx) || ctx->precise);
+        const bool eager_f64 =
+            alpha_aux && ctx->precision_opt != 0 && (probe_due(ctx) || ctx->precise || ctx->precision_opt == 1);
         if (eager_x3) {
             if (layout != ctx->x3_layout) ctx->x3_I0 = 0;
             const int64_t xI0 = std::max<int64_t>(std::min(ctx->x3_I0, I0), 0);
