@@ -184,40 +184,90 @@ def dist_info(backend):
 
 
 def run_launch_check(a, world, rank):
-    """The multi-rank path without a GPU (gloo on CPU tensors): the same cut
-    broadcast and key all-gather the GPU ranks run, on synthetic per-query
-    costs and scores; rank 0 prints a JSON line with what the ranks saw."""
+    """The multi-rank path without a GPU (gloo on CPU tensors), at the sizes the
+    driver's 8-GPU run uses: the cost-cut broadcast of a
+    C4-sized (10^6-query) cost vector that only rank 0 knows
+    (dist.cost_balanced_range), the key all-gather combined both ways -- host
+    (allreduce_key) and through the reduce hook the GPU path uses
+    (allreduce_key_dev; here a host stand-in for the device reduction) -- and
+    the full-grid exchange for the frontier (dist.sharded_subgoal: lo/hi/S
+    all-gathered from uneven row blocks, GetNextSubgoal on every rank).  Rank
+    0 prints a JSON line with what the ranks saw."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    from safe_bayesian_optimization_amd.dist import allreduce_key, balanced_cuts, combine_keys
+    from safe_bayesian_optimization_amd import node as ND
+    from safe_bayesian_optimization_amd.dist import (allreduce_key, allreduce_key_dev, balanced_cuts, combine_keys,
+                                                     cost_balanced_range, key_tensor_to_pairs, rank_cuts,
+                                                     sharded_subgoal)
+    from safe_bayesian_optimization_amd.terrain import CONFIGS
 
     if world > 1:
         dist.init_process_group("gloo")
-    m = 1 << 16
+    _, gw, gh = CONFIGS["C4"]
+    m = gw * gh
     rng = np.random.default_rng(123)
-    cost = rng.uniform(0.5, 2.0, m)
+    # a C4-shaped cost: more tiles in the middle rows than at the edges, noisy
+    rows = np.repeat(np.sin(np.linspace(0.1, np.pi - 0.1, gh)), gw)
+    cost = (0.5 + rows + 0.3 * rng.uniform(size=m)).astype(np.float32)
     score = np.round(rng.uniform(0.0, 4.0, m), 2)   # ties across shards
-    cuts = torch.tensor(balanced_cuts(cost, world) if rank == 0 else [0] * (world + 1), dtype=torch.int64)
-    if world > 1:
-        dist.broadcast(cuts, 0)
-    lo, hi = int(cuts[rank]), int(cuts[rank + 1])
+
+    class _Rank0Costs:   # only rank 0's "mapper" knows the costs: the cut must come from the broadcast
+        def query_cost(self, qx, qy):
+            return cost if rank == 0 else np.ones(m, np.float32)
+
+    q = torch.zeros(m)
+    lo, hi = cost_balanced_range(_Rank0Costs(), q, q, rank, world)
+    cuts = rank_cuts(lo, hi)
     j = int(np.argmax(score[lo:hi])) if hi > lo else -1
     s = float(score[lo + j]) if j >= 0 else 0.0
     key = torch.tensor([np.array([s]).view(np.int64)[0], lo + j if j >= 0 else -1], dtype=torch.int64)
+    want = combine_keys([(float(score.max()), int(np.argmax(score)))])
     best = allreduce_key(key)
-    ok = best == combine_keys([(float(score.max()), int(np.argmax(score)))])
+
+    def host_reduce(gathered, out):
+        sc, ix = combine_keys(key_tensor_to_pairs(gathered))
+        return torch.tensor([np.array([sc]).view(np.int64)[0], ix], dtype=torch.int64)
+
+    best_dev = key_tensor_to_pairs(allreduce_key_dev(key, host_reduce))[0]
+    # the frontier exchange on a smaller grid with uneven cuts (random costs)
+    w, h = 300, 200
+    xs, ys = np.linspace(-3.0, 3.0, w), np.linspace(-2.0, 2.0, h)
+    Dx, Dy = np.tile(xs, h), np.repeat(ys, w)
+    mu = np.sin(1.3 * Dx) * np.cos(0.9 * Dy) * 3 + 0.2 * Dx
+    sd = 0.05 + 0.5 * np.abs(np.sin(0.7 * Dx + Dy))
+    glo = mu - 2.0 * sd
+    ghi = mu + 2.0 * sd
+    gs = (glo > -1.0).astype(np.uint8)
+    fcuts = balanced_cuts(np.random.default_rng(7).gamma(1.0, 1.0, w * h), world, align=1)
+    a0, a1 = fcuts[rank], fcuts[rank + 1]
+    t = lambda v: torch.as_tensor(np.ascontiguousarray(v))  # noqa: E731
+    goal = (2.0, 1.5)
+
+    def fn(Dx_, Dy_, lo_, hi_, s_, w_, h_, gx, gy):
+        return ND.next_subgoal(Dx_, Dy_, lo_.numpy(), hi_.numpy(), s_.numpy(), w_, h_, gx, gy)
+
+    sub = sharded_subgoal(fn, Dx, Dy, t(glo[a0:a1]), t(ghi[a0:a1]), t(gs[a0:a1]), rank_cuts(a0, a1), w, h, goal)
+    sub_want = ND.next_subgoal(Dx, Dy, glo, ghi, gs, w, h, *goal)
+    ok = best == want and best_dev == want and sub == sub_want and sub_want >= 0
+    flags = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(flags, op=dist.ReduceOp.MIN)
     info = dist_info(a.backend)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
+        share = [float(cost[c0:c1].sum()) for c0, c1 in zip(cuts, cuts[1:])]
         print(json.dumps({"metric": METRIC, "value": None, "unit": "grid-points/s", "n_gpus": world,
-                          "launch_check": True, "argmax_matches_global": bool(ok), "cuts": [int(c) for c in cuts],
-                          "config": {"workload": "launch-check", "parallelism": f"m-shard{world}" if world > 1
-                                     else "single"}, **info}), flush=True)
-    return 0 if ok else 1
+                          "launch_check": True, "argmax_matches_global": bool(flags[0]), "cuts": cuts,
+                          "cost_share_max_over_mean": max(share) / (sum(share) / len(share)),
+                          "subgoal": {"index": sub, "want": sub_want, "cuts": fcuts},
+                          "config": {"workload": "launch-check (C4-sized costs)", "M": m,
+                                     "parallelism": f"m-shard{world}" if world > 1 else "single"}, **info}),
+              flush=True)
+    return 0 if bool(flags[0]) else 1
 
 
 def _max_over_ranks(vals, dev, world, backend):
@@ -236,7 +286,8 @@ def run_sweep(a, dev, world, rank):
 
     from safe_bayesian_optimization_amd import TerrainMapper, synthetic
     from safe_bayesian_optimization_amd import _native as N
-    from safe_bayesian_optimization_amd.dist import allreduce_key, cost_balanced_range, shard_range
+    from safe_bayesian_optimization_amd.dist import (allreduce_key, allreduce_key_dev, cost_balanced_range,
+                                                     key_tensor_to_pairs, shard_range)
     from safe_bayesian_optimization_amd.gp import _to_hyper
     from safe_bayesian_optimization_amd.terrain import CONFIGS
 
@@ -342,10 +393,17 @@ def run_sweep(a, dev, world, rank):
     fill_bytes = 4.0 * n * n + 8.0 * n
     del Kbuf
 
+    best_key = torch.empty(2, dtype=torch.int64, device=dev)
+
     def step():
         gm.tick(qx, qy, wl.beta, wl.f_min, score=N.SCORE_WIDTH, index_offset=lo, outputs=outs, key_out=key,
                 async_=True)
-        return allreduce_key(key if a.backend == "nccl" else key.cpu())
+        if a.backend == "nccl" or not a.pg:
+            # RCCL all-gather of the 16-byte keys, combined on the device (no
+            # per-tick host sync); at one rank without a process group the
+            # device combine of the one key
+            return allreduce_key_dev(key, gm.ctx.reduce_keys, out=best_key)
+        return allreduce_key(key.cpu())     # gloo: host tensors, host combine
 
     for _ in range(a.warmup):
         step()
@@ -358,6 +416,8 @@ def run_sweep(a, dev, world, rank):
     for _ in range(a.steps):
         best = step()
     torch.cuda.synchronize()
+    if not isinstance(best, tuple):
+        best = key_tensor_to_pairs(best)[0]
     if a.pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -432,8 +492,9 @@ def run_sweep(a, dev, world, rank):
     traffic, traffic_src = pmc_traffic(a.config, n, m_total, m)
     regimes = None
     if world == 1 and not a.no_regimes:
-        regimes = {"dense": run_regime_dense(a, gm, prof, step, n, m),
-                   "lpsc_stress_box": run_regime_stress(a, gm, prof, dev, n, gw, gh)}
+        regimes = {"dense": run_regime_dense(a, gm, prof, step, n, m)}
+        regimes["append1"] = run_regime_append1(a, gm, dev, wl, qx, qy, outs, key, fit_ms, ms_per_step)
+        regimes["lpsc_stress_box"] = run_regime_stress(a, gm, prof, dev, n, gw, gh)
     if cpu is not None:
         cpu["gpu_over_cpu"] = value / cpu["value"]
         if regimes:
@@ -527,6 +588,47 @@ def run_regime_dense(a, gm, prof, step, n, m):
         gm.set_option(N.SBO_OPT_TILE_SKIP, -1)
     return _regime_line(a, "dense", f"{a.config} tick, SBO_OPT_TILE_SKIP=0 (no skipping, all tiles at six products)",
                         m, n, *res)
+
+
+def run_regime_append1(a, gm, dev, wl, qx, qy, outs, key, fit_ms, tick_ms, iters=50):
+    """The node's steady state: the reference requests a new
+    map on every spatial_data_size change (node.cpp:552-566) and the publisher
+    adds one point per second (turtlesim_spatial_publisher.py:43), so the real
+    per-change cost is a one-point sbo_append (block Cholesky update, the new
+    row of L^-1, the last row block repacked) plus one full tick -- not the
+    refit `end_to_end` prices.  `iters` appends of one point each (new points
+    uniform over the training box, terrain.more_points), a full tick after
+    each, the pair timed together; the context keeps the appended points."""
+    import torch
+
+    from safe_bayesian_optimization_amd.terrain import more_points
+    ax, ay, aobs = more_points(wl, iters + 1, seed=2024)
+    f32 = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
+    AX, AY, AO = f32(ax), f32(ay), f32(aobs)
+
+    def one(i):
+        gm.append(AX[i:i + 1], AY[i:i + 1], AO[i:i + 1])
+        gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs, key_out=key, async_=True)
+
+    one(iters)     # warmup (the append path's code objects and buffers)
+    torch.cuda.synchronize()
+    t_app = 0.0
+    t0 = time.perf_counter()
+    for i in range(iters):
+        t1 = time.perf_counter()
+        gm.append(AX[i:i + 1], AY[i:i + 1], AO[i:i + 1])   # synchronous (the previous tick has finished)
+        t_app += time.perf_counter() - t1
+        gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs, key_out=key, async_=True)
+        torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / iters
+    m = qx.numel()
+    return {"what": f"{iters} x (sbo_append of 1 point + a full tick) after the {wl.name} fit "
+                    f"(N {wl.x.size} -> {wl.x.size + iters + 1})",
+            "value": m / wall, "unit": "grid-points/s", "ms_per_step": wall * 1e3,
+            "append_ms_avg": t_app * 1e3 / iters, "tick_ms_avg": wall * 1e3 - t_app * 1e3 / iters,
+            "vs_refit_end_to_end": {"refit_plus_tick_ms": fit_ms + tick_ms,
+                                    "speedup": (fit_ms + tick_ms) / (wall * 1e3)},
+            "precise_sweep": gm.precision()[0], "n_after": gm.n}
 
 
 def run_regime_stress(a, gm, prof, dev, n, gw, gh):
@@ -720,7 +822,10 @@ def cpu_baseline_streaming(gm, wl, chunks, budget_s):
     xs, ys = wl.x.astype(np.float32)[o], wl.y.astype(np.float32)[o]
     bp = O.BlasPredictor(L, alpha, xs, ys, h.length_scale, h.sf2, h.prior_mean)
     with threadpool_limits(limits=threads, user_api="blas"):
-        # append of the last batch on the CPU (its inputs: the leading factor)
+        # an append of b points on the CPU: the factor's last b rows against
+        # its leading n0 x n0 block.  (With SBO_OPT_RESORT the factor's rows
+        # are in k-d order after a re-sort, so these b rows are not the
+        # caller's last batch but the same sizes: n0 x b solve, b x b update)
         L11 = np.ascontiguousarray(L[:n0, :n0])
         t0 = time.perf_counter()
         K22 = O.rbf_fill_f32in(xs[n0:], ys[n0:], h.length_scale, h.sf2, h.noise_level).astype(np.float32)
@@ -746,7 +851,8 @@ def cpu_baseline_streaming(gm, wl, chunks, budget_s):
     step_s = (t_app + t_tick) * scale
     return {"value": wl.qx.size / step_s, "unit": "grid-points/s", "cores": threads, "host_cpus": total,
             "kind": "port", "append_s_last": t_app, "tick_s_last": t_tick, "n2_scale": scale,
-            "sample": f"last iteration (N {n0} -> {n}): CPU block append + a dense tick over {k2} of the "
+            "sample": f"last iteration sizes (N {n0} -> {n}; the factor's last {b} rows against its leading "
+                      f"block, rows in k-d order after a re-sort): CPU block append + a dense tick over {k2} of the "
                       f"{wl.qx.size} grid points (oracle.BlasPredictor: OpenMP K*, sgemv, OpenBLAS strsm), "
                       f"extrapolated to the grid and scaled by mean(N_i^2)/N_last^2 = {scale:.3f} over the 50 "
                       f"iterations"}

@@ -149,6 +149,13 @@ SBO_API sbo_status sbo_query_cost(sbo_ctx *ctx, const float *qx, const float *qy
 /* Combine two shard keys (the cross-rank reduction of sbo_tick / sbo_argmax). */
 SBO_API sbo_key sbo_key_combine(sbo_key a, sbo_key b);
 
+/* Reduce n keys (e.g. the P keys of a cross-rank all-gather) to one by the
+ * sbo_key_combine rule.  With SBO_DEVICE_PTRS keys and out are device
+ * pointers and the reduction is one workgroup on the context's stream (with
+ * SBO_ASYNC nothing synchronises: the combined key stays on the device, so a
+ * sharded tick needs no host round trip per step); otherwise host memory. */
+SBO_API sbo_status sbo_keys_reduce(sbo_ctx *ctx, const sbo_key *keys, int64_t n, sbo_key *out, uint32_t flags);
+
 /* Host-side node logic (no device needed) ---------------------------------
  * FindSafetyContourIndices() (:418-497): rasterise safe into a
  * height x width image with the node's int-truncated bounds, trace external
@@ -346,9 +353,10 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * in f64 from the fit's f64 inverse, K* in f64, f64 MFMA
  * (v_mfma_f64_16x16x4_f64) and f64 sums; about 3-5x the fast sweep's time on
  * the same tiles.  -1: every sbo_fit (and an sbo_append once N grew by a
- * quarter since the last probe) sweeps a 32 x 32 grid over the training box
- * both ways and ticks with the precise sweep when the fast sweep's variance
- * error there, max |d var| / max var, exceeds 7e-6 (the 1e-5 contract less a margin;
+ * quarter since the last probe, SBO_OPT_REPROBE) sweeps a probe set -- a
+ * 32 x 32 grid over the training box and up to 512 training locations
+ * (sbo_get_probe) -- both ways and ticks with the precise sweep when the fast
+ * sweep's variance error there, max |d var| / max var, exceeds 7e-6 (the 1e-5 contract less a margin;
  * 7e-6 * 2^(20 - B) for a looser SBO_OPT_SKIP_BUDGET B < 20):
  * dense data, where the variance is orders below sf2 and sf2 - |V|^2 cancels
  * (config/lpsc.yaml's own box at N = 16384).  The precise sweep's skip budget
@@ -405,6 +413,18 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
 #define SBO_OPT_INV_BASE 18
 #define SBO_OPT_INV_PANELS 19
 #define SBO_OPT_INV_LEAVES 20
+/* SBO_OPT_REPROBE (percent, default 25; 0: every append): with
+ * SBO_OPT_PRECISION -1, an sbo_append runs the precision probe again once N
+ * has grown by this share since the last probe (every sbo_fit probes). */
+#define SBO_OPT_REPROBE 21
+/* SBO_OPT_PRECISE_KERNEL (1 default | 0): the precise sweep's arithmetic --
+ * 1 A = sf2 L^-1 and K* as five base-128 int8 digit slices each, the 15
+ * leading slice products on the int8 matrix cores (v_mfma_i32_16x16x64_i8,
+ * exact int32 sums), combined in f64 per k-tile (an Ozaki-style sliced
+ * product; predict_oz.hip); 0 every product and sum in f64 on the f64 matrix
+ * cores (v_mfma_f64_16x16x4_f64; predict_f64.hip).  Both meet the 1e-5
+ * contract where the fast sweep cannot (SBO_OPT_PRECISION). */
+#define SBO_OPT_PRECISE_KERNEL 22
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe
@@ -413,6 +433,21 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
  * variance (-1 when no probe ran).  SBO_E_STATE before a fit. */
 SBO_API sbo_status sbo_get_precision(const sbo_ctx *ctx, int *precise, double *probe_err, double *probe_var_min,
                                      double *probe_var_max);
+
+/* The last precision probe in detail (SBO_OPT_PRECISION): its query set is a
+ * 32 x 32 grid over the training box (m_grid points) and m_train training
+ * locations (every (n / m_train)-th stored point); err = the fast sweep's
+ * max |d var| over both / the largest variance of both (the decision's
+ * number, also sbo_get_precision's probe_err), err_grid / err_train = each
+ * part's own max |d var| / its own largest variance.  err* = -1 when no
+ * probe ran.  SBO_E_STATE before a fit. */
+typedef struct sbo_probe {
+    int32_t precise, m_grid, m_train, pad_;
+    int64_t n_at_probe;
+    double err, err_grid, err_train;
+    double var_min, var_max, var_max_grid, var_max_train;
+} sbo_probe;
+SBO_API sbo_status sbo_get_probe(const sbo_ctx *ctx, sbo_probe *out);
 
 /* The K* tile cutoff in effect (auto or fixed) and the norms it was derived from. */
 SBO_API sbo_status sbo_get_skip(const sbo_ctx *ctx, int *cutoff_log2, double *max_row_l1, double *alpha_l1);

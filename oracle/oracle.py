@@ -55,6 +55,7 @@ def lib():
                                   _f64p, _f64p, _i64, _f64p, _f64p]
         L.orc_predict_f32.argtypes = [_f32p, _f32p, _f32p, _f32p, _i64, _dbl, _dbl, _dbl,
                                       _f32p, _f32p, _i64, _f32p, _f32p]
+        L.orc_predict_mean.argtypes = [_f64p, _f64p, _f64p, _i64, _dbl, _dbl, _dbl, _f64p, _f64p, _i64, _f64p]
         L.orc_compute_sets.argtypes = [_f64p, _f64p, _i64, _dbl, _dbl, _f64p, _f64p, _u8p]
         L.orc_argmax.argtypes = [_f64p, ctypes.c_void_p, _i64, ctypes.POINTER(_dbl)]
         L.orc_argmax.restype = _i64
@@ -154,6 +155,15 @@ def predict(Lcm, alpha, x, y, qx, qy, ell=0.4, sf2=1.0, m0=0.0):
     lib().orc_predict(np.ascontiguousarray(Lcm, np.float64).reshape(-1), _c(alpha, np.float64),
                       _c(x, np.float64), _c(y, np.float64), n, ell, sf2, m0, qx, qy, m, mu, var)
     return mu, var
+
+
+def predict_mean(alpha, x, y, qx, qy, ell=0.4, sf2=1.0, m0=0.0):
+    """fp64 posterior mean alone (O(n) per query: whole grids)."""
+    qx = _c(qx, np.float64); qy = _c(qy, np.float64)
+    mu = np.empty(qx.size, np.float64)
+    lib().orc_predict_mean(_c(alpha, np.float64), _c(x, np.float64), _c(y, np.float64), alpha.size, ell, sf2, m0,
+                           qx, qy, qx.size, mu)
+    return mu
 
 
 def predict_f32(Lcm, alpha, x, y, qx, qy, ell=0.4, sf2=1.0, m0=0.0):

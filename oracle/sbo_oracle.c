@@ -284,6 +284,26 @@ ORC_EXPORT void NAME(const REAL *L, const REAL *alpha, const REAL *X, const REAL
 ORC_DEFINE_PREDICT(double, exp, sqrt, orc_predict)
 ORC_DEFINE_PREDICT(float, expf, sqrtf, orc_predict_f32)
 
+/* The posterior mean alone (a3, the `values` the node copies into mu_,
+ * src/safe_bayesian_optimization_node.cpp:642): mu_q = m0 + sum_i alpha_i
+ * sf2 exp(-|x_i - q|^2 / (2 l^2)), in f64, the same terms and order as
+ * orc_predict's acc_mu -- O(n) per query, so the tests can hold the mean of a
+ * whole 10^6-point grid to the oracle (tests/test_gpu_precision.py). */
+ORC_EXPORT void orc_predict_mean(const double *alpha, const double *X, const double *Y, int64_t n, double ell,
+                                 double sf2, double m0, const double *qx, const double *qy, int64_t m, double *mu)
+{
+    const double inv2l2 = 1.0 / (2.0 * ell * ell);
+    _Pragma("omp parallel for schedule(static, 256)")
+    for (int64_t q = 0; q < m; ++q) {
+        double acc = 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+            const double dx = X[i] - qx[q], dy = Y[i] - qy[q];
+            acc += alpha[i] * (sf2 * exp(-(dx * dx + dy * dy) * inv2l2));
+        }
+        mu[q] = m0 + acc;
+    }
+}
+
 /* ------------------------------------------------------------------------ */
 /* a6+a7: ComputeConfidenceIntervals + UpdateSafeSet                          */
 /*   src/safe_bayesian_optimization_node.cpp:411-416 and :409               */
@@ -526,6 +546,11 @@ ORC_EXPORT int64_t orc_next_subgoal(const double *Dx, const double *Dy,
         const size_t fi = pairs[t].i;
         if (wid[fi] > best_w) { best_w = wid[fi]; best = (int64_t)fi; }
     }
+    /* Deliberate divergence, "given the builder's restatement": when no
+     * frontier width exceeds -1 (every width NaN, e.g. a NaN sigma), the
+     * node's best_index stays -1 and it reads frontier_indices[-1]
+     * (node.cpp:537-549, undefined behaviour); the restatement returns -1
+     * ("no subgoal", as node.cpp:503-506 does for an empty frontier). */
     const int64_t r = best >= 0 ? F[best] : -1;
     free(wid);
     free(pairs);

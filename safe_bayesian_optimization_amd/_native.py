@@ -33,7 +33,7 @@ EXPORTS = (
     "sbo_get_order", "sbo_profile_work", "sbo_profile_mfma", "sbo_debug_x3_stamps", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
     "sbo_get_bounds", "sbo_get_jitter", "sbo_get_tile_bounds", "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
     "sbo_polygon_correct", "sbo_polydist", "sbo_point_within", "sbo_project_subgoal", "sbo_get_precision",
-    "sbo_kd_order",
+    "sbo_kd_order", "sbo_get_probe", "sbo_keys_reduce",
 )
 SBO_OPT_INVERSE_BITS = 1
 SBO_OPT_SPATIAL_ORDER = 2
@@ -55,6 +55,8 @@ SBO_OPT_CHOL_GEMM = 17
 SBO_OPT_INV_BASE = 18
 SBO_OPT_INV_PANELS = 19
 SBO_OPT_INV_LEAVES = 20
+SBO_OPT_REPROBE = 21
+SBO_OPT_PRECISE_KERNEL = 22
 
 
 class SboError(RuntimeError):
@@ -74,6 +76,13 @@ class sbo_hyper(ctypes.Structure):
 
 class sbo_key(ctypes.Structure):
     _fields_ = [("score", ctypes.c_double), ("idx", ctypes.c_int64)]
+
+
+class sbo_probe(ctypes.Structure):
+    _fields_ = [("precise", ctypes.c_int32), ("m_grid", ctypes.c_int32), ("m_train", ctypes.c_int32),
+                ("pad_", ctypes.c_int32), ("n_at_probe", ctypes.c_int64), ("err", ctypes.c_double),
+                ("err_grid", ctypes.c_double), ("err_train", ctypes.c_double), ("var_min", ctypes.c_double),
+                ("var_max", ctypes.c_double), ("var_max_grid", ctypes.c_double), ("var_max_train", ctypes.c_double)]
 
 
 _lib = None
@@ -129,6 +138,8 @@ def lib():
     L.sbo_query_cost.restype = st
     L.sbo_key_combine.argtypes = [sbo_key, sbo_key]
     L.sbo_key_combine.restype = sbo_key
+    L.sbo_keys_reduce.argtypes = [vp, vp, i64, vp, u32]
+    L.sbo_keys_reduce.restype = st
     L.sbo_find_safety_contour_indices.argtypes = [vp, vp, vp, i64, i32, i32, vp, i64, ctypes.POINTER(i64)]
     L.sbo_find_safety_contour_indices.restype = st
     L.sbo_next_subgoal.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, dbl, dbl]
@@ -162,6 +173,8 @@ def lib():
     L.sbo_get_precision.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(dbl), ctypes.POINTER(dbl),
                                     ctypes.POINTER(dbl)]
     L.sbo_get_precision.restype = st
+    L.sbo_get_probe.argtypes = [vp, ctypes.POINTER(sbo_probe)]
+    L.sbo_get_probe.restype = st
     L.sbo_get_order.argtypes = [vp, vp]
     L.sbo_get_order.restype = st
     L.sbo_kd_order.argtypes = [vp, vp, i64, i64, vp]

@@ -222,7 +222,9 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float *__restrict__ A, i
                 if (c >= w || bad) continue;   // uniform
                 const int j = jb + c;
                 const float djj = lane_value(p0[c], c);   // row j is lane c's first row
-                if (!(djj > 0.0f) || !(djj < __builtin_huge_valf())) {
+                // a pivot below FLT_MIN (denormal, flushed or zero) is not
+                // positive definite either: its v_rsq_f32 may overflow
+                if (!(djj >= 1.17549435e-38f) || !(djj < __builtin_huge_valf())) {
                     bad = j + 1;
                     continue;
                 }
@@ -375,7 +377,8 @@ __global__ __launch_bounds__(256) void chol_diag_mfma_kernel(float *__restrict__
                 // block never stores)
                 const int j = jb + c;
                 const float djj = lane_value(p0[c], c);   // row j is lane c's first row
-                if (bad == 0 && (!(djj > 0.0f) || !(djj < __builtin_huge_valf()))) bad = j + 1;
+                // (pivots below FLT_MIN fail too: v_rsq_f32 of a denormal may overflow)
+                if (bad == 0 && (!(djj >= 1.17549435e-38f) || !(djj < __builtin_huge_valf()))) bad = j + 1;
                 // every lane, no row tests: the lanes above the diagonal
                 // (row < column) compute values of the upper triangle that
                 // nothing reads (the lane-mask per column and row would be

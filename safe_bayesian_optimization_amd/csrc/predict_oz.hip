@@ -1,0 +1,479 @@
+// predict_oz.hip -- the precise predictive sweep on the int8 matrix cores
+// (round 4; SBO_OPT_PRECISE_KERNEL 1): V = A K*^T with
+// A = sf2 L^-1 and K* both cut into five base-128 int8 digit slices, the slice
+// products accumulated EXACTLY in int32 by v_mfma_i32_16x16x64_i8 and combined
+// in f64 once per k-tile (an Ozaki-style sliced product).
+//
+// Why: on the mapping node's own box (config/lpsc.yaml:32-37) the fast split
+// sweep misses the 1e-5 contract by 40x because it accumulates terms far larger
+// than their sum (|A| |k| >> |A k|) in f32; predict_f64.hip
+// meets it with f64 MFMA at 0.75 of the 78.6 TF f64 peak, and that pipe has no
+// headroom left.  The i8 MFMA runs a 16x16x64 block in the cycles the bf16
+// MFMA spends on 16x16x32 (MI355X_MICROARCH.md, matrix cores: 2x bf16 per
+// clock) and sums its products exactly, so the rounding the contract cannot
+// afford is gone and what is left is the slicing:
+//   A: per (16-row block, k-tile) a power of two 2^eA > 1.01 max|A|; digits by
+//      successive rounding, A = 2^eA sum_s d_s 128^-(s+1) + O(2^eA 128^-5 / 2),
+//      |d_0| <= 127, |d_s| <= 64 (pack_oz_kernel, once per fit / append);
+//   K*: in f64 (exp2 of the f64 distance), per (query, k-tile) a power of two
+//      2^eK > 1.01 max K*, X = rint(K* 2^(35 - eK)) split into the same
+//      balanced digits by integer arithmetic in the sweep;
+//   product: the pairs (s, u) with s + u <= 4 (15 of 25; the dropped ones sit
+//      below 128^-7 of the tile's |A| |K*| scale), level l = s + u chained in
+//      one int32 accumulator (no overflow: 64 products of |d| <= 127 per pair,
+//      worst level sum < 2^21), the five levels combined exactly in f64 per
+//      16x16 block: T = (l0 128 + l1) 2^21 + (l2 128 + l3) 2^7 + l4 (< 2^49),
+//      V += T 2^(eA + eK - 42).
+// Emulated on the host at N = 8192 on the lpsc box (tools/r4_emulate_ozaki.py):
+// normwise variance error 1.2e-6 against f64 (the f32-rounded A alone: 6.5e-5),
+// the same with a per-row scale; truncated digits or four digits miss.
+//
+// Work items, the tick plan and the persistent walk are predict_f64_kernel's:
+// workgroup = 256 rows x 128 queries, eight waves, wave w owns queries
+// 16w..16w+15 and all 256 rows as sixteen 16-row blocks of f64 accumulators
+// (128 VGPRs).  A stage is half a k-tile's ROWS (128 rows x 64 k x 5 digits =
+// 40 KiB, + the eight block exponents, + on the first half the tile's 64
+// coordinates and sf2 alpha), double buffered by LDS-DMA, one barrier per
+// stage; K*'s digits are built on the first half and kept in registers for the
+// second.  Inside a stage the digits are in MFMA fragment order ([digit][block]
+// [lane][16 B]), so a lane's A operand of one MFMA is one conflict-free
+// ds_read_b128.
+#include <cstdint>
+
+#include "sbo_internal.hpp"
+
+namespace sbo {
+namespace {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kOzDigits = 5;                      // base-128 digits per operand
+constexpr int kOzBits = 7 * kOzDigits;            // 35
+constexpr int kOzRB = kBM / 16;                   // 16-row blocks per item (per wave)
+constexpr int kOzHalfRB = kOzRB / 2;              // blocks per stage
+constexpr int kOzPlane = kOzHalfRB * 64 * 16;     // one digit plane of a stage: 8 KiB
+constexpr int kOzA = kOzDigits * kOzPlane;        // 40 KiB of digits per stage
+constexpr int kOzTileBytes = 2 * kOzA;            // one packed tile: 80 KiB
+constexpr int kOzE = 64;                          // the stage's block exponents (8 x int32, padded)
+constexpr int kOzC = kBK * 4 * 2 + kBK * 8;       // per k-tile: x, y (f32) + sf2 alpha (f64) = 1 KiB
+constexpr int kOzSlot = kOzA + kOzE + kOzC;
+constexpr int kOzWaves = kBN / 16;                // 8
+constexpr int kOzThreads = 64 * kOzWaves;
+constexpr int kOzDescWin = 64;                    // item descriptors (int4) per 1 KiB window
+constexpr int kOzListWin = 512;                   // tile-list entries (u16) per 1 KiB window
+constexpr int kOzSmem = 2 * kOzSlot + 4096;       // two stage slots + two descriptor and two list windows
+// balanced-digit offset: 64 at each of the four lower base-128 positions
+constexpr uint32_t kOzBias = 64u * (1u + 128u + 16384u + 2097152u);
+static_assert(kOzA % (1024 * kOzWaves) == 0, "stage digits: whole 1 KiB LDS-DMA pieces per wave");
+
+__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
+    return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+// K*'s five digit operands for this lane's 16 k (k = 16 g + j, g = lane >> 4)
+// and its query, from the tile's coordinates in LDS: X = rint(K* 2^(35 - eK))
+// (f64, exact), Y = X + bias, top digit Y >> 28, the four lower digits the
+// 7-bit fields of Y's low 28 bits less 64 -- spread into bytes and transposed
+// four k at a time so that digit u of k = 16 g + j is byte j of kd[u].  The
+// per-(query, tile) exponent eK needs the max over all 64 k: the four lanes
+// l, l ^ 16, l ^ 32, l ^ 48 hold them.  Also mu += K* sf2 alpha (wmean = 1 on
+// the last row block).
+__device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, int g, double xq, double yq, double cexp,
+                                             double wmean, i32x4 (&kd)[kOzDigits], int &eK, double &mu) {
+    const float *px = reinterpret_cast<const float *>(pc) + 16 * g;
+    const float *py = reinterpret_cast<const float *>(pc + kBK * 4) + 16 * g;
+    const double *pa = reinterpret_cast<const double *>(pc + kBK * 8) + 16 * g;
+    // pass 1: the exponent from an f32 estimate of every K* (v_exp_f32, a few
+    // ulp; the 1.01 margin covers it), so that pass 2 can cut each f64 K* into
+    // digits as soon as it is computed (four live at a time, not sixteen)
+    float kmax = 0.0f;
+    const float cexpf = (float)cexp;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const float dx = px[j] - (float)xq, dy = py[j] - (float)yq;
+        kmax = fmaxf(kmax, __builtin_amdgcn_exp2f(cexpf * fmaf(dy, dy, dx * dx)));
+    }
+    kmax = fmaxf(kmax, __shfl_xor(kmax, 16));
+    kmax = fmaxf(kmax, __shfl_xor(kmax, 32));
+    // 2^eK > 1.01 kmax, so K* 2^-eK < 0.99 and the top digit stays <= 127
+    int e = 0;
+    (void)frexpf(kmax * 1.01f, &e);
+    eK = kmax > 0.0f ? e : 0;
+    const double sc = ldexp(1.0, kOzBits - eK);
+#pragma unroll
+    for (int m4 = 0; m4 < 4; ++m4) {
+        uint32_t lo[4], hi[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = 4 * m4 + i;
+            const double dx = (double)px[j] - xq, dy = (double)py[j] - yq;
+            const double kv = exp2(cexp * fma(dy, dy, dx * dx));
+            mu = fma(kv, pa[j] * wmean, mu);
+            const double Y = rint(kv * sc) + (double)kOzBias;                // < 2^35, exact
+            const double Yh = floor(Y * 0x1p-28);
+            hi[i] = (uint32_t)Yh;
+            const uint32_t L = (uint32_t)fma(-Yh, 0x1p28, Y);               // Y mod 2^28, exact
+            // the four 7-bit fields into bytes 3..0 (digit u = 1 in byte 3),
+            // each less 64 as a two's-complement byte: b < 64 -> b | 0xC0,
+            // b >= 64 -> b ^ 0x40
+            uint32_t s = ((L >> 21) & 0x7Fu) << 24 | ((L >> 14) & 0x7Fu) << 16 | ((L >> 7) & 0x7Fu) << 8 |
+                         (L & 0x7Fu);
+            lo[i] = (s ^ 0x40404040u) | ((~s & 0x40404040u) << 1);
+        }
+        // 4 x 4 byte transpose: byte i of the dword for digit u = byte (4 - u) of lo[i]
+        const uint32_t p01a = __builtin_amdgcn_perm(lo[1], lo[0], 0x05010400u);   // lo0.b0 lo1.b0 lo0.b1 lo1.b1
+        const uint32_t p01b = __builtin_amdgcn_perm(lo[1], lo[0], 0x07030602u);   // lo0.b2 lo1.b2 lo0.b3 lo1.b3
+        const uint32_t p23a = __builtin_amdgcn_perm(lo[3], lo[2], 0x05010400u);
+        const uint32_t p23b = __builtin_amdgcn_perm(lo[3], lo[2], 0x07030602u);
+        kd[4][m4] = (int)__builtin_amdgcn_perm(p23a, p01a, 0x05040100u);          // bytes 0 of lo0..lo3
+        kd[3][m4] = (int)__builtin_amdgcn_perm(p23a, p01a, 0x07060302u);          // bytes 1
+        kd[2][m4] = (int)__builtin_amdgcn_perm(p23b, p01b, 0x05040100u);          // bytes 2
+        kd[1][m4] = (int)__builtin_amdgcn_perm(p23b, p01b, 0x07060302u);          // bytes 3
+        kd[0][m4] = (int)(hi[0] | hi[1] << 8 | hi[2] << 16 | hi[3] << 24);
+    }
+}
+
+// The 15 digit products of one 16x16 block, combined exactly and added to acc
+// scaled by 2^(eA + eK - 42).
+__device__ __forceinline__ void block_products(const i32x4 (&ad)[kOzDigits], const i32x4 (&kd)[kOzDigits],
+                                               double S, f64x4 &acc) {
+    const i32x4 z = {0, 0, 0, 0};
+    i32x4 l0 = mfma_i8(ad[0], kd[0], z);
+    i32x4 l1 = mfma_i8(ad[0], kd[1], z);
+    l1 = mfma_i8(ad[1], kd[0], l1);
+    i32x4 l2 = mfma_i8(ad[0], kd[2], z);
+    l2 = mfma_i8(ad[1], kd[1], l2);
+    l2 = mfma_i8(ad[2], kd[0], l2);
+    i32x4 l3 = mfma_i8(ad[0], kd[3], z);
+    l3 = mfma_i8(ad[1], kd[2], l3);
+    l3 = mfma_i8(ad[2], kd[1], l3);
+    l3 = mfma_i8(ad[3], kd[0], l3);
+    i32x4 l4 = mfma_i8(ad[0], kd[4], z);
+    l4 = mfma_i8(ad[1], kd[3], l4);
+    l4 = mfma_i8(ad[2], kd[2], l4);
+    l4 = mfma_i8(ad[3], kd[1], l4);
+    l4 = mfma_i8(ad[4], kd[0], l4);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const int h01 = l0[v] * 128 + l1[v];      // |.| < 2^28
+        const int h23 = l2[v] * 128 + l3[v];
+        const double t = fma(fma((double)h01, 16384.0, (double)h23), 128.0, (double)l4[v]);   // exact, < 2^49
+        acc[v] = fma(t, S, acc[v]);
+    }
+}
+
+// One stage: the eight 16-row blocks of the staged half, all in one code path
+// per half (the accumulators are indexed statically).
+template <int H>
+__device__ __forceinline__ void stage_blocks(const char *__restrict__ slot, int lane, const i32x4 (&kd)[kOzDigits],
+                                             int eK, f64x4 (&acc)[kOzRB]) {
+    const int *eA = reinterpret_cast<const int *>(slot + kOzA);
+    const i32x4 *pa = reinterpret_cast<const i32x4 *>(slot) + lane;
+#pragma unroll
+    for (int rb = 0; rb < kOzHalfRB; ++rb) {
+        i32x4 ad[kOzDigits];
+#pragma unroll
+        for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[s * (kOzPlane / 16) + rb * 64];
+        const double S = ldexp(1.0, __builtin_amdgcn_readfirstlane(eA[rb]) + eK - 6 * 7);
+        block_products(ad, kd, S, acc[H * kOzHalfRB + rb]);
+    }
+}
+
+__global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
+    const char *__restrict__ aoz, const int *__restrict__ eoz, const char *__restrict__ koz,
+    const int4 *__restrict__ desc, const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P,
+    int n_items, int nI, const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp,
+    double cexp, double m0, double *__restrict__ part, double *__restrict__ mean) {
+    __shared__ __attribute__((aligned(16))) char smem[kOzSmem];
+    const int bid = blockIdx.x;
+    const int rng = (P % 8 == 0) ? (bid % 8) * (P / 8) + bid / 8 : bid;
+    // (bounds are clamped so that a corrupt plan cannot address outside the buffers)
+    const int k0 = max(seg[rng], 0), k1 = min(seg[rng + 1], n_items);
+    if (k0 >= k1) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int r = lane & 15;
+    const int g = lane >> 4;
+    const int4 *dwin = reinterpret_cast<const int4 *>(smem + 2 * kOzSlot);
+    const unsigned short *lwin = reinterpret_cast<const unsigned short *>(smem + 2 * kOzSlot + 2048);
+
+    // LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction, lane
+    // linear), issued from inline asm as in predict_f64_kernel: every wave
+    // moves 5 KiB of each 40 KiB stage; wave 0 lanes 0-1 the stage's eight
+    // block exponents, wave 1 the tile's coordinates on its first half.
+    typedef __attribute__((address_space(3))) char lds_char;
+    const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
+    const uint32_t lds_wave = lds_smem + (uint32_t)__builtin_amdgcn_readfirstlane(wave) * 1024u;
+    const uint32_t lds_dwin = lds_smem + 2u * kOzSlot;
+    const uint32_t lds_lwin = lds_dwin + 2048u;
+    const char *gA = aoz + wave * 1024 + lane * 16;
+    const char *gE = reinterpret_cast<const char *>(eoz) + lane * 16;
+    const char *gC = koz + lane * 16;
+    const char *gD = reinterpret_cast<const char *>(desc) + lane * 16;
+    const char *gL = reinterpret_cast<const char *>(tl) + lane * 16;
+#define SBO_OZ_DMA16(gsrc, ldst)                                                                         \
+    do {                                                                                                 \
+        uint32_t keep_;                                                                                  \
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t" \
+                     "s_mov_b32 m0, %0"                                                                  \
+                     : "=&s"(keep_)                                                                      \
+                     : "v"(gsrc), "s"(ldst)                                                              \
+                     : "memory");                                                                        \
+    } while (0)
+    // stage (packed tile T_ of k-tile kt_, row half h_) into slot buf
+#define SBO_OZ_STAGE(T_, kt_, h_, buf)                                                                   \
+    do {                                                                                                 \
+        const char *s_ = gA + (int64_t)(T_) * kOzTileBytes + (h_) * kOzA;                                \
+        const uint32_t d_ = __builtin_amdgcn_readfirstlane(lds_wave + (uint32_t)(buf) * kOzSlot);        \
+        _Pragma("unroll") for (int j_ = 0; j_ < kOzA / (1024 * kOzWaves); ++j_)                          \
+            SBO_OZ_DMA16(s_ + j_ * kOzWaves * 1024, d_ + (uint32_t)(j_ * kOzWaves * 1024));              \
+        if (wave == 0 && lane < 2)                                                                       \
+            SBO_OZ_DMA16(gE + (int64_t)(T_) * 64 + (h_) * 32,                                            \
+                         __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA)));     \
+        if (wave == 1 && (h_) == 0)                                                                      \
+            SBO_OZ_DMA16(gC + (int64_t)(kt_) * kOzC,                                                     \
+                         __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA + kOzE))); \
+    } while (0)
+#define SBO_OZ_DESC_WINDOW(w_)                                                                           \
+    do {                                                                                                 \
+        if (wave == 1) SBO_OZ_DMA16(gD + (int64_t)(w_) * 1024, lds_dwin + (uint32_t)((w_) & 1) * 1024u); \
+    } while (0)
+#define SBO_OZ_LIST_WINDOW(w_)                                                                           \
+    do {                                                                                                 \
+        if (wave == 2) SBO_OZ_DMA16(gL + (int64_t)(w_) * 1024, lds_lwin + (uint32_t)((w_) & 1) * 1024u); \
+    } while (0)
+    auto desc_at = [&](int k) {  // wave-uniform descriptor from its (loaded) window
+        const int4 d = dwin[((k / kOzDescWin) & 1) * kOzDescWin + k % kOzDescWin];
+        const int I = min(max(__builtin_amdgcn_readfirstlane(d.x), 0), nI - 1);
+        return make_int4(I, __builtin_amdgcn_readfirstlane(d.y), __builtin_amdgcn_readfirstlane(d.z),
+                         __builtin_amdgcn_readfirstlane(d.w));
+    };
+    auto entry_off = [](const int4 &d) {
+        return (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
+    };
+    auto list_at = [&](uint64_t e, int I) {  // the k-tile of tile-list entry e (level code ignored)
+        const int t = __builtin_amdgcn_readfirstlane((int)lwin[((e / kOzListWin) & 1) * kOzListWin + e % kOzListWin]) &
+                      ((1 << kLevelShift) - 1);
+        return min(t, kTilesPerRowBlockStep * (I + 1) - 1);
+    };
+
+    // ---- prologue: the first two windows of each kind, the first stage
+    SBO_OZ_DESC_WINDOW(k0 / kOzDescWin);
+    SBO_OZ_DESC_WINDOW(k0 / kOzDescWin + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int4 dc = desc_at(k0);
+    uint64_t e = entry_off(dc);
+    SBO_OZ_LIST_WINDOW(e / kOzListWin);
+    SBO_OZ_LIST_WINDOW(e / kOzListWin + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int t = list_at(e, dc.x);
+    SBO_OZ_STAGE(tile_start(dc.x) + t, t, 0, 0);
+    int64_t q = (int64_t)dc.y * kBN + wave * 16 + r;
+    double xq = (double)qx[q < m ? q : m - 1], yq = (double)qy[q < m ? q : m - 1];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    f64x4 acc[kOzRB];
+#pragma unroll
+    for (int rb = 0; rb < kOzRB; ++rb) acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    i32x4 kd[kOzDigits];
+    int eK = 0;
+    double mu = 0.0;
+    int k = k0, j = 0, h = 0, cur = 0;
+    for (;;) {
+        const int cnt = dc.w & 0xffff;
+        // the next stage: the other half of this tile, the next tile of this
+        // item, or the first tile of item k + 1
+        int kn = k, jn = j, hn = h + 1;
+        if (hn == 2) {
+            hn = 0;
+            jn = j + 1;
+            if (jn >= cnt) {
+                kn = k + 1;
+                jn = 0;
+            }
+        }
+        const bool more = kn < k1;
+        int4 dn = dc;
+        int tn = t;
+        double xqn = xq, yqn = yq;
+        if (more) {
+            if (kn != k) {
+                dn = desc_at(kn);
+                if (kn % kOzDescWin == 0) SBO_OZ_DESC_WINDOW(kn / kOzDescWin + 1);
+                const int64_t qn = (int64_t)dn.y * kBN + wave * 16 + r;
+                xqn = (double)qx[qn < m ? qn : m - 1];
+                yqn = (double)qy[qn < m ? qn : m - 1];
+            }
+            if (hn == 0) {
+                const uint64_t en = e + 1;
+                if (en % kOzListWin == 0) SBO_OZ_LIST_WINDOW(en / kOzListWin + 1);
+                tn = list_at(en, dn.x);
+            }
+            SBO_OZ_STAGE(tile_start(dn.x) + tn, tn, hn, cur ^ 1);
+        }
+        const char *slot = smem + cur * kOzSlot;
+        const int I = dc.x;
+        if (h == 0) {
+            kstar_digits(slot + kOzA + kOzE, g, xq, yq, cexp, I == nI - 1 ? 1.0 : 0.0, kd, eK, mu);
+            stage_blocks<0>(slot, lane, kd, eK, acc);
+        } else {
+            stage_blocks<1>(slot, lane, kd, eK, acc);
+        }
+        if (h == 1 && j == cnt - 1) {
+            // item done: column sums of V^2 over its 256 rows; lane l holds
+            // rows 4 (l >> 4) + v of every 16-row block, column l & 15
+            double sum = 0.0;
+#pragma unroll
+            for (int rb = 0; rb < kOzRB; ++rb) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) sum = fma(acc[rb][c], acc[rb][c], sum);
+                acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
+            }
+            sum += __shfl_xor(sum, 16);
+            sum += __shfl_xor(sum, 32);
+            const bool writer = lane < 16 && q < m;
+            if (writer) part[(int64_t)I * ldp + q] = sum;
+            if (I == nI - 1) {
+                mu += __shfl_xor(mu, 16);
+                mu += __shfl_xor(mu, 32);
+                if (writer) mean[q] = m0 + mu;
+                mu = 0.0;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (!more) break;
+        if (kn != k) {
+            k = kn;
+            dc = dn;
+            xq = xqn;
+            yq = yqn;
+            q = (int64_t)dc.y * kBN + wave * 16 + r;
+        }
+        if (hn == 0) ++e;
+        j = jn;
+        h = hn;
+        t = tn;
+        cur ^= 1;
+    }
+#undef SBO_OZ_STAGE
+#undef SBO_OZ_DESC_WINDOW
+#undef SBO_OZ_LIST_WINDOW
+#undef SBO_OZ_DMA16
+}
+
+// A = sf2 L^-1 (from the fit's f64 inverse, lower, column-major, lda ld) into
+// int8 digit tiles for row blocks I >= I0: tile (I, t) at tile_start(I) + t,
+// 80 KiB = [row half h][digit s][16-row block rb][lane l][byte j], element
+// (row 128 h + 16 rb + (l & 15), k = 64 t + 16 (l >> 4) + j); the exponent of
+// each 16-row block at eoz[16 (tile_start(I) + t) + 8 h + rb].  One workgroup
+// per tile, one thread per row: its 64 values, the block max by a 16-lane
+// reduction, then the digits of 16 consecutive k packed into one 16-B store
+// per (digit, k group).  grid.x = k-tiles of the longest row block, grid.y =
+// row block I - I0.
+__global__ __launch_bounds__(256) void pack_oz_kernel(const double *__restrict__ Linv, int64_t ld, int64_t n,
+                                                      double sf2, int64_t I0, char *__restrict__ aoz,
+                                                      int *__restrict__ eoz) {
+    const int64_t I = I0 + blockIdx.y;
+    const int64_t kb = blockIdx.x;
+    if (kb >= (I + 1) * kTilesPerRowBlockStep) return;
+    const int64_t T = tile_start(I) + kb;
+    const int rr = threadIdx.x;                 // row within the row block
+    const int64_t row = I * kBM + rr;
+    double v[kBK];
+    double amax = 0.0;
+#pragma unroll
+    for (int c = 0; c < kBK; ++c) {
+        const int64_t col = kb * kBK + c;
+        v[c] = (row < n && col < n && col <= row) ? sf2 * Linv[row + col * ld] : 0.0;
+        amax = fmax(amax, fabs(v[c]));
+    }
+    // the 16-row block's max: lanes 16 b .. 16 b + 15 of the wave
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) amax = fmax(amax, __shfl_xor(amax, o));
+    int eA = -900;                               // an all-zero block: digits 0, scale negligible
+    if (amax > 0.0) {
+        int e;
+        (void)frexp(amax * 1.01, &e);           // 2^e > 1.01 max |A|: |A| 2^-e < 0.99
+        eA = e;
+    }
+    const int sub = rr >> 4, h = sub >> 3, rb = sub & 7;
+    if ((rr & 15) == 0) eoz[T * 16 + sub] = eA;
+    const double sc = ldexp(1.0, -eA);
+    char *base = aoz + T * (int64_t)kOzTileBytes + h * kOzA + rb * 1024;
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+        uint32_t w[kOzDigits][4];
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            double x = eA > -900 ? v[16 * gg + jj] * sc : 0.0;
+#pragma unroll
+            for (int s = 0; s < kOzDigits; ++s) {
+                x *= 128.0;
+                const double d = rint(x);
+                x -= d;                          // exact; |x| <= 1/2 from the second digit on
+                const uint32_t b = (uint32_t)(int)d & 0xFFu;
+                if ((jj & 3) == 0) w[s][jj >> 2] = b;
+                else w[s][jj >> 2] |= b << (8 * (jj & 3));
+            }
+        }
+        const int l = (rr & 15) + 16 * gg;
+#pragma unroll
+        for (int s = 0; s < kOzDigits; ++s) {
+            uint4 *dst = reinterpret_cast<uint4 *>(base + s * kOzPlane + l * 16);
+            *dst = make_uint4(w[s][0], w[s][1], w[s][2], w[s][3]);
+        }
+    }
+}
+
+// Per k-tile: x[64], y[64] (f32, as stored), sf2 alpha[64] (f64, alpha from
+// the f64 solve); padding rows: the first point's coordinates, alpha 0.
+__global__ void pack_koz_kernel(const float *__restrict__ x, const float *__restrict__ y,
+                                const double *__restrict__ alpha, int64_t n, int64_t npad, double sf2,
+                                char *__restrict__ koz) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= npad) return;
+    char *c = koz + (k / kBK) * kOzC;
+    const int o = (int)(k % kBK);
+    const bool in = k < n;
+    reinterpret_cast<float *>(c)[o] = in ? x[k] : x[0];
+    reinterpret_cast<float *>(c + kBK * 4)[o] = in ? y[k] : y[0];
+    reinterpret_cast<double *>(c + kBK * 8)[o] = in ? sf2 * alpha[k] : 0.0;
+}
+
+}  // namespace
+
+size_t oz_operand_bytes(int64_t npad) { return (size_t)kOzTileBytes * (size_t)total_tiles(npad / kBM); }
+size_t oz_exp_bytes(int64_t npad) { return 64 * (size_t)total_tiles(npad / kBM); }
+size_t oz_coord_bytes(int64_t npad) { return (size_t)kOzC * (size_t)(npad / kBK); }
+
+hipError_t launch_pack_oz(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
+                          double sf2, const float *x, const float *y, const double *alpha, char *aoz, int *eoz,
+                          char *koz) {
+    const int64_t nI = npad / kBM;
+    if (I0 < nI) {
+        hipLaunchKernelGGL(pack_oz_kernel, dim3((unsigned)(nI * kTilesPerRowBlockStep), (unsigned)(nI - I0)),
+                           dim3(256), 0, s, Linv, ld, n, sf2, I0, aoz, eoz);
+    }
+    hipLaunchKernelGGL(pack_koz_kernel, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, s, x, y, alpha, n, npad,
+                       sf2, koz);
+    return hipGetLastError();
+}
+
+hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, const char *koz, const int4 *desc,
+                             const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
+                             const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
+                             double *mean) {
+    if (nI <= 0 || m <= 0) return hipSuccess;
+    const double cexp = -1.0 / (2.0 * ell * ell * 0.69314718055994530942);
+    hipLaunchKernelGGL(predict_oz_kernel, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc, tl, seg, P,
+                       n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean);
+    return hipGetLastError();
+}
+
+}  // namespace sbo

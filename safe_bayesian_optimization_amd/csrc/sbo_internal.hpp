@@ -175,9 +175,16 @@ struct sbo_ctx {
     bool precise = false;        // the sweep ticks run in effect
     sbo::DevBuf alpha64;         // alpha from the f64 solve (length cap)
     sbo::DevBuf a64, kc64;       // f64 packed operand and coordinates, derived lazily
-    int64_t a64_I0 = 0;          // first row block whose f64 operand is stale
+    sbo::DevBuf aoz, eoz, koz;   // int8 digit operand, its block exponents, coordinates (predict_oz.hip)
+    int precise_kernel = 1;      // SBO_OPT_PRECISE_KERNEL: 0 the f64 MFMA sweep, 1 the int8 sliced sweep
+    int64_t a64_I0 = 0;          // first row block whose precise operand (of precise_kernel) is stale
     int64_t probe_n = 0;         // training points at the last probe (0: none)
     double probe_err = -1.0, probe_vmin = 0.0, probe_vmax = 0.0;  // fast sweep's error on the probe, var range
+    // the probe's two parts: its grid over the training box, and training
+    // locations (where the variance is smallest); each part's own normwise error
+    double probe_err_grid = -1.0, probe_err_train = -1.0, probe_vmax_grid = 0.0, probe_vmax_train = 0.0;
+    int probe_m_grid = 0, probe_m_train = 0;
+    int reprobe_pct = 25;        // SBO_OPT_REPROBE: appends re-probe once N grew by this share (0: every append)
     bool inv_batched = true;      // SBO_OPT_INV_LEAVES: the recursion's base cases in one batched dtrtri
     bool inv_leaves_done = false; // (set while a recursion runs whose base cases are already inverted)
     int64_t widened_n = 0;       // blocked_potrf widened the factor into Linv (n) for refresh_operand
@@ -373,6 +380,22 @@ hipError_t launch_predict_f64(hipStream_t s, const double *a64, const double *kc
                               const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
                               const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
                               double *mean);
+// The int8 sliced precise sweep (predict_oz.hip, SBO_OPT_PRECISE_KERNEL 1):
+// A = sf2 L^-1 from the fit's f64 inverse as five base-128 int8 digit slices
+// per 16-row block and k-tile (80 KiB per packed tile) with a power-of-two
+// exponent per block (oz_exp_bytes: 16 int32 per tile), per k-tile x, y (f32)
+// and sf2 alpha (f64).  The sweep reads the same plan as launch_predict_f64 and
+// writes the same f64 partials and mean.
+size_t oz_operand_bytes(int64_t npad);
+size_t oz_exp_bytes(int64_t npad);
+size_t oz_coord_bytes(int64_t npad);
+hipError_t launch_pack_oz(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
+                          double sf2, const float *x, const float *y, const double *alpha, char *aoz, int *eoz,
+                          char *koz);
+hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, const char *koz, const int4 *desc,
+                             const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
+                             const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
+                             double *mean);
 // Morton ordering of the queries (query_order.hip): workspace of
 // query_order_bytes(m); returns the permutation and the gathered coordinates
 // (all inside the workspace).

@@ -105,6 +105,26 @@ class Context:
                                          int(width), int(height), float(gx), float(gy), ctypes.byref(idx), fl))
         return int(idx.value)
 
+    def reduce_keys(self, keys, out=None, *, async_: bool = True):
+        """Combine n raw 16-byte keys ((n, 2) or (2n,) int64: f64 score bits,
+        i64 index) into one (sbo_keys_reduce).  Device tensors stay on the
+        device -- the reduction runs on this context's stream, no host sync
+        with async_ -- and the (2,) int64 result tensor is returned; host
+        arrays return a (score, index) pair."""
+        n = int((keys.numel() if _is_dev(keys) else np.asarray(keys).size) // 2)
+        if _is_dev(keys):
+            import torch
+            keys = keys.contiguous()
+            if out is None:
+                out = torch.empty(2, dtype=torch.int64, device=keys.device)
+            fl = N.SBO_DEVICE_PTRS | (N.SBO_ASYNC if async_ else 0)
+            self.check(self._lib.sbo_keys_reduce(self.handle, _ptr(keys), n, _ptr(out), fl))
+            return out
+        k = np.ascontiguousarray(np.asarray(keys, np.int64).reshape(-1))
+        r = N.sbo_key()
+        self.check(self._lib.sbo_keys_reduce(self.handle, ctypes.c_void_p(k.ctypes.data), n, ctypes.byref(r), 0))
+        return r.score, int(r.idx)
+
     def close(self) -> None:
         if getattr(self, "handle", None):
             self._lib.sbo_destroy(self.handle)
@@ -246,6 +266,15 @@ class TerrainMapper:
         self.ctx.check(self._lib.sbo_get_precision(self.ctx.handle, ctypes.byref(p), ctypes.byref(e),
                                                    ctypes.byref(vmin), ctypes.byref(vmax)))
         return bool(p.value), e.value, vmin.value, vmax.value
+
+    def probe_info(self) -> dict:
+        """The last precision probe in detail (sbo_get_probe): its grid and
+        training-location parts, each part's own normwise variance error and
+        the combined one the decision used."""
+        from ._native import sbo_probe
+        p = sbo_probe()
+        self.ctx.check(self._lib.sbo_get_probe(self.ctx.handle, ctypes.byref(p)))
+        return {f: getattr(p, f) for f, _ in sbo_probe._fields_ if f != "pad_"}
 
     def set_option(self, option: int, value: int) -> None:
         self.ctx.check(self._lib.sbo_set_option(self.ctx.handle, int(option), int(value)))

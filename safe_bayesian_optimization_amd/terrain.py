@@ -87,6 +87,8 @@ class Workload:
     hyper: Hyper
     f_min: float
     beta: float = 2.0    # config/safe_bayesian_optimization.yaml:4
+    side: float | None = None   # the square the observation field is defined on (more_points)
+    seed: int = 0
 
 
 def smooth_field(px, py, side: float, ell: float, seed: int, bumps: int = 32):
@@ -120,7 +122,7 @@ def synthetic(n: int, grid_w: int, grid_h: int | None = None, seed: int = 0,
     QY, QX = np.meshgrid(gy, gx, indexing="ij")
     f_min = float(np.percentile(obs, 40.0))
     return Workload(name or f"synthetic_n{n}_g{grid_w}x{grid_h}", x, y, obs, QX.reshape(-1), QY.reshape(-1),
-                    grid_w, grid_h, hyper, f_min)
+                    grid_w, grid_h, hyper, f_min, side=side, seed=seed)
 
 
 def synthetic_box(n: int, grid_w: int, grid_h: int, x_range=(0.0, 1.0), y_range=(0.0, 2.5), seed: int = 0,
@@ -143,7 +145,94 @@ def synthetic_box(n: int, grid_w: int, grid_h: int, x_range=(0.0, 1.0), y_range=
     QY, QX = np.meshgrid(gy, gx, indexing="ij")
     f_min = float(np.percentile(obs, 40.0))
     return Workload(name or f"lpsc_box_n{n}_g{grid_w}x{grid_h}", x, y, obs, QX.reshape(-1), QY.reshape(-1),
-                    grid_w, grid_h, hyper, f_min)
+                    grid_w, grid_h, hyper, f_min, seed=seed)
+
+
+def robot_path(n: int, side: float, seed: int = 0, v_max: float = 0.3, w_max: float = 1.0):
+    """Training locations shaped like the publisher's stream: 30 points
+    uniform within radius 1 of the start pose (turtlesim_spatial_publisher.py
+    :111-149), then one sample per second at the robot pose (:43, :151-183).
+
+    The robot follows waypoints the way reactive_navigation drives it: heading
+    turned toward the waypoint at <= ``w_max`` rad/s, speed
+    min(v_max, leg speed, distance) (config/reactive_planner.yaml:9-12: gains
+    1.0, 0.3 m/s, 1 rad/s), and it waits a few ticks at every waypoint (the
+    planner replans on each new sample, :552-566).  Leg speeds are U[0.02,
+    v_max]: slow legs lay dense lines of points (one per 0.02 units, l/20),
+    fast ones sparse ones, dwells exact duplicates -- clustered, path-shaped
+    data on a domain of side ``side`` that the path covers only in part."""
+    u = uniform(seed ^ 0xBA7, 8 * n + 64)
+    ang = 2.0 * math.pi * u[0:60:2]
+    dist = u[1:60:2]
+    c = side / 2.0
+    x = np.empty(n)
+    y = np.empty(n)
+    k0 = min(30, n)
+    x[:k0] = np.clip(c + dist[:k0] * np.cos(ang[:k0]), 0.1, side - 0.1)
+    y[:k0] = np.clip(c + dist[:k0] * np.sin(ang[:k0]), 0.1, side - 0.1)
+    px, py, th = c, c, 0.0
+    wx = wy = c
+    leg_v = v_max
+    dwell = 0
+    j = 64
+    for i in range(k0, n):
+        if dwell > 0:
+            dwell -= 1
+        else:
+            dx, dy = wx - px, wy - py
+            d = math.hypot(dx, dy)
+            if d < 0.05:
+                # a new waypoint 2-10 units away, inside the domain; dwell 0-8 ticks
+                a = 2.0 * math.pi * u[j]
+                r = 2.0 + 8.0 * u[j + 1]
+                wx = min(max(px + r * math.cos(a), 0.5), side - 0.5)
+                wy = min(max(py + r * math.sin(a), 0.5), side - 0.5)
+                leg_v = 0.02 + (v_max - 0.02) * u[j + 2]
+                dwell = int(9 * u[j + 3])
+                j += 4
+            else:
+                err = math.atan2(dy, dx) - th
+                err = (err + math.pi) % (2.0 * math.pi) - math.pi
+                th += max(-w_max, min(w_max, err))
+                v = min(leg_v, d) * max(0.0, math.cos(err))
+                px = min(max(px + v * math.cos(th), 0.1), side - 0.1)
+                py = min(max(py + v * math.sin(th), 0.1), side - 0.1)
+        x[i], y[i] = px, py
+    return x, y
+
+
+def path_workload(n: int, grid_w: int = 1000, grid_h: int | None = None, side: float | None = None, seed: int = 0,
+                  hyper: Hyper | None = None, name: str | None = None) -> Workload:
+    """Path-clustered workload: ``robot_path`` training
+    locations on a square of side 150 l (60 units at l = 0.4) by default,
+    observations = smooth field + N(0, sn2), a grid_w x grid_h query grid over
+    the data bounds, f_min = 40th percentile of the observations."""
+    hyper = hyper or Hyper()
+    grid_h = grid_h or grid_w
+    side = side or 150.0 * hyper.length_scale
+    x, y = robot_path(n, side, seed)
+    obs = smooth_field(x, y, side, hyper.length_scale, seed) + math.sqrt(hyper.sn2) * normal(seed + 1, n)
+    gx = np.linspace(x.min(), x.max(), grid_w)
+    gy = np.linspace(y.min(), y.max(), grid_h)
+    QY, QX = np.meshgrid(gy, gx, indexing="ij")
+    f_min = float(np.percentile(obs, 40.0))
+    return Workload(name or f"path_n{n}_g{grid_w}x{grid_h}", x, y, obs, QX.reshape(-1), QY.reshape(-1),
+                    grid_w, grid_h, hyper, f_min, side=side, seed=seed)
+
+
+def more_points(wl: Workload, k: int, seed: int = 99):
+    """k further measurements for a synthetic workload (the node's trigger:
+    one new point per spatial_data_size change, node.cpp:552-566): locations
+    uniform over the training points' bounding box, observations from the
+    workload's own field + N(0, sn2).  Returns (x, y, obs) as f64 arrays."""
+    if wl.side is None:
+        raise ValueError("more_points: workload without a field square (synthetic / path_workload only)")
+    u = uniform(seed ^ 0xADD, 2 * k)
+    x = wl.x.min() + u[0::2] * (wl.x.max() - wl.x.min())
+    y = wl.y.min() + u[1::2] * (wl.y.max() - wl.y.min())
+    h = wl.hyper
+    obs = smooth_field(x, y, wl.side, h.length_scale, wl.seed) + math.sqrt(h.sn2) * normal(seed + 7, k)
+    return x, y, obs
 
 
 def make_terrain_csv(rows: int = 48, cols: int = 64, seed: int = 7) -> np.ndarray:

@@ -153,18 +153,24 @@ def _bench(*args, env=None, timeout=240):
     return r.returncode, (json.loads(lines[-1]) if lines else None), r
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_launches_its_own_ranks(world):
     """`python bench.py --gpus N` with no WORLD_SIZE starts N ranks itself
     (torch.distributed.run on 127.0.0.1); the JSON line reports the world
-    size and backend the collective saw, the cut broadcast and key all-gather
-    give the global argmax (gloo, CPU rehearsal of the GPU path)."""
-    rc, line, r = _bench("--gpus", str(world), "--launch-check")
+    size and backend the collective saw; on a C4-sized (10^6) cost vector the
+    cut broadcast balances the work, the key all-gather (host combine and the
+    device-path reduce hook) gives the global argmax, and the sharded subgoal
+    over uneven row blocks equals the single-rank one (gloo, CPU rehearsal of
+    the driver's 8-GPU run)."""
+    rc, line, r = _bench("--gpus", str(world), "--launch-check", timeout=600)
     assert rc == 0, r.stderr[-2000:]
     assert line["n_gpus"] == world and line["world_size"] == world and line["backend"] == "gloo"
     assert line["config"]["parallelism"] == f"m-shard{world}"
     assert line["argmax_matches_global"] is True
-    assert line["cuts"][0] == 0 and line["cuts"][-1] == 1 << 16 and len(line["cuts"]) == world + 1
+    assert line["cuts"][0] == 0 and line["cuts"][-1] == 10 ** 6 and len(line["cuts"]) == world + 1
+    assert all(c % 128 == 0 for c in line["cuts"][1:-1])
+    assert line["cost_share_max_over_mean"] < 1.01
+    assert line["subgoal"]["index"] == line["subgoal"]["want"] >= 0
 
 
 def test_bench_rejects_gpus_world_mismatch():

@@ -1069,6 +1069,18 @@ def test_inverse_overlap_is_bitwise(mapper, n):
     gm.fit(wl.x, wl.y, wl.obs)
     mu2, sd2 = gm.predict(wl.qx, wl.qy)
     assert np.array_equal(mu2, got[0][2]) and np.array_equal(sd2, got[0][3])
+    # an overlapped fit that fails NOT_SPD, then a rocSOLVER-spotrf
+    # refit (SBO_OPT_CHOLESKY 0) of the same n on the same context must not
+    # reuse the failed fit's first inverse half
+    with pytest.raises(N.NotSPDError):
+        bad.fit(x, y, wl.obs)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_CHOLESKY, 0)
+    gm.fit(wl.x, wl.y, wl.obs)
+    mu3, sd3 = gm.predict(wl.qx, wl.qy)
+    omu, ovar = oracle_given_factor(gm, wl)
+    assert nrel(mu3, omu) < REL_TOL and nrel(sd3.astype(np.float64) ** 2, ovar) < REL_TOL
+    gm.set_option(N.SBO_OPT_CHOLESKY, 1)
     gm.set_option(N.SBO_OPT_INV_OVERLAP, 0)
 
 
@@ -1266,18 +1278,28 @@ def test_precision_levels(mapper):
 
 
 # ------------------------------------------- precise (f64) sweep, SBO_OPT_PRECISION
+# the precise kernels' tolerances against the fp64 oracle: the f64 sweep to
+# f64 rounding (f32 outputs: 1e-6), the int8 sliced sweep to its slicing
+# (emulated 1.2e-6 on the lpsc box at N = 8192, tools/r4_emulate_ozaki.py)
+PRECISE_TOL = {0: (1e-6, 1e-6), 1: (1e-6, 4e-6)}
+
+
+@pytest.mark.parametrize("kernel", [0, 1])
 @pytest.mark.parametrize("n,gw,gh,box", [(2048, 64, 48, False), (3000, 90, 70, True), (700, 40, 30, True)])
-def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box):
-    """SBO_OPT_PRECISION = 1: A = sf2 L^-1 in f64, K* in f64, f64 MFMA and sums
-    -- against the fp64 oracle given the same factor, alpha solved from it in
-    f64 (the f32 alpha the fast sweep uses would add its own rounding times
-    |K*| to the mean: 1.5e-6 after the N = 700 box's append), to f64-level
-    agreement (the budgeted skip at 2^-B of the smallest probe variance), on
-    the default domain and on the lpsc.yaml box (dense data, small
-    variance)."""
+def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box, kernel):
+    """SBO_OPT_PRECISION = 1: the f64 sweep (SBO_OPT_PRECISE_KERNEL 0: A =
+    sf2 L^-1 in f64, K* in f64, f64 MFMA and sums) and the int8 sliced sweep
+    (1: five int8 digit slices of each, exact int32 slice products, f64
+    combination) against the fp64 oracle given the same factor, alpha solved
+    from it in f64 (the f32 alpha the fast sweep uses would add its own
+    rounding times |K*| to the mean: 1.5e-6 after the N = 700 box's append),
+    under the budgeted skip at 2^-B of the smallest probe variance, on the
+    default domain and on the lpsc.yaml box (dense data, small variance)."""
     from safe_bayesian_optimization_amd.terrain import synthetic_box
+    tmu, tvar = PRECISE_TOL[kernel]
     wl = synthetic_box(n, gw, gh, seed=n) if box else synthetic(n, gw, gh, seed=n + 1)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
     gm.set_option(N.SBO_OPT_PRECISION, 1)
     try:
         gm.fit(wl.x, wl.y, wl.obs)
@@ -1288,10 +1310,10 @@ def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box):
         key = gm.tick(wl.qx, wl.qy, wl.beta, wl.f_min, outputs=out)
         omu, ovar = oracle_given_factor64(gm, wl)
         emu, evar = nrel(out["mu"], omu), nrel(out["sd"].astype(np.float64) ** 2, ovar)
-        print(f"precise N={n} box={box}: mu {emu:.2e} var {evar:.2e} (fast sweep on the probe: {perr:.2e}, "
-              f"probe var {vmin:.2e}..{vmax:.2e})")
+        print(f"precise kernel {kernel} N={n} box={box}: mu {emu:.2e} var {evar:.2e} (fast sweep on the probe: "
+              f"{perr:.2e}, probe var {vmin:.2e}..{vmax:.2e})")
         # the outputs are f32: mu and sigma rounded once (sigma^2 within 2 ulp)
-        assert emu < 1e-6 and evar < 1e-6
+        assert emu < tmu and evar < tvar
         olo, ohi, osafe = O.compute_sets(out["mu"], out["sd"], wl.beta, wl.f_min)
         assert np.array_equal(out["lo"], olo) and np.array_equal(out["safe"], osafe)
         assert key.idx == O.argmax(ohi - olo, osafe)[0]
@@ -1301,9 +1323,37 @@ def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box):
         wl2 = type(wl)(wl.name, np.concatenate([wl.x, wl.x[:37] + 0.013]), np.concatenate([wl.y, wl.y[:37]]),
                        np.concatenate([wl.obs, wl.obs[:37]]), wl.qx, wl.qy, gw, gh, wl.hyper, wl.f_min)
         omu2, ovar2 = oracle_given_factor64(gm, wl2)
-        assert nrel(mu2, omu2) < 1e-6 and nrel(sd2.astype(np.float64) ** 2, ovar2) < 1e-6
+        assert nrel(mu2, omu2) < tmu and nrel(sd2.astype(np.float64) ** 2, ovar2) < tvar
     finally:
         gm.set_option(N.SBO_OPT_PRECISION, -1)
+        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 1)
+
+
+def test_int8_mfma_k_layout(mapper):
+    """The int8 sliced sweep assumes only that v_mfma_i32_16x16x64_i8 maps
+    byte j of lane l's A and B fragments to the same k: a K* tile with one
+    nonzero query per lane group and digits only in chosen bytes would expose
+    a mismatch as wrong sums.  Checked end to end instead at tiny sizes where
+    every tile is dense: N = 64 / 65 / 130 points (one, two, three k-tiles,
+    ragged), a handful of queries, the int8 sweep against the f64 sweep."""
+    from safe_bayesian_optimization_amd.terrain import synthetic_box
+    for n in (64, 65, 130):
+        wl = synthetic_box(n, 7, 5, seed=n)
+        outs = {}
+        for kernel in (0, 1):
+            gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+            gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
+            gm.set_option(N.SBO_OPT_PRECISION, 1)
+            gm.fit(wl.x, wl.y, wl.obs)
+            outs[kernel] = gm.predict(wl.qx, wl.qy)
+        gm.set_option(N.SBO_OPT_PRECISION, -1)
+        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 1)
+        omu, ovar = oracle_given_factor64(gm, wl)
+        for kernel in (0, 1):
+            mu, sd = outs[kernel]
+            emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
+            print(f"N={n} kernel {kernel}: mu {emu:.2e} var {evar:.2e}")
+            assert emu < PRECISE_TOL[kernel][0] and evar < PRECISE_TOL[kernel][1], (n, kernel)
 
 
 def test_precision_auto_probe(mapper):
