@@ -520,7 +520,7 @@ def run_sweep(a, dev, world, rank):
                    "outputs_written": not a.no_outputs,
                    "precision": {"precise_sweep": prec[0], "probe_fast_sweep_variance_error": prec[1],
                                  "probe_var_min": prec[2], "probe_var_max": prec[3],
-                                 "rule": "SBO_OPT_PRECISION -1: f64 sweep when the probe error > 7e-6"}},
+                                 "rule": "SBO_OPT_PRECISION -1: the precise sweep when the probe error > 5e-6"}},
         "roofline": dict(predict_roofline(a.variant, exec_flops_launch, pred_ms, mfma_flops_launch, levels_launch,
                                           prec[0]),
                          traffic=traffic,

@@ -356,8 +356,8 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * quarter since the last probe, SBO_OPT_REPROBE) sweeps a probe set -- a
  * 32 x 32 grid over the training box and up to 512 training locations
  * (sbo_get_probe) -- both ways and ticks with the precise sweep when the fast
- * sweep's variance error there, max |d var| / max var, exceeds 7e-6 (the 1e-5 contract less a margin;
- * 7e-6 * 2^(20 - B) for a looser SBO_OPT_SKIP_BUDGET B < 20):
+ * sweep's variance error there, max |d var| / max var, exceeds 5e-6 (the 1e-5 contract over the largest whole-grid / probe ratio measured, 1.77;
+ * 5e-6 * 2^(20 - B) for a looser SBO_OPT_SKIP_BUDGET B < 20):
  * dense data, where the variance is orders below sf2 and sf2 - |V|^2 cancels
  * (config/lpsc.yaml's own box at N = 16384).  The precise sweep's skip budget
  * is 2^-B times the smallest probe variance (SBO_OPT_SKIP_BUDGET = B).  Needs

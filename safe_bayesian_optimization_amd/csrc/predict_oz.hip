@@ -21,9 +21,9 @@
 //   product: the pairs (s, u) with s + u <= 4 (15 of 25; the dropped ones sit
 //      below 128^-7 of the tile's |A| |K*| scale), level l = s + u chained in
 //      one int32 accumulator (no overflow: 64 products of |d| <= 127 per pair,
-//      worst level sum < 2^21), the five levels combined exactly in f64 per
-//      16x16 block: T = (l0 128 + l1) 2^21 + (l2 128 + l3) 2^7 + l4 (< 2^49),
-//      V += T 2^(eA + eK - 42).
+//      worst level sum < 2^21), the five levels combined in f64 per 16x16
+//      block: T = (l0 128 + l1) 2^14 + l2 128 + l3 + round(l4 / 128) (< 2^42;
+//      exact but for level 4's last seven bits), V += T 2^(eA + eK - 35).
 // Emulated on the host at N = 8192 on the lpsc box (tools/r4_emulate_ozaki.py):
 // normwise variance error 1.2e-6 against f64 (the f32-rounded A alone: 6.5e-5),
 // the same with a per-row scale; truncated digits or four digits miss.
@@ -48,50 +48,77 @@ namespace {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kOzDigits = 5;                      // base-128 digits per operand
+constexpr int kOzDigits = 5;                      // base-128 digits of A
 constexpr int kOzBits = 7 * kOzDigits;            // 35
+constexpr int kOzKDigits = 4;                     // base-128 digits of K*
+constexpr int kOzKBits = 7 * kOzKDigits;          // 28
 constexpr int kOzRB = kBM / 16;                   // 16-row blocks per item (per wave)
 constexpr int kOzHalfRB = kOzRB / 2;              // blocks per stage
 constexpr int kOzPlane = kOzHalfRB * 64 * 16;     // one digit plane of a stage: 8 KiB
 constexpr int kOzA = kOzDigits * kOzPlane;        // 40 KiB of digits per stage
 constexpr int kOzTileBytes = 2 * kOzA;            // one packed tile: 80 KiB
 constexpr int kOzE = 64;                          // the stage's block exponents (8 x int32, padded)
-constexpr int kOzC = kBK * 4 * 2 + kBK * 8;       // per k-tile: x, y (f32) + sf2 alpha (f64) = 1 KiB
+constexpr int kOzC = 3 * kBK * 8;                 // per k-tile: x, y, sf2 alpha (f64) = 1.5 KiB
 constexpr int kOzSlot = kOzA + kOzE + kOzC;
 constexpr int kOzWaves = kBN / 16;                // 8
 constexpr int kOzThreads = 64 * kOzWaves;
 constexpr int kOzDescWin = 64;                    // item descriptors (int4) per 1 KiB window
 constexpr int kOzListWin = 512;                   // tile-list entries (u16) per 1 KiB window
-constexpr int kOzSmem = 2 * kOzSlot + 4096;       // two stage slots + two descriptor and two list windows
-// balanced-digit offset: 64 at each of the four lower base-128 positions
-constexpr uint32_t kOzBias = 64u * (1u + 128u + 16384u + 2097152u);
+constexpr int kOzSmem = 2 * kOzSlot + 4096 + 512; // two stage slots + two descriptor and two list windows + 2^(j/64)
+// K*'s digits: X = rint(K* 2^(28 - eK)) + bias, bias = 64 at the three lower
+// base-128 positions, by one f64 add of 2^52 + bias (the add rounds to an
+// integer and leaves X + bias in the low mantissa bits)
+constexpr uint32_t kOzBias = 64u * (1u + 128u + 16384u);
+constexpr double kOzMagic = 4503599627370496.0 + (double)kOzBias;
 static_assert(kOzA % (1024 * kOzWaves) == 0, "stage digits: whole 1 KiB LDS-DMA pieces per wave");
 
 __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
     return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
 }
 
-// K*'s five digit operands for this lane's 16 k (k = 16 g + j, g = lane >> 4)
-// and its query, from the tile's coordinates in LDS: X = rint(K* 2^(35 - eK))
-// (f64, exact), Y = X + bias, top digit Y >> 28, the four lower digits the
-// 7-bit fields of Y's low 28 bits less 64 -- spread into bytes and transposed
-// four k at a time so that digit u of k = 16 g + j is byte j of kd[u].  The
-// per-(query, tile) exponent eK needs the max over all 64 k: the four lanes
-// l, l ^ 16, l ^ 32, l ^ 48 hold them.  Also mu += K* sf2 alpha (wmean = 1 on
-// the last row block).
-__device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, int g, double xq, double yq, double cexp,
-                                             double wmean, i32x4 (&kd)[kOzDigits], int &eK, double &mu) {
-    const float *px = reinterpret_cast<const float *>(pc) + 16 * g;
-    const float *py = reinterpret_cast<const float *>(pc + kBK * 4) + 16 * g;
-    const double *pa = reinterpret_cast<const double *>(pc + kBK * 8) + 16 * g;
+// 2^u in f64 for the K* digits (u <= 0): u = e + j/64 + r, |r| <= 1/128,
+// 2^u = 2^e T[j] P(r) with T[j] = 2^(j/64) from an LDS table and P the degree-5
+// Taylor polynomial of 2^r (truncation < (ln2/128)^6 / 720 < 2^-45 relative,
+// the table and the Horner steps a few 2^-53): 11 f64 operations instead of
+// the library exp2's ~30 -- the digits keep 35 bits of K* 2^-eK.  Returns
+// T[j] P(r) and sets e (the caller folds 2^e into its scale).
+__device__ __forceinline__ double exp2_tab(double u, const double *__restrict__ T, int &e) {
+    const double m = rint(u * 64.0);
+    const double r = fma(m, -0.015625, u);
+    const int mi = (int)m;
+    e = mi >> 6;                      // floor(m / 64): arithmetic shift
+    const double t = T[mi & 63];
+    constexpr double c1 = 0.69314718055994530942, c2 = 0.24022650695910071233, c3 = 0.055504108664821579953,
+                     c4 = 0.0096181291076284771620, c5 = 0.0013333558146428443423;
+    const double p = fma(fma(fma(fma(fma(c5, r, c4), r, c3), r, c2), r, c1), r, 1.0);
+    return t * p;
+}
+
+// K*'s four digit operands for this lane's 16 k (k = 16 g + j, g = lane >> 4)
+// and its query, from the tile's coordinates in LDS: Y = rint(K* 2^(28 - eK))
+// + bias as the low 28 bits of K* 2^(28 - eK) + 2^52 + bias (f64, exact), top
+// digit Y >> 21, the three lower digits the 7-bit fields below it less 64 --
+// spread into bytes and transposed four k at a time so that digit u of k =
+// 16 g + j is byte j of kd[u].  The per-(query, tile) exponent eK needs the max
+// over all 64 k: the four lanes l, l ^ 16, l ^ 32, l ^ 48 hold them.  Four
+// digits (28 bits) suffice for K*: its f32 rounding alone moved the lpsc box's
+// variance by only 2.6e-6 (tools/r4_emulate_ozaki.py), against 6.5e-5 for A.
+// On the last row block (mean) also mu += K* sf2 alpha.
+template <bool MEAN>
+__device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, const double *__restrict__ T2, int g,
+                                             double xq, double yq, double cexp, i32x4 (&kd)[kOzKDigits], int &eK,
+                                             double &mu) {
+    const double *px = reinterpret_cast<const double *>(pc) + 16 * g;
+    const double *py = reinterpret_cast<const double *>(pc + kBK * 8) + 16 * g;
+    const double *pa = reinterpret_cast<const double *>(pc + kBK * 16) + 16 * g;
     // pass 1: the exponent from an f32 estimate of every K* (v_exp_f32, a few
     // ulp; the 1.01 margin covers it), so that pass 2 can cut each f64 K* into
     // digits as soon as it is computed (four live at a time, not sixteen)
     float kmax = 0.0f;
-    const float cexpf = (float)cexp;
+    const float cexpf = (float)cexp, xqf = (float)xq, yqf = (float)yq;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        const float dx = px[j] - (float)xq, dy = py[j] - (float)yq;
+        const float dx = (float)px[j] - xqf, dy = (float)py[j] - yqf;
         kmax = fmaxf(kmax, __builtin_amdgcn_exp2f(cexpf * fmaf(dy, dy, dx * dx)));
     }
     kmax = fmaxf(kmax, __shfl_xor(kmax, 16));
@@ -100,86 +127,102 @@ __device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, int g,
     int e = 0;
     (void)frexpf(kmax * 1.01f, &e);
     eK = kmax > 0.0f ? e : 0;
-    const double sc = ldexp(1.0, kOzBits - eK);
+    const int esc = kOzKBits - eK;
 #pragma unroll
     for (int m4 = 0; m4 < 4; ++m4) {
-        uint32_t lo[4], hi[4];
+        uint32_t lo[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int j = 4 * m4 + i;
-            const double dx = (double)px[j] - xq, dy = (double)py[j] - yq;
-            const double kv = exp2(cexp * fma(dy, dy, dx * dx));
-            mu = fma(kv, pa[j] * wmean, mu);
-            const double Y = rint(kv * sc) + (double)kOzBias;                // < 2^35, exact
-            const double Yh = floor(Y * 0x1p-28);
-            hi[i] = (uint32_t)Yh;
-            const uint32_t L = (uint32_t)fma(-Yh, 0x1p28, Y);               // Y mod 2^28, exact
-            // the four 7-bit fields into bytes 3..0 (digit u = 1 in byte 3),
-            // each less 64 as a two's-complement byte: b < 64 -> b | 0xC0,
-            // b >= 64 -> b ^ 0x40
-            uint32_t s = ((L >> 21) & 0x7Fu) << 24 | ((L >> 14) & 0x7Fu) << 16 | ((L >> 7) & 0x7Fu) << 8 |
-                         (L & 0x7Fu);
-            lo[i] = (s ^ 0x40404040u) | ((~s & 0x40404040u) << 1);
+            const double dx = px[j] - xq, dy = py[j] - yq;
+            int ex;
+            const double kt = exp2_tab(cexp * fma(dy, dy, dx * dx), T2, ex);   // K* = kt 2^ex
+            if (MEAN) mu = fma(ldexp(kt, ex), pa[j], mu);
+            const uint32_t Y = (uint32_t)__builtin_bit_cast(uint64_t, ldexp(kt, ex + esc) + kOzMagic);
+            // the four 7-bit fields into bytes 3..0 (the top digit in byte 3);
+            // the three lower ones less 64 as two's-complement bytes:
+            // b < 64 -> b | 0xC0, b >= 64 -> b ^ 0x40
+            const uint32_t sp = ((Y >> 21) & 0x7Fu) << 24 | ((Y >> 14) & 0x7Fu) << 16 | ((Y >> 7) & 0x7Fu) << 8 |
+                                (Y & 0x7Fu);
+            lo[i] = (sp ^ 0x00404040u) | ((~sp & 0x00404040u) << 1);
         }
-        // 4 x 4 byte transpose: byte i of the dword for digit u = byte (4 - u) of lo[i]
+        // 4 x 4 byte transpose: byte i of the dword for digit u = byte (3 - u) of lo[i]
         const uint32_t p01a = __builtin_amdgcn_perm(lo[1], lo[0], 0x05010400u);   // lo0.b0 lo1.b0 lo0.b1 lo1.b1
         const uint32_t p01b = __builtin_amdgcn_perm(lo[1], lo[0], 0x07030602u);   // lo0.b2 lo1.b2 lo0.b3 lo1.b3
         const uint32_t p23a = __builtin_amdgcn_perm(lo[3], lo[2], 0x05010400u);
         const uint32_t p23b = __builtin_amdgcn_perm(lo[3], lo[2], 0x07030602u);
-        kd[4][m4] = (int)__builtin_amdgcn_perm(p23a, p01a, 0x05040100u);          // bytes 0 of lo0..lo3
-        kd[3][m4] = (int)__builtin_amdgcn_perm(p23a, p01a, 0x07060302u);          // bytes 1
-        kd[2][m4] = (int)__builtin_amdgcn_perm(p23b, p01b, 0x05040100u);          // bytes 2
-        kd[1][m4] = (int)__builtin_amdgcn_perm(p23b, p01b, 0x07060302u);          // bytes 3
-        kd[0][m4] = (int)(hi[0] | hi[1] << 8 | hi[2] << 16 | hi[3] << 24);
+        kd[3][m4] = (int)__builtin_amdgcn_perm(p23a, p01a, 0x05040100u);          // bytes 0 of lo0..lo3
+        kd[2][m4] = (int)__builtin_amdgcn_perm(p23a, p01a, 0x07060302u);          // bytes 1
+        kd[1][m4] = (int)__builtin_amdgcn_perm(p23b, p01b, 0x05040100u);          // bytes 2
+        kd[0][m4] = (int)__builtin_amdgcn_perm(p23b, p01b, 0x07060302u);          // bytes 3: the top digit
     }
 }
 
-// The 15 digit products of one 16x16 block, combined exactly and added to acc
-// scaled by 2^(eA + eK - 42).
-__device__ __forceinline__ void block_products(const i32x4 (&ad)[kOzDigits], const i32x4 (&kd)[kOzDigits],
+// The 14 digit products of one 16x16 block (A digit s, K* digit u, s + u <=
+// 4, u <= 3), combined and added to acc scaled by 2^(eA + eK - 35): level 4 is
+// folded into level 3 rounded to a level-3 unit (2^-36 of the tile's scale
+// 2^(eA + eK), below the dropped level 5's share), the rest exactly: T =
+// (l0 128 + l1) 2^14 + l2 128 + l3 + [l4 / 128] in level-3 units, two
+// conversions and two f64 operations per value.
+__device__ __forceinline__ void block_products(const i32x4 (&ad)[kOzDigits], const i32x4 (&kd)[kOzKDigits],
                                                double S, f64x4 &acc) {
+    // ordered by A digit (each ad[s] dies after its group; the int32 sums are
+    // exact, so the order does not change the result)
     const i32x4 z = {0, 0, 0, 0};
     i32x4 l0 = mfma_i8(ad[0], kd[0], z);
     i32x4 l1 = mfma_i8(ad[0], kd[1], z);
-    l1 = mfma_i8(ad[1], kd[0], l1);
     i32x4 l2 = mfma_i8(ad[0], kd[2], z);
-    l2 = mfma_i8(ad[1], kd[1], l2);
-    l2 = mfma_i8(ad[2], kd[0], l2);
     i32x4 l3 = mfma_i8(ad[0], kd[3], z);
+    l1 = mfma_i8(ad[1], kd[0], l1);
+    l2 = mfma_i8(ad[1], kd[1], l2);
     l3 = mfma_i8(ad[1], kd[2], l3);
+    i32x4 l4 = mfma_i8(ad[1], kd[3], z);
+    l2 = mfma_i8(ad[2], kd[0], l2);
     l3 = mfma_i8(ad[2], kd[1], l3);
-    l3 = mfma_i8(ad[3], kd[0], l3);
-    i32x4 l4 = mfma_i8(ad[0], kd[4], z);
-    l4 = mfma_i8(ad[1], kd[3], l4);
     l4 = mfma_i8(ad[2], kd[2], l4);
+    l3 = mfma_i8(ad[3], kd[0], l3);
     l4 = mfma_i8(ad[3], kd[1], l4);
     l4 = mfma_i8(ad[4], kd[0], l4);
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-        const int h01 = l0[v] * 128 + l1[v];      // |.| < 2^28
-        const int h23 = l2[v] * 128 + l3[v];
-        const double t = fma(fma((double)h01, 16384.0, (double)h23), 128.0, (double)l4[v]);   // exact, < 2^49
+        const int h01 = l0[v] * 128 + l1[v];                      // |.| < 2^28
+        const int h23 = l2[v] * 128 + l3[v] + ((l4[v] + 64) >> 7);
+        const double t = fma((double)h01, 16384.0, (double)h23);  // exact, < 2^42
         acc[v] = fma(t, S, acc[v]);
     }
 }
 
 // One stage: the eight 16-row blocks of the staged half, all in one code path
 // per half (the accumulators are indexed statically).
-template <int H>
-__device__ __forceinline__ void stage_blocks(const char *__restrict__ slot, int lane, const i32x4 (&kd)[kOzDigits],
+template <int H, bool PF>
+__device__ __forceinline__ void stage_blocks(const char *__restrict__ slot, int lane, const i32x4 (&kd)[kOzKDigits],
                                              int eK, f64x4 (&acc)[kOzRB]) {
     const int *eA = reinterpret_cast<const int *>(slot + kOzA);
     const i32x4 *pa = reinterpret_cast<const i32x4 *>(slot) + lane;
+    // PF: the next block's A digits are read while this block's products run
+    i32x4 ad[kOzDigits];
+#pragma unroll
+    for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[s * (kOzPlane / 16)];
 #pragma unroll
     for (int rb = 0; rb < kOzHalfRB; ++rb) {
-        i32x4 ad[kOzDigits];
+        i32x4 an[kOzDigits];
+        if (!PF) {
 #pragma unroll
-        for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[s * (kOzPlane / 16) + rb * 64];
-        const double S = ldexp(1.0, __builtin_amdgcn_readfirstlane(eA[rb]) + eK - 6 * 7);
+            for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[s * (kOzPlane / 16) + rb * 64];
+        } else if (rb + 1 < kOzHalfRB) {
+#pragma unroll
+            for (int s = 0; s < kOzDigits; ++s) an[s] = pa[s * (kOzPlane / 16) + (rb + 1) * 64];
+        }
+        const double S = ldexp(1.0, __builtin_amdgcn_readfirstlane(eA[rb]) + eK - kOzBits);
         block_products(ad, kd, S, acc[H * kOzHalfRB + rb]);
+        if (PF && rb + 1 < kOzHalfRB) {
+#pragma unroll
+            for (int s = 0; s < kOzDigits; ++s) ad[s] = an[s];
+        }
     }
 }
 
+template <bool PF>
 __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     const char *__restrict__ aoz, const int *__restrict__ eoz, const char *__restrict__ koz,
     const int4 *__restrict__ desc, const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P,
@@ -198,6 +241,8 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     const int g = lane >> 4;
     const int4 *dwin = reinterpret_cast<const int4 *>(smem + 2 * kOzSlot);
     const unsigned short *lwin = reinterpret_cast<const unsigned short *>(smem + 2 * kOzSlot + 2048);
+    double *T2 = reinterpret_cast<double *>(smem + 2 * kOzSlot + 4096);
+    if (tid < 64) T2[tid] = exp2((double)tid * 0.015625);   // (visible after the prologue's barriers)
 
     // LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction, lane
     // linear), issued from inline asm as in predict_f64_kernel: every wave
@@ -232,9 +277,10 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
         if (wave == 0 && lane < 2)                                                                       \
             SBO_OZ_DMA16(gE + (int64_t)(T_) * 64 + (h_) * 32,                                            \
                          __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA)));     \
-        if (wave == 1 && (h_) == 0)                                                                      \
-            SBO_OZ_DMA16(gC + (int64_t)(kt_) * kOzC,                                                     \
-                         __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA + kOzE))); \
+        if ((h_) == 0 && (wave == 1 || (wave == 3 && lane < (kOzC - 1024) / 16)))                       \
+            SBO_OZ_DMA16(gC + (int64_t)(kt_) * kOzC + (wave == 3 ? 1024 : 0),                            \
+                         __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA + kOzE +   \
+                                                                              (wave == 3 ? 1024 : 0))));     \
     } while (0)
 #define SBO_OZ_DESC_WINDOW(w_)                                                                           \
     do {                                                                                                 \
@@ -280,7 +326,7 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     f64x4 acc[kOzRB];
 #pragma unroll
     for (int rb = 0; rb < kOzRB; ++rb) acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
-    i32x4 kd[kOzDigits];
+    i32x4 kd[kOzKDigits];
     int eK = 0;
     double mu = 0.0;
     int k = k0, j = 0, h = 0, cur = 0;
@@ -319,10 +365,13 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
         const char *slot = smem + cur * kOzSlot;
         const int I = dc.x;
         if (h == 0) {
-            kstar_digits(slot + kOzA + kOzE, g, xq, yq, cexp, I == nI - 1 ? 1.0 : 0.0, kd, eK, mu);
-            stage_blocks<0>(slot, lane, kd, eK, acc);
+            if (I == nI - 1)
+                kstar_digits<true>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
+            else
+                kstar_digits<false>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
+            stage_blocks<0, PF>(slot, lane, kd, eK, acc);
         } else {
-            stage_blocks<1>(slot, lane, kd, eK, acc);
+            stage_blocks<1, PF>(slot, lane, kd, eK, acc);
         }
         if (h == 1 && j == cnt - 1) {
             // item done: column sums of V^2 over its 256 rows; lane l holds
@@ -431,8 +480,8 @@ __global__ __launch_bounds__(256) void pack_oz_kernel(const double *__restrict__
     }
 }
 
-// Per k-tile: x[64], y[64] (f32, as stored), sf2 alpha[64] (f64, alpha from
-// the f64 solve); padding rows: the first point's coordinates, alpha 0.
+// Per k-tile: x[64], y[64] (f64 of the stored f32), sf2 alpha[64] (f64, alpha
+// from the f64 solve); padding rows: the first point's coordinates, alpha 0.
 __global__ void pack_koz_kernel(const float *__restrict__ x, const float *__restrict__ y,
                                 const double *__restrict__ alpha, int64_t n, int64_t npad, double sf2,
                                 char *__restrict__ koz) {
@@ -441,9 +490,9 @@ __global__ void pack_koz_kernel(const float *__restrict__ x, const float *__rest
     char *c = koz + (k / kBK) * kOzC;
     const int o = (int)(k % kBK);
     const bool in = k < n;
-    reinterpret_cast<float *>(c)[o] = in ? x[k] : x[0];
-    reinterpret_cast<float *>(c + kBK * 4)[o] = in ? y[k] : y[0];
-    reinterpret_cast<double *>(c + kBK * 8)[o] = in ? sf2 * alpha[k] : 0.0;
+    reinterpret_cast<double *>(c)[o] = (double)(in ? x[k] : x[0]);
+    reinterpret_cast<double *>(c + kBK * 8)[o] = (double)(in ? y[k] : y[0]);
+    reinterpret_cast<double *>(c + kBK * 16)[o] = in ? sf2 * alpha[k] : 0.0;
 }
 
 }  // namespace
@@ -468,11 +517,15 @@ hipError_t launch_pack_oz(hipStream_t s, const double *Linv, int64_t ld, int64_t
 hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, const char *koz, const int4 *desc,
                              const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
                              const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
-                             double *mean) {
+                             double *mean, int variant) {
     if (nI <= 0 || m <= 0) return hipSuccess;
     const double cexp = -1.0 / (2.0 * ell * ell * 0.69314718055994530942);
-    hipLaunchKernelGGL(predict_oz_kernel, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc, tl, seg, P,
-                       n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean);
+    if (variant == 2)   // A/B: the next block's A digits prefetched (more registers, spills)
+        hipLaunchKernelGGL(predict_oz_kernel<true>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc, tl,
+                           seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean);
+    else
+        hipLaunchKernelGGL(predict_oz_kernel<false>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc,
+                           tl, seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean);
     return hipGetLastError();
 }
 

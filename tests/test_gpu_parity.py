@@ -1367,13 +1367,13 @@ def test_precision_auto_probe(mapper):
     gm.fit(wl.x, wl.y, wl.obs)
     precise, perr, vmin, vmax = gm.precision()
     print(f"C2-like: precise={precise} probe err {perr:.2e} var {vmin:.2e}..{vmax:.2e}")
-    assert not precise and 0.0 <= perr < 7e-6
+    assert not precise and 0.0 <= perr < 5e-6
     wb = synthetic_box(6000, 60, 150, seed=9)
     gb = TerrainMapper(0, wb.hyper, ctx=mapper.ctx)
     gb.fit(wb.x, wb.y, wb.obs)
     precise, perr, vmin, vmax = gb.precision()
     print(f"lpsc box N=6000: precise={precise} probe err {perr:.2e} var {vmin:.2e}..{vmax:.2e}")
-    assert precise and perr > 7e-6 and vmax < 0.1
+    assert precise and perr > 5e-6 and vmax < 0.1
     mu_p, sd_p = gb.predict(wb.qx, wb.qy)
     gb.set_option(N.SBO_OPT_PRECISION, 0)
     assert not gb.precision()[0]

@@ -8,4 +8,6 @@ step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > $O/$name.log 2
 step small 300 python -u -m pytest tests/test_gpu_parity.py -k "int8_mfma_k_layout" -x -v -s --timeout 200 --timeout-method thread
 step precise 600 python -u -m pytest tests/test_gpu_parity.py -k "precise or precision" -x -v -s --timeout 300 --timeout-method thread
 step ab 600 python -u tools/r4_oz_ab.py 16384 1024
+step probegrid 600 python -u tools/r4_probe_vs_grid.py
+step fitc2 300 rocprofv3 --kernel-trace --stats -d $O/fitc2 -o run --output-format csv -- python3 tools/fit_timing.py --n 2048 --reps 5
 echo done
