@@ -522,7 +522,7 @@ def run_sweep(a, dev, world, rank):
                                  "probe_var_min": prec[2], "probe_var_max": prec[3],
                                  "rule": "SBO_OPT_PRECISION -1: the precise sweep when the probe error > 5e-6"}},
         "roofline": dict(predict_roofline(a.variant, exec_flops_launch, pred_ms, mfma_flops_launch, levels_launch,
-                                          prec[0]),
+                                          prec[0], gm.probe_info()["precise_kernel"]),
                          traffic=traffic,
                          traffic_source=traffic_src, avg_launch_ms=pred_ms, max_rank_launch_ms=pred_ms_max,
                          dense_flops_per_launch=dense_flops_launch,
@@ -565,10 +565,11 @@ def _timed_ticks(prof, step, steps):
     return wall, pr["predict_ms"] / k, pr["predict_flops"] / k, pr["mfma_flops"] / k, [x / k for x in pr["tiles_by_level"]]
 
 
-def _regime_line(a, name, how, m, n, wall, ms, flops, mflops, levels, extra=None, precise=False):
+def _regime_line(a, name, how, m, n, wall, ms, flops, mflops, levels, extra=None, precise=False, precise_kernel=1):
     dense = float(n) * float(n) * m
     r = {"what": how, "value": m / wall, "unit": "grid-points/s", "ms_per_step": wall * 1e3,
-         "roofline": dict(predict_roofline(a.variant, flops, ms, mflops, levels, precise), avg_launch_ms=ms,
+         "roofline": dict(predict_roofline(a.variant, flops, ms, mflops, levels, precise, precise_kernel),
+                          avg_launch_ms=ms,
                           dense_flops_per_launch=dense, executed_fraction_of_dense=flops / dense,
                           dense_equivalent_tflops=dense / (ms * 1e-3) / 1e12)}
     if extra:
@@ -657,8 +658,26 @@ def run_regime_stress(a, gm, prof, dev, n, gw, gh):
         gm.tick(qx, qy, wl.beta, wl.f_min, score=N.SCORE_WIDTH, outputs=outs, key_out=key, async_=True)
 
     precise, perr, vmin, vmax = gm.precision()
+    pinfo = gm.probe_info()
+    pk = pinfo["precise_kernel"]
     res = _timed_ticks(prof, step, a.regime_steps)
     sd_default = outs["sd"].clone()
+    # the other precise kernel on the same fit (f64 MFMA when the default is
+    # the int8 sliced one): time and whole-grid variance difference
+    other = None
+    if precise:
+        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 0 if pk >= 1 else 1)
+        try:
+            ores = _timed_ticks(prof, step, 1)
+        finally:
+            gm.set_option(N.SBO_OPT_PRECISE_KERNEL, pk)
+        v_o = outs["sd"].double() ** 2
+        v_d = sd_default.double() ** 2
+        other = _regime_line(a, "lpsc_stress_box other precise kernel",
+                             f"SBO_OPT_PRECISE_KERNEL = {0 if pk >= 1 else 1} on the same fit", m, n, *ores,
+                             precise=True, precise_kernel=0 if pk >= 1 else 1)
+        other["variance_difference_vs_default"] = float((v_o - v_d).abs().max() / v_d.abs().max())
+        other["default_speedup_over_this"] = other["ms_per_step"] / (res[0] * 1e3)
     # the fast split sweep on the same fit, and its variance error against the
     # precise sweep over the whole grid (device against device; the tests
     # measure both against the fp64 oracle: tests/test_gpu_headline.py)
@@ -677,9 +696,13 @@ def run_regime_stress(a, gm, prof, dev, n, gw, gh):
                         extra={"fit_ms": fit_ms, "kstar_cutoff_log2": gm.skip_info()[0],
                                "end_to_end": end_to_end(m, fit_ms, res[0] * 1e3),
                                "precise_sweep": precise,
+                               "precise_kernel": pk,
                                "probe": {"fast_sweep_variance_error": perr, "var_min": vmin, "var_max": vmax,
-                                         "how": "32 x 32 grid over the training box, fast vs precise sweep"},
-                               "fast_sweep": fast}, precise=precise)
+                                         "err_grid": pinfo["err_grid"], "err_train": pinfo["err_train"],
+                                         "how": "32 x 32 grid over the training box + 512 training locations, "
+                                                "fast vs precise sweep"},
+                               "other_precise_kernel": other,
+                               "fast_sweep": fast}, precise=precise, precise_kernel=pk)
 
 
 def dtype_of(variant):
@@ -687,9 +710,11 @@ def dtype_of(variant):
 
 
 PEAK_F64_MFMA_TFLOPS = 78.6    # MI355X spec: dense FP64 matrix (v_mfma_f64_16x16x4_f64)
+PEAK_I8_MFMA_TOPS = 5000.0     # MI355X_MICROARCH.md: i8 16x16x64 = 2x the bf16 rate per clock (dense)
+OZ_PRODUCTS = 14               # predict_oz.hip: int8 digit-slice products per f64 product
 
 
-def predict_roofline(variant, flops_f32, ms, mfma_flops, levels, precise=False):
+def predict_roofline(variant, flops_f32, ms, mfma_flops, levels, precise=False, precise_kernel=1):
     """Roofline of the predictive kernel.  flops_f32 = the algorithmic work of
     one launch, 2*BM*BN*BK per multiplied k-tile (device counter); mfma_flops
     = the matrix-core work it issued (device counter: 2*BM*BN*BK per bf16
@@ -698,6 +723,14 @@ def predict_roofline(variant, flops_f32, ms, mfma_flops, levels, precise=False):
     the dense bf16 (split sweeps) or f32 peak."""
     f32_tf = flops_f32 / (ms * 1e-3) / 1e12
     ach = mfma_flops / (ms * 1e-3) / 1e12
+    if precise and precise_kernel >= 1:
+        tops = OZ_PRODUCTS * flops_f32 / (ms * 1e-3) / 1e12
+        return {"kernel": "predict_oz_kernel (V = sf2 L^-1 K*^T from five A x four K* int8 digit slices: 14 "
+                          "v_mfma_i32_16x16x64_i8 products per f64 product, exact int32 sums, f64 combination)",
+                "bound": "mfma", "achieved": tops, "peak": PEAK_I8_MFMA_TOPS, "unit": "TOPS (int8)",
+                "frac": tops / PEAK_I8_MFMA_TOPS, "int8_ops_per_launch": OZ_PRODUCTS * flops_f32,
+                "algorithmic_flops_per_launch": flops_f32, "f64_equivalent_tflops": f32_tf,
+                "f64_equivalent_over_f64_peak": f32_tf / PEAK_F64_MFMA_TFLOPS}
     if precise:
         return {"kernel": "predict_f64_kernel (V = sf2 L^-1 K*^T in f64: v_mfma_f64_16x16x4_f64, f64 K* and sums)",
                 "bound": "mfma", "achieved": f32_tf, "peak": PEAK_F64_MFMA_TFLOPS, "unit": "TFLOP/s",

@@ -442,7 +442,7 @@ SBO_API sbo_status sbo_get_precision(const sbo_ctx *ctx, int *precise, double *p
  * part's own max |d var| / its own largest variance.  err* = -1 when no
  * probe ran.  SBO_E_STATE before a fit. */
 typedef struct sbo_probe {
-    int32_t precise, m_grid, m_train, pad_;
+    int32_t precise, m_grid, m_train, precise_kernel;   /* precise_kernel: SBO_OPT_PRECISE_KERNEL in effect */
     int64_t n_at_probe;
     double err, err_grid, err_train;
     double var_min, var_max, var_max_grid, var_max_train;

@@ -80,7 +80,7 @@ class sbo_key(ctypes.Structure):
 
 class sbo_probe(ctypes.Structure):
     _fields_ = [("precise", ctypes.c_int32), ("m_grid", ctypes.c_int32), ("m_train", ctypes.c_int32),
-                ("pad_", ctypes.c_int32), ("n_at_probe", ctypes.c_int64), ("err", ctypes.c_double),
+                ("precise_kernel", ctypes.c_int32), ("n_at_probe", ctypes.c_int64), ("err", ctypes.c_double),
                 ("err_grid", ctypes.c_double), ("err_train", ctypes.c_double), ("var_min", ctypes.c_double),
                 ("var_max", ctypes.c_double), ("var_max_grid", ctypes.c_double), ("var_max_train", ctypes.c_double)]
 

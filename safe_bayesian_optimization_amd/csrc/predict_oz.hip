@@ -194,35 +194,30 @@ __device__ __forceinline__ void block_products(const i32x4 (&ad)[kOzDigits], con
 
 // One stage: the eight 16-row blocks of the staged half, all in one code path
 // per half (the accumulators are indexed statically).
-template <int H, bool PF>
+template <int H>
 __device__ __forceinline__ void stage_blocks(const char *__restrict__ slot, int lane, const i32x4 (&kd)[kOzKDigits],
                                              int eK, f64x4 (&acc)[kOzRB]) {
     const int *eA = reinterpret_cast<const int *>(slot + kOzA);
     const i32x4 *pa = reinterpret_cast<const i32x4 *>(slot) + lane;
-    // PF: the next block's A digits are read while this block's products run
-    i32x4 ad[kOzDigits];
-#pragma unroll
-    for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[s * (kOzPlane / 16)];
+    // (prefetching the next block's digits here measured slower: the extra
+    // 20 registers spill; SBO_OPT_PRECISE_KERNEL A/B, round 4)
 #pragma unroll
     for (int rb = 0; rb < kOzHalfRB; ++rb) {
-        i32x4 an[kOzDigits];
-        if (!PF) {
+        i32x4 ad[kOzDigits];
 #pragma unroll
-            for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[s * (kOzPlane / 16) + rb * 64];
-        } else if (rb + 1 < kOzHalfRB) {
-#pragma unroll
-            for (int s = 0; s < kOzDigits; ++s) an[s] = pa[s * (kOzPlane / 16) + (rb + 1) * 64];
-        }
+        for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[s * (kOzPlane / 16) + rb * 64];
         const double S = ldexp(1.0, __builtin_amdgcn_readfirstlane(eA[rb]) + eK - kOzBits);
         block_products(ad, kd, S, acc[H * kOzHalfRB + rb]);
-        if (PF && rb + 1 < kOzHalfRB) {
-#pragma unroll
-            for (int s = 0; s < kOzDigits; ++s) ad[s] = an[s];
-        }
     }
 }
 
-template <bool PF>
+// STAG (default): the waves of a SIMD (w and w + 4) build K*'s digits at
+// different times, so that one wave's K* work (VALU only) runs beside the
+// other's products (matrix pipe): waves 0-3 build tile t's digits at the top
+// of its first stage, waves 4-7 at the top of the tile before's second stage
+// (a second digit set, from next-tile coordinates staged with that stage).
+// !STAG: every wave at the top of the tile's first stage (A/B).
+template <bool STAG>
 __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     const char *__restrict__ aoz, const int *__restrict__ eoz, const char *__restrict__ koz,
     const int4 *__restrict__ desc, const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P,
@@ -267,7 +262,8 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
                      : "v"(gsrc), "s"(ldst)                                                              \
                      : "memory");                                                                        \
     } while (0)
-    // stage (packed tile T_ of k-tile kt_, row half h_) into slot buf
+    // stage (packed tile T_, row half h_) into slot buf, with the coordinates
+    // of k-tile kt_ (none: kt_ < 0)
 #define SBO_OZ_STAGE(T_, kt_, h_, buf)                                                                   \
     do {                                                                                                 \
         const char *s_ = gA + (int64_t)(T_) * kOzTileBytes + (h_) * kOzA;                                \
@@ -277,7 +273,7 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
         if (wave == 0 && lane < 2)                                                                       \
             SBO_OZ_DMA16(gE + (int64_t)(T_) * 64 + (h_) * 32,                                            \
                          __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA)));     \
-        if ((h_) == 0 && (wave == 1 || (wave == 3 && lane < (kOzC - 1024) / 16)))                       \
+        if ((kt_) >= 0 && (wave == 1 || (wave == 3 && lane < (kOzC - 1024) / 16)))                      \
             SBO_OZ_DMA16(gC + (int64_t)(kt_) * kOzC + (wave == 3 ? 1024 : 0),                            \
                          __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA + kOzE +   \
                                                                               (wave == 3 ? 1024 : 0))));     \
@@ -318,6 +314,7 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     __syncthreads();
     int t = list_at(e, dc.x);
     SBO_OZ_STAGE(tile_start(dc.x) + t, t, 0, 0);
+    const bool bw = STAG && wave >= 4;    // builds the next tile's digits a stage early
     int64_t q = (int64_t)dc.y * kBN + wave * 16 + r;
     double xq = (double)qx[q < m ? q : m - 1], yq = (double)qy[q < m ? q : m - 1];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -326,9 +323,10 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     f64x4 acc[kOzRB];
 #pragma unroll
     for (int rb = 0; rb < kOzRB; ++rb) acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
-    i32x4 kd[kOzKDigits];
-    int eK = 0;
-    double mu = 0.0;
+    i32x4 kd[kOzKDigits], kd2[kOzKDigits];
+    int eK = 0, eK2 = 0;
+    double mu = 0.0, mu2 = 0.0;
+    bool have = false;                    // (bw) kd already holds this tile's digits
     int k = k0, j = 0, h = 0, cur = 0;
     for (;;) {
         const int cnt = dc.w & 0xffff;
@@ -347,6 +345,11 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
         int4 dn = dc;
         int tn = t;
         double xqn = xq, yqn = yq;
+        int kt2 = -1;                     // (h == 0) the k-tile after this one, staged with the second half
+        if (STAG && more && h == 0) {
+            const int kn2 = j + 1 < cnt ? k : k + 1;
+            if (kn2 < k1) kt2 = list_at(e + 1, kn2 != k ? desc_at(kn2).x : dc.x);
+        }
         if (more) {
             if (kn != k) {
                 dn = desc_at(kn);
@@ -360,18 +363,30 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
                 if (en % kOzListWin == 0) SBO_OZ_LIST_WINDOW(en / kOzListWin + 1);
                 tn = list_at(en, dn.x);
             }
-            SBO_OZ_STAGE(tile_start(dn.x) + tn, tn, hn, cur ^ 1);
+            SBO_OZ_STAGE(tile_start(dn.x) + tn, hn == 0 ? tn : kt2, hn, cur ^ 1);
         }
         const char *slot = smem + cur * kOzSlot;
         const int I = dc.x;
         if (h == 0) {
-            if (I == nI - 1)
-                kstar_digits<true>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
-            else
-                kstar_digits<false>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
-            stage_blocks<0, PF>(slot, lane, kd, eK, acc);
+            if (!have) {
+                if (I == nI - 1)
+                    kstar_digits<true>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
+                else
+                    kstar_digits<false>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
+            }
+            have = false;
+            stage_blocks<0>(slot, lane, kd, eK, acc);
         } else {
-            stage_blocks<1, PF>(slot, lane, kd, eK, acc);
+            // (bw) the next tile's digits first (its coordinates came with this
+            // stage; its item's queries are xqn, yqn; its mean terms go to
+            // mu2 until this item's end)
+            if (bw && more) {
+                if (dn.x == nI - 1)
+                    kstar_digits<true>(slot + kOzA + kOzE, T2, g, xqn, yqn, cexp, kd2, eK2, mu2);
+                else
+                    kstar_digits<false>(slot + kOzA + kOzE, T2, g, xqn, yqn, cexp, kd2, eK2, mu2);
+            }
+            stage_blocks<1>(slot, lane, kd, eK, acc);
         }
         if (h == 1 && j == cnt - 1) {
             // item done: column sums of V^2 over its 256 rows; lane l holds
@@ -393,6 +408,14 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
                 if (writer) mean[q] = m0 + mu;
                 mu = 0.0;
             }
+        }
+        if (bw && h == 1 && more) {
+            mu += mu2;
+            mu2 = 0.0;
+#pragma unroll
+            for (int u = 0; u < kOzKDigits; ++u) kd[u] = kd2[u];
+            eK = eK2;
+            have = true;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -520,11 +543,11 @@ hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, con
                              double *mean, int variant) {
     if (nI <= 0 || m <= 0) return hipSuccess;
     const double cexp = -1.0 / (2.0 * ell * ell * 0.69314718055994530942);
-    if (variant == 2)   // A/B: the next block's A digits prefetched (more registers, spills)
-        hipLaunchKernelGGL(predict_oz_kernel<true>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc, tl,
+    if (variant == 2)   // A/B: every wave builds K*'s digits at the top of the tile (no staggering)
+        hipLaunchKernelGGL(predict_oz_kernel<false>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc, tl,
                            seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean);
     else
-        hipLaunchKernelGGL(predict_oz_kernel<false>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc,
+        hipLaunchKernelGGL(predict_oz_kernel<true>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc,
                            tl, seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean);
     return hipGetLastError();
 }

@@ -2059,6 +2059,7 @@ SBO_API sbo_status sbo_get_probe(const sbo_ctx *ctx, sbo_probe *out) {
     if (!ctx->fitted) return SBO_E_STATE;
     *out = sbo_probe{};
     out->precise = ctx->precise ? 1 : 0;
+    out->precise_kernel = ctx->precise_kernel;
     out->n_at_probe = ctx->probe_n;
     if (ctx->probe_n == 0) {
         out->err = out->err_grid = out->err_train = -1.0;

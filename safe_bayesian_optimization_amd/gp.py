@@ -274,7 +274,7 @@ class TerrainMapper:
         from ._native import sbo_probe
         p = sbo_probe()
         self.ctx.check(self._lib.sbo_get_probe(self.ctx.handle, ctypes.byref(p)))
-        return {f: getattr(p, f) for f, _ in sbo_probe._fields_ if f != "pad_"}
+        return {f: getattr(p, f) for f, _ in sbo_probe._fields_}
 
     def set_option(self, option: int, value: int) -> None:
         self.ctx.check(self._lib.sbo_set_option(self.ctx.handle, int(option), int(value)))
