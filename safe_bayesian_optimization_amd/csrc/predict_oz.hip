@@ -211,13 +211,11 @@ __device__ __forceinline__ void stage_blocks(const char *__restrict__ slot, int 
     }
 }
 
-// STAG (default): the waves of a SIMD (w and w + 4) build K*'s digits at
-// different times, so that one wave's K* work (VALU only) runs beside the
-// other's products (matrix pipe): waves 0-3 build tile t's digits at the top
-// of its first stage, waves 4-7 at the top of the tile before's second stage
-// (a second digit set, from next-tile coordinates staged with that stage).
-// !STAG: every wave at the top of the tile's first stage (A/B).
-template <bool STAG>
+// Every wave builds its K* digits at the top of a tile's first stage.  (A/B,
+// round 4: staggering the two waves of a SIMD -- waves 4-7 building the next
+// tile's digits a stage early, so that one wave's VALU work overlaps the
+// other's products -- needs a second digit set; at 87 spilled registers it
+// ran at 4517 ms against 2296 on the lpsc box and was dropped.)
 __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     const char *__restrict__ aoz, const int *__restrict__ eoz, const char *__restrict__ koz,
     const int4 *__restrict__ desc, const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P,
@@ -314,7 +312,6 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     __syncthreads();
     int t = list_at(e, dc.x);
     SBO_OZ_STAGE(tile_start(dc.x) + t, t, 0, 0);
-    const bool bw = STAG && wave >= 4;    // builds the next tile's digits a stage early
     int64_t q = (int64_t)dc.y * kBN + wave * 16 + r;
     double xq = (double)qx[q < m ? q : m - 1], yq = (double)qy[q < m ? q : m - 1];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -323,10 +320,9 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     f64x4 acc[kOzRB];
 #pragma unroll
     for (int rb = 0; rb < kOzRB; ++rb) acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
-    i32x4 kd[kOzKDigits], kd2[kOzKDigits];
-    int eK = 0, eK2 = 0;
-    double mu = 0.0, mu2 = 0.0;
-    bool have = false;                    // (bw) kd already holds this tile's digits
+    i32x4 kd[kOzKDigits];
+    int eK = 0;
+    double mu = 0.0;
     int k = k0, j = 0, h = 0, cur = 0;
     for (;;) {
         const int cnt = dc.w & 0xffff;
@@ -345,11 +341,6 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
         int4 dn = dc;
         int tn = t;
         double xqn = xq, yqn = yq;
-        int kt2 = -1;                     // (h == 0) the k-tile after this one, staged with the second half
-        if (STAG && more && h == 0) {
-            const int kn2 = j + 1 < cnt ? k : k + 1;
-            if (kn2 < k1) kt2 = list_at(e + 1, kn2 != k ? desc_at(kn2).x : dc.x);
-        }
         if (more) {
             if (kn != k) {
                 dn = desc_at(kn);
@@ -363,29 +354,17 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
                 if (en % kOzListWin == 0) SBO_OZ_LIST_WINDOW(en / kOzListWin + 1);
                 tn = list_at(en, dn.x);
             }
-            SBO_OZ_STAGE(tile_start(dn.x) + tn, hn == 0 ? tn : kt2, hn, cur ^ 1);
+            SBO_OZ_STAGE(tile_start(dn.x) + tn, hn == 0 ? tn : -1, hn, cur ^ 1);
         }
         const char *slot = smem + cur * kOzSlot;
         const int I = dc.x;
         if (h == 0) {
-            if (!have) {
-                if (I == nI - 1)
-                    kstar_digits<true>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
-                else
-                    kstar_digits<false>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
-            }
-            have = false;
+            if (I == nI - 1)
+                kstar_digits<true>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
+            else
+                kstar_digits<false>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
             stage_blocks<0>(slot, lane, kd, eK, acc);
         } else {
-            // (bw) the next tile's digits first (its coordinates came with this
-            // stage; its item's queries are xqn, yqn; its mean terms go to
-            // mu2 until this item's end)
-            if (bw && more) {
-                if (dn.x == nI - 1)
-                    kstar_digits<true>(slot + kOzA + kOzE, T2, g, xqn, yqn, cexp, kd2, eK2, mu2);
-                else
-                    kstar_digits<false>(slot + kOzA + kOzE, T2, g, xqn, yqn, cexp, kd2, eK2, mu2);
-            }
             stage_blocks<1>(slot, lane, kd, eK, acc);
         }
         if (h == 1 && j == cnt - 1) {
@@ -408,14 +387,6 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
                 if (writer) mean[q] = m0 + mu;
                 mu = 0.0;
             }
-        }
-        if (bw && h == 1 && more) {
-            mu += mu2;
-            mu2 = 0.0;
-#pragma unroll
-            for (int u = 0; u < kOzKDigits; ++u) kd[u] = kd2[u];
-            eK = eK2;
-            have = true;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -540,15 +511,11 @@ hipError_t launch_pack_oz(hipStream_t s, const double *Linv, int64_t ld, int64_t
 hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, const char *koz, const int4 *desc,
                              const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
                              const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
-                             double *mean, int variant) {
+                             double *mean) {
     if (nI <= 0 || m <= 0) return hipSuccess;
     const double cexp = -1.0 / (2.0 * ell * ell * 0.69314718055994530942);
-    if (variant == 2)   // A/B: every wave builds K*'s digits at the top of the tile (no staggering)
-        hipLaunchKernelGGL(predict_oz_kernel<false>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc, tl,
-                           seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean);
-    else
-        hipLaunchKernelGGL(predict_oz_kernel<true>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc,
-                           tl, seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean);
+    hipLaunchKernelGGL(predict_oz_kernel, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc, tl, seg, P,
+                       n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean);
     return hipGetLastError();
 }
 

@@ -1290,7 +1290,7 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
             SBO_HIP(sbo::launch_predict_oz(ctx->stream, ctx->aoz.as<char>(), ctx->eoz.as<int>(), ctx->koz.as<char>(),
                                            desc, tl, seg, P, (int)(nIc * ((ms + sbo::kBN - 1) / sbo::kBN)), (int)nIc,
                                            qx, qy, ms, ldp, ctx->hyper.length_scale, ctx->hyper.prior_mean,
-                                           ctx->part.as<double>(), ctx->mean.as<double>(), ctx->precise_kernel));
+                                           ctx->part.as<double>(), ctx->mean.as<double>()));
         else
             SBO_HIP(sbo::launch_predict_f64(ctx->stream, ctx->a64.as<double>(), ctx->kc64.as<double>(), desc, tl, seg,
                                             P, (int)(nIc * ((ms + sbo::kBN - 1) / sbo::kBN)), (int)nIc, qx, qy, ms,
@@ -1963,7 +1963,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             return SBO_OK;
         case SBO_OPT_KERNEL_VARIANT:
             SBO_CHECK(sbo::variant_allowed((int)value), SBO_E_INVAL,
-                      "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 2, 3, 9, 10, 13, 22)");
+                      "SBO_OPT_KERNEL_VARIANT: not a sweep of this build (product: 0, 1, 3, 22)");
             ctx->kernel_variant = (int)value;
             return SBO_OK;
         case SBO_OPT_INV_BASE:
@@ -2002,8 +2002,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->chol_reserve = (int)value;
             return SBO_OK;
         case SBO_OPT_PRECISE_KERNEL:
-            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL,
-                      "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA), 1 (int8) or 2 (int8, A/B variant)");
+            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA) or 1 (int8)");
             if ((ctx->precise_kernel == 0) != (value == 0)) ctx->a64_I0 = 0;   // the other operand: derive it all
             ctx->precise_kernel = (int)value;
             return SBO_OK;

@@ -315,7 +315,7 @@ inline bool variant_allowed(int v) {
 #ifdef SBO_DIAG
     return v >= 0 && v <= 61;
 #else
-    return v == 0 || v == 1 || v == 2 || v == 3 || v == 9 || v == 10 || v == 13 || v == 22;
+    return v == 0 || v == 1 || v == 3 || v == 22;
 #endif
 }
 inline int x3_layout(int variant) { return (variant == 13 || variant == 14) ? 1 : 0; }
@@ -395,7 +395,7 @@ hipError_t launch_pack_oz(hipStream_t s, const double *Linv, int64_t ld, int64_t
 hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, const char *koz, const int4 *desc,
                              const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
                              const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
-                             double *mean, int variant = 1);
+                             double *mean);
 // Morton ordering of the queries (query_order.hip): workspace of
 // query_order_bytes(m); returns the permutation and the gathered coordinates
 // (all inside the workspace).
