@@ -1104,26 +1104,6 @@ __global__ void tile_box_kernel(const float *__restrict__ x, const float *__rest
 // (f32 coordinate differences and exp2), amplified by A, dominates what is
 // left (tools/variant_accuracy.py: 5e-6 at N = 16384 for either outer type).
 constexpr int kStageFloats = kTileFloats + 3 * kBK;
-#ifdef SBO_STAMPS
-// diagnostic build only: per-workgroup s_memtime stamps (entry, list built,
-// first stage in, sweep done), HW_ID/XCC_ID, row block and tile count
-constexpr int64_t kStampSlots = 1 << 20;
-__device__ unsigned long long sbo_stamps[kStampSlots * 6];
-// per (workgroup < 64, wave): cycles summed over the sweep steps in four
-// segments -- barrier exit -> stage issued, -> tile MFMAs + outer sum done,
-// -> epilogue + vmcnt(0) done, -> next barrier exit -- and the step count
-__device__ unsigned long long sbo_wstamps[64 * 8 * 5];
-}  // namespace
-extern "C" __attribute__((visibility("default"))) int sbo_debug_stamps(void *dst, int64_t slots) {
-    if (slots > kStampSlots) slots = kStampSlots;
-    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(sbo_stamps), (size_t)slots * 6 * 8, 0, hipMemcpyDeviceToHost);
-}
-extern "C" __attribute__((visibility("default"))) int sbo_debug_wave_stamps(void *dst) {
-    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(sbo_wstamps), sizeof(unsigned long long) * 64 * 8 * 5, 0,
-                                    hipMemcpyDeviceToHost);
-}
-namespace {
-#endif
 constexpr int kPredictWaves = kBN / 16;
 constexpr int kPredictThreads = 64 * kPredictWaves;
 constexpr int kDescWindow = 64;          // item descriptors (int4) per 1 KiB LDS window
@@ -1910,9 +1890,6 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     const int wave = tid >> 6;
     const int g = lane >> 4;   // k within the step
     const int r = lane & 15;   // row within a 16-row block / query within the wave
-#ifdef SBO_STAMPS
-    const unsigned long long st0 = __builtin_amdgcn_s_memtime();
-#endif
 
     // LDS: two stages, then two descriptor windows and two tile-list windows
     // (1 KiB each), refilled one window ahead by LDS-DMA
@@ -2005,9 +1982,6 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     float xq = qx[q < m ? q : m - 1], yq = qy[q < m ? q : m - 1];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#ifdef SBO_STAMPS
-    const unsigned long long st1 = __builtin_amdgcn_s_memtime();
-#endif
 
     OT outer[kRowBlocks][4];
 #pragma unroll
@@ -2017,11 +1991,6 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
     double mu = 0.0;
     f32x4 acc[kRowBlocks];
     int k = k0, j = 0, cur = 0;
-#ifdef SBO_STAMPS
-#define SBO_T(v) do { __builtin_amdgcn_sched_barrier(0); asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) :: "memory"); __builtin_amdgcn_sched_barrier(0); } while (0)
-    unsigned long long wseg[4] = {0, 0, 0, 0}, ta, tb, tc, td;
-    SBO_T(ta);
-#endif
     for (;;) {
         const int cnt = dc.w & 0xffff;
         // the next step: (k, j+1), or the first tile of item k+1
@@ -2049,10 +2018,6 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
         const float4 *pa = reinterpret_cast<const float4 *>(smem + cur * kStageFloats) + g * 16 + r;
         const float *pc = smem + cur * kStageFloats + kTileFloats + g * (kBK / 4);
         const int I = dc.x;
-#ifdef SBO_STAMPS
-        SBO_T(tb);
-        wseg[0] += tb - ta;
-#endif
         if (I == nI - 1)
             tile_steps<true>(pa, pc, xq, yq, cexp, acc, mu);
         else
@@ -2061,10 +2026,6 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
         for (int rb = 0; rb < kRowBlocks; ++rb)
 #pragma unroll
             for (int c = 0; c < 4; ++c) outer[rb][c] += (OT)acc[rb][c];
-#ifdef SBO_STAMPS
-        SBO_T(tc);
-        wseg[1] += tc - tb;
-#endif
         if (j == cnt - 1) {
             // item done: column sums of V^2 over its rows; lanes l, l+16,
             // l+32, l+48 hold four row quarters of column l&15 of every block
@@ -2088,15 +2049,7 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef SBO_STAMPS
-        SBO_T(td);
-        wseg[2] += td - tc;
-#endif
         __syncthreads();
-#ifdef SBO_STAMPS
-        SBO_T(ta);
-        wseg[3] += ta - td;
-#endif
         if (!more) break;
         if (kn != k) {
             k = kn;
@@ -2109,26 +2062,6 @@ __global__ __launch_bounds__(kPredictThreads, 1) void predict_kernel(
         ++e;
         cur ^= 1;
     }
-#ifdef SBO_STAMPS
-    if (lane == 0 && bid < 64) {
-        unsigned long long *ws = sbo_wstamps + (bid * 8 + wave) * 5;
-        for (int i = 0; i < 4; ++i) ws[i] = wseg[i];
-        ws[4] = e + 1 - entry_off(desc[k0]);
-    }
-#undef SBO_T
-    if (tid == 0 && bid < kStampSlots) {
-        const unsigned long long st3 = __builtin_amdgcn_s_memtime();
-        unsigned hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(hw), "=s"(xcc));
-        unsigned long long *slot = sbo_stamps + bid * 6;
-        slot[0] = st0;
-        slot[1] = st1;
-        slot[2] = st1;
-        slot[3] = st3;
-        slot[4] = ((unsigned long long)xcc << 32) | hw;
-        slot[5] = ((unsigned long long)(unsigned)(k1 - k0) << 32) | (unsigned)(e + 1 - entry_off(desc[k0]));
-    }
-#endif
 #undef SBO_STAGE
 #undef SBO_DESC_WINDOW
 #undef SBO_LIST_WINDOW

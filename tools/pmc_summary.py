@@ -11,7 +11,13 @@ import json
 import sys
 
 
+TICKS = 2   # tools/collect_pmc.sh runs tools/run_predict.py --ticks 2
+
+
 def per_kernel(path, counter):
+    """Per kernel: the counter summed per dispatch, averaged over the last
+    TICKS dispatches (the ticks' sweeps; earlier ones are the fit's precision
+    probe, a 1536-point sweep with another traffic profile)."""
     vals = {}
     for f in glob.glob(path + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
@@ -23,17 +29,21 @@ def per_kernel(path, counter):
             if k:
                 vals.setdefault(k, {}).setdefault(r["Dispatch_Id"], 0.0)
                 vals[k][r["Dispatch_Id"]] += float(r["Counter_Value"])
-    return {k: sum(v.values()) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+    last = {k: [v[d] for d in sorted(v, key=int)[-TICKS:]] for k, v in vals.items()}
+    return {k: sum(v) / len(v) for k, v in last.items()}, {k: len(v) for k, v in last.items()}
 
 
 def main(out, cfg, dst):
     fetch, nf = per_kernel(out + "/fetch", "FETCH_SIZE")
     write, nw = per_kernel(out + "/write", "WRITE_SIZE")
     dur = {}
-    for f in glob.glob(out + "/trace/**/*kernel_stats.csv", recursive=True):
-        for r in csv.DictReader(open(f)):
-            if "predict_kernel" in r["Name"] or "predict_x3_kernel" in r["Name"]:
-                dur["predict_kernel"] = float(r["AverageNs"]) * 1e-6
+    for f in glob.glob(out + "/trace/**/*kernel_trace.csv", recursive=True):
+        rows = [r for r in csv.DictReader(open(f))
+                if "predict_kernel" in r["Kernel_Name"] or "predict_x3_kernel" in r["Kernel_Name"]]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        last = rows[-TICKS:]
+        if last:
+            dur["predict_kernel"] = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last) / len(last) * 1e-6
     res = {"config": cfg, "units": "bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)"}
     for k in fetch:
         fb = 2.0 * fetch[k] * 1024.0
