@@ -418,7 +418,7 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * has grown by this share since the last probe (every sbo_fit probes). */
 #define SBO_OPT_REPROBE 21
 /* SBO_OPT_PRECISE_KERNEL (1 default | 0): the precise sweep's arithmetic --
- * 1 A = sf2 L^-1 as five and K* as four base-128 int8 digit slices, the 14
+ * 1 A = sf2 L^-1 as five and K* as four balanced base-256 int8 digit slices, the 14
  * leading slice products on the int8 matrix cores (v_mfma_i32_16x16x64_i8,
  * exact int32 sums), combined in f64 per k-tile (an Ozaki-style sliced
  * product; predict_oz.hip); 0 every product and sum in f64 on the f64 matrix

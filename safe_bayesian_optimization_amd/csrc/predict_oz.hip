@@ -1,8 +1,9 @@
 // predict_oz.hip -- the precise predictive sweep on the int8 matrix cores
 // (round 4; SBO_OPT_PRECISE_KERNEL 1): V = A K*^T with
-// A = sf2 L^-1 and K* both cut into five base-128 int8 digit slices, the slice
-// products accumulated EXACTLY in int32 by v_mfma_i32_16x16x64_i8 and combined
-// in f64 once per k-tile (an Ozaki-style sliced product).
+// A = sf2 L^-1 cut into five and K* into four balanced base-256 int8 digit
+// slices, the slice products accumulated EXACTLY in int32 by
+// v_mfma_i32_16x16x64_i8 and combined in f64 once per k-tile (an Ozaki-style
+// sliced product).
 //
 // Why: on the mapping node's own box (config/lpsc.yaml:32-37) the fast split
 // sweep misses the 1e-5 contract by 40x because it accumulates terms far larger
@@ -12,21 +13,29 @@
 // MFMA spends on 16x16x32 (MI355X_MICROARCH.md, matrix cores: 2x bf16 per
 // clock) and sums its products exactly, so the rounding the contract cannot
 // afford is gone and what is left is the slicing:
-//   A: per (16-row block, k-tile) a power of two 2^eA > 1.01 max|A|; digits by
-//      successive rounding, A = 2^eA sum_s d_s 128^-(s+1) + O(2^eA 128^-5 / 2),
-//      |d_0| <= 127, |d_s| <= 64 (pack_oz_kernel, once per fit / append);
+//   A: per (16-row block, k-tile) a power of two 2^eA > 1.01 max|A|, the
+//      integer XA = rint(A 2^(39 - eA)) (|XA| < 2^39 / 1.01) in five balanced
+//      base-256 digits, XA = sum_s D_s 2^(32 - 8 s): the bytes of XA +
+//      0x80808080, less 128 but for the top one, so |D_s| <= 128 and |D_0| <=
+//      127 (pack_oz_kernel, once per fit / append);
 //   K*: in f64 (exp2 of the f64 distance), per (query, k-tile) a power of two
-//      2^eK > 1.01 max K*, X = rint(K* 2^(35 - eK)) split into the same
-//      balanced digits by integer arithmetic in the sweep;
-//   product: the pairs (s, u) with s + u <= 4 (15 of 25; the dropped ones sit
-//      below 128^-7 of the tile's |A| |K*| scale), level l = s + u chained in
-//      one int32 accumulator (no overflow: 64 products of |d| <= 127 per pair,
-//      worst level sum < 2^21), the five levels combined in f64 per 16x16
-//      block: T = (l0 128 + l1) 2^14 + l2 128 + l3 + round(l4 / 128) (< 2^42;
-//      exact but for level 4's last seven bits), V += T 2^(eA + eK - 35).
-// Emulated on the host at N = 8192 on the lpsc box (tools/r4_emulate_ozaki.py):
-// normwise variance error 1.2e-6 against f64 (the f32-rounded A alone: 6.5e-5),
-// the same with a per-row scale; truncated digits or four digits miss.
+//      2^eK > 1.01 max K*, X = rint(K* 2^(31 - eK)) < 2^31 / 1.01 in four such
+//      digits E_u 2^(24 - 8 u), read straight from the mantissa of one f64 add
+//      (K* 2^(31 - eK) + 2^52 + 0x808080: the bytes of X + 0x808080, the three
+//      lower ones XOR 0x80) in the sweep;
+//   product: the 14 pairs (s, u) with s + u <= 4 (u <= 3; the dropped ones sit
+//      below 2^-38 of the tile's |A| |K*| scale), level L = s + u chained in one
+//      int32 accumulator (no overflow: 64 products of |D| |E| <= 2^14 per pair,
+//      at most four pairs per level, < 2^22), the five levels combined in f64
+//      per 16x16 block: T = (l0 256 + l1) 2^16 + l2 256 + l3 + round(l4 / 256)
+//      (< 2^45; exact but for level 4's last eight bits), V += T 2^(eA + eK - 38).
+// (Round 4's first form cut both into base-128 digits by successive rounding:
+// 35 bits of A, 28 of K*, the same 14 products, but twelve integer operations
+// per K* value to spread 7-bit fields into bytes -- a quarter of the kernel's
+// VALU.)  Emulated on the host at N = 8192 on the lpsc box
+// (tools/r4_emulate_ozaki.py, base 128): normwise variance error 1.2e-6
+// against f64 (the f32-rounded A alone: 6.5e-5); truncated digits or
+// three-digit K* miss.
 //
 // Work items, the tick plan and the persistent walk are predict_f64_kernel's:
 // workgroup = 256 rows x 128 queries, eight waves, wave w owns queries
@@ -48,28 +57,29 @@ namespace {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kOzDigits = 5;                      // base-128 digits of A
-constexpr int kOzBits = 7 * kOzDigits;            // 35
-constexpr int kOzKDigits = 4;                     // base-128 digits of K*
-constexpr int kOzKBits = 7 * kOzKDigits;          // 28
+constexpr int kOzDigits = 5;                      // base-256 digits of A: XA = rint(A 2^(39 - eA))
+constexpr int kOzKDigits = 4;                     // base-256 digits of K*: X = rint(K* 2^(31 - eK))
+constexpr int kOzKBits = 31;
+constexpr int kOzScale = 38;                      // V += T 2^(eA + eK - 38), T in level-3 units
 constexpr int kOzRB = kBM / 16;                   // 16-row blocks per item (per wave)
 constexpr int kOzHalfRB = kOzRB / 2;              // blocks per stage
 constexpr int kOzPlane = kOzHalfRB * 64 * 16;     // one digit plane of a stage: 8 KiB
 constexpr int kOzA = kOzDigits * kOzPlane;        // 40 KiB of digits per stage
 constexpr int kOzTileBytes = 2 * kOzA;            // one packed tile: 80 KiB
 constexpr int kOzE = 64;                          // the stage's block exponents (8 x int32, padded)
-constexpr int kOzC = 3 * kBK * 8;                 // per k-tile: x, y, sf2 alpha (f64) = 1.5 KiB
+constexpr int kOzC = 3 * kBK * 8 + 2 * kBK * 4;   // per k-tile: x, y, sf2 alpha (f64), x, y (f32) = 2 KiB
 constexpr int kOzSlot = kOzA + kOzE + kOzC;
 constexpr int kOzWaves = kBN / 16;                // 8
 constexpr int kOzThreads = 64 * kOzWaves;
 constexpr int kOzDescWin = 64;                    // item descriptors (int4) per 1 KiB window
 constexpr int kOzListWin = 512;                   // tile-list entries (u16) per 1 KiB window
 constexpr int kOzSmem = 2 * kOzSlot + 4096 + 512; // two stage slots + two descriptor and two list windows + 2^(j/64)
-// K*'s digits: X = rint(K* 2^(28 - eK)) + bias, bias = 64 at the three lower
-// base-128 positions, by one f64 add of 2^52 + bias (the add rounds to an
+// K*'s digits: X = rint(K* 2^(31 - eK)) + bias, bias = 128 at the three lower
+// base-256 positions, by one f64 add of 2^52 + bias (the add rounds to an
 // integer and leaves X + bias in the low mantissa bits)
-constexpr uint32_t kOzBias = 64u * (1u + 128u + 16384u);
+constexpr uint32_t kOzBias = 0x808080u;
 constexpr double kOzMagic = 4503599627370496.0 + (double)kOzBias;
+static_assert(kOzC == 2048, "a tile's coordinates: two 1 KiB LDS-DMA pieces");
 static_assert(kOzA % (1024 * kOzWaves) == 0, "stage digits: whole 1 KiB LDS-DMA pieces per wave");
 
 __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
@@ -78,10 +88,10 @@ __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
 
 // 2^u in f64 for the K* digits (u <= 0): u = e + j/64 + r, |r| <= 1/128,
 // 2^u = 2^e T[j] P(r) with T[j] = 2^(j/64) from an LDS table and P the degree-5
-// Taylor polynomial of 2^r (truncation < (ln2/128)^6 / 720 < 2^-45 relative,
-// the table and the Horner steps a few 2^-53): 11 f64 operations instead of
-// the library exp2's ~30 -- the digits keep 35 bits of K* 2^-eK.  Returns
-// T[j] P(r) and sets e (the caller folds 2^e into its scale).
+// the degree-4 Taylor polynomial of 2^r (truncation < (ln2/128)^5 / 120 <
+// 2^-44 relative, the table and the Horner steps a few 2^-53): 10 f64
+// operations instead of the library exp2's ~30 -- the digits keep 31 bits of
+// K* 2^-eK.  Returns T[j] P(r) and sets e (the caller folds 2^e into its scale).
 __device__ __forceinline__ double exp2_tab(double u, const double *__restrict__ T, int &e) {
     const double m = rint(u * 64.0);
     const double r = fma(m, -0.015625, u);
@@ -89,21 +99,23 @@ __device__ __forceinline__ double exp2_tab(double u, const double *__restrict__ 
     e = mi >> 6;                      // floor(m / 64): arithmetic shift
     const double t = T[mi & 63];
     constexpr double c1 = 0.69314718055994530942, c2 = 0.24022650695910071233, c3 = 0.055504108664821579953,
-                     c4 = 0.0096181291076284771620, c5 = 0.0013333558146428443423;
-    const double p = fma(fma(fma(fma(fma(c5, r, c4), r, c3), r, c2), r, c1), r, 1.0);
+                     c4 = 0.0096181291076284771620;
+    const double p = fma(fma(fma(fma(c4, r, c3), r, c2), r, c1), r, 1.0);
     return t * p;
 }
 
 // K*'s four digit operands for this lane's 16 k (k = 16 g + j, g = lane >> 4)
-// and its query, from the tile's coordinates in LDS: Y = rint(K* 2^(28 - eK))
-// + bias as the low 28 bits of K* 2^(28 - eK) + 2^52 + bias (f64, exact), top
-// digit Y >> 21, the three lower digits the 7-bit fields below it less 64 --
-// spread into bytes and transposed four k at a time so that digit u of k =
-// 16 g + j is byte j of kd[u].  The per-(query, tile) exponent eK needs the max
-// over all 64 k: the four lanes l, l ^ 16, l ^ 32, l ^ 48 hold them.  Four
-// digits (28 bits) suffice for K*: its f32 rounding alone moved the lpsc box's
-// variance by only 2.6e-6 (tools/r4_emulate_ozaki.py), against 6.5e-5 for A.
-// On the last row block (mean) also mu += K* sf2 alpha.
+// and its query, from the tile's coordinates in LDS: Y = rint(K* 2^(31 - eK))
+// + bias as the low 32 bits of K* 2^(31 - eK) + 2^52 + bias (f64, exact); its
+// bytes are the digits, the top one in byte 3 and the three lower ones XOR
+// 0x80 (byte - 128 in two's complement) -- transposed four k at a time so that
+// digit u of k = 16 g + j is byte j of kd[u].  The per-(query, tile) exponent
+// eK needs the max over all 64 k: the four lanes l, l ^ 16, l ^ 32, l ^ 48
+// hold them; the max K* is the min distance's, so pass 1 is the f32 distance
+// alone (the stored f32 coordinates) and one v_exp_f32 per lane.  Four digits
+// (31 bits) suffice for K*: its f32 rounding (24 bits) alone moved the lpsc
+// box's variance by only 2.6e-6 (tools/r4_emulate_ozaki.py), against 6.5e-5
+// for A.  On the last row block (mean) also mu += K* sf2 alpha.
 template <bool MEAN>
 __device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, const double *__restrict__ T2, int g,
                                              double xq, double yq, double cexp, i32x4 (&kd)[kOzKDigits], int &eK,
@@ -111,18 +123,22 @@ __device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, const 
     const double *px = reinterpret_cast<const double *>(pc) + 16 * g;
     const double *py = reinterpret_cast<const double *>(pc + kBK * 8) + 16 * g;
     const double *pa = reinterpret_cast<const double *>(pc + kBK * 16) + 16 * g;
-    // pass 1: the exponent from an f32 estimate of every K* (v_exp_f32, a few
-    // ulp; the 1.01 margin covers it), so that pass 2 can cut each f64 K* into
-    // digits as soon as it is computed (four live at a time, not sixteen)
-    float kmax = 0.0f;
-    const float cexpf = (float)cexp, xqf = (float)xq, yqf = (float)yq;
+    const float *px32 = reinterpret_cast<const float *>(pc + kBK * 24) + 16 * g;
+    const float *py32 = reinterpret_cast<const float *>(pc + kBK * 28) + 16 * g;
+    // pass 1: the exponent from an f32 estimate of the largest K* (the min
+    // distance, v_exp_f32: a few ulp; the 1.01 margin covers it), so that pass
+    // 2 can cut each f64 K* into digits as soon as it is computed (four live
+    // at a time, not sixteen)
+    const float xqf = (float)xq, yqf = (float)yq;
+    float dmin = 3.0e38f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        const float dx = (float)px[j] - xqf, dy = (float)py[j] - yqf;
-        kmax = fmaxf(kmax, __builtin_amdgcn_exp2f(cexpf * fmaf(dy, dy, dx * dx)));
+        const float dx = px32[j] - xqf, dy = py32[j] - yqf;
+        dmin = fminf(dmin, fmaf(dy, dy, dx * dx));
     }
-    kmax = fmaxf(kmax, __shfl_xor(kmax, 16));
-    kmax = fmaxf(kmax, __shfl_xor(kmax, 32));
+    dmin = fminf(dmin, __shfl_xor(dmin, 16));
+    dmin = fminf(dmin, __shfl_xor(dmin, 32));
+    const float kmax = __builtin_amdgcn_exp2f((float)cexp * dmin);
     // 2^eK > 1.01 kmax, so K* 2^-eK < 0.99 and the top digit stays <= 127
     int e = 0;
     (void)frexpf(kmax * 1.01f, &e);
@@ -139,12 +155,7 @@ __device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, const 
             const double kt = exp2_tab(cexp * fma(dy, dy, dx * dx), T2, ex);   // K* = kt 2^ex
             if (MEAN) mu = fma(ldexp(kt, ex), pa[j], mu);
             const uint32_t Y = (uint32_t)__builtin_bit_cast(uint64_t, ldexp(kt, ex + esc) + kOzMagic);
-            // the four 7-bit fields into bytes 3..0 (the top digit in byte 3);
-            // the three lower ones less 64 as two's-complement bytes:
-            // b < 64 -> b | 0xC0, b >= 64 -> b ^ 0x40
-            const uint32_t sp = ((Y >> 21) & 0x7Fu) << 24 | ((Y >> 14) & 0x7Fu) << 16 | ((Y >> 7) & 0x7Fu) << 8 |
-                                (Y & 0x7Fu);
-            lo[i] = (sp ^ 0x00404040u) | ((~sp & 0x00404040u) << 1);
+            lo[i] = Y ^ 0x00808080u;   // top digit in byte 3; the lower ones byte - 128
         }
         // 4 x 4 byte transpose: byte i of the dword for digit u = byte (3 - u) of lo[i]
         const uint32_t p01a = __builtin_amdgcn_perm(lo[1], lo[0], 0x05010400u);   // lo0.b0 lo1.b0 lo0.b1 lo1.b1
@@ -159,11 +170,10 @@ __device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, const 
 }
 
 // The 14 digit products of one 16x16 block (A digit s, K* digit u, s + u <=
-// 4, u <= 3), combined and added to acc scaled by 2^(eA + eK - 35): level 4 is
-// folded into level 3 rounded to a level-3 unit (2^-36 of the tile's scale
-// 2^(eA + eK), below the dropped level 5's share), the rest exactly: T =
-// (l0 128 + l1) 2^14 + l2 128 + l3 + [l4 / 128] in level-3 units, two
-// conversions and two f64 operations per value.
+// 4, u <= 3), combined and added to acc scaled by 2^(eA + eK - 38): level 4 is
+// folded into level 3 rounded to a level-3 unit (2^-39 of the tile's scale
+// 2^(eA + eK)), the rest exactly: T = (l0 256 + l1) 2^16 + l2 256 + l3 +
+// [l4 / 256] in level-3 units, two conversions and two f64 operations per value.
 __device__ __forceinline__ void block_products(const i32x4 (&ad)[kOzDigits], const i32x4 (&kd)[kOzKDigits],
                                                double S, f64x4 &acc) {
     // ordered by A digit (each ad[s] dies after its group; the int32 sums are
@@ -185,9 +195,9 @@ __device__ __forceinline__ void block_products(const i32x4 (&ad)[kOzDigits], con
     l4 = mfma_i8(ad[4], kd[0], l4);
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-        const int h01 = l0[v] * 128 + l1[v];                      // |.| < 2^28
-        const int h23 = l2[v] * 128 + l3[v] + ((l4[v] + 64) >> 7);
-        const double t = fma((double)h01, 16384.0, (double)h23);  // exact, < 2^42
+        const int h01 = l0[v] * 256 + l1[v];                      // |.| < 2^29
+        const int h23 = l2[v] * 256 + l3[v] + ((l4[v] + 128) >> 8);  // |.| < 2^30
+        const double t = fma((double)h01, 65536.0, (double)h23);  // exact, < 2^45
         acc[v] = fma(t, S, acc[v]);
     }
 }
@@ -206,7 +216,7 @@ __device__ __forceinline__ void stage_blocks(const char *__restrict__ slot, int 
         i32x4 ad[kOzDigits];
 #pragma unroll
         for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[s * (kOzPlane / 16) + rb * 64];
-        const double S = ldexp(1.0, __builtin_amdgcn_readfirstlane(eA[rb]) + eK - kOzBits);
+        const double S = ldexp(1.0, __builtin_amdgcn_readfirstlane(eA[rb]) + eK - kOzScale);
         block_products(ad, kd, S, acc[H * kOzHalfRB + rb]);
     }
 }
@@ -271,7 +281,7 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
         if (wave == 0 && lane < 2)                                                                       \
             SBO_OZ_DMA16(gE + (int64_t)(T_) * 64 + (h_) * 32,                                            \
                          __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA)));     \
-        if ((kt_) >= 0 && (wave == 1 || (wave == 3 && lane < (kOzC - 1024) / 16)))                      \
+        if ((kt_) >= 0 && (wave == 1 || wave == 3))                                                      \
             SBO_OZ_DMA16(gC + (int64_t)(kt_) * kOzC + (wave == 3 ? 1024 : 0),                            \
                          __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA + kOzE +   \
                                                                               (wave == 3 ? 1024 : 0))));     \
@@ -447,22 +457,22 @@ __global__ __launch_bounds__(256) void pack_oz_kernel(const double *__restrict__
     }
     const int sub = rr >> 4, h = sub >> 3, rb = sub & 7;
     if ((rr & 15) == 0) eoz[T * 16 + sub] = eA;
-    const double sc = ldexp(1.0, -eA);
     char *base = aoz + T * (int64_t)kOzTileBytes + h * kOzA + rb * 1024;
 #pragma unroll
     for (int gg = 0; gg < 4; ++gg) {
         uint32_t w[kOzDigits][4];
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) {
-            double x = eA > -900 ? v[16 * gg + jj] * sc : 0.0;
+            // XA = rint(A 2^(39 - eA)), |XA| < 2^39 / 1.01; the bytes of XA +
+            // 0x80808080 are the digits (the four lower ones + 128)
+            const int64_t xa = eA > -900 ? (int64_t)rint(ldexp(v[16 * gg + jj], 39 - eA)) : 0;
+            const uint64_t yv = (uint64_t)(xa + 0x80808080ll);
 #pragma unroll
             for (int s = 0; s < kOzDigits; ++s) {
-                x *= 128.0;
-                const double d = rint(x);
-                x -= d;                          // exact; |x| <= 1/2 from the second digit on
-                const uint32_t b = (uint32_t)(int)d & 0xFFu;
-                if ((jj & 3) == 0) w[s][jj >> 2] = b;
-                else w[s][jj >> 2] |= b << (8 * (jj & 3));
+                const uint32_t b = (uint32_t)(yv >> (8 * (kOzDigits - 1 - s))) & 0xFFu;
+                const uint32_t d = s == 0 ? b : (b ^ 0x80u);
+                if ((jj & 3) == 0) w[s][jj >> 2] = d;
+                else w[s][jj >> 2] |= d << (8 * (jj & 3));
             }
         }
         const int l = (rr & 15) + 16 * gg;
@@ -475,7 +485,8 @@ __global__ __launch_bounds__(256) void pack_oz_kernel(const double *__restrict__
 }
 
 // Per k-tile: x[64], y[64] (f64 of the stored f32), sf2 alpha[64] (f64, alpha
-// from the f64 solve); padding rows: the first point's coordinates, alpha 0.
+// from the f64 solve), x[64], y[64] (the stored f32, for the sweep's pass-1
+// distance); padding rows: the first point's coordinates, alpha 0.
 __global__ void pack_koz_kernel(const float *__restrict__ x, const float *__restrict__ y,
                                 const double *__restrict__ alpha, int64_t n, int64_t npad, double sf2,
                                 char *__restrict__ koz) {
@@ -487,6 +498,8 @@ __global__ void pack_koz_kernel(const float *__restrict__ x, const float *__rest
     reinterpret_cast<double *>(c)[o] = (double)(in ? x[k] : x[0]);
     reinterpret_cast<double *>(c + kBK * 8)[o] = (double)(in ? y[k] : y[0]);
     reinterpret_cast<double *>(c + kBK * 16)[o] = in ? sf2 * alpha[k] : 0.0;
+    reinterpret_cast<float *>(c + kBK * 24)[o] = in ? x[k] : x[0];
+    reinterpret_cast<float *>(c + kBK * 28)[o] = in ? y[k] : y[0];
 }
 
 }  // namespace
