@@ -425,6 +425,10 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * cores (v_mfma_f64_16x16x4_f64; predict_f64.hip).  Both meet the 1e-5
  * contract where the fast sweep cannot (SBO_OPT_PRECISION). */
 #define SBO_OPT_PRECISE_KERNEL 22
+/* SBO_OPT_TABLE_MB (default 2048): device memory budget, MiB, of the K* table
+ * SBO_OPT_PRECISE_KERNEL 3 sweeps through (the queries run in chunks of as
+ * many 128-query blocks as fit it; at least one). */
+#define SBO_OPT_TABLE_MB 23
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe

@@ -57,6 +57,7 @@ SBO_OPT_INV_PANELS = 19
 SBO_OPT_INV_LEAVES = 20
 SBO_OPT_REPROBE = 21
 SBO_OPT_PRECISE_KERNEL = 22
+SBO_OPT_TABLE_MB = 23
 
 
 class SboError(RuntimeError):

@@ -80,6 +80,16 @@ constexpr int kOzSmem = 2 * kOzSlot + 4096 + 512; // two stage slots + two descr
 constexpr uint32_t kOzBias = 0x808080u;
 constexpr double kOzMagic = 4503599627370496.0 + (double)kOzBias;
 static_assert(kOzC == 2048, "a tile's coordinates: two 1 KiB LDS-DMA pieces");
+// K* table (SBO_OPT_PRECISE_KERNEL 3): per (query block, k-tile) the sweep's
+// digit operands, [wave][digit][lane][16 B] = 32 KiB, then eK per query (128 x
+// int32) and the tile's mean terms per query (128 x f64, sum over its 64 k)
+constexpr int kKztDigits = kOzWaves * kOzKDigits * 1024;   // 32 KiB
+constexpr int kKztE = kKztDigits;                          // + 512 B
+constexpr int kKztMu = kKztE + kBN * 4;                    // + 1 KiB
+constexpr int kKzt = kKztMu + kBN * 8;                     // 34304 B per (query block, k-tile)
+constexpr int kOzSlotT = kOzA + kOzE + kKzt;
+constexpr int kOzSmemT = 2 * kOzSlotT + 4096 + 512;
+static_assert(kOzSmemT <= 160 * 1024, "two table-mode stage slots must fit the LDS");
 static_assert(kOzA % (1024 * kOzWaves) == 0, "stage digits: whole 1 KiB LDS-DMA pieces per wave");
 
 __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
@@ -226,12 +236,19 @@ __device__ __forceinline__ void stage_blocks(const char *__restrict__ slot, int 
 // tile's digits a stage early, so that one wave's VALU work overlaps the
 // other's products -- needs a second digit set; at 87 spilled registers it
 // ran at 4517 ms against 2296 on the lpsc box and was dropped.)
+// MODE 0: K*'s digits built in the sweep; 2 (TABLE): read from the K* table
+// (kstar_table_kernel, one pass per query block and k-tile instead of one per
+// row block), staged with each tile's first stage; 1 (diagnostic build only,
+// wrong results): not built -- the bound on what the K* work costs the sweep.
+template <int MODE>
 __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     const char *__restrict__ aoz, const int *__restrict__ eoz, const char *__restrict__ koz,
     const int4 *__restrict__ desc, const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P,
     int n_items, int nI, const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp,
-    double cexp, double m0, double *__restrict__ part, double *__restrict__ mean) {
-    __shared__ __attribute__((aligned(16))) char smem[kOzSmem];
+    double cexp, double m0, double *__restrict__ part, double *__restrict__ mean, const char *__restrict__ kzt) {
+    constexpr bool NOKSTAR = MODE == 1, TABLE = MODE == 2;
+    constexpr int kSlot = TABLE ? kOzSlotT : kOzSlot;
+    __shared__ __attribute__((aligned(16))) char smem[TABLE ? kOzSmemT : kOzSmem];
     const int bid = blockIdx.x;
     const int rng = (P % 8 == 0) ? (bid % 8) * (P / 8) + bid / 8 : bid;
     // (bounds are clamped so that a corrupt plan cannot address outside the buffers)
@@ -242,9 +259,9 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     const int wave = tid >> 6;
     const int r = lane & 15;
     const int g = lane >> 4;
-    const int4 *dwin = reinterpret_cast<const int4 *>(smem + 2 * kOzSlot);
-    const unsigned short *lwin = reinterpret_cast<const unsigned short *>(smem + 2 * kOzSlot + 2048);
-    double *T2 = reinterpret_cast<double *>(smem + 2 * kOzSlot + 4096);
+    const int4 *dwin = reinterpret_cast<const int4 *>(smem + 2 * kSlot);
+    const unsigned short *lwin = reinterpret_cast<const unsigned short *>(smem + 2 * kSlot + 2048);
+    double *T2 = reinterpret_cast<double *>(smem + 2 * kSlot + 4096);
     if (tid < 64) T2[tid] = exp2((double)tid * 0.015625);   // (visible after the prologue's barriers)
 
     // LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction, lane
@@ -254,13 +271,16 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     typedef __attribute__((address_space(3))) char lds_char;
     const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
     const uint32_t lds_wave = lds_smem + (uint32_t)__builtin_amdgcn_readfirstlane(wave) * 1024u;
-    const uint32_t lds_dwin = lds_smem + 2u * kOzSlot;
+    const uint32_t lds_dwin = lds_smem + 2u * kSlot;
     const uint32_t lds_lwin = lds_dwin + 2048u;
     const char *gA = aoz + wave * 1024 + lane * 16;
     const char *gE = reinterpret_cast<const char *>(eoz) + lane * 16;
     const char *gC = koz + lane * 16;
     const char *gD = reinterpret_cast<const char *>(desc) + lane * 16;
     const char *gL = reinterpret_cast<const char *>(tl) + lane * 16;
+    const char *gZ = kzt + lane * 16;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const int nkt = kTilesPerRowBlockStep * nI;
 #define SBO_OZ_DMA16(gsrc, ldst)                                                                         \
     do {                                                                                                 \
         uint32_t keep_;                                                                                  \
@@ -271,19 +291,28 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
                      : "memory");                                                                        \
     } while (0)
     // stage (packed tile T_, row half h_) into slot buf, with the coordinates
-    // of k-tile kt_ (none: kt_ < 0)
-#define SBO_OZ_STAGE(T_, kt_, h_, buf)                                                                   \
+    // of k-tile kt_ (TABLE: its K* table piece for query block qb_; none: kt_ < 0)
+#define SBO_OZ_STAGE(T_, kt_, h_, buf, qb_)                                                              \
     do {                                                                                                 \
         const char *s_ = gA + (int64_t)(T_) * kOzTileBytes + (h_) * kOzA;                                \
-        const uint32_t d_ = __builtin_amdgcn_readfirstlane(lds_wave + (uint32_t)(buf) * kOzSlot);        \
+        const uint32_t d_ = __builtin_amdgcn_readfirstlane(lds_wave + (uint32_t)(buf) * kSlot);          \
         _Pragma("unroll") for (int j_ = 0; j_ < kOzA / (1024 * kOzWaves); ++j_)                          \
             SBO_OZ_DMA16(s_ + j_ * kOzWaves * 1024, d_ + (uint32_t)(j_ * kOzWaves * 1024));              \
         if (wave == 0 && lane < 2)                                                                       \
             SBO_OZ_DMA16(gE + (int64_t)(T_) * 64 + (h_) * 32,                                            \
-                         __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA)));     \
-        if ((kt_) >= 0 && (wave == 1 || wave == 3))                                                      \
+                         __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kSlot + kOzA)));       \
+        if (TABLE) {                                                                                     \
+            if ((kt_) >= 0) {                                                                            \
+                const char *z_ = gZ + ((int64_t)(qb_) * nkt + (kt_)) * kKzt;                              \
+                const uint32_t zd_ = __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kSlot + kOzA + kOzE)); \
+                _Pragma("unroll") for (int u_ = 0; u_ < kOzKDigits; ++u_)                                \
+                    SBO_OZ_DMA16(z_ + wave * 4096 + u_ * 1024, zd_ + (uint32_t)(wave_u * 4096 + u_ * 1024)); \
+                if (wave == 0 && lane < 32) SBO_OZ_DMA16(z_ + kKztE, zd_ + (uint32_t)kKztE);             \
+                if (wave == 1) SBO_OZ_DMA16(z_ + kKztMu, zd_ + (uint32_t)kKztMu);                        \
+            }                                                                                            \
+        } else if ((kt_) >= 0 && (wave == 1 || wave == 3))                                               \
             SBO_OZ_DMA16(gC + (int64_t)(kt_) * kOzC + (wave == 3 ? 1024 : 0),                            \
-                         __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOzSlot + kOzA + kOzE +   \
+                         __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kSlot + kOzA + kOzE +     \
                                                                               (wave == 3 ? 1024 : 0))));     \
     } while (0)
 #define SBO_OZ_DESC_WINDOW(w_)                                                                           \
@@ -321,7 +350,7 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int t = list_at(e, dc.x);
-    SBO_OZ_STAGE(tile_start(dc.x) + t, t, 0, 0);
+    SBO_OZ_STAGE(tile_start(dc.x) + t, t, 0, 0, dc.y);
     int64_t q = (int64_t)dc.y * kBN + wave * 16 + r;
     double xq = (double)qx[q < m ? q : m - 1], yq = (double)qy[q < m ? q : m - 1];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -364,12 +393,24 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
                 if (en % kOzListWin == 0) SBO_OZ_LIST_WINDOW(en / kOzListWin + 1);
                 tn = list_at(en, dn.x);
             }
-            SBO_OZ_STAGE(tile_start(dn.x) + tn, hn == 0 ? tn : -1, hn, cur ^ 1);
+            SBO_OZ_STAGE(tile_start(dn.x) + tn, hn == 0 ? tn : -1, hn, cur ^ 1, dn.y);
         }
-        const char *slot = smem + cur * kOzSlot;
+        const char *slot = smem + cur * kSlot;
         const int I = dc.x;
         if (h == 0) {
-            if (I == nI - 1)
+            if (NOKSTAR) {
+#pragma unroll
+                for (int u = 0; u < kOzKDigits; ++u) kd[u] = i32x4{lane + u, lane ^ u, 3 * u, t};
+                eK = -8;
+            } else if (TABLE) {
+                const char *tz = slot + kOzA + kOzE;
+#pragma unroll
+                for (int u = 0; u < kOzKDigits; ++u)
+                    kd[u] = *reinterpret_cast<const i32x4 *>(tz + wave * 4096 + u * 1024 + lane * 16);
+                eK = *reinterpret_cast<const int *>(tz + kKztE + (wave * 16 + r) * 4);
+                // the tile's mean terms (summed over its 64 k) once per query
+                if (I == nI - 1 && g == 0) mu += *reinterpret_cast<const double *>(tz + kKztMu + (wave * 16 + r) * 8);
+            } else if (I == nI - 1)
                 kstar_digits<true>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
             else
                 kstar_digits<false>(slot + kOzA + kOzE, T2, g, xq, yq, cexp, kd, eK, mu);
@@ -418,6 +459,39 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
 #undef SBO_OZ_DESC_WINDOW
 #undef SBO_OZ_LIST_WINDOW
 #undef SBO_OZ_DMA16
+}
+
+// The K* table of nq query blocks (SBO_OPT_PRECISE_KERNEL 3): one workgroup per
+// (k-tile t, query block), each wave its 16 queries' digit operands exactly as
+// the sweep builds them (kstar_digits), eK per query and the tile's mean terms
+// per query -- once per (query block, k-tile) instead of once per row block
+// that reads the tile (up to nI times).  grid = (nkt, nq).
+__global__ __launch_bounds__(kOzThreads) void kstar_table_kernel(const char *__restrict__ koz,
+                                                                 const float *__restrict__ qx,
+                                                                 const float *__restrict__ qy, int64_t m, int nkt,
+                                                                 double cexp, char *__restrict__ kzt) {
+    __shared__ double T2[64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r = lane & 15;
+    if (tid < 64) T2[tid] = exp2((double)tid * 0.015625);
+    __syncthreads();
+    const int t = blockIdx.x;
+    const int64_t qb = blockIdx.y;
+    const int64_t q = qb * kBN + wave * 16 + r;
+    const double xq = (double)qx[q < m ? q : m - 1], yq = (double)qy[q < m ? q : m - 1];
+    i32x4 kd[kOzKDigits];
+    int eK = 0;
+    double mu = 0.0;
+    kstar_digits<true>(koz + (int64_t)t * kOzC, T2, g, xq, yq, cexp, kd, eK, mu);
+    mu += __shfl_xor(mu, 16);
+    mu += __shfl_xor(mu, 32);
+    char *out = kzt + (qb * nkt + t) * (int64_t)kKzt;
+#pragma unroll
+    for (int u = 0; u < kOzKDigits; ++u)
+        *reinterpret_cast<i32x4 *>(out + wave * 4096 + u * 1024 + lane * 16) = kd[u];
+    if (g == 0) {
+        reinterpret_cast<int *>(out + kKztE)[wave * 16 + r] = eK;
+        reinterpret_cast<double *>(out + kKztMu)[wave * 16 + r] = mu;
+    }
 }
 
 // A = sf2 L^-1 (from the fit's f64 inverse, lower, column-major, lda ld) into
@@ -524,12 +598,39 @@ hipError_t launch_pack_oz(hipStream_t s, const double *Linv, int64_t ld, int64_t
 hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, const char *koz, const int4 *desc,
                              const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
                              const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
-                             double *mean) {
+                             double *mean, int variant, const char *kzt) {
     if (nI <= 0 || m <= 0) return hipSuccess;
     const double cexp = -1.0 / (2.0 * ell * ell * 0.69314718055994530942);
-    hipLaunchKernelGGL(predict_oz_kernel, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc, tl, seg, P,
-                       n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean);
+#ifdef SBO_DIAG
+    if (variant == 9) {   // timing bound: no K* digits (wrong results)
+        hipLaunchKernelGGL(predict_oz_kernel<1>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc,
+                           tl, seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean, kzt);
+        return hipGetLastError();
+    }
+#endif
+    if (variant == 3) {   // K*'s digits from the table
+        if (!kzt) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(predict_oz_kernel<2>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc,
+                           tl, seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean, kzt);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(predict_oz_kernel<0>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc, tl,
+                       seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean, kzt);
     return hipGetLastError();
 }
 
+}  // namespace sbo
+
+namespace sbo {
+size_t oz_table_bytes(int64_t npad) { return (size_t)kKzt * (size_t)(npad / kBK); }   // per query block
+
+hipError_t launch_kstar_table(hipStream_t s, const char *koz, const float *qx, const float *qy, int64_t m,
+                              int64_t npad, double ell, int64_t nq, char *kzt) {
+    if (m <= 0 || nq <= 0) return hipSuccess;
+    const double cexp = -1.0 / (2.0 * ell * ell * 0.69314718055994530942);
+    const int nkt = (int)(npad / kBK);
+    hipLaunchKernelGGL(kstar_table_kernel, dim3((unsigned)nkt, (unsigned)nq), dim3(kOzThreads), 0, s, koz, qx, qy, m,
+                       nkt, cexp, kzt);
+    return hipGetLastError();
+}
 }  // namespace sbo

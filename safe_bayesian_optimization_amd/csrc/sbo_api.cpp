@@ -1263,11 +1263,14 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
                   "split the queries into shards");
     }
     SBO_HIP(ctx->plan_work.reserve(sbo::predict_work_bytes(ctx->npad, ms, P)));
-    SBO_HIP(sbo::launch_plan(ctx->stream, ctx->kbox.as<float4>(), ctx->npad, qx, qy, ms, ldp,
-                             (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan, ctx->part.as<float>(),
-                             ctx->mean.as<float>(),
-                             ctx->prof && !cost ? ctx->counters.as<unsigned long long>() : nullptr, P,
-                             ctx->plan_work.as<void>(), ctx->plan_work.capacity()));
+    // (the K* table's precise sweep plans each chunk of query blocks itself)
+    const bool chunked = precise && ctx->precise_kernel == 3 && !cost;
+    if (!chunked)
+        SBO_HIP(sbo::launch_plan(ctx->stream, ctx->kbox.as<float4>(), ctx->npad, qx, qy, ms, ldp,
+                                 (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan,
+                                 ctx->part.as<float>(), ctx->mean.as<float>(),
+                                 ctx->prof && !cost ? ctx->counters.as<unsigned long long>() : nullptr, P,
+                                 ctx->plan_work.as<void>(), ctx->plan_work.capacity()));
     if (cost) {  // sbo_query_cost: the plan's work per query, no sweep
         SBO_HIP(ctx->qcost.reserve(sizeof(float) * (size_t)((ms + sbo::kBN - 1) / sbo::kBN)));
         SBO_HIP(sbo::launch_plan_cost(ctx->stream, ctx->npad, ms, P, ctx->plan_work.as<void>(), perm,
@@ -1284,18 +1287,49 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         const int4 *desc = nullptr;
         const unsigned short *tl = nullptr;
         const int *seg = nullptr;
+        if (chunked) {
+            // SBO_OPT_PRECISE_KERNEL 3: the queries in chunks of Qc blocks --
+            // each chunk's plan, its K* table (every k-tile of its query
+            // blocks, once) and the sweep reading it; the table is sized by
+            // SBO_OPT_TABLE_MB (2 GiB: a 10^6-point grid at N = 16384 runs in
+            // 33 chunks of 244 query blocks).  An item's result does not
+            // depend on the chunking (plans are per query block).
+            const int64_t nQ = (ms + sbo::kBN - 1) / sbo::kBN;
+            const size_t per_qb = sbo::oz_table_bytes(ctx->npad);
+            const int64_t Qc = std::clamp<int64_t>((int64_t)(((size_t)ctx->table_mb << 20) / per_qb), 1, nQ);
+            SBO_HIP(ctx->kzt.reserve(per_qb * (size_t)Qc));
+            double *pd = ctx->part.as<double>(), *md = ctx->mean.as<double>();
+            Bracket br(ctx, ctx->ev_predict);
+            for (int64_t qb0 = 0; qb0 < nQ; qb0 += Qc) {
+                const int64_t c0 = qb0 * sbo::kBN, mc = std::min<int64_t>(Qc * sbo::kBN, ms - c0);
+                const int64_t nq = (mc + sbo::kBN - 1) / sbo::kBN;
+                SBO_HIP(sbo::launch_plan(ctx->stream, ctx->kbox.as<float4>(), ctx->npad, qx + c0, qy + c0, mc, ldp,
+                                         (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan,
+                                         reinterpret_cast<float *>(pd + c0), reinterpret_cast<float *>(md + c0),
+                                         ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr, P,
+                                         ctx->plan_work.as<void>(), ctx->plan_work.capacity()));
+                SBO_HIP(sbo::launch_kstar_table(ctx->stream, ctx->koz.as<char>(), qx + c0, qy + c0, mc, ctx->npad,
+                                                ctx->hyper.length_scale, nq, ctx->kzt.as<char>()));
+                sbo::plan_views(ctx->npad, mc, P, ctx->plan_work.as<void>(), &desc, &tl, &seg);
+                SBO_HIP(sbo::launch_predict_oz(ctx->stream, ctx->aoz.as<char>(), ctx->eoz.as<int>(),
+                                               ctx->koz.as<char>(), desc, tl, seg, P, (int)(nIc * nq), (int)nIc,
+                                               qx + c0, qy + c0, mc, ldp, ctx->hyper.length_scale,
+                                               ctx->hyper.prior_mean, pd + c0, md + c0, 3, ctx->kzt.as<char>()));
+            }
+        } else {
         sbo::plan_views(ctx->npad, ms, P, ctx->plan_work.as<void>(), &desc, &tl, &seg);
         Bracket br(ctx, ctx->ev_predict);
         if (ctx->precise_kernel >= 1)
             SBO_HIP(sbo::launch_predict_oz(ctx->stream, ctx->aoz.as<char>(), ctx->eoz.as<int>(), ctx->koz.as<char>(),
                                            desc, tl, seg, P, (int)(nIc * ((ms + sbo::kBN - 1) / sbo::kBN)), (int)nIc,
                                            qx, qy, ms, ldp, ctx->hyper.length_scale, ctx->hyper.prior_mean,
-                                           ctx->part.as<double>(), ctx->mean.as<double>()));
+                                           ctx->part.as<double>(), ctx->mean.as<double>(), ctx->precise_kernel));
         else
             SBO_HIP(sbo::launch_predict_f64(ctx->stream, ctx->a64.as<double>(), ctx->kc64.as<double>(), desc, tl, seg,
                                             P, (int)(nIc * ((ms + sbo::kBN - 1) / sbo::kBN)), (int)nIc, qx, qy, ms,
                                             ldp, ctx->hyper.length_scale, ctx->hyper.prior_mean,
                                             ctx->part.as<double>(), ctx->mean.as<double>()));
+        }
     } else if (ctx->kernel_variant >= 2) {
         // split-operand sweep: derive the bf16 planes of any repacked row
         // block, and give the kernel whole 128-query blocks to read
@@ -2002,9 +2036,19 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->chol_reserve = (int)value;
             return SBO_OK;
         case SBO_OPT_PRECISE_KERNEL:
-            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA) or 1 (int8)");
+#ifdef SBO_DIAG
+            SBO_CHECK(value == 0 || value == 1 || value == 3 || value == 9, SBO_E_INVAL,
+                      "SBO_OPT_PRECISE_KERNEL: 0, 1, 3 or 9 (diagnostic)");
+#else
+            SBO_CHECK(value == 0 || value == 1 || value == 3, SBO_E_INVAL,
+                      "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA), 1 (int8) or 3 (int8, K* table)");
+#endif
             if ((ctx->precise_kernel == 0) != (value == 0)) ctx->a64_I0 = 0;   // the other operand: derive it all
             ctx->precise_kernel = (int)value;
+            return SBO_OK;
+        case SBO_OPT_TABLE_MB:
+            SBO_CHECK(value >= 1 && value <= (int64_t(1) << 20), SBO_E_INVAL, "SBO_OPT_TABLE_MB must be in [1, 2^20]");
+            ctx->table_mb = value;
             return SBO_OK;
         case SBO_OPT_REPROBE:
             SBO_CHECK(value >= 0 && value <= 1000, SBO_E_INVAL, "SBO_OPT_REPROBE must be in [0, 1000] (percent)");

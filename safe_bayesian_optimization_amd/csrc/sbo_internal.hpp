@@ -176,6 +176,7 @@ struct sbo_ctx {
     sbo::DevBuf alpha64;         // alpha from the f64 solve (length cap)
     sbo::DevBuf a64, kc64;       // f64 packed operand and coordinates, derived lazily
     sbo::DevBuf aoz, eoz, koz;   // int8 digit operand, its block exponents, coordinates (predict_oz.hip)
+    sbo::DevBuf kzt;             // the int8 sweep's K* table of one chunk of query blocks (SBO_OPT_PRECISE_KERNEL 3)
     int precise_kernel = 1;      // SBO_OPT_PRECISE_KERNEL: 0 the f64 MFMA sweep, 1 the int8 sliced sweep
     int64_t a64_I0 = 0;          // first row block whose precise operand (of precise_kernel) is stale
     int64_t probe_n = 0;         // training points at the last probe (0: none)
@@ -184,6 +185,7 @@ struct sbo_ctx {
     // locations (where the variance is smallest); each part's own normwise error
     double probe_err_grid = -1.0, probe_err_train = -1.0, probe_vmax_grid = 0.0, probe_vmax_train = 0.0;
     int probe_m_grid = 0, probe_m_train = 0;
+    int64_t table_mb = 2048;     // SBO_OPT_TABLE_MB: the K* table's memory budget (SBO_OPT_PRECISE_KERNEL 3)
     int reprobe_pct = 25;        // SBO_OPT_REPROBE: appends re-probe once N grew by this share (0: every append)
     bool inv_batched = true;      // SBO_OPT_INV_LEAVES: the recursion's base cases in one batched dtrtri
     bool inv_leaves_done = false; // (set while a recursion runs whose base cases are already inverted)
@@ -395,7 +397,12 @@ hipError_t launch_pack_oz(hipStream_t s, const double *Linv, int64_t ld, int64_t
 hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, const char *koz, const int4 *desc,
                              const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
                              const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
-                             double *mean);
+                             double *mean, int variant = 1, const char *kzt = nullptr);
+// The K* table (SBO_OPT_PRECISE_KERNEL 3): bytes per query block, and the
+// table of nq query blocks of the queries qx/qy (m of them) for every k-tile.
+size_t oz_table_bytes(int64_t npad);
+hipError_t launch_kstar_table(hipStream_t s, const char *koz, const float *qx, const float *qy, int64_t m,
+                              int64_t npad, double ell, int64_t nq, char *kzt);
 // Morton ordering of the queries (query_order.hip): workspace of
 // query_order_bytes(m); returns the permutation and the gathered coordinates
 // (all inside the workspace).

@@ -1284,10 +1284,10 @@ def test_precision_levels(mapper):
 # the precise kernels' tolerances against the fp64 oracle: the f64 sweep to
 # f64 rounding (f32 outputs: 1e-6), the int8 sliced sweep to its slicing
 # (emulated 1.2e-6 on the lpsc box at N = 8192, tools/r4_emulate_ozaki.py)
-PRECISE_TOL = {0: (1e-6, 1e-6), 1: (1e-6, 4e-6)}
+PRECISE_TOL = {0: (1e-6, 1e-6), 1: (1e-6, 4e-6), 3: (1e-6, 4e-6)}
 
 
-@pytest.mark.parametrize("kernel", [0, 1])
+@pytest.mark.parametrize("kernel", [0, 1, 3])
 @pytest.mark.parametrize("n,gw,gh,box", [(2048, 64, 48, False), (3000, 90, 70, True), (700, 40, 30, True)])
 def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box, kernel):
     """SBO_OPT_PRECISION = 1: the f64 sweep (SBO_OPT_PRECISE_KERNEL 0: A =
@@ -1343,7 +1343,7 @@ def test_int8_mfma_k_layout(mapper):
     for n in (64, 65, 130):
         wl = synthetic_box(n, 7, 5, seed=n)
         outs = {}
-        for kernel in (0, 1):
+        for kernel in (0, 1, 3):
             gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
             gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
             gm.set_option(N.SBO_OPT_PRECISION, 1)
@@ -1352,7 +1352,7 @@ def test_int8_mfma_k_layout(mapper):
         gm.set_option(N.SBO_OPT_PRECISION, -1)
         gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 1)
         omu, ovar = oracle_given_factor64(gm, wl)
-        for kernel in (0, 1):
+        for kernel in (0, 1, 3):
             mu, sd = outs[kernel]
             emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
             print(f"N={n} kernel {kernel}: mu {emu:.2e} var {evar:.2e}")
@@ -1394,3 +1394,38 @@ def test_precision_auto_probe(mapper):
         b.set_option(N.SBO_OPT_PRECISION, 1)      # no f64 inverse travels with a state
     assert not b.precision()[0]
     b.close()
+
+
+def test_kstar_table_chunks(mapper):
+    """SBO_OPT_PRECISE_KERNEL 3 (the int8 sweep reading K*'s digits from a
+    table built once per query block and k-tile, the queries in chunks that fit
+    SBO_OPT_TABLE_MB): the same digits as the in-sweep K* of kernel 1, so sigma
+    is bitwise kernel 1's (the mean sums its per-tile terms in another order:
+    within 1e-12); bitwise the same for any chunking (1 MiB: one query block
+    per chunk on this N) and sweep partition, on the lpsc box with a ragged
+    last query block."""
+    from safe_bayesian_optimization_amd.terrain import synthetic_box
+    wl = synthetic_box(3000, 61, 29, seed=5)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_PRECISION, 1)
+    try:
+        gm.fit(wl.x, wl.y, wl.obs)
+        res = {}
+        for kernel, mb, groups in ((1, 2048, 0), (3, 2048, 0), (3, 1, 0), (3, 1, 7), (3, 3, 1000)):
+            gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
+            gm.set_option(N.SBO_OPT_TABLE_MB, mb)
+            gm.set_option(N.SBO_OPT_SWEEP_GROUPS, groups)
+            res[(kernel, mb, groups)] = gm.predict(wl.qx, wl.qy)
+        base = res[(3, 2048, 0)]
+        for k, (mu, sd) in res.items():
+            assert np.array_equal(sd, res[(1, 2048, 0)][1]), k
+            if k[0] == 3:
+                assert np.array_equal(mu, base[0]) and np.array_equal(sd, base[1]), k
+        assert nrel(base[0], res[(1, 2048, 0)][0].astype(np.float64)) < 1e-6
+        omu, ovar = oracle_given_factor64(gm, wl)
+        assert nrel(base[0], omu) < PRECISE_TOL[3][0] and nrel(base[1].astype(np.float64) ** 2, ovar) < PRECISE_TOL[3][1]
+    finally:
+        gm.set_option(N.SBO_OPT_SWEEP_GROUPS, 0)
+        gm.set_option(N.SBO_OPT_TABLE_MB, 2048)
+        gm.set_option(N.SBO_OPT_PRECISION, -1)
+        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 1)
