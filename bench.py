@@ -673,22 +673,25 @@ def run_regime_stress(a, gm, prof, dev, n, gw, gh):
     pk = pinfo["precise_kernel"]
     res = _timed_ticks(prof, step, a.regime_steps)
     sd_default = outs["sd"].clone()
-    # the other precise kernel on the same fit (f64 MFMA when the default is
-    # the int8 sliced one): time and whole-grid variance difference
-    other = None
+    # the other precise kernels on the same fit (the f64 MFMA sweep, and the
+    # int8 sweep building K*'s digits itself when the default reads the K*
+    # table): time and whole-grid variance difference
+    others = {}
     if precise:
-        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 0 if pk >= 1 else 1)
-        try:
-            ores = _timed_ticks(prof, step, 1)
-        finally:
-            gm.set_option(N.SBO_OPT_PRECISE_KERNEL, pk)
-        v_o = outs["sd"].double() ** 2
-        v_d = sd_default.double() ** 2
-        other = _regime_line(a, "lpsc_stress_box other precise kernel",
-                             f"SBO_OPT_PRECISE_KERNEL = {0 if pk >= 1 else 1} on the same fit", m, n, *ores,
-                             precise=True, precise_kernel=0 if pk >= 1 else 1)
-        other["variance_difference_vs_default"] = float((v_o - v_d).abs().max() / v_d.abs().max())
-        other["default_speedup_over_this"] = other["ms_per_step"] / (res[0] * 1e3)
+        for ok in ([0, 1] if pk == 3 else [0 if pk >= 1 else 1]):
+            gm.set_option(N.SBO_OPT_PRECISE_KERNEL, ok)
+            try:
+                ores = _timed_ticks(prof, step, 1)
+            finally:
+                gm.set_option(N.SBO_OPT_PRECISE_KERNEL, pk)
+            v_o = outs["sd"].double() ** 2
+            v_d = sd_default.double() ** 2
+            o = _regime_line(a, "lpsc_stress_box other precise kernel", f"SBO_OPT_PRECISE_KERNEL = {ok} on the same fit",
+                             m, n, *ores, precise=True, precise_kernel=ok)
+            o["variance_difference_vs_default"] = float((v_o - v_d).abs().max() / v_d.abs().max())
+            o["default_speedup_over_this"] = o["ms_per_step"] / (res[0] * 1e3)
+            others[ok] = o
+    other = others.get(0)
     # the fast split sweep on the same fit, and its variance error against the
     # precise sweep over the whole grid (device against device; the tests
     # measure both against the fp64 oracle: tests/test_gpu_headline.py)
@@ -713,6 +716,7 @@ def run_regime_stress(a, gm, prof, dev, n, gw, gh):
                                          "how": "32 x 32 grid over the training box + 512 training locations, "
                                                 "fast vs precise sweep"},
                                "other_precise_kernel": other,
+                               "int8_in_sweep_kstar": others.get(1),
                                "fast_sweep": fast}, precise=precise, precise_kernel=pk)
 
 
@@ -736,8 +740,12 @@ def predict_roofline(variant, flops_f32, ms, mfma_flops, levels, precise=False, 
     ach = mfma_flops / (ms * 1e-3) / 1e12
     if precise and precise_kernel >= 1:
         tops = OZ_PRODUCTS * flops_f32 / (ms * 1e-3) / 1e12
+        table = ("; K*'s digits from the K* table, built once per query block and k-tile, the queries in chunks "
+                 "(plan + table + sweep per chunk, all in the time)" if precise_kernel == 3 else
+                 "; K*'s digits built in the sweep")
         return {"kernel": "predict_oz_kernel (V = sf2 L^-1 K*^T from five A x four K* int8 digit slices: 14 "
-                          "v_mfma_i32_16x16x64_i8 products per f64 product, exact int32 sums, f64 combination)",
+                          "v_mfma_i32_16x16x64_i8 products per f64 product, exact int32 sums, f64 combination"
+                          + table + ")",
                 "bound": "mfma", "achieved": tops, "peak": PEAK_I8_MFMA_TOPS, "unit": "TOPS (int8)",
                 "frac": tops / PEAK_I8_MFMA_TOPS, "int8_ops_per_launch": OZ_PRODUCTS * flops_f32,
                 "algorithmic_flops_per_launch": flops_f32, "f64_equivalent_tflops": f32_tf,

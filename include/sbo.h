@@ -417,13 +417,16 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * SBO_OPT_PRECISION -1, an sbo_append runs the precision probe again once N
  * has grown by this share since the last probe (every sbo_fit probes). */
 #define SBO_OPT_REPROBE 21
-/* SBO_OPT_PRECISE_KERNEL (1 default | 0): the precise sweep's arithmetic --
+/* SBO_OPT_PRECISE_KERNEL (3 default | 1 | 0): the precise sweep's arithmetic --
  * 1 A = sf2 L^-1 as five and K* as four balanced base-256 int8 digit slices, the 14
  * leading slice products on the int8 matrix cores (v_mfma_i32_16x16x64_i8,
  * exact int32 sums), combined in f64 per k-tile (an Ozaki-style sliced
- * product; predict_oz.hip); 0 every product and sum in f64 on the f64 matrix
- * cores (v_mfma_f64_16x16x4_f64; predict_f64.hip).  Both meet the 1e-5
- * contract where the fast sweep cannot (SBO_OPT_PRECISION). */
+ * product; predict_oz.hip), K*'s digits built in the sweep for every row
+ * block that reads a k-tile; 3 the same products with K*'s digits read from a
+ * table built once per (128-query block, k-tile) (the queries in chunks that
+ * fit SBO_OPT_TABLE_MB; sigma bitwise kernel 1's); 0 every product and sum in
+ * f64 on the f64 matrix cores (v_mfma_f64_16x16x4_f64; predict_f64.hip).  All
+ * meet the 1e-5 contract where the fast sweep cannot (SBO_OPT_PRECISION). */
 #define SBO_OPT_PRECISE_KERNEL 22
 /* SBO_OPT_TABLE_MB (default 2048): device memory budget, MiB, of the K* table
  * SBO_OPT_PRECISE_KERNEL 3 sweeps through (the queries run in chunks of as

@@ -1215,6 +1215,8 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     // timing diagnostic (diagnostic build only): the drop-only plan
     // with every kept tile at level SBO_LVL_FORCE -- outside the error budget
     if (const char *e = getenv("SBO_LVL_FORCE"); e && plan.levels) plan.levels = 2 + std::clamp(atoi(e), 0, 2);
+    // the level increments' rank keys (SkipPlan::lvl_key), "k0,k1" -- re-calibration A/B
+    if (const char *e = getenv("SBO_LVL_KEY")) (void)sscanf(e, "%f,%f", &plan.lvl_key[0], &plan.lvl_key[1]);
 #endif
     if (ctx->query_order && plan.L > 0 && m > sbo::kBN) {
         int32_t *p = nullptr;

@@ -1329,7 +1329,7 @@ def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box, kernel):
         assert nrel(mu2, omu2) < tmu and nrel(sd2.astype(np.float64) ** 2, ovar2) < tvar
     finally:
         gm.set_option(N.SBO_OPT_PRECISION, -1)
-        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 1)
+        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 3)
 
 
 def test_int8_mfma_k_layout(mapper):
@@ -1350,7 +1350,7 @@ def test_int8_mfma_k_layout(mapper):
             gm.fit(wl.x, wl.y, wl.obs)
             outs[kernel] = gm.predict(wl.qx, wl.qy)
         gm.set_option(N.SBO_OPT_PRECISION, -1)
-        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 1)
+        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 3)
         omu, ovar = oracle_given_factor64(gm, wl)
         for kernel in (0, 1, 3):
             mu, sd = outs[kernel]
@@ -1428,4 +1428,4 @@ def test_kstar_table_chunks(mapper):
         gm.set_option(N.SBO_OPT_SWEEP_GROUPS, 0)
         gm.set_option(N.SBO_OPT_TABLE_MB, 2048)
         gm.set_option(N.SBO_OPT_PRECISION, -1)
-        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 1)
+        gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 3)
