@@ -500,7 +500,7 @@ def run_sweep(a, dev, world, rank):
         if regimes:
             d = regimes["dense"]
             cpu["gpu_dense_over_cpu"] = d["value"] / cpu["value"]
-            best = max(b["value"] for b in cpu["by_threads"])
+            best_cpu = max(b["value"] for b in cpu["by_threads"])
             for b in cpu["by_threads"]:
                 if b["value"] < cpu["value"]:
                     # more threads ran slower than the headline share (OpenBLAS
@@ -510,7 +510,7 @@ def run_sweep(a, dev, world, rank):
                     continue
                 b["gpu_dense_over_cpu"] = d["value"] / b["value"]
                 b["gpu_over_cpu"] = value / b["value"]
-            cpu["gpu_dense_over_best_cpu"] = d["value"] / best
+            cpu["gpu_dense_over_best_cpu"] = d["value"] / best_cpu
             cpu["gpu_default_over_gpu_dense"] = value / d["value"]
             cpu["ratios"] = ("gpu_dense_over_cpu: hardware (the same dense algorithm on both; "
                              "gpu_dense_over_best_cpu against the fastest thread count measured); "

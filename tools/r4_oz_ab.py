@@ -3,6 +3,7 @@
 1000 x 1000 grid: ms per tick (HIP events of the sweep launch, sbo_profile),
 and the variance / mean error of each against the fp64 oracle given the
 device factor on a sample.  GPU diagnostic (tools/), one JSON line.
+OZ_KERNELS: the kernels (default "1 0"); TABLE_MB: SBO_OPT_TABLE_MB.
     python tools/r4_oz_ab.py [n] [sample]"""
 import ctypes
 import json
@@ -40,6 +41,8 @@ def main():
     t = lambda a: torch.tensor(f32(a), device=dev)  # noqa: E731
     res = {"n": n}
     kernels = [int(k) for k in os.environ.get("OZ_KERNELS", "1 0").split()]
+    if os.environ.get("TABLE_MB"):
+        gm.set_option(N.SBO_OPT_TABLE_MB, int(os.environ["TABLE_MB"]))
     for kernel in kernels:
         gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
         torch.cuda.synchronize()
