@@ -428,7 +428,8 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * f64 on the f64 matrix cores (v_mfma_f64_16x16x4_f64; predict_f64.hip).  All
  * meet the 1e-5 contract where the fast sweep cannot (SBO_OPT_PRECISION). */
 #define SBO_OPT_PRECISE_KERNEL 22
-/* SBO_OPT_TABLE_MB (default 2048): device memory budget, MiB, of the K* table
+/* SBO_OPT_TABLE_MB (default 0 = automatic: 1/32 of the free device memory,
+ * within [256 MiB, 8 GiB]): device memory budget, MiB, of the K* table
  * SBO_OPT_PRECISE_KERNEL 3 sweeps through (the queries run in chunks of as
  * many 128-query blocks as fit it; at least one). */
 #define SBO_OPT_TABLE_MB 23

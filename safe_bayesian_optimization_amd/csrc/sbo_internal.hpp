@@ -185,7 +185,7 @@ struct sbo_ctx {
     // locations (where the variance is smallest); each part's own normwise error
     double probe_err_grid = -1.0, probe_err_train = -1.0, probe_vmax_grid = 0.0, probe_vmax_train = 0.0;
     int probe_m_grid = 0, probe_m_train = 0;
-    int64_t table_mb = 2048;     // SBO_OPT_TABLE_MB: the K* table's memory budget (SBO_OPT_PRECISE_KERNEL 3)
+    int64_t table_mb = 0;        // SBO_OPT_TABLE_MB: the K* table's memory budget (SBO_OPT_PRECISE_KERNEL 3; 0: auto)
     int reprobe_pct = 25;        // SBO_OPT_REPROBE: appends re-probe once N grew by this share (0: every append)
     bool inv_batched = true;      // SBO_OPT_INV_LEAVES: the recursion's base cases in one batched dtrtri
     bool inv_leaves_done = false; // (set while a recursion runs whose base cases are already inverted)

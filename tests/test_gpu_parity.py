@@ -1411,7 +1411,7 @@ def test_kstar_table_chunks(mapper):
     try:
         gm.fit(wl.x, wl.y, wl.obs)
         res = {}
-        for kernel, mb, groups in ((1, 2048, 0), (3, 2048, 0), (3, 1, 0), (3, 1, 7), (3, 3, 1000)):
+        for kernel, mb, groups in ((1, 2048, 0), (3, 2048, 0), (3, 0, 0), (3, 1, 0), (3, 1, 7), (3, 3, 1000)):
             gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
             gm.set_option(N.SBO_OPT_TABLE_MB, mb)
             gm.set_option(N.SBO_OPT_SWEEP_GROUPS, groups)
@@ -1426,6 +1426,6 @@ def test_kstar_table_chunks(mapper):
         assert nrel(base[0], omu) < PRECISE_TOL[3][0] and nrel(base[1].astype(np.float64) ** 2, ovar) < PRECISE_TOL[3][1]
     finally:
         gm.set_option(N.SBO_OPT_SWEEP_GROUPS, 0)
-        gm.set_option(N.SBO_OPT_TABLE_MB, 2048)
+        gm.set_option(N.SBO_OPT_TABLE_MB, 0)
         gm.set_option(N.SBO_OPT_PRECISION, -1)
         gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 3)
