@@ -116,6 +116,13 @@ __global__ __launch_bounds__(256) void pack_operand_kernel(const T *__restrict__
 }
 
 // dst[i + j*ldd] = src[i + j*lds] (f32 -> f64), i < m, j < n; lower: zero above the diagonal.
+// out[j * stride] = (float)d[j]: a row of the f32 factor from an f64 vector
+__global__ void narrow_strided_kernel(const double *__restrict__ d, int64_t n, float *__restrict__ out,
+                                      int64_t stride) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) out[j * stride] = (float)d[j];
+}
+
 __global__ void widen_kernel(const float *__restrict__ src, int64_t lds, int64_t m, int lower,
                              double *__restrict__ dst, int64_t ldd) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2340,6 +2347,12 @@ hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n,
 
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out) {
     hipLaunchKernelGGL(narrow_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_narrow_strided(hipStream_t s, const double *d, int64_t n, float *out, int64_t stride) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(narrow_strided_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, n, out, stride);
     return hipGetLastError();
 }
 

@@ -67,6 +67,12 @@ sbo_status finish(sbo_ctx *ctx, uint32_t flags) {
 // always suffice.
 int64_t info_slots(int64_t n) { return std::max<int64_t>(64, n / 512 + 2); }
 
+// Appends of at most this many points solve their factor rows, extend the
+// inverse and update alpha by matrix-vector products with the kept f64
+// inverse (bandwidth-bound, one pass over its lower triangle per point);
+// larger batches use the blocked level-3 forms.
+constexpr int64_t kAppendInvRows = 8;
+
 // X = L^-1 in place for the lower-triangular f64 matrix at Li (column-major,
 // lda ld; its strictly upper part is zero), by the block recursion
 //     [A 0; B C]^-1 = [A^-1 0; -C^-1 B A^-1  C^-1].
@@ -563,9 +569,20 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)sbo::round_up(b, 256) * (size_t)ld));
             double *S = ctx->scratch.as<double>();
             const double zero = 0.0;
-            SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)b,
-                                   (rocblas_int)n_old, (rocblas_int)n_old, &one, T, (rocblas_int)ld, Li,
-                                   (rocblas_int)ld, &zero, S, (rocblas_int)b));
+            if (b <= kAppendInvRows) {
+                // row by row: S[r,:]^T = Li^T T[r,:]^T, one dtrmv over the
+                // lower triangle (the dgemm read the whole n_old^2 square)
+                for (int64_t r = 0; r < b; ++r) {
+                    SBO_BLAS(rocblas_dcopy(ctx->blas, (rocblas_int)n_old, T + r, (rocblas_int)ld, S + r, (rocblas_int)b));
+                    SBO_BLAS(rocblas_dtrmv(ctx->blas, rocblas_fill_lower, rocblas_operation_transpose,
+                                           rocblas_diagonal_non_unit, (rocblas_int)n_old, Li, (rocblas_int)ld, S + r,
+                                           (rocblas_int)b));
+                }
+            } else {
+                SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)b,
+                                       (rocblas_int)n_old, (rocblas_int)n_old, &one, T, (rocblas_int)ld, Li,
+                                       (rocblas_int)ld, &zero, S, (rocblas_int)b));
+            }
             SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)b,
                                    (rocblas_int)n_old, (rocblas_int)b, &minus_one, L22i, (rocblas_int)ld, S,
                                    (rocblas_int)b, &zero, T, (rocblas_int)ld));
@@ -610,8 +627,17 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         // only feed the coordinate pack: on aux_stream (blas_aux) beside the
         // operand pack, row sums and tile norms, which read only L^-1 (C4:
         // 0.75 ms off the fit's critical path).
-        SBO_HIP(ctx->alpha64.reserve(sizeof(double) * (size_t)std::max(npad, ld)));
-        double *d = ctx->alpha64.as<double>();
+        // An append of a few points updates alpha instead (z = L^-1 r kept from
+        // the last refresh): z's new entries are the inverse's new rows times
+        // r, and alpha += (new rows)^T z_new over all n -- two dgemv over b
+        // rows instead of two passes over the whole triangle (0.8 ms at C4).
+        const bool inc_alpha = incr && ctx->z_n == n_old && n - n_old <= kAppendInvRows;
+        SBO_HIP(grow_keep(ctx, ctx->alpha64, sizeof(double) * (size_t)std::max(npad, ld),
+                          inc_alpha ? sizeof(double) * (size_t)n_old : 0));
+        SBO_HIP(grow_keep(ctx, ctx->zvec, sizeof(double) * (size_t)std::max(npad, ld),
+                          inc_alpha ? sizeof(double) * (size_t)n_old : 0));
+        ctx->z_n = 0;
+        double *d = ctx->alpha64.as<double>(), *zv = ctx->zvec.as<double>();
         alpha_aux = ctx->blas_aux && ctx->aux_stream && ctx->ev_panel && ctx->ev_pack;
         hipStream_t sa = alpha_aux ? ctx->aux_stream : ctx->stream;
         rocblas_handle ha = alpha_aux ? ctx->blas_aux : ctx->blas;
@@ -619,11 +645,27 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             SBO_HIP(hipEventRecord(ctx->ev_panel, ctx->stream));
             SBO_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0));
         }
-        SBO_HIP(sbo::launch_widen_sub(sa, ctx->obs.as<float>(), ctx->hyper.prior_mean, n, d));
-        SBO_BLAS(rocblas_dtrmv(ha, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit,
-                               (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
-        SBO_BLAS(rocblas_dtrmv(ha, rocblas_fill_lower, rocblas_operation_transpose, rocblas_diagonal_non_unit,
-                               (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
+        if (inc_alpha) {
+            const int64_t b = n - n_old;
+            const double one = 1.0, zero = 0.0;
+            SBO_HIP(ctx->rvec.reserve(sizeof(double) * (size_t)n));
+            double *rv = ctx->rvec.as<double>();
+            SBO_HIP(sbo::launch_widen_sub(sa, ctx->obs.as<float>(), ctx->hyper.prior_mean, n, rv));
+            SBO_BLAS(rocblas_set_pointer_mode(ha, rocblas_pointer_mode_host));
+            SBO_BLAS(rocblas_dgemv(ha, rocblas_operation_none, (rocblas_int)b, (rocblas_int)n, &one, Li + n_old,
+                                   (rocblas_int)ld, rv, 1, &zero, zv + n_old, 1));
+            SBO_HIP(hipMemsetAsync(d + n_old, 0, sizeof(double) * (size_t)b, sa));
+            SBO_BLAS(rocblas_dgemv(ha, rocblas_operation_transpose, (rocblas_int)b, (rocblas_int)n, &one, Li + n_old,
+                                   (rocblas_int)ld, zv + n_old, 1, &one, d, 1));
+        } else {
+            SBO_HIP(sbo::launch_widen_sub(sa, ctx->obs.as<float>(), ctx->hyper.prior_mean, n, d));
+            SBO_BLAS(rocblas_dtrmv(ha, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit,
+                                   (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
+            SBO_HIP(hipMemcpyAsync(zv, d, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, sa));
+            SBO_BLAS(rocblas_dtrmv(ha, rocblas_fill_lower, rocblas_operation_transpose, rocblas_diagonal_non_unit,
+                                   (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
+        }
+        ctx->z_n = n;
         SBO_HIP(sbo::launch_narrow(sa, d, n, alpha));
         if (alpha_aux) SBO_HIP(hipEventRecord(ctx->ev_trail, ctx->aux_stream));
         ctx->a64_I0 = std::min(ctx->a64_I0, I0);
@@ -1677,9 +1719,24 @@ SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, cons
     SBO_HIP(sbo::launch_rbf_fill(ctx->stream, xs + n0, ys + n0, b, xs + n0, ys + n0, b, ld, ell, sf2, sn2, true, L22));
     const float one = 1.0f, minus_one = -1.0f;
     SBO_BLAS(rocblas_set_pointer_mode(ctx->blas, rocblas_pointer_mode_host));
-    SBO_BLAS(rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
-                           rocblas_diagonal_non_unit, (rocblas_int)b, (rocblas_int)n0, &one, L, (rocblas_int)ld, L21,
-                           (rocblas_int)ld));
+    if (ctx->inverse_bits == 64 && ctx->linv_n == n0 && b <= kAppendInvRows) {
+        // a few points (the node's one per change): L21 row by row from the
+        // kept f64 inverse, L21[r,:]^T = L11^-1 K21[r,:]^T, one dtrmv over its
+        // lower triangle per point, rounded to f32 once -- rocBLAS strsm ran
+        // the 1 x n0 solve as ~250 small launches (6.3 ms at C4)
+        SBO_HIP(ctx->rvec.reserve(sizeof(double) * (size_t)n0));
+        double *w = ctx->rvec.as<double>();
+        for (int64_t r = 0; r < b; ++r) {
+            SBO_HIP(sbo::launch_widen(ctx->stream, L21 + r, ld, 1, n0, false, w, 1));
+            SBO_BLAS(rocblas_dtrmv(ctx->blas, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit,
+                                   (rocblas_int)n0, ctx->Linv.as<double>(), (rocblas_int)ld, w, 1));
+            SBO_HIP(sbo::launch_narrow_strided(ctx->stream, w, n0, L21 + r, ld));
+        }
+    } else {
+        SBO_BLAS(rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
+                               rocblas_diagonal_non_unit, (rocblas_int)b, (rocblas_int)n0, &one, L, (rocblas_int)ld,
+                               L21, (rocblas_int)ld));
+    }
     // K22 -= L21 L21^T as a full b x b sgemm (rocBLAS's ssyrk ran its
     // small-n kernels at ~250 us here; the strict upper half it also writes
     // is never read), then the block's own factorization

@@ -174,6 +174,8 @@ struct sbo_ctx {
     sbo::DevBuf restage;         // the re-sort's staging copy of all points
     bool precise = false;        // the sweep ticks run in effect
     sbo::DevBuf alpha64;         // alpha from the f64 solve (length cap)
+    sbo::DevBuf zvec, rvec;      // z = L^-1 (y - m0) (f64, valid for z_n points: appends update alpha from it), r scratch
+    int64_t z_n = 0;
     sbo::DevBuf a64, kc64;       // f64 packed operand and coordinates, derived lazily
     sbo::DevBuf aoz, eoz, koz;   // int8 digit operand, its block exponents, coordinates (predict_oz.hip)
     sbo::DevBuf kzt;             // the int8 sweep's K* table of one chunk of query blocks (SBO_OPT_PRECISE_KERNEL 3)
@@ -349,6 +351,8 @@ hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb,
 // d = (double)in - v;  out = (float)d
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out);
+// out[j * stride] = (float)d[j], j < n
+hipError_t launch_narrow_strided(hipStream_t s, const double *d, int64_t n, float *out, int64_t stride);
 // row_l1[i] = sum_j |A_ij| over the packed operand (f64), rows of row blocks >= I0.
 hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t I0, double *row_l1);
 // Per k-tile bounding boxes of the (internally ordered) training points.

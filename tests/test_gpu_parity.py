@@ -990,6 +990,49 @@ def test_append_incremental_inverse(mapper):
     gm.set_option(N.SBO_OPT_RESORT, 25)
 
 
+def test_small_append_inverse_rows(mapper):
+    """Appends of at most 8 points (sbo_append's kAppendInvRows) take the
+    factor's new rows from the kept f64 inverse (one dtrmv per point instead
+    of rocBLAS strsm), extend the inverse by dtrmv and update alpha from the
+    kept z = L^-1 r; 9 points take the level-3 path.  After each: the new
+    factor rows equal K21 L11^-T solved in f64 from the device's own L11 (to
+    f32 rounding), alpha equals the f64 solve with the device factor, and the
+    posterior the oracle's -- through 1, 3, 8 and 9-point appends."""
+    from scipy.linalg import solve_triangular
+    wl = synthetic(1100, 30, 30, seed=41)
+    h = wl.hyper
+    gm = TerrainMapper(0, h, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_RESORT, 0)
+    try:
+        gm.fit(wl.x[:600], wl.y[:600], wl.obs[:600])
+        a = 600
+        for b in (1, 3, 8, 9, 1):
+            L_old, _ = gm.factor()
+            gm.append(wl.x[a:a + b], wl.y[a:a + b], wl.obs[a:a + b])
+            a += b
+            n = gm.n
+            L, alpha = gm.factor()
+            o = gm.order()
+            xs, ys = f32(wl.x)[o].astype(np.float64), f32(wl.y)[o].astype(np.float64)
+            n0 = n - b
+            assert np.array_equal(L[:n0, :n0], L_old)          # the leading block is untouched
+            K21 = h.sf2 * np.exp(-((xs[n0:, None] - xs[None, :n0]) ** 2 + (ys[n0:, None] - ys[None, :n0]) ** 2)
+                                 / (2 * h.length_scale ** 2))
+            L21_ref = solve_triangular(L[:n0, :n0].astype(np.float64), K21.T, lower=True).T
+            e21 = np.abs(L[n0:, :n0] - L21_ref).max() / np.abs(L21_ref).max()
+            r = f32(wl.obs)[o].astype(np.float64) - h.prior_mean
+            L64 = L.astype(np.float64)
+            a_ref = solve_triangular(L64.T, solve_triangular(L64, r, lower=True), lower=False)
+            ea = np.abs(alpha - a_ref).max() / np.abs(a_ref).max()
+            print(f"append {b}: factor rows {e21:.2e}, alpha {ea:.2e}")
+            assert e21 < 2e-6 and ea < 1e-5, (b, e21, ea)
+        mu, sd = gm.predict(wl.qx, wl.qy)
+        omu, ovar = oracle_given_factor(gm, wl)
+        assert nrel(mu, omu) < REL_TOL and nrel(sd.astype(np.float64) ** 2, ovar) < REL_TOL
+    finally:
+        gm.set_option(N.SBO_OPT_RESORT, 25)
+
+
 @pytest.mark.parametrize("n", [2049, 4100, 5000])
 def test_recursive_inverse_matches_dtrtri(mapper, n):
     """The fit's f64 L^-1 by the library's block recursion (SBO_OPT_INVERSE =
