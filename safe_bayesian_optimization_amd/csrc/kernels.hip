@@ -116,6 +116,24 @@ __global__ __launch_bounds__(256) void pack_operand_kernel(const T *__restrict__
 }
 
 // dst[i + j*ldd] = src[i + j*lds] (f32 -> f64), i < m, j < n; lower: zero above the diagonal.
+// out[r] = sum_c A[r + c * ld] x[c], c < n, for a few rows r of a column-major
+// f64 matrix (one workgroup per row; strided lanes, then a fixed-order tree:
+// deterministic) -- rocBLAS dgemv ran a 1 x 16384 strided row in ~300 us
+__global__ __launch_bounds__(256) void row_dot_kernel(const double *__restrict__ A, int64_t ld, int64_t n,
+                                                      const double *__restrict__ x, double *__restrict__ out) {
+    __shared__ double red[256];
+    const int64_t r = blockIdx.x;
+    double s = 0.0;
+    for (int64_t c = threadIdx.x; c < n; c += 256) s = fma(A[r + c * ld], x[c], s);
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o >= 1; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[r] = red[0];
+}
+
 // out[j * stride] = (float)d[j]: a row of the f32 factor from an f64 vector
 __global__ void narrow_strided_kernel(const double *__restrict__ d, int64_t n, float *__restrict__ out,
                                       int64_t stride) {
@@ -2347,6 +2365,13 @@ hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n,
 
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out) {
     hipLaunchKernelGGL(narrow_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_row_dot(hipStream_t s, const double *A, int64_t ld, int64_t rows, int64_t n, const double *x,
+                          double *out) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(row_dot_kernel, dim3((unsigned)rows), dim3(256), 0, s, A, ld, n, x, out);
     return hipGetLastError();
 }
 

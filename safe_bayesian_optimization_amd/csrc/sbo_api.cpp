@@ -647,13 +647,12 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         }
         if (inc_alpha) {
             const int64_t b = n - n_old;
-            const double one = 1.0, zero = 0.0;
+            const double one = 1.0;
             SBO_HIP(ctx->rvec.reserve(sizeof(double) * (size_t)n));
             double *rv = ctx->rvec.as<double>();
             SBO_HIP(sbo::launch_widen_sub(sa, ctx->obs.as<float>(), ctx->hyper.prior_mean, n, rv));
             SBO_BLAS(rocblas_set_pointer_mode(ha, rocblas_pointer_mode_host));
-            SBO_BLAS(rocblas_dgemv(ha, rocblas_operation_none, (rocblas_int)b, (rocblas_int)n, &one, Li + n_old,
-                                   (rocblas_int)ld, rv, 1, &zero, zv + n_old, 1));
+            SBO_HIP(sbo::launch_row_dot(sa, Li + n_old, ld, b, n, rv, zv + n_old));
             SBO_HIP(hipMemsetAsync(d + n_old, 0, sizeof(double) * (size_t)b, sa));
             SBO_BLAS(rocblas_dgemv(ha, rocblas_operation_transpose, (rocblas_int)b, (rocblas_int)n, &one, Li + n_old,
                                    (rocblas_int)ld, zv + n_old, 1, &one, d, 1));

@@ -351,6 +351,9 @@ hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb,
 // d = (double)in - v;  out = (float)d
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out);
+// out[r] = sum_c A[r + c ld] x[c] (c < n) for rows r < rows of a column-major f64 matrix
+hipError_t launch_row_dot(hipStream_t s, const double *A, int64_t ld, int64_t rows, int64_t n, const double *x,
+                          double *out);
 // out[j * stride] = (float)d[j], j < n
 hipError_t launch_narrow_strided(hipStream_t s, const double *d, int64_t n, float *out, int64_t stride);
 // row_l1[i] = sum_j |A_ij| over the packed operand (f64), rows of row blocks >= I0.
