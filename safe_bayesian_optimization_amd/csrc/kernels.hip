@@ -134,6 +134,14 @@ __global__ __launch_bounds__(256) void row_dot_kernel(const double *__restrict__
     if (threadIdx.x == 0) out[r] = red[0];
 }
 
+// out[i + j * ldo] = (float)d[i + j * ldd] (i < m, j = blockIdx.y)
+__global__ void narrow_2d_kernel(const double *__restrict__ d, int64_t ldd, int64_t m, float *__restrict__ out,
+                                 int64_t ldo) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t j = blockIdx.y;
+    if (i < m) out[i + j * ldo] = (float)d[i + j * ldd];
+}
+
 // out[j * stride] = (float)d[j]: a row of the f32 factor from an f64 vector
 __global__ void narrow_strided_kernel(const double *__restrict__ d, int64_t n, float *__restrict__ out,
                                       int64_t stride) {
@@ -2372,6 +2380,14 @@ hipError_t launch_row_dot(hipStream_t s, const double *A, int64_t ld, int64_t ro
                           double *out) {
     if (rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(row_dot_kernel, dim3((unsigned)rows), dim3(256), 0, s, A, ld, n, x, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_narrow_2d(hipStream_t s, const double *d, int64_t ldd, int64_t m, int64_t n, float *out,
+                            int64_t ldo) {
+    if (m <= 0 || n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(narrow_2d_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)n), dim3(256), 0, s, d, ldd, m,
+                       out, ldo);
     return hipGetLastError();
 }
 

@@ -67,11 +67,15 @@ sbo_status finish(sbo_ctx *ctx, uint32_t flags) {
 // always suffice.
 int64_t info_slots(int64_t n) { return std::max<int64_t>(64, n / 512 + 2); }
 
-// Appends of at most this many points solve their factor rows, extend the
-// inverse and update alpha by matrix-vector products with the kept f64
-// inverse (bandwidth-bound, one pass over its lower triangle per point);
-// larger batches use the blocked level-3 forms.
+// Appends of at most kAppendInvRows points solve their factor rows and extend
+// the inverse by matrix-vector products with the kept f64 inverse
+// (bandwidth-bound, one pass over its lower triangle per point); up to
+// kAppendInvGemm points the factor rows by one f64 GEMM with it (rocBLAS strsm
+// of a b x n block ran as hundreds of small launches); alpha is updated from
+// the kept z = L^-1 r up to kAppendInvGemm points too.  Larger batches: the
+// blocked level-3 forms.
 constexpr int64_t kAppendInvRows = 8;
+constexpr int64_t kAppendInvGemm = 256;
 
 // X = L^-1 in place for the lower-triangular f64 matrix at Li (column-major,
 // lda ld; its strictly upper part is zero), by the block recursion
@@ -631,7 +635,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         // the last refresh): z's new entries are the inverse's new rows times
         // r, and alpha += (new rows)^T z_new over all n -- two dgemv over b
         // rows instead of two passes over the whole triangle (0.8 ms at C4).
-        const bool inc_alpha = incr && ctx->z_n == n_old && n - n_old <= kAppendInvRows;
+        const bool inc_alpha = incr && ctx->z_n == n_old && n - n_old <= kAppendInvGemm;
         SBO_HIP(grow_keep(ctx, ctx->alpha64, sizeof(double) * (size_t)std::max(npad, ld),
                           inc_alpha ? sizeof(double) * (size_t)n_old : 0));
         SBO_HIP(grow_keep(ctx, ctx->zvec, sizeof(double) * (size_t)std::max(npad, ld),
@@ -1731,6 +1735,17 @@ SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, cons
                                    (rocblas_int)n0, ctx->Linv.as<double>(), (rocblas_int)ld, w, 1));
             SBO_HIP(sbo::launch_narrow_strided(ctx->stream, w, n0, L21 + r, ld));
         }
+    } else if (ctx->inverse_bits == 64 && ctx->linv_n == n0 && b <= kAppendInvGemm) {
+        // a batch: L21 = K21 L11^-T as one f64 GEMM with the kept inverse
+        // (its strict upper part is zero), rounded to f32 once
+        SBO_HIP(ctx->rvec.reserve(sizeof(double) * (size_t)n0 * (size_t)b * 2));
+        double *kw = ctx->rvec.as<double>(), *cw = kw + (size_t)n0 * (size_t)b;
+        const double done = 1.0, dzero = 0.0;
+        SBO_HIP(sbo::launch_widen(ctx->stream, L21, ld, b, n0, false, kw, b));
+        SBO_BLAS(rocblas_dgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)b,
+                               (rocblas_int)n0, (rocblas_int)n0, &done, kw, (rocblas_int)b, ctx->Linv.as<double>(),
+                               (rocblas_int)ld, &dzero, cw, (rocblas_int)b));
+        SBO_HIP(sbo::launch_narrow_2d(ctx->stream, cw, b, b, n0, L21, ld));
     } else {
         SBO_BLAS(rocblas_strsm(ctx->blas, rocblas_side_right, rocblas_fill_lower, rocblas_operation_transpose,
                                rocblas_diagonal_non_unit, (rocblas_int)b, (rocblas_int)n0, &one, L, (rocblas_int)ld,

@@ -354,6 +354,9 @@ hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out);
 // out[r] = sum_c A[r + c ld] x[c] (c < n) for rows r < rows of a column-major f64 matrix
 hipError_t launch_row_dot(hipStream_t s, const double *A, int64_t ld, int64_t rows, int64_t n, const double *x,
                           double *out);
+// out[i + j ldo] = (float)d[i + j ldd], i < m, j < n
+hipError_t launch_narrow_2d(hipStream_t s, const double *d, int64_t ldd, int64_t m, int64_t n, float *out,
+                            int64_t ldo);
 // out[j * stride] = (float)d[j], j < n
 hipError_t launch_narrow_strided(hipStream_t s, const double *d, int64_t n, float *out, int64_t stride);
 // row_l1[i] = sum_j |A_ij| over the packed operand (f64), rows of row blocks >= I0.

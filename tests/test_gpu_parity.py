@@ -993,11 +993,13 @@ def test_append_incremental_inverse(mapper):
 def test_small_append_inverse_rows(mapper):
     """Appends of at most 8 points (sbo_append's kAppendInvRows) take the
     factor's new rows from the kept f64 inverse (one dtrmv per point instead
-    of rocBLAS strsm), extend the inverse by dtrmv and update alpha from the
-    kept z = L^-1 r; 9 points take the level-3 path.  After each: the new
-    factor rows equal K21 L11^-T solved in f64 from the device's own L11 (to
-    f32 rounding), alpha equals the f64 solve with the device factor, and the
-    posterior the oracle's -- through 1, 3, 8 and 9-point appends."""
+    of rocBLAS strsm) and extend the inverse by dtrmv; up to 256 points
+    (kAppendInvGemm) the rows by one f64 GEMM with the inverse; alpha is
+    updated from the kept z = L^-1 r up to 256 points; 257 take the level-3
+    path.  After each: the leading block is untouched, the new factor rows
+    equal K21 L11^-T solved in f64 from the device's own L11 (to f32
+    rounding), alpha equals the f64 solve with the device factor, and the
+    posterior the oracle's -- through 1, 3, 8, 9, 200 and 257-point appends."""
     from scipy.linalg import solve_triangular
     wl = synthetic(1100, 30, 30, seed=41)
     h = wl.hyper
@@ -1006,7 +1008,7 @@ def test_small_append_inverse_rows(mapper):
     try:
         gm.fit(wl.x[:600], wl.y[:600], wl.obs[:600])
         a = 600
-        for b in (1, 3, 8, 9, 1):
+        for b in (1, 3, 8, 9, 200, 257, 1):
             L_old, _ = gm.factor()
             gm.append(wl.x[a:a + b], wl.y[a:a + b], wl.obs[a:a + b])
             a += b
