@@ -58,6 +58,7 @@ SBO_OPT_INV_LEAVES = 20
 SBO_OPT_REPROBE = 21
 SBO_OPT_PRECISE_KERNEL = 22
 SBO_OPT_TABLE_MB = 23
+SBO_OPT_INV_OZ = 24
 
 
 class SboError(RuntimeError):

@@ -1,0 +1,262 @@
+// ozgemm.hip -- an f64 GEMM emulated on the int8 matrix cores (Ozaki-style
+// slices), for the fit's f64 triangular inverse (SBO_OPT_INV_OZ, round 4).
+//
+// Why: the inverse's products are rocBLAS dgemms at 0.93 of the 78.6 TF f64
+// MFMA peak (~24 ms of the C4 fit, ~20 at the peak);
+// v_mfma_i32_16x16x64_i8 runs 2x the bf16 rate (5 POPS) and sums exactly.
+// C = alpha op(A) B, A (m x K) and B (K x n) column-major f64:
+//   each row of A and each column of B gets a power of two 2^e > 1.01 max|.|
+//   over its K entries and the integer X = rint(a 2^(8 ND - 1 - e)) (|X| <
+//   2^(8 ND - 1) / 1.01) cut into ND balanced base-256 digits (the bytes of X +
+//   0x80..80, less 128 but for the top one: every digit in [-128, 127]);
+//   level L = s + u < ND of the digit products (s of A, u of B) is summed
+//   EXACTLY in int32 over all K (at most ND pairs of 64 products of <= 2^14
+//   per MFMA, K <= 16384: < 2^31), the levels combined once per element in
+//   f64 at the end: C = alpha 2^(eA + eB - 8 ND - 6) sum_L l_L 256^(ND-1-L).
+// The dropped levels (s + u >= ND) and the rounding of X bound the error by
+// about ND K 2^(14 - 8 ND - 2) of K max|row| max|col| -- relative to the
+// row and column maxima, not to |A| |B| elementwise as a dgemm's is.
+//
+// Operand layout (gz_pack_kernel): rows of 16 (A's rows, B's columns) by
+// k-blocks of 64, [row block][k block][digit][1 KiB] with lane r + 16 g of a
+// 1 KiB piece holding row r's bytes k = 16 g .. 16 g + 15 -- the MFMA's
+// fragment order, so a stage is copied linearly by LDS-DMA and every operand
+// read is one conflict-free ds_read_b128.
+// GEMM (gz_gemm_kernel): workgroup = 128 rows of A x 64 columns of B, four
+// waves of 32 x 64 (two A blocks held in registers, the four B blocks loaded
+// in turn), ND x 8 int32 accumulator blocks per wave; a stage is one k-block
+// (12 ND KiB), double buffered, one barrier per k-block.  Lower-triangular
+// operands start / stop the k loop at the tile's diagonal.
+#include <cstdint>
+
+#include "sbo_internal.hpp"
+
+namespace sbo {
+namespace {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kGzTM = 128;   // rows of A per workgroup
+constexpr int kGzTN = 64;    // columns of B per workgroup
+constexpr int kGzBK = 64;    // k per stage
+constexpr int kGzMaxK = 16384;
+
+__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
+    return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+// One row block (16 rows) per workgroup: the rows' maxima over all K, then
+// their digits.  Row i's entry k is M[i + k ld] (ROWS_OF_COLMAJOR: the rows of
+// a column-major matrix, A) or M[k + i ld] (its columns, B); tri 1 keeps only
+// k <= i (A lower triangular), 2 only k >= i (B lower triangular).  Rows >=
+// rows and k >= K are zero.  ex[i]: the row's exponent (-900: all zero).
+template <int ND, bool ROWS_OF_COLMAJOR>
+__global__ __launch_bounds__(256) void gz_pack_kernel(const double *__restrict__ M, int64_t ld, int64_t rows,
+                                                      int64_t K, int Kb, int tri, char *__restrict__ out,
+                                                      int *__restrict__ ex) {
+    __shared__ double red[4][16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t rb = blockIdx.x;
+    const int64_t i = rb * 16 + r;
+    auto at = [&](int64_t k) -> double {
+        if (i >= rows || k >= K) return 0.0;
+        if ((tri == 1 && k > i) || (tri == 2 && k < i)) return 0.0;
+        return ROWS_OF_COLMAJOR ? M[i + k * ld] : M[k + i * ld];
+    };
+    double amax = 0.0;
+    for (int kb = wave; kb < Kb; kb += 4) {
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) amax = fmax(amax, fabs(at((int64_t)kb * kGzBK + 16 * g + jj)));
+    }
+    amax = fmax(amax, __shfl_xor(amax, 16));
+    amax = fmax(amax, __shfl_xor(amax, 32));
+    if (g == 0) red[wave][r] = amax;
+    __syncthreads();
+    amax = fmax(fmax(red[0][r], red[1][r]), fmax(red[2][r], red[3][r]));
+    int e = -900;
+    if (amax > 0.0) {
+        (void)frexp(amax * 1.01, &e);   // 2^e > 1.01 max: |a| 2^-e < 0.99
+    }
+    if (wave == 0 && g == 0) ex[i] = e;
+    constexpr int kBits = 8 * ND - 1;
+    // the bias: 0x80 in each of the ND - 1 lower bytes
+    constexpr int64_t kBias = (int64_t)(((uint64_t)1 << (8 * (ND - 1))) - 1) / 255 * 128;
+    for (int kb = wave; kb < Kb; kb += 4) {
+        uint32_t w[ND][4];
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const double a = at((int64_t)kb * kGzBK + 16 * g + jj);
+            const int64_t x = e > -900 ? (int64_t)rint(ldexp(a, kBits - e)) : 0;
+            const uint64_t y = (uint64_t)(x + kBias);
+#pragma unroll
+            for (int s = 0; s < ND; ++s) {
+                const uint32_t b = (uint32_t)(y >> (8 * (ND - 1 - s))) & 0xFFu;
+                const uint32_t d = s == 0 ? b : (b ^ 0x80u);
+                if ((jj & 3) == 0) w[s][jj >> 2] = d;
+                else w[s][jj >> 2] |= d << (8 * (jj & 3));
+            }
+        }
+        char *base = out + ((rb * Kb + kb) * ND) * 1024 + lane * 16;
+#pragma unroll
+        for (int s = 0; s < ND; ++s)
+            *reinterpret_cast<uint4 *>(base + s * 1024) = make_uint4(w[s][0], w[s][1], w[s][2], w[s][3]);
+    }
+}
+
+// C (m x n, ldc) = alpha A B (+ C when beta1) from the packed operands (A:
+// rows, B: columns, Kb k-blocks each).  triA: A lower triangular (a tile's k
+// loop stops after its last row's diagonal block); triB: B lower triangular
+// (starts at its first column's).
+template <int ND>
+__global__ __launch_bounds__(256, 1) void gz_gemm_kernel(const char *__restrict__ Ad, const int *__restrict__ eA,
+                                                         const char *__restrict__ Bd, const int *__restrict__ eB,
+                                                         int64_t m, int64_t n, int Kb, int tilesM, double *__restrict__ C,
+                                                         int64_t ldc, double alpha, int beta1, int triA, int triB) {
+    constexpr int kPieces = (kGzTM / 16 + kGzTN / 16) * ND;   // 1 KiB pieces per stage
+    constexpr int kStage = kPieces * 1024;
+    __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+    // consecutive workgroups walk down a column of tiles (B's columns stay in
+    // L2 across them); the XCD round robin spreads each column over the XCDs
+    const int tm = blockIdx.x % tilesM, tn = blockIdx.x / tilesM;
+    const int64_t i0 = (int64_t)tm * kGzTM, j0 = (int64_t)tn * kGzTN;
+    int kb0 = 0, kb1 = Kb;
+    if (triB) kb0 = (int)(j0 / kGzBK);
+    if (triA) kb1 = min(Kb, (int)((i0 + kGzTM - 1) / kGzBK) + 1);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+
+    typedef __attribute__((address_space(3))) char lds_char;
+    const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
+    const char *gA = Ad + (i0 / 16) * (int64_t)Kb * ND * 1024 + lane * 16;
+    const char *gB = Bd + (j0 / 16) * (int64_t)Kb * ND * 1024 + lane * 16;
+#define SBO_GZ_DMA16(gsrc, ldst)                                                                         \
+    do {                                                                                                 \
+        uint32_t keep_;                                                                                  \
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t" \
+                     "s_mov_b32 m0, %0"                                                                  \
+                     : "=&s"(keep_)                                                                      \
+                     : "v"(gsrc), "s"(ldst)                                                              \
+                     : "memory");                                                                        \
+    } while (0)
+    // stage k-block kb_ into buffer buf_: piece p = wave + 4 q; A's pieces
+    // first (row block p / ND, digit p % ND), then B's
+    auto stage = [&](int kb_, int buf_) {
+#pragma unroll
+        for (int q = 0; q < kPieces / 4; ++q) {
+            const int p = wave_u + 4 * q;
+            const int pa = p < (kGzTM / 16) * ND ? p : p - (kGzTM / 16) * ND;
+            const int blk = pa / ND, s = pa % ND;
+            const char *src = (p < (kGzTM / 16) * ND ? gA : gB) + ((int64_t)blk * Kb + kb_) * ND * 1024 + s * 1024;
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)(buf_ * kStage + p * 1024));
+            SBO_GZ_DMA16(src, dst);
+        }
+    };
+    static_assert(kPieces % 4 == 0, "whole pieces per wave");
+
+    i32x4 acc[2][kGzTN / 16][ND];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < kGzTN / 16; ++c)
+#pragma unroll
+            for (int L = 0; L < ND; ++L) acc[a][c][L] = i32x4{0, 0, 0, 0};
+
+    if (kb0 < kb1) {
+        stage(kb0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    int cur = 0;
+    for (int kb = kb0; kb < kb1; ++kb) {
+        if (kb + 1 < kb1) stage(kb + 1, cur ^ 1);
+        const i32x4 *sA = reinterpret_cast<const i32x4 *>(smem + cur * kStage) + lane;
+        const i32x4 *sB = sA + (kGzTM / 16) * ND * 64;
+        i32x4 ad[2][ND];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int s = 0; s < ND; ++s) ad[a][s] = sA[((2 * wave + a) * ND + s) * 64];
+#pragma unroll
+        for (int c = 0; c < kGzTN / 16; ++c) {
+            i32x4 bd[ND];
+#pragma unroll
+            for (int u = 0; u < ND; ++u) bd[u] = sB[(c * ND + u) * 64];
+#pragma unroll
+            for (int u = 0; u < ND; ++u)
+#pragma unroll
+                for (int s = 0; s + u < ND; ++s)
+#pragma unroll
+                    for (int a = 0; a < 2; ++a) acc[a][c][s + u] = mfma_i8(ad[a][s], bd[u], acc[a][c][s + u]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        cur ^= 1;
+    }
+#undef SBO_GZ_DMA16
+    // combine: lane l holds rows 4 (l >> 4) + v of each A block, column l & 15
+    // of each B block
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int c = 0; c < kGzTN / 16; ++c) {
+        const int64_t j = j0 + 16 * c + cl;
+        if (j >= n) continue;
+        const int ej = eB[j];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int64_t i = i0 + 32 * wave + 16 * a + 4 * g + v;
+                if (i >= m) continue;
+                double t = (double)acc[a][c][ND - 1][v];
+#pragma unroll
+                for (int L = ND - 2; L >= 0; --L)
+                    t = fma((double)acc[a][c][L][v], ldexp(1.0, 8 * (ND - 1 - L)), t);
+                const double val = alpha * ldexp(t, eA[i] + ej - 8 * ND - 6);
+                double *dst = C + i + j * ldc;
+                *dst = beta1 ? *dst + val : val;
+            }
+        }
+    }
+}
+
+template <int ND>
+hipError_t gz_run(hipStream_t s, const double *A, int64_t lda, int triA, const double *B, int64_t ldb, int triB,
+                  int64_t m, int64_t n, int64_t K, double alpha, bool beta1, double *C, int64_t ldc, char *ws) {
+    const int Kb = (int)((K + kGzBK - 1) / kGzBK);
+    const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, np = (n + kGzTN - 1) / kGzTN * kGzTN;
+    char *pa = ws;
+    char *pb = pa + mp * (int64_t)Kb * kGzBK * ND;
+    int *ea = reinterpret_cast<int *>(pb + np * (int64_t)Kb * kGzBK * ND);
+    int *eb = ea + mp;
+    hipLaunchKernelGGL((gz_pack_kernel<ND, true>), dim3((unsigned)(mp / 16)), dim3(256), 0, s, A, lda, m, K, Kb,
+                       triA ? 1 : 0, pa, ea);
+    hipLaunchKernelGGL((gz_pack_kernel<ND, false>), dim3((unsigned)(np / 16)), dim3(256), 0, s, B, ldb, n, K, Kb,
+                       triB ? 2 : 0, pb, eb);
+    const int tilesM = (int)(mp / kGzTM), tilesN = (int)(np / kGzTN);
+    hipLaunchKernelGGL((gz_gemm_kernel<ND>), dim3((unsigned)(tilesM * tilesN)), dim3(256), 0, s, pa, ea, pb, eb, m,
+                       n, Kb, tilesM, C, ldc, alpha, beta1 ? 1 : 0, triA, triB);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t gz_workspace_bytes(int64_t m, int64_t n, int64_t K, int nd) {
+    const int64_t Kp = (K + kGzBK - 1) / kGzBK * kGzBK;
+    const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, np = (n + kGzTN - 1) / kGzTN * kGzTN;
+    return (size_t)((mp + np) * Kp * nd + 4 * (mp + np)) + 256;
+}
+
+hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, int triA, const double *B,
+                          int64_t ldb, int triB, int64_t m, int64_t n, int64_t K, double alpha, bool beta1,
+                          double *C, int64_t ldc, char *ws) {
+    if (m <= 0 || n <= 0) return hipSuccess;
+    if (K <= 0 || K > kGzMaxK) return hipErrorInvalidValue;
+    switch (nd) {
+        case 5: return gz_run<5>(s, A, lda, triA, B, ldb, triB, m, n, K, alpha, beta1, C, ldc, ws);
+        case 6: return gz_run<6>(s, A, lda, triA, B, ldb, triB, m, n, K, alpha, beta1, C, ldc, ws);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace sbo

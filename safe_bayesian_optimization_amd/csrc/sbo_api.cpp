@@ -138,10 +138,18 @@ int64_t inverse_panel(const sbo_ctx *ctx, int64_t h) {
 }
 
 sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                              double *scr, int &slot, bool a_done = false) {
+                              double *scr, int &slot, bool a_done = false, bool oz = false) {
     const int64_t h = inverse_split(n, ctx->inv_base), m = n - h;
     if (!a_done)
         if (sbo_status st = inverse_lower_f64(ctx, hb, Li, h, ld, scr, slot); st != SBO_OK) return st;
+    if (oz) {   // S = L21 A^-1 in one sliced GEMM (A^-1 lower triangular)
+        hipStream_t st;
+        SBO_BLAS(rocblas_get_stream(hb, &st));
+        SBO_HIP(ctx->gzws.reserve(sbo::gz_workspace_bytes(m, h, h, ctx->inv_oz)));
+        SBO_HIP(sbo::launch_gz_gemm(st, ctx->inv_oz, Li + h, ld, 0, Li, ld, 1, m, h, h, 1.0, false, S, m,
+                                    ctx->gzws.as<char>()));
+        return SBO_OK;
+    }
     SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
     const double one = 1.0, zero = 0.0;
     const int64_t nb = inverse_panel(ctx, h);
@@ -156,11 +164,19 @@ sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64
 
 // C^-1 (recursion scratch scr; skipped when c_done), then X21 = -C^-1 S
 sbo_status inverse_second_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                               double *scr, int &slot, bool c_done = false) {
+                               double *scr, int &slot, bool c_done = false, bool oz = false) {
     const int64_t h = inverse_split(n, ctx->inv_base), m = n - h;
     double *B = Li + h, *C = Li + h + h * ld;
     if (!c_done)
         if (sbo_status st = inverse_lower_f64(ctx, hb, C, m, ld, scr, slot); st != SBO_OK) return st;
+    if (oz) {   // X21 = -C^-1 S in one sliced GEMM (C^-1 lower triangular)
+        hipStream_t st;
+        SBO_BLAS(rocblas_get_stream(hb, &st));
+        SBO_HIP(ctx->gzws.reserve(sbo::gz_workspace_bytes(m, h, m, ctx->inv_oz)));
+        SBO_HIP(sbo::launch_gz_gemm(st, ctx->inv_oz, C, ld, 1, S, m, 0, m, h, m, -1.0, false, B, ld,
+                                    ctx->gzws.as<char>()));
+        return SBO_OK;
+    }
     SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
     const double minus_one = -1.0, zero = 0.0;
     const int64_t nb = inverse_panel(ctx, h);
@@ -232,12 +248,15 @@ sbo_status inverse_lower_f64_par(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld
         return st;
     }
     SBO_HIP(hipEventRecord(ctx->ev_trail, ctx->aux_stream));
-    if (sbo_status st = inverse_first_half(ctx, ctx->blas, Li, n, ld, S, scrA, slot, true); st != SBO_OK) {
+    // SBO_OPT_INV_OZ: the two top-level products on the int8 matrix cores
+    // (both on `stream`, one workspace; K <= 16384)
+    const bool oz = ctx->inv_oz != 0 && h <= 16384 && m <= 16384;
+    if (sbo_status st = inverse_first_half(ctx, ctx->blas, Li, n, ld, S, scrA, slot, true, oz); st != SBO_OK) {
         (void)hipStreamSynchronize(ctx->aux_stream);
         return st;
     }
     SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
-    return inverse_second_half(ctx, ctx->blas, Li, n, ld, S, nullptr, slot, true);
+    return inverse_second_half(ctx, ctx->blas, Li, n, ld, S, nullptr, slot, true, oz);
 }
 
 sbo_status check_hyper(sbo_ctx *ctx, const sbo_hyper &h) {
@@ -2126,6 +2145,10 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
 #endif
             if ((ctx->precise_kernel == 0) != (value == 0)) ctx->a64_I0 = 0;   // the other operand: derive it all
             ctx->precise_kernel = (int)value;
+            return SBO_OK;
+        case SBO_OPT_INV_OZ:
+            SBO_CHECK(value == 0 || value == 5 || value == 6, SBO_E_INVAL, "SBO_OPT_INV_OZ must be 0, 5 or 6");
+            ctx->inv_oz = (int)value;
             return SBO_OK;
         case SBO_OPT_TABLE_MB:
             SBO_CHECK(value >= 0 && value <= (int64_t(1) << 20), SBO_E_INVAL,

@@ -111,6 +111,7 @@ struct sbo_ctx {
     hipEvent_t ev_half = nullptr, ev_inv = nullptr;
     int64_t inv_base = 2048;     // SBO_OPT_INV_BASE: dtrtri base case of the recursive inverse
     int64_t inv_panels = 16;     // SBO_OPT_INV_PANELS: dgemm panels per product of the recursion
+    int inv_oz = 0;              // SBO_OPT_INV_OZ: digits of the int8-sliced top-level products (0: dgemm)
     int64_t early_inv_n = 0;     // n of a factor whose inverse's first half is done (refresh_operand finishes it)
     int inv_slot = 0;            // info slots the first half used (1 .. inv_slot)
     std::string err;
@@ -178,6 +179,7 @@ struct sbo_ctx {
     int64_t z_n = 0;
     sbo::DevBuf a64, kc64;       // f64 packed operand and coordinates, derived lazily
     sbo::DevBuf aoz, eoz, koz;   // int8 digit operand, its block exponents, coordinates (predict_oz.hip)
+    sbo::DevBuf gzws;            // the int8-sliced GEMM's packed operands (SBO_OPT_INV_OZ)
     sbo::DevBuf kzt;             // the int8 sweep's K* table of one chunk of query blocks (SBO_OPT_PRECISE_KERNEL 3)
     int precise_kernel = 3;      // SBO_OPT_PRECISE_KERNEL: 0 the f64 MFMA sweep, 1 the int8 sliced sweep, 3 the same reading the K* table
     int64_t a64_I0 = 0;          // first row block whose precise operand (of precise_kernel) is stale
@@ -413,6 +415,14 @@ hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, con
 size_t oz_table_bytes(int64_t npad);
 hipError_t launch_kstar_table(hipStream_t s, const char *koz, const float *qx, const float *qy, int64_t m,
                               int64_t npad, double ell, int64_t nq, char *kzt);
+// The int8-sliced f64 GEMM (ozgemm.hip): C (m x n, ldc) = alpha A B (+ C when
+// beta1), A (m x K, lda) and B (K x n, ldb) column-major f64, triA / triB: the
+// operand is lower triangular (its upper part is not read); nd digits (5, 6);
+// K <= 16384; workspace of gz_workspace_bytes(m, n, K, nd).
+size_t gz_workspace_bytes(int64_t m, int64_t n, int64_t K, int nd);
+hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, int triA, const double *B,
+                          int64_t ldb, int triB, int64_t m, int64_t n, int64_t K, double alpha, bool beta1,
+                          double *C, int64_t ldc, char *ws);
 // Morton ordering of the queries (query_order.hip): workspace of
 // query_order_bytes(m); returns the permutation and the gathered coordinates
 // (all inside the workspace).

@@ -1081,6 +1081,46 @@ def test_recursive_inverse_matches_dtrtri(mapper, n):
     gm.set_option(N.SBO_OPT_INV_LEAVES, 1)
 
 
+@pytest.mark.skip(reason="SBO_OPT_INV_OZ awaits its first GPU validation")
+@pytest.mark.parametrize("digits", [5, 6])
+@pytest.mark.parametrize("n,box", [(4100, False), (5000, False), (3000, True)])
+def test_sliced_inverse(mapper, n, box, digits):
+    """SBO_OPT_INV_OZ = 5 / 6: the recursive inverse's two top-level products
+    (S = L21 A^-1, X21 = -C^-1 S) as the int8-sliced f64 GEMM
+    (csrc/ozgemm.hip; N = 4100 leaves a 4-row lower block: padded tiles):
+    L^-1 against the f64 triangular solve of the device factor, and the
+    posterior -- the fast sweep, and the precise int8 sweep on the lpsc box
+    (its contract's workload) -- against the fp64 oracle."""
+    from scipy.linalg import solve_triangular
+    from safe_bayesian_optimization_amd.terrain import synthetic_box
+    wl = synthetic_box(n, 40, 30, seed=n) if box else synthetic(n, 24, 20, seed=n + 7)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    gm.set_option(N.SBO_OPT_INV_OZ, digits)
+    try:
+        gm.fit(wl.x, wl.y, wl.obs)
+        L, _ = gm.factor()
+        A = np.zeros((n, n), np.float32)
+        gm.ctx.check(N.lib().sbo_get_inverse(gm.ctx.handle, A.ctypes.data))
+        ref = wl.hyper.sf2 * solve_triangular(L.astype(np.float64), np.eye(n), lower=True)
+        err = np.abs(np.tril(A) - ref).max() / np.abs(ref).max()
+        print(f"n={n} box={box} digits={digits}: L^-1 max rel err {err:.2e}")
+        assert err < 1e-6
+        assert not np.triu(A, 1).any()
+        for prec in ((0, 1) if box else (0,)):
+            gm.set_option(N.SBO_OPT_PRECISION, prec)
+            mu, sd = gm.predict(wl.qx, wl.qy)
+            omu, ovar = oracle_given_factor64(gm, wl) if prec else oracle_given_factor(gm, wl)
+            tmu, tvar = PRECISE_TOL[3] if prec else (REL_TOL, REL_TOL)
+            emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
+            print(f"  precision {prec}: mu {emu:.2e} var {evar:.2e}")
+            assert emu < tmu and evar < tvar
+    finally:
+        gm.set_option(N.SBO_OPT_INV_OZ, 0)
+        gm.set_option(N.SBO_OPT_PRECISION, -1)
+    with pytest.raises(N.SboError):
+        gm.set_option(N.SBO_OPT_INV_OZ, 7)
+
+
 @pytest.mark.parametrize("n", [4100, 5000])
 def test_inverse_overlap_is_bitwise(mapper, n):
     """SBO_OPT_INV_OVERLAP = R: the recursive inverse's first half runs beside

@@ -3,7 +3,8 @@
 1000 x 1000 grid: ms per tick (HIP events of the sweep launch, sbo_profile),
 and the variance / mean error of each against the fp64 oracle given the
 device factor on a sample.  GPU diagnostic (tools/), one JSON line.
-OZ_KERNELS: the kernels (default "1 0"); TABLE_MB: SBO_OPT_TABLE_MB.
+OZ_KERNELS: the kernels (default "1 0"); TABLE_MB: SBO_OPT_TABLE_MB; INV_OZ:
+SBO_OPT_INV_OZ (the fit's inverse by the int8-sliced GEMM).
     python tools/r4_oz_ab.py [n] [sample]"""
 import ctypes
 import json
@@ -43,6 +44,8 @@ def main():
     kernels = [int(k) for k in os.environ.get("OZ_KERNELS", "1 0").split()]
     if os.environ.get("TABLE_MB"):
         gm.set_option(N.SBO_OPT_TABLE_MB, int(os.environ["TABLE_MB"]))
+    if os.environ.get("INV_OZ"):
+        gm.set_option(N.SBO_OPT_INV_OZ, int(os.environ["INV_OZ"]))
     for kernel in kernels:
         gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
         torch.cuda.synchronize()
