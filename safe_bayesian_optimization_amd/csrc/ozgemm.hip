@@ -17,7 +17,7 @@
 // about ND K 2^(14 - 8 ND - 2) of K max|row| max|col| -- relative to the
 // row and column maxima, not to |A| |B| elementwise as a dgemm's is.
 //
-// Operand layout (gz_pack_kernel): rows of 16 (A's rows, B's columns) by
+// Operand layout (gz_max_kernel, gz_digits_kernel): rows of 16 (A's rows, B's columns) by
 // k-blocks of 64, [row block][k block][digit][1 KiB] with lane r + 16 g of a
 // 1 KiB piece holding row r's bytes k = 16 g .. 16 g + 15 -- the MFMA's
 // fragment order, so a stage is copied linearly by LDS-DMA and every operand
@@ -45,63 +45,85 @@ __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
     return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
 }
 
-// One row block (16 rows) per workgroup: the rows' maxima over all K, then
-// their digits.  Row i's entry k is M[i + k ld] (ROWS_OF_COLMAJOR: the rows of
-// a column-major matrix, A) or M[k + i ld] (its columns, B); tri 1 keeps only
-// k <= i (A lower triangular), 2 only k >= i (B lower triangular).  Rows >=
-// rows and k >= K are zero.  ex[i]: the row's exponent (-900: all zero).
-template <int ND, bool ROWS_OF_COLMAJOR>
-__global__ __launch_bounds__(256) void gz_pack_kernel(const double *__restrict__ M, int64_t ld, int64_t rows,
-                                                      int64_t K, int Kb, int tri, char *__restrict__ out,
-                                                      int *__restrict__ ex) {
+// Operand entry k of row i: M[i + k ld] (ROWS_OF_COLMAJOR: the rows of a
+// column-major matrix, A) or M[k + i ld] (its columns, B); tri 1 keeps only
+// k <= i (A lower triangular), 2 only k >= i (B lower triangular); rows >=
+// rows and k >= K are zero.
+template <bool ROWS_OF_COLMAJOR>
+__device__ __forceinline__ double gz_at(const double *__restrict__ M, int64_t ld, int64_t rows, int64_t K, int tri,
+                                        int64_t i, int64_t k) {
+    if (i >= rows || k >= K) return 0.0;
+    if ((tri == 1 && k > i) || (tri == 2 && k < i)) return 0.0;
+    return ROWS_OF_COLMAJOR ? M[i + k * ld] : M[k + i * ld];
+}
+
+// Pass 1: each row's max |entry| over a chunk of 1024 k (16 rows x 1024 k per
+// workgroup, grid = row blocks x chunks), combined across chunks by a 64-bit
+// atomic max on the (non-negative) double's bits.  rmax zeroed beforehand.
+template <bool ROWS_OF_COLMAJOR>
+__global__ __launch_bounds__(256) void gz_max_kernel(const double *__restrict__ M, int64_t ld, int64_t rows,
+                                                     int64_t K, int tri, unsigned long long *__restrict__ rmax) {
     __shared__ double red[4][16];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 15, g = lane >> 4;
-    const int64_t rb = blockIdx.x;
-    const int64_t i = rb * 16 + r;
-    auto at = [&](int64_t k) -> double {
-        if (i >= rows || k >= K) return 0.0;
-        if ((tri == 1 && k > i) || (tri == 2 && k < i)) return 0.0;
-        return ROWS_OF_COLMAJOR ? M[i + k * ld] : M[k + i * ld];
-    };
+    const int64_t i = (int64_t)blockIdx.x * 16 + r;
+    const int64_t k0 = (int64_t)blockIdx.y * 1024 + wave * 256 + g * 16;
     double amax = 0.0;
-    for (int kb = wave; kb < Kb; kb += 4) {
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) amax = fmax(amax, fabs(at((int64_t)kb * kGzBK + 16 * g + jj)));
-    }
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj)
+            amax = fmax(amax, fabs(gz_at<ROWS_OF_COLMAJOR>(M, ld, rows, K, tri, i, k0 + 64 * c + jj)));
     amax = fmax(amax, __shfl_xor(amax, 16));
     amax = fmax(amax, __shfl_xor(amax, 32));
     if (g == 0) red[wave][r] = amax;
     __syncthreads();
-    amax = fmax(fmax(red[0][r], red[1][r]), fmax(red[2][r], red[3][r]));
-    int e = -900;
-    if (amax > 0.0) {
-        (void)frexp(amax * 1.01, &e);   // 2^e > 1.01 max: |a| 2^-e < 0.99
+    if (wave == 0 && g == 0 && i < rows) {
+        amax = fmax(fmax(red[0][r], red[1][r]), fmax(red[2][r], red[3][r]));
+        if (amax > 0.0) atomicMax(rmax + i, (unsigned long long)__double_as_longlong(amax));
     }
-    if (wave == 0 && g == 0) ex[i] = e;
+}
+
+// Pass 2: the digits, 16 rows x 4 k-blocks per workgroup (one per wave; grid
+// = row blocks x ceil(Kb / 4)); thread (r, g) cuts row r's k = 16 g .. 16 g +
+// 15 of its k-block into ND bytes each and stores them as one 16-B word per
+// digit.  ex[i]: the row's exponent (-900: an all-zero row).
+template <int ND, bool ROWS_OF_COLMAJOR>
+__global__ __launch_bounds__(256) void gz_digits_kernel(const double *__restrict__ M, int64_t ld, int64_t rows,
+                                                        int64_t K, int Kb, int tri,
+                                                        const unsigned long long *__restrict__ rmax,
+                                                        char *__restrict__ out, int *__restrict__ ex) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t rb = blockIdx.x;
+    const int64_t i = rb * 16 + r;
+    const int kb = (int)blockIdx.y * 4 + wave;
+    const double amax = i < rows ? __longlong_as_double((long long)rmax[i]) : 0.0;
+    int e = -900;
+    if (amax > 0.0) (void)frexp(amax * 1.01, &e);   // 2^e > 1.01 max: |a| 2^-e < 0.99
+    if (blockIdx.y == 0 && wave == 0 && g == 0) ex[i] = e;
+    if (kb >= Kb) return;
     constexpr int kBits = 8 * ND - 1;
     // the bias: 0x80 in each of the ND - 1 lower bytes
     constexpr int64_t kBias = (int64_t)(((uint64_t)1 << (8 * (ND - 1))) - 1) / 255 * 128;
-    for (int kb = wave; kb < Kb; kb += 4) {
-        uint32_t w[ND][4];
+    uint32_t w[ND][4];
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-            const double a = at((int64_t)kb * kGzBK + 16 * g + jj);
-            const int64_t x = e > -900 ? (int64_t)rint(ldexp(a, kBits - e)) : 0;
-            const uint64_t y = (uint64_t)(x + kBias);
+    for (int jj = 0; jj < 16; ++jj) {
+        const double a = gz_at<ROWS_OF_COLMAJOR>(M, ld, rows, K, tri, i, (int64_t)kb * kGzBK + 16 * g + jj);
+        const int64_t x = e > -900 ? (int64_t)rint(ldexp(a, kBits - e)) : 0;
+        const uint64_t y = (uint64_t)(x + kBias);
 #pragma unroll
-            for (int s = 0; s < ND; ++s) {
-                const uint32_t b = (uint32_t)(y >> (8 * (ND - 1 - s))) & 0xFFu;
-                const uint32_t d = s == 0 ? b : (b ^ 0x80u);
-                if ((jj & 3) == 0) w[s][jj >> 2] = d;
-                else w[s][jj >> 2] |= d << (8 * (jj & 3));
-            }
+        for (int s = 0; s < ND; ++s) {
+            const uint32_t b = (uint32_t)(y >> (8 * (ND - 1 - s))) & 0xFFu;
+            const uint32_t d = s == 0 ? b : (b ^ 0x80u);
+            if ((jj & 3) == 0) w[s][jj >> 2] = d;
+            else w[s][jj >> 2] |= d << (8 * (jj & 3));
         }
-        char *base = out + ((rb * Kb + kb) * ND) * 1024 + lane * 16;
-#pragma unroll
-        for (int s = 0; s < ND; ++s)
-            *reinterpret_cast<uint4 *>(base + s * 1024) = make_uint4(w[s][0], w[s][1], w[s][2], w[s][3]);
     }
+    char *base = out + ((rb * Kb + kb) * ND) * 1024 + lane * 16;
+#pragma unroll
+    for (int s = 0; s < ND; ++s)
+        *reinterpret_cast<uint4 *>(base + s * 1024) = make_uint4(w[s][0], w[s][1], w[s][2], w[s][3]);
 }
 
 // C (m x n, ldc) = alpha A B (+ C when beta1) from the packed operands (A:
@@ -117,7 +139,9 @@ __global__ __launch_bounds__(256, 1) void gz_gemm_kernel(const char *__restrict_
     constexpr int kStage = kPieces * 1024;
     __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
     // consecutive workgroups walk down a column of tiles (B's columns stay in
-    // L2 across them); the XCD round robin spreads each column over the XCDs
+    // L2 across them); the XCD round robin spreads each column over the XCDs.
+    // (Longest tiles first for a triangular A measured slower: 7.3 -> 9.3 ms
+    // at 8192^3.)
     const int tm = blockIdx.x % tilesM, tn = blockIdx.x / tilesM;
     const int64_t i0 = (int64_t)tm * kGzTM, j0 = (int64_t)tn * kGzTN;
     int kb0 = 0, kb1 = Kb;
@@ -227,12 +251,21 @@ hipError_t gz_run(hipStream_t s, const double *A, int64_t lda, int triA, const d
     const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, np = (n + kGzTN - 1) / kGzTN * kGzTN;
     char *pa = ws;
     char *pb = pa + mp * (int64_t)Kb * kGzBK * ND;
-    int *ea = reinterpret_cast<int *>(pb + np * (int64_t)Kb * kGzBK * ND);
+    unsigned long long *ma = reinterpret_cast<unsigned long long *>(pb + np * (int64_t)Kb * kGzBK * ND);
+    unsigned long long *mb = ma + mp;
+    int *ea = reinterpret_cast<int *>(mb + np);
     int *eb = ea + mp;
-    hipLaunchKernelGGL((gz_pack_kernel<ND, true>), dim3((unsigned)(mp / 16)), dim3(256), 0, s, A, lda, m, K, Kb,
-                       triA ? 1 : 0, pa, ea);
-    hipLaunchKernelGGL((gz_pack_kernel<ND, false>), dim3((unsigned)(np / 16)), dim3(256), 0, s, B, ldb, n, K, Kb,
-                       triB ? 2 : 0, pb, eb);
+    hipError_t err = hipMemsetAsync(ma, 0, sizeof(unsigned long long) * (size_t)(mp + np), s);
+    if (err != hipSuccess) return err;
+    const unsigned chunks = (unsigned)((K + 1023) / 1024), kq = (unsigned)((Kb + 3) / 4);
+    hipLaunchKernelGGL((gz_max_kernel<true>), dim3((unsigned)(mp / 16), chunks), dim3(256), 0, s, A, lda, m, K,
+                       triA ? 1 : 0, ma);
+    hipLaunchKernelGGL((gz_max_kernel<false>), dim3((unsigned)(np / 16), chunks), dim3(256), 0, s, B, ldb, n, K,
+                       triB ? 2 : 0, mb);
+    hipLaunchKernelGGL((gz_digits_kernel<ND, true>), dim3((unsigned)(mp / 16), kq), dim3(256), 0, s, A, lda, m, K,
+                       Kb, triA ? 1 : 0, ma, pa, ea);
+    hipLaunchKernelGGL((gz_digits_kernel<ND, false>), dim3((unsigned)(np / 16), kq), dim3(256), 0, s, B, ldb, n, K,
+                       Kb, triB ? 2 : 0, mb, pb, eb);
     const int tilesM = (int)(mp / kGzTM), tilesN = (int)(np / kGzTN);
     hipLaunchKernelGGL((gz_gemm_kernel<ND>), dim3((unsigned)(tilesM * tilesN)), dim3(256), 0, s, pa, ea, pb, eb, m,
                        n, Kb, tilesM, C, ldc, alpha, beta1 ? 1 : 0, triA, triB);
@@ -244,7 +277,7 @@ hipError_t gz_run(hipStream_t s, const double *A, int64_t lda, int triA, const d
 size_t gz_workspace_bytes(int64_t m, int64_t n, int64_t K, int nd) {
     const int64_t Kp = (K + kGzBK - 1) / kGzBK * kGzBK;
     const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, np = (n + kGzTN - 1) / kGzTN * kGzTN;
-    return (size_t)((mp + np) * Kp * nd + 4 * (mp + np)) + 256;
+    return (size_t)((mp + np) * Kp * nd + 12 * (mp + np)) + 256;
 }
 
 hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, int triA, const double *B,
