@@ -433,13 +433,15 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * SBO_OPT_PRECISE_KERNEL 3 sweeps through (the queries run in chunks of as
  * many 128-query blocks as fit it; at least one). */
 #define SBO_OPT_TABLE_MB 23
-/* SBO_OPT_INV_OZ (default 0: rocBLAS dgemm; 5 or 6): the recursive f64
+/* SBO_OPT_INV_OZ (default 6; 5; 0: rocBLAS dgemm): the recursive f64
  * inverse's two top-level products (S = L21 A^-1, X21 = -C^-1 S; N <= 32768)
  * as an f64 GEMM emulated on the int8 matrix cores -- each row / column cut
  * into that many base-256 digits under its own power of two, the digit
  * products summed exactly in int32, combined in f64 (csrc/ozgemm.hip).  Its
  * error is relative to a row's and a column's largest entries (2^-40 / 2^-48
- * of them for 5 / 6 digits), not to each product's. */
+ * of them for 5 / 6 digits), not to each product's: six digits move the
+ * posterior by ~1e-7 against the dgemm fit, five by up to 4e-6 (not for the
+ * precise regime).  The SBO_OPT_INV_OVERLAP fit keeps the dgemm products. */
 #define SBO_OPT_INV_OZ 24
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 

@@ -65,6 +65,23 @@ __global__ __launch_bounds__(256) void gz_max_kernel(const double *__restrict__ 
                                                      int64_t K, int tri, unsigned long long *__restrict__ rmax) {
     __shared__ double red[4][16];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if constexpr (!ROWS_OF_COLMAJOR) {
+        // columns of M (k contiguous): each wave reads 4 of the 16 rows, a
+        // row's 1024 k as 16 coalesced 512-B wave loads
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t i = (int64_t)blockIdx.x * 16 + 4 * wave + q;
+            double amax = 0.0;
+#pragma unroll
+            for (int c = 0; c < 16; ++c)
+                amax = fmax(amax, fabs(gz_at<false>(M, ld, rows, K, tri, i, (int64_t)blockIdx.y * 1024 + 64 * c + lane)));
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) amax = fmax(amax, __shfl_xor(amax, o));
+            if (lane == 0 && i < rows && amax > 0.0)
+                atomicMax(rmax + i, (unsigned long long)__double_as_longlong(amax));
+        }
+        return;
+    }
     const int r = lane & 15, g = lane >> 4;
     const int64_t i = (int64_t)blockIdx.x * 16 + r;
     const int64_t k0 = (int64_t)blockIdx.y * 1024 + wave * 256 + g * 16;
@@ -102,14 +119,30 @@ __global__ __launch_bounds__(256) void gz_digits_kernel(const double *__restrict
     int e = -900;
     if (amax > 0.0) (void)frexp(amax * 1.01, &e);   // 2^e > 1.01 max: |a| 2^-e < 0.99
     if (blockIdx.y == 0 && wave == 0 && g == 0) ex[i] = e;
-    if (kb >= Kb) return;
     constexpr int kBits = 8 * ND - 1;
     // the bias: 0x80 in each of the ND - 1 lower bytes
     constexpr int64_t kBias = (int64_t)(((uint64_t)1 << (8 * (ND - 1))) - 1) / 255 * 128;
     uint32_t w[ND][4];
+    // columns of M (k contiguous): the workgroup's 16 rows x 256 k staged
+    // through LDS by coalesced wave loads (a row per wave load, rows padded
+    // to 257 doubles), then read back in the digit order
+    __shared__ double stage[ROWS_OF_COLMAJOR ? 1 : 16 * 257];
+    if constexpr (!ROWS_OF_COLMAJOR) {
+        const int64_t kbase = (int64_t)blockIdx.y * 4 * kGzBK;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rr = 4 * wave + q;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                stage[rr * 257 + 64 * c + lane] = gz_at<false>(M, ld, rows, K, tri, rb * 16 + rr, kbase + 64 * c + lane);
+        }
+    }
+    __syncthreads();
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) {
-        const double a = gz_at<ROWS_OF_COLMAJOR>(M, ld, rows, K, tri, i, (int64_t)kb * kGzBK + 16 * g + jj);
+        const double a = ROWS_OF_COLMAJOR
+                             ? gz_at<true>(M, ld, rows, K, tri, i, (int64_t)kb * kGzBK + 16 * g + jj)
+                             : stage[r * 257 + 64 * wave + 16 * g + jj];
         const int64_t x = e > -900 ? (int64_t)rint(ldexp(a, kBits - e)) : 0;
         const uint64_t y = (uint64_t)(x + kBias);
 #pragma unroll
@@ -120,6 +153,7 @@ __global__ __launch_bounds__(256) void gz_digits_kernel(const double *__restrict
             else w[s][jj >> 2] |= d << (8 * (jj & 3));
         }
     }
+    if (kb >= Kb) return;
     char *base = out + ((rb * Kb + kb) * ND) * 1024 + lane * 16;
 #pragma unroll
     for (int s = 0; s < ND; ++s)

@@ -111,7 +111,7 @@ struct sbo_ctx {
     hipEvent_t ev_half = nullptr, ev_inv = nullptr;
     int64_t inv_base = 2048;     // SBO_OPT_INV_BASE: dtrtri base case of the recursive inverse
     int64_t inv_panels = 16;     // SBO_OPT_INV_PANELS: dgemm panels per product of the recursion
-    int inv_oz = 0;              // SBO_OPT_INV_OZ: digits of the int8-sliced top-level products (0: dgemm)
+    int inv_oz = 6;              // SBO_OPT_INV_OZ: digits of the int8-sliced top-level products (0: dgemm)
     int64_t early_inv_n = 0;     // n of a factor whose inverse's first half is done (refresh_operand finishes it)
     int inv_slot = 0;            // info slots the first half used (1 .. inv_slot)
     std::string err;

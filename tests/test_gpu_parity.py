@@ -1097,6 +1097,7 @@ def test_sliced_inverse(mapper, n, box, digits):
     wl = synthetic_box(n, 40, 30, seed=n) if box else synthetic(n, 24, 20, seed=n + 7)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
     try:
+        gm.set_option(N.SBO_OPT_INV_OZ, 0)
         gm.fit(wl.x, wl.y, wl.obs)
         mu_ref, _ = gm.predict(wl.qx, wl.qy)
         gm.set_option(N.SBO_OPT_INV_OZ, digits)
@@ -1120,7 +1121,7 @@ def test_sliced_inverse(mapper, n, box, digits):
             if not prec:
                 assert nrel(mu, mu_ref.astype(np.float64)) < 1e-6
     finally:
-        gm.set_option(N.SBO_OPT_INV_OZ, 0)
+        gm.set_option(N.SBO_OPT_INV_OZ, 6)
         gm.set_option(N.SBO_OPT_PRECISION, -1)
     with pytest.raises(N.SboError):
         gm.set_option(N.SBO_OPT_INV_OZ, 7)
@@ -1130,9 +1131,11 @@ def test_sliced_inverse(mapper, n, box, digits):
 def test_inverse_overlap_is_bitwise(mapper, n):
     """SBO_OPT_INV_OVERLAP = R: the recursive inverse's first half runs beside
     the Cholesky's last steps on a CU-masked stream.  The inverse, alpha and
-    the posterior are bitwise those of the serial fit for every R; a NOT_SPD
-    fit with the overlap on reports the error and leaves the context usable."""
+    the posterior are bitwise those of the serial fit for every R (both with
+    the dgemm top-level products, SBO_OPT_INV_OZ 0); a NOT_SPD fit with the
+    overlap on reports the error and leaves the context usable."""
     wl = synthetic(n, 24, 20, seed=n + 11)
+    mapper.set_option(N.SBO_OPT_INV_OZ, 0)
     got = {}
     for ov in (0, 32, 128, 0):
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
@@ -1175,6 +1178,7 @@ def test_inverse_overlap_is_bitwise(mapper, n):
     assert nrel(mu3, omu) < REL_TOL and nrel(sd3.astype(np.float64) ** 2, ovar) < REL_TOL
     gm.set_option(N.SBO_OPT_CHOLESKY, 1)
     gm.set_option(N.SBO_OPT_INV_OVERLAP, 0)
+    gm.set_option(N.SBO_OPT_INV_OZ, 6)
 
 
 # ------------------------------------------------------ full-size properties
