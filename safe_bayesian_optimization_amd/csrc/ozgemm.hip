@@ -160,15 +160,18 @@ __global__ __launch_bounds__(256) void gz_digits_kernel(const double *__restrict
         *reinterpret_cast<uint4 *>(base + s * 1024) = make_uint4(w[s][0], w[s][1], w[s][2], w[s][3]);
 }
 
-// C (m x n, ldc) = alpha A B (+ C when beta1) from the packed operands (A:
-// rows, B: columns, Kb k-blocks each).  triA: A lower triangular (a tile's k
-// loop stops after its last row's diagonal block); triB: B lower triangular
-// (starts at its first column's).
+// C (m x n, ldc; transposed into C^T's storage with kGzTransC) = alpha op(A)
+// op(B) (+ C with kGzBeta1) from the packed operands (op(A)'s rows, op(B)'s
+// columns, Kb k-blocks each).  kGzTriA: op(A) lower triangular (a tile's k
+// loop stops after its last row's diagonal block); kGzTriBLower / Upper:
+// op(B) lower / upper triangular (the loop starts at the tile's first column's
+// diagonal block / stops after its last column's).
 template <int ND>
 __global__ __launch_bounds__(256, 1) void gz_gemm_kernel(const char *__restrict__ Ad, const int *__restrict__ eA,
                                                          const char *__restrict__ Bd, const int *__restrict__ eB,
                                                          int64_t m, int64_t n, int Kb, int tilesM, double *__restrict__ C,
-                                                         int64_t ldc, double alpha, int beta1, int triA, int triB) {
+                                                         int64_t ldc, double alpha, unsigned flags) {
+    const bool triA = flags & kGzTriA, beta1 = flags & kGzBeta1, transC = flags & kGzTransC;
     constexpr int kPieces = (kGzTM / 16 + kGzTN / 16) * ND;   // 1 KiB pieces per stage
     constexpr int kStage = kPieces * 1024;
     __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
@@ -176,11 +179,15 @@ __global__ __launch_bounds__(256, 1) void gz_gemm_kernel(const char *__restrict_
     // L2 across them); the XCD round robin spreads each column over the XCDs.
     // (Longest tiles first for a triangular A measured slower: 7.3 -> 9.3 ms
     // at 8192^3.)
-    const int tm = blockIdx.x % tilesM, tn = blockIdx.x / tilesM;
+    // An upper-triangular op(B): its longest columns (the last) first
+    const int tilesN = (int)(gridDim.x / tilesM);
+    const int tm = blockIdx.x % tilesM;
+    const int tn = (flags & kGzTriBUpper) ? tilesN - 1 - (int)(blockIdx.x / tilesM) : (int)(blockIdx.x / tilesM);
     const int64_t i0 = (int64_t)tm * kGzTM, j0 = (int64_t)tn * kGzTN;
     int kb0 = 0, kb1 = Kb;
-    if (triB) kb0 = (int)(j0 / kGzBK);
-    if (triA) kb1 = min(Kb, (int)((i0 + kGzTM - 1) / kGzBK) + 1);
+    if (flags & kGzTriBLower) kb0 = (int)(j0 / kGzBK);
+    if (flags & kGzTriBUpper) kb1 = min(Kb, (int)((j0 + kGzTN - 1) / kGzBK) + 1);
+    if (triA) kb1 = min(kb1, (int)((i0 + kGzTM - 1) / kGzBK) + 1);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
 
@@ -271,7 +278,7 @@ __global__ __launch_bounds__(256, 1) void gz_gemm_kernel(const char *__restrict_
                 for (int L = ND - 2; L >= 0; --L)
                     t = fma((double)acc[a][c][L][v], ldexp(1.0, 8 * (ND - 1 - L)), t);
                 const double val = alpha * ldexp(t, eA[i] + ej - 8 * ND - 6);
-                double *dst = C + i + j * ldc;
+                double *dst = transC ? C + j + i * ldc : C + i + j * ldc;
                 *dst = beta1 ? *dst + val : val;
             }
         }
@@ -279,8 +286,8 @@ __global__ __launch_bounds__(256, 1) void gz_gemm_kernel(const char *__restrict_
 }
 
 template <int ND>
-hipError_t gz_run(hipStream_t s, const double *A, int64_t lda, int triA, const double *B, int64_t ldb, int triB,
-                  int64_t m, int64_t n, int64_t K, double alpha, bool beta1, double *C, int64_t ldc, char *ws) {
+hipError_t gz_run(hipStream_t s, const double *A, int64_t lda, const double *B, int64_t ldb, int64_t m, int64_t n,
+                  int64_t K, double alpha, double *C, int64_t ldc, unsigned flags, char *ws) {
     const int Kb = (int)((K + kGzBK - 1) / kGzBK);
     const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, np = (n + kGzTN - 1) / kGzTN * kGzTN;
     char *pa = ws;
@@ -292,17 +299,30 @@ hipError_t gz_run(hipStream_t s, const double *A, int64_t lda, int triA, const d
     hipError_t err = hipMemsetAsync(ma, 0, sizeof(unsigned long long) * (size_t)(mp + np), s);
     if (err != hipSuccess) return err;
     const unsigned chunks = (unsigned)((K + 1023) / 1024), kq = (unsigned)((Kb + 3) / 4);
-    hipLaunchKernelGGL((gz_max_kernel<true>), dim3((unsigned)(mp / 16), chunks), dim3(256), 0, s, A, lda, m, K,
-                       triA ? 1 : 0, ma);
-    hipLaunchKernelGGL((gz_max_kernel<false>), dim3((unsigned)(np / 16), chunks), dim3(256), 0, s, B, ldb, n, K,
-                       triB ? 2 : 0, mb);
-    hipLaunchKernelGGL((gz_digits_kernel<ND, true>), dim3((unsigned)(mp / 16), kq), dim3(256), 0, s, A, lda, m, K,
-                       Kb, triA ? 1 : 0, ma, pa, ea);
-    hipLaunchKernelGGL((gz_digits_kernel<ND, false>), dim3((unsigned)(np / 16), kq), dim3(256), 0, s, B, ldb, n, K,
-                       Kb, triB ? 2 : 0, mb, pb, eb);
+    // the rows of op(A) and the columns of op(B): rows of a column-major
+    // matrix (strided k) or its columns (contiguous k); pack masks 1: k <= row,
+    // 2: k >= row
+    const int ta = (flags & kGzTriA) ? 1 : 0;
+    const int tb = (flags & kGzTriBLower) ? 2 : (flags & kGzTriBUpper) ? 1 : 0;
+    const dim3 ga((unsigned)(mp / 16), chunks), gb((unsigned)(np / 16), chunks);
+    const dim3 da((unsigned)(mp / 16), kq), db((unsigned)(np / 16), kq);
+    if (flags & kGzTransA) {
+        hipLaunchKernelGGL((gz_max_kernel<false>), ga, dim3(256), 0, s, A, lda, m, K, ta, ma);
+        hipLaunchKernelGGL((gz_digits_kernel<ND, false>), da, dim3(256), 0, s, A, lda, m, K, Kb, ta, ma, pa, ea);
+    } else {
+        hipLaunchKernelGGL((gz_max_kernel<true>), ga, dim3(256), 0, s, A, lda, m, K, ta, ma);
+        hipLaunchKernelGGL((gz_digits_kernel<ND, true>), da, dim3(256), 0, s, A, lda, m, K, Kb, ta, ma, pa, ea);
+    }
+    if (flags & kGzTransB) {
+        hipLaunchKernelGGL((gz_max_kernel<true>), gb, dim3(256), 0, s, B, ldb, n, K, tb, mb);
+        hipLaunchKernelGGL((gz_digits_kernel<ND, true>), db, dim3(256), 0, s, B, ldb, n, K, Kb, tb, mb, pb, eb);
+    } else {
+        hipLaunchKernelGGL((gz_max_kernel<false>), gb, dim3(256), 0, s, B, ldb, n, K, tb, mb);
+        hipLaunchKernelGGL((gz_digits_kernel<ND, false>), db, dim3(256), 0, s, B, ldb, n, K, Kb, tb, mb, pb, eb);
+    }
     const int tilesM = (int)(mp / kGzTM), tilesN = (int)(np / kGzTN);
     hipLaunchKernelGGL((gz_gemm_kernel<ND>), dim3((unsigned)(tilesM * tilesN)), dim3(256), 0, s, pa, ea, pb, eb, m,
-                       n, Kb, tilesM, C, ldc, alpha, beta1 ? 1 : 0, triA, triB);
+                       n, Kb, tilesM, C, ldc, alpha, flags);
     return hipGetLastError();
 }
 
@@ -314,14 +334,14 @@ size_t gz_workspace_bytes(int64_t m, int64_t n, int64_t K, int nd) {
     return (size_t)((mp + np) * Kp * nd + 12 * (mp + np)) + 256;
 }
 
-hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, int triA, const double *B,
-                          int64_t ldb, int triB, int64_t m, int64_t n, int64_t K, double alpha, bool beta1,
-                          double *C, int64_t ldc, char *ws) {
+hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, const double *B, int64_t ldb,
+                          int64_t m, int64_t n, int64_t K, double alpha, double *C, int64_t ldc, unsigned flags,
+                          char *ws) {
     if (m <= 0 || n <= 0) return hipSuccess;
     if (K <= 0 || K > kGzMaxK) return hipErrorInvalidValue;
     switch (nd) {
-        case 5: return gz_run<5>(s, A, lda, triA, B, ldb, triB, m, n, K, alpha, beta1, C, ldc, ws);
-        case 6: return gz_run<6>(s, A, lda, triA, B, ldb, triB, m, n, K, alpha, beta1, C, ldc, ws);
+        case 5: return gz_run<5>(s, A, lda, B, ldb, m, n, K, alpha, C, ldc, flags, ws);
+        case 6: return gz_run<6>(s, A, lda, B, ldb, m, n, K, alpha, C, ldc, flags, ws);
         default: return hipErrorInvalidValue;
     }
 }

@@ -415,14 +415,23 @@ hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, con
 size_t oz_table_bytes(int64_t npad);
 hipError_t launch_kstar_table(hipStream_t s, const char *koz, const float *qx, const float *qy, int64_t m,
                               int64_t npad, double ell, int64_t nq, char *kzt);
-// The int8-sliced f64 GEMM (ozgemm.hip): C (m x n, ldc) = alpha A B (+ C when
-// beta1), A (m x K, lda) and B (K x n, ldb) column-major f64, triA / triB: the
-// operand is lower triangular (its upper part is not read); nd digits (5, 6);
-// K <= 16384; workspace of gz_workspace_bytes(m, n, K, nd).
+// The int8-sliced f64 GEMM (ozgemm.hip): C (m x n, ldc) = alpha op(A) op(B)
+// (+ C), column-major f64, op(A) m x K (A itself K x m with kGzTransA), op(B)
+// K x n (n x K with kGzTransB); a triangular operand's zero part is not read;
+// kGzTransC stores C^T (C then points at n x m storage, ldc its leading
+// dimension); nd digits (5, 6); K <= 16384; workspace of
+// gz_workspace_bytes(m, n, K, nd).
+constexpr unsigned kGzTriA = 1;        // op(A) lower triangular: a_ik = 0 for k > i
+constexpr unsigned kGzTransA = 2;
+constexpr unsigned kGzTriBLower = 4;   // op(B) lower triangular: b_kj = 0 for k < j
+constexpr unsigned kGzTriBUpper = 8;   // op(B) upper triangular: b_kj = 0 for k > j
+constexpr unsigned kGzTransB = 16;
+constexpr unsigned kGzTransC = 32;
+constexpr unsigned kGzBeta1 = 64;      // C += instead of C =
 size_t gz_workspace_bytes(int64_t m, int64_t n, int64_t K, int nd);
-hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, int triA, const double *B,
-                          int64_t ldb, int triB, int64_t m, int64_t n, int64_t K, double alpha, bool beta1,
-                          double *C, int64_t ldc, char *ws);
+hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, const double *B, int64_t ldb,
+                          int64_t m, int64_t n, int64_t K, double alpha, double *C, int64_t ldc, unsigned flags,
+                          char *ws);
 // Morton ordering of the queries (query_order.hip): workspace of
 // query_order_bytes(m); returns the permutation and the gathered coordinates
 // (all inside the workspace).

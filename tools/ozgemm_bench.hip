@@ -10,11 +10,12 @@
 // Build: make -C safe_bayesian_optimization_amd build/ozgemm.o, then
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I safe_bayesian_optimization_amd/csrc \
 //     tools/ozgemm_bench.hip safe_bayesian_optimization_amd/build/ozgemm.o -lrocsolver -lrocblas -o lib/ozgemm_bench
-// Usage: lib/ozgemm_bench N xw yw ell nd reps
+// Usage: lib/ozgemm_bench N xw yw ell nd reps [p2_transposed 1|0]
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -48,6 +49,7 @@ int main(int argc, char **argv) {
     const double ell = argc > 4 ? std::atof(argv[4]) : 0.4;
     const int nd = argc > 5 ? std::atoi(argv[5]) : 6;
     const int reps = argc > 6 ? std::atoi(argv[6]) : 5;
+    const int tr = argc > 7 ? std::atoi(argv[7]) : 1;   // P2 in the transposed form (1) or directly (0)
     const int64_t h = N / 2, m = N - h;
     std::vector<double> hx(N), hy(N);
     uint64_t st = 0x9E3779B97F4A7C15ull;
@@ -94,7 +96,7 @@ int main(int argc, char **argv) {
     const double one = 1.0, zero = 0.0, mone = -1.0;
     const double *L21 = L + h, *Li11 = Li, *Li22 = Li + h + h * N, *Li21 = Li + h;
     char *ws;
-    const size_t wsb = sbo::gz_workspace_bytes(m, h, h, nd);
+    const size_t wsb = std::max(sbo::gz_workspace_bytes(m, h, h, nd), sbo::gz_workspace_bytes(h, m, m, nd));
     CK(hipMalloc(&ws, wsb));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -110,10 +112,14 @@ int main(int argc, char **argv) {
                          &mone, Li22, (rocblas_int)N, S1, (rocblas_int)m, &zero, X1, (rocblas_int)m));
         CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&t, e0, e1)); t_d2 = std::min(t_d2, t);
         CK(hipEventRecord(e0, 0));
-        CK(sbo::launch_gz_gemm(0, nd, L21, N, 0, Li11, N, 1, m, h, h, 1.0, false, S2, m, ws));
+        CK(sbo::launch_gz_gemm(0, nd, L21, N, Li11, N, m, h, h, 1.0, S2, m, sbo::kGzTriBLower, ws));
         CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&t, e0, e1)); t_z1 = std::min(t_z1, t);
         CK(hipEventRecord(e0, 0));
-        CK(sbo::launch_gz_gemm(0, nd, Li22, N, 1, S2, m, 0, m, h, m, -1.0, false, X2, m, ws));
+        if (tr)   // X^T = -S^T Li22^T, stored transposed into X (the library's form)
+            CK(sbo::launch_gz_gemm(0, nd, S2, m, Li22, N, h, m, m, -1.0, X2, m,
+                                   sbo::kGzTransA | sbo::kGzTransB | sbo::kGzTriBUpper | sbo::kGzTransC, ws));
+        else
+            CK(sbo::launch_gz_gemm(0, nd, Li22, N, S2, m, m, h, m, -1.0, X2, m, sbo::kGzTriA, ws));
         CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&t, e0, e1)); t_z2 = std::min(t_z2, t);
     }
     // errors against dtrtri's Li21 (host)
@@ -138,8 +144,9 @@ int main(int argc, char **argv) {
     const double fl1 = (double)m * h * h, fl2 = (double)m * h * m;   // 2 m h K / 2 (triangular)
     std::printf("  P1 S = L21 Li11 (%lld x %lld x %lld, tri B): dgemm %.3f ms (%.1f TF useful), sliced %.3f ms (%.1f TF)\n",
                 (long long)m, (long long)h, (long long)h, t_d1, fl1 / t_d1 * 1e-9, t_z1, fl1 / t_z1 * 1e-9);
-    std::printf("  P2 X = -Li22 S (%lld x %lld x %lld, tri A): dgemm %.3f ms (%.1f TF useful), sliced %.3f ms (%.1f TF)\n",
-                (long long)m, (long long)h, (long long)m, t_d2, fl2 / t_d2 * 1e-9, t_z2, fl2 / t_z2 * 1e-9);
+    std::printf("  P2 X = -Li22 S (%lld x %lld x %lld, %s): dgemm %.3f ms (%.1f TF useful), sliced %.3f ms (%.1f TF)\n",
+                (long long)m, (long long)h, (long long)m, tr ? "as X^T = -S^T Li22^T" : "tri A", t_d2, fl2 / t_d2 * 1e-9,
+                t_z2, fl2 / t_z2 * 1e-9);
     report("S sliced vs dgemm", s2, s1);
     report("X dgemm vs dtrtri", a, ref);
     report("X sliced vs dtrtri", b, ref);
