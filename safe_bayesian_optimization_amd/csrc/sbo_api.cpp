@@ -123,7 +123,14 @@ int inverse_base_cases(int64_t n, int64_t base) {
 }
 
 sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                             int &slot);
+                             int &slot, sbo::DevBuf *ozws = nullptr);
+// SBO_OPT_INV_OZ: a level of the recursion whose split is at least
+// kInvOzMinSplit runs its two products as the sliced GEMM (K <= 16384); the
+// 2048 level's products stay dgemms
+constexpr int64_t kInvOzMinSplit = 4096;
+bool oz_level(const sbo_ctx *ctx, int64_t h, int64_t m) {
+    return ctx->inv_oz != 0 && h >= kInvOzMinSplit && h <= 16384 && m <= 16384;
+}
 
 // A^-1 (recursion scratch scr), then S = B A^-1
 // dgemm panel width of a product of the recursion at split h: h / panels,
@@ -138,16 +145,16 @@ int64_t inverse_panel(const sbo_ctx *ctx, int64_t h) {
 }
 
 sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                              double *scr, int &slot, bool a_done = false, bool oz = false) {
+                              double *scr, int &slot, bool a_done = false, sbo::DevBuf *ozws = nullptr) {
     const int64_t h = inverse_split(n, ctx->inv_base), m = n - h;
     if (!a_done)
-        if (sbo_status st = inverse_lower_f64(ctx, hb, Li, h, ld, scr, slot); st != SBO_OK) return st;
-    if (oz) {   // S = L21 A^-1 in one sliced GEMM (A^-1 lower triangular)
+        if (sbo_status st = inverse_lower_f64(ctx, hb, Li, h, ld, scr, slot, ozws); st != SBO_OK) return st;
+    if (ozws && oz_level(ctx, h, m)) {   // S = L21 A^-1 in one sliced GEMM (A^-1 lower triangular)
         hipStream_t st;
         SBO_BLAS(rocblas_get_stream(hb, &st));
-        SBO_HIP(ctx->gzws.reserve(sbo::gz_workspace_bytes(m, h, h, ctx->inv_oz)));
+        SBO_HIP(ozws->reserve(sbo::gz_workspace_bytes(m, h, h, ctx->inv_oz)));
         SBO_HIP(sbo::launch_gz_gemm(st, ctx->inv_oz, Li + h, ld, Li, ld, m, h, h, 1.0, S, m, sbo::kGzTriBLower,
-                                    ctx->gzws.as<char>()));
+                                    ozws->as<char>()));
         return SBO_OK;
     }
     SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
@@ -164,22 +171,22 @@ sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64
 
 // C^-1 (recursion scratch scr; skipped when c_done), then X21 = -C^-1 S
 sbo_status inverse_second_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                               double *scr, int &slot, bool c_done = false, bool oz = false) {
+                               double *scr, int &slot, bool c_done = false, sbo::DevBuf *ozws = nullptr) {
     const int64_t h = inverse_split(n, ctx->inv_base), m = n - h;
     double *B = Li + h, *C = Li + h + h * ld;
     if (!c_done)
-        if (sbo_status st = inverse_lower_f64(ctx, hb, C, m, ld, scr, slot); st != SBO_OK) return st;
-    if (oz) {
+        if (sbo_status st = inverse_lower_f64(ctx, hb, C, m, ld, scr, slot, ozws); st != SBO_OK) return st;
+    if (ozws && oz_level(ctx, h, m)) {
         // X21 = -C^-1 S in one sliced GEMM, as X21^T = -S^T C^-T: the
         // triangular operand then bounds the k loop per column tile, so the
         // workgroups of one column run in step as in S = L21 A^-1 (the direct
         // form, C^-1 as a lower-triangular op(A): 7.4 vs 5.x ms at C4)
         hipStream_t st;
         SBO_BLAS(rocblas_get_stream(hb, &st));
-        SBO_HIP(ctx->gzws.reserve(sbo::gz_workspace_bytes(h, m, m, ctx->inv_oz)));
+        SBO_HIP(ozws->reserve(sbo::gz_workspace_bytes(h, m, m, ctx->inv_oz)));
         SBO_HIP(sbo::launch_gz_gemm(st, ctx->inv_oz, S, m, C, ld, h, m, m, -1.0, B, ld,
                                     sbo::kGzTransA | sbo::kGzTransB | sbo::kGzTriBUpper | sbo::kGzTransC,
-                                    ctx->gzws.as<char>()));
+                                    ozws->as<char>()));
         return SBO_OK;
     }
     SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
@@ -195,7 +202,7 @@ sbo_status inverse_second_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int6
 }
 
 sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
-                             int &slot) {
+                             int &slot, sbo::DevBuf *ozws) {
     if (n <= ctx->inv_base) {
         rocblas_int *info = ctx->info.as<rocblas_int>() + 1 + slot++;
         if (!ctx->inv_leaves_done)
@@ -204,8 +211,9 @@ sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_
         return SBO_OK;
     }
     const int64_t h = inverse_split(n, ctx->inv_base), m = n - h;
-    if (sbo_status st = inverse_first_half(ctx, hb, Li, n, ld, S, S + h * m, slot); st != SBO_OK) return st;
-    return inverse_second_half(ctx, hb, Li, n, ld, S, S + h * m, slot);
+    if (sbo_status st = inverse_first_half(ctx, hb, Li, n, ld, S, S + h * m, slot, false, ozws); st != SBO_OK)
+        return st;
+    return inverse_second_half(ctx, hb, Li, n, ld, S, S + h * m, slot, false, ozws);
 }
 
 // Every base case of the recursion over the n columns at Li -- the b x b
@@ -244,24 +252,33 @@ sbo_status inverse_lower_f64_par(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld
     const int64_t h = inverse_split(n, ctx->inv_base), m = n - h;
     double *scrA = S + h * m, *scrC = scrA + inverse_scratch(h, ctx->inv_base);
     int slotC = inverse_base_cases(h, ctx->inv_base);
+    // SBO_OPT_INV_OZ: the products of the levels with splits >= 4096 on the
+    // int8 matrix cores (oz_level), one workspace per stream, sized up front
+    // (a reserve that reallocates mid-fit would wait for the device)
+    sbo::DevBuf *ozA = nullptr, *ozC = nullptr;
+    if (ctx->inv_oz != 0 && oz_level(ctx, h, m)) {
+        SBO_HIP(ctx->gzws.reserve(std::max(sbo::gz_workspace_bytes(m, h, h, ctx->inv_oz),
+                                           sbo::gz_workspace_bytes(h, m, m, ctx->inv_oz))));
+        SBO_HIP(ctx->gzws_aux.reserve(sbo::gz_workspace_bytes(m, m, m, ctx->inv_oz)));
+        ozA = &ctx->gzws;
+        ozC = &ctx->gzws_aux;
+    }
     SBO_HIP(hipEventRecord(ctx->ev_panel, ctx->stream));            // Li widened
-    if (sbo_status st = inverse_lower_f64(ctx, ctx->blas, Li, h, ld, scrA, slot); st != SBO_OK) return st;
+    if (sbo_status st = inverse_lower_f64(ctx, ctx->blas, Li, h, ld, scrA, slot, ozA); st != SBO_OK) return st;
     SBO_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0));
     SBO_BLAS(rocblas_set_pointer_mode(ctx->blas_aux, rocblas_pointer_mode_host));
-    if (sbo_status st = inverse_lower_f64(ctx, ctx->blas_aux, Li + h + h * ld, m, ld, scrC, slotC); st != SBO_OK) {
+    if (sbo_status st = inverse_lower_f64(ctx, ctx->blas_aux, Li + h + h * ld, m, ld, scrC, slotC, ozC);
+        st != SBO_OK) {
         (void)hipStreamSynchronize(ctx->aux_stream);
         return st;
     }
     SBO_HIP(hipEventRecord(ctx->ev_trail, ctx->aux_stream));
-    // SBO_OPT_INV_OZ: the two top-level products on the int8 matrix cores
-    // (both on `stream`, one workspace; K <= 16384)
-    const bool oz = ctx->inv_oz != 0 && h <= 16384 && m <= 16384;
-    if (sbo_status st = inverse_first_half(ctx, ctx->blas, Li, n, ld, S, scrA, slot, true, oz); st != SBO_OK) {
+    if (sbo_status st = inverse_first_half(ctx, ctx->blas, Li, n, ld, S, scrA, slot, true, ozA); st != SBO_OK) {
         (void)hipStreamSynchronize(ctx->aux_stream);
         return st;
     }
     SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
-    return inverse_second_half(ctx, ctx->blas, Li, n, ld, S, nullptr, slot, true, oz);
+    return inverse_second_half(ctx, ctx->blas, Li, n, ld, S, nullptr, slot, true, ozA);
 }
 
 sbo_status check_hyper(sbo_ctx *ctx, const sbo_hyper &h) {

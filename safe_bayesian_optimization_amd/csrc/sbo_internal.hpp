@@ -180,6 +180,7 @@ struct sbo_ctx {
     sbo::DevBuf a64, kc64;       // f64 packed operand and coordinates, derived lazily
     sbo::DevBuf aoz, eoz, koz;   // int8 digit operand, its block exponents, coordinates (predict_oz.hip)
     sbo::DevBuf gzws;            // the int8-sliced GEMM's packed operands (SBO_OPT_INV_OZ)
+    sbo::DevBuf gzws_aux;        //   and those of the products on aux_stream (the inverse's second half)
     sbo::DevBuf kzt;             // the int8 sweep's K* table of one chunk of query blocks (SBO_OPT_PRECISE_KERNEL 3)
     int precise_kernel = 3;      // SBO_OPT_PRECISE_KERNEL: 0 the f64 MFMA sweep, 1 the int8 sliced sweep, 3 the same reading the K* table
     int64_t a64_I0 = 0;          // first row block whose precise operand (of precise_kernel) is stale
