@@ -434,13 +434,14 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * many 128-query blocks as fit it; at least one). */
 #define SBO_OPT_TABLE_MB 23
 /* SBO_OPT_INV_OZ (default 6; 5; 0: rocBLAS dgemm): the recursive f64
- * inverse's two top-level products (S = L21 A^-1, X21 = -C^-1 S; N <= 32768)
+ * inverse's products at splits of 4096 and more (S = L21 A^-1, X21 = -C^-1 S;
+ * N <= 32768)
  * as an f64 GEMM emulated on the int8 matrix cores -- each row / column cut
  * into that many base-256 digits under its own power of two, the digit
  * products summed exactly in int32, combined in f64 (csrc/ozgemm.hip).  Its
  * error is relative to a row's and a column's largest entries (2^-40 / 2^-48
  * of them for 5 / 6 digits), not to each product's: six digits move the
- * posterior by ~1e-7 against the dgemm fit, five by up to 4e-6 (not for the
+ * posterior by < 5e-7 against the dgemm fit, five by up to 4e-6 (not for the
  * precise regime).  The SBO_OPT_INV_OVERLAP fit keeps the dgemm products. */
 #define SBO_OPT_INV_OZ 24
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
