@@ -322,6 +322,10 @@ def run_sweep(a, dev, world, rank):
     gm.fit(X, Y, OBS)
     torch.cuda.synchronize()
     fit_ms = (time.perf_counter() - t0) * 1e3
+    # the warm refit's inverse accuracy guard (SBO_OPT_INV_CHECK: its measured
+    # share of the variance error, whether it fell back to dgemm, device ms on
+    # its own stream beside the operand packs)
+    inv_chk = gm.inverse_check()
     # SURVEY.md 8(e) alternative: rank 0 fits, the packed predictive state is
     # broadcast (RCCL) and imported elsewhere -- timed beside the replicated fit
     fit_bcast = None
@@ -543,6 +547,7 @@ def run_sweep(a, dev, world, rank):
                           "unit": "GB/s", "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None,
                           "avg_launch_ms": fill_ms, "algorithmic_bytes": fill_bytes},
         "fit_ms": fit_ms, "fit_first_ms": fit_first_ms, "fit_broadcast": fit_bcast,
+        "inverse_check": inv_chk,
         "end_to_end": end_to_end(m_all, fit_ms_max, ms_per_step),
         "argmax": {"index": best[1], "score": best[0]},
         "subgoal": subgoal,
@@ -711,6 +716,7 @@ def run_regime_stress(a, gm, prof, dev, n, gw, gh):
                                "end_to_end": end_to_end(m, fit_ms, res[0] * 1e3),
                                "precise_sweep": precise,
                                "precise_kernel": pk,
+                               "inverse_check": gm.inverse_check(),
                                "probe": {"fast_sweep_variance_error": perr, "var_min": vmin, "var_max": vmax,
                                          "err_grid": pinfo["err_grid"], "err_train": pinfo["err_train"],
                                          "how": "32 x 32 grid over the training box + 512 training locations, "

@@ -444,7 +444,43 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * posterior by < 5e-7 against the dgemm fit, five by up to 4e-6 (not for the
  * precise regime).  The SBO_OPT_INV_OVERLAP fit keeps the dgemm products. */
 #define SBO_OPT_INV_OZ 24
+/* SBO_OPT_INV_CHECK (default 1; 0 off; 2 after every full inverse): the
+ * fit's run-time accuracy guard of its f64 inverse X.  On 64 queries (a 4 x 4
+ * lattice over the training box and 48 training locations) it forms V0 = X k
+ * and one refinement against the f32 factor, V1 = V0 + X (k - L V0), in f64,
+ * and takes err = max |(sf2 - |V0|^2) - (sf2 - |V1|^2)| / max (sf2 - |V1|^2):
+ * the inverse's own share of the variance error, which the precision probe
+ * cannot see (its two sweeps read the same inverse).  With 1 it runs after an
+ * inverse whose products were int8-sliced (SBO_OPT_INV_OZ); when err exceeds
+ * 5e-7 (a twentieth of the 1e-5 contract) the fit recomputes the inverse with
+ * dgemm products and checks it again (sbo_get_inverse_check).  Runs on a
+ * stream of its own beside the fit's operand packs. */
+#define SBO_OPT_INV_CHECK 25
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
+
+/* The last inverse check (SBO_OPT_INV_CHECK) of the current fit: ran = 1 if
+ * it ran; fired = 1 if err exceeded tol and the inverse was recomputed with
+ * dgemm products (err_fallback: the same measure on that inverse, -1 when it
+ * did not fire); digits = the SBO_OPT_INV_OZ digits of the checked inverse
+ * (0: dgemm); err over all queries, err_grid / err_train over the lattice /
+ * the training locations (each normalised by its own largest variance);
+ * var_max the guard set's largest variance; ms the check's device time (both
+ * checks when it fired).  Appends keep the fit's result (their new rows are
+ * dgemm / dtrmv products). */
+typedef struct sbo_inv_check {
+    int32_t ran, fired, digits, m;
+    double err, err_grid, err_train, err_fallback, tol, var_max, ms;
+} sbo_inv_check;
+SBO_API sbo_status sbo_get_inverse_check(const sbo_ctx *ctx, sbo_inv_check *out);
+
+/* Release the fit-time and tick-time workspaces the context keeps between
+ * calls for speed (the recursive inverse's scratch and the int8-sliced GEMM's
+ * packed operands -- about 2.1 GB at N = 16384, 8.5 GB at 32768 -- the inverse
+ * check's, the append re-sort's staging copy and the precise sweep's K* table,
+ * up to SBO_OPT_TABLE_MB); they are allocated again on the next call that
+ * needs them.  The fitted state (factor, inverse, operands) stays.  Waits for
+ * the context's streams. */
+SBO_API sbo_status sbo_trim(sbo_ctx *ctx);
 
 /* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe
  * (SBO_OPT_PRECISION): the fast sweep's normwise variance error against the

@@ -33,7 +33,7 @@ EXPORTS = (
     "sbo_get_order", "sbo_profile_work", "sbo_profile_mfma", "sbo_debug_x3_stamps", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
     "sbo_get_bounds", "sbo_get_jitter", "sbo_get_tile_bounds", "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
     "sbo_polygon_correct", "sbo_polydist", "sbo_point_within", "sbo_project_subgoal", "sbo_get_precision",
-    "sbo_kd_order", "sbo_get_probe", "sbo_keys_reduce",
+    "sbo_kd_order", "sbo_get_probe", "sbo_keys_reduce", "sbo_get_inverse_check", "sbo_trim",
 )
 SBO_OPT_INVERSE_BITS = 1
 SBO_OPT_SPATIAL_ORDER = 2
@@ -59,6 +59,7 @@ SBO_OPT_REPROBE = 21
 SBO_OPT_PRECISE_KERNEL = 22
 SBO_OPT_TABLE_MB = 23
 SBO_OPT_INV_OZ = 24
+SBO_OPT_INV_CHECK = 25
 
 
 class SboError(RuntimeError):
@@ -85,6 +86,13 @@ class sbo_probe(ctypes.Structure):
                 ("precise_kernel", ctypes.c_int32), ("n_at_probe", ctypes.c_int64), ("err", ctypes.c_double),
                 ("err_grid", ctypes.c_double), ("err_train", ctypes.c_double), ("var_min", ctypes.c_double),
                 ("var_max", ctypes.c_double), ("var_max_grid", ctypes.c_double), ("var_max_train", ctypes.c_double)]
+
+
+class sbo_inv_check(ctypes.Structure):
+    _fields_ = [("ran", ctypes.c_int32), ("fired", ctypes.c_int32), ("digits", ctypes.c_int32), ("m", ctypes.c_int32),
+                ("err", ctypes.c_double), ("err_grid", ctypes.c_double), ("err_train", ctypes.c_double),
+                ("err_fallback", ctypes.c_double), ("tol", ctypes.c_double), ("var_max", ctypes.c_double),
+                ("ms", ctypes.c_double)]
 
 
 _lib = None
@@ -177,6 +185,10 @@ def lib():
     L.sbo_get_precision.restype = st
     L.sbo_get_probe.argtypes = [vp, ctypes.POINTER(sbo_probe)]
     L.sbo_get_probe.restype = st
+    L.sbo_get_inverse_check.argtypes = [vp, ctypes.POINTER(sbo_inv_check)]
+    L.sbo_get_inverse_check.restype = st
+    L.sbo_trim.argtypes = [vp]
+    L.sbo_trim.restype = st
     L.sbo_get_order.argtypes = [vp, vp]
     L.sbo_get_order.restype = st
     L.sbo_kd_order.argtypes = [vp, vp, i64, i64, vp]

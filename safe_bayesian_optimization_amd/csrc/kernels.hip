@@ -87,11 +87,12 @@ __global__ void sub_scalar_kernel(const float *__restrict__ in, float v, int64_t
     if (i < n) out[i] = in[i] - v;
 }
 
+// (columns j = blockIdx.y + c gridDim.y: grid.y is capped at kMaxGridY)
 __global__ void copy_lower_kernel(const float *__restrict__ src, int64_t lds, int64_t n,
                                   float *__restrict__ dst, int64_t ldd) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t j = blockIdx.y;
-    if (i < n) dst[i + j * ldd] = i >= j ? src[i + j * lds] : 0.0f;
+    if (i >= n) return;
+    for (int64_t j = blockIdx.y; j < n; j += gridDim.y) dst[i + j * ldd] = i >= j ? src[i + j * lds] : 0.0f;
 }
 
 // ------------------------------------------------------------ operand pack
@@ -135,11 +136,11 @@ __global__ __launch_bounds__(256) void row_dot_kernel(const double *__restrict__
 }
 
 // out[i + j * ldo] = (float)d[i + j * ldd] (i < m, j = blockIdx.y)
-__global__ void narrow_2d_kernel(const double *__restrict__ d, int64_t ldd, int64_t m, float *__restrict__ out,
-                                 int64_t ldo) {
+__global__ void narrow_2d_kernel(const double *__restrict__ d, int64_t ldd, int64_t m, int64_t n,
+                                 float *__restrict__ out, int64_t ldo) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t j = blockIdx.y;
-    if (i < m) out[i + j * ldo] = (float)d[i + j * ldd];
+    if (i >= m) return;
+    for (int64_t j = blockIdx.y; j < n; j += gridDim.y) out[i + j * ldo] = (float)d[i + j * ldd];
 }
 
 // out[j * stride] = (float)d[j]: a row of the f32 factor from an f64 vector
@@ -149,11 +150,12 @@ __global__ void narrow_strided_kernel(const double *__restrict__ d, int64_t n, f
     if (j < n) out[j * stride] = (float)d[j];
 }
 
-__global__ void widen_kernel(const float *__restrict__ src, int64_t lds, int64_t m, int lower,
+__global__ void widen_kernel(const float *__restrict__ src, int64_t lds, int64_t m, int64_t n, int lower,
                              double *__restrict__ dst, int64_t ldd) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t j = blockIdx.y;
-    if (i < m) dst[i + j * ldd] = (!lower || i >= j) ? (double)src[i + j * lds] : 0.0;
+    if (i >= m) return;
+    for (int64_t j = blockIdx.y; j < n; j += gridDim.y)
+        dst[i + j * ldd] = (!lower || i >= j) ? (double)src[i + j * lds] : 0.0;
 }
 
 // Per k-tile coordinates, step-major per lane group: k = 4p + g is stored at
@@ -2256,8 +2258,9 @@ hipError_t launch_sub_scalar(hipStream_t s, const float *in, float v, int64_t n,
 
 hipError_t launch_copy_lower(hipStream_t s, const float *src, int64_t ld_src, int64_t n, float *dst,
                              int64_t ld_dst) {
-    hipLaunchKernelGGL(copy_lower_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)n), dim3(256), 0, s,
-                       src, ld_src, n, dst, ld_dst);
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(copy_lower_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)std::min<int64_t>(n, kMaxGridY)),
+                       dim3(256), 0, s, src, ld_src, n, dst, ld_dst);
     return hipGetLastError();
 }
 
@@ -2308,8 +2311,8 @@ hipError_t launch_pack_operand(hipStream_t s, const double *Linv, int64_t ld, in
 hipError_t launch_widen(hipStream_t s, const float *src, int64_t ld_src, int64_t m, int64_t n, bool lower,
                         double *dst, int64_t ld_dst) {
     if (m <= 0 || n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(widen_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)n), dim3(256), 0, s, src, ld_src,
-                       m, lower ? 1 : 0, dst, ld_dst);
+    hipLaunchKernelGGL(widen_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)std::min<int64_t>(n, kMaxGridY)),
+                       dim3(256), 0, s, src, ld_src, m, n, lower ? 1 : 0, dst, ld_dst);
     return hipGetLastError();
 }
 
@@ -2386,8 +2389,8 @@ hipError_t launch_row_dot(hipStream_t s, const double *A, int64_t ld, int64_t ro
 hipError_t launch_narrow_2d(hipStream_t s, const double *d, int64_t ldd, int64_t m, int64_t n, float *out,
                             int64_t ldo) {
     if (m <= 0 || n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(narrow_2d_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)n), dim3(256), 0, s, d, ldd, m,
-                       out, ldo);
+    hipLaunchKernelGGL(narrow_2d_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)std::min<int64_t>(n, kMaxGridY)),
+                       dim3(256), 0, s, d, ldd, m, n, out, ldo);
     return hipGetLastError();
 }
 

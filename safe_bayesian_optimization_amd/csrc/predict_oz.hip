@@ -126,19 +126,11 @@ __device__ __forceinline__ double exp2_tab(double u, const double *__restrict__ 
 // (31 bits) suffice for K*: its f32 rounding (24 bits) alone moved the lpsc
 // box's variance by only 2.6e-6 (tools/r4_emulate_ozaki.py), against 6.5e-5
 // for A.  On the last row block (mean) also mu += K* sf2 alpha.
-template <bool MEAN>
-__device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, const double *__restrict__ T2, int g,
-                                             double xq, double yq, double cexp, i32x4 (&kd)[kOzKDigits], int &eK,
-                                             double &mu) {
-    const double *px = reinterpret_cast<const double *>(pc) + 16 * g;
-    const double *py = reinterpret_cast<const double *>(pc + kBK * 8) + 16 * g;
-    const double *pa = reinterpret_cast<const double *>(pc + kBK * 16) + 16 * g;
+// pass 1 of kstar_digits: the smallest f32 squared distance from the query
+// to the tile's 64 points (this lane's 16, then the four lanes of a query)
+__device__ __forceinline__ float kstar_dmin(const char *__restrict__ pc, int g, double xq, double yq) {
     const float *px32 = reinterpret_cast<const float *>(pc + kBK * 24) + 16 * g;
     const float *py32 = reinterpret_cast<const float *>(pc + kBK * 28) + 16 * g;
-    // pass 1: the exponent from an f32 estimate of the largest K* (the min
-    // distance, v_exp_f32: a few ulp; the 1.01 margin covers it), so that pass
-    // 2 can cut each f64 K* into digits as soon as it is computed (four live
-    // at a time, not sixteen)
     const float xqf = (float)xq, yqf = (float)yq;
     float dmin = 3.0e38f;
 #pragma unroll
@@ -148,11 +140,23 @@ __device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, const 
     }
     dmin = fminf(dmin, __shfl_xor(dmin, 16));
     dmin = fminf(dmin, __shfl_xor(dmin, 32));
+    return dmin;
+}
+// the exponent: 2^eK > 1.01 kmax, so K* 2^-eK < 0.99 and the top digit stays <= 127
+__device__ __forceinline__ int kstar_exp(float dmin, double cexp) {
     const float kmax = __builtin_amdgcn_exp2f((float)cexp * dmin);
-    // 2^eK > 1.01 kmax, so K* 2^-eK < 0.99 and the top digit stays <= 127
     int e = 0;
     (void)frexpf(kmax * 1.01f, &e);
-    eK = kmax > 0.0f ? e : 0;
+    return kmax > 0.0f ? e : 0;
+}
+// pass 2: the digits under a given exponent eK
+template <bool MEAN>
+__device__ __forceinline__ void kstar_digits_e(const char *__restrict__ pc, const double *__restrict__ T2, int g,
+                                               double xq, double yq, double cexp, int eK, i32x4 (&kd)[kOzKDigits],
+                                               double &mu) {
+    const double *px = reinterpret_cast<const double *>(pc) + 16 * g;
+    const double *py = reinterpret_cast<const double *>(pc + kBK * 8) + 16 * g;
+    const double *pa = reinterpret_cast<const double *>(pc + kBK * 16) + 16 * g;
     const int esc = kOzKBits - eK;
 #pragma unroll
     for (int m4 = 0; m4 < 4; ++m4) {
@@ -177,6 +181,17 @@ __device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, const 
         kd[1][m4] = (int)__builtin_amdgcn_perm(p23b, p01b, 0x05040100u);          // bytes 2
         kd[0][m4] = (int)__builtin_amdgcn_perm(p23b, p01b, 0x07060302u);          // bytes 3: the top digit
     }
+}
+// pass 1 (the exponent from an f32 estimate of the largest K*: the min
+// distance, v_exp_f32, a few ulp -- the 1.01 margin covers it), so that pass
+// 2 can cut each f64 K* into digits as soon as it is computed (four live at a
+// time, not sixteen)
+template <bool MEAN>
+__device__ __forceinline__ void kstar_digits(const char *__restrict__ pc, const double *__restrict__ T2, int g,
+                                             double xq, double yq, double cexp, i32x4 (&kd)[kOzKDigits], int &eK,
+                                             double &mu) {
+    eK = kstar_exp(kstar_dmin(pc, g, xq, yq), cexp);
+    kstar_digits_e<MEAN>(pc, T2, g, xq, yq, cexp, eK, kd, mu);
 }
 
 // The 14 digit products of one 16x16 block (A digit s, K* digit u, s + u <=
@@ -469,28 +484,29 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
 __global__ __launch_bounds__(kOzThreads) void kstar_table_kernel(const char *__restrict__ koz,
                                                                  const float *__restrict__ qx,
                                                                  const float *__restrict__ qy, int64_t m, int nkt,
-                                                                 double cexp, char *__restrict__ kzt) {
+                                                                 int64_t nq, double cexp, char *__restrict__ kzt) {
     __shared__ double T2[64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r = lane & 15;
     if (tid < 64) T2[tid] = exp2((double)tid * 0.015625);
     __syncthreads();
     const int t = blockIdx.x;
-    const int64_t qb = blockIdx.y;
-    const int64_t q = qb * kBN + wave * 16 + r;
-    const double xq = (double)qx[q < m ? q : m - 1], yq = (double)qy[q < m ? q : m - 1];
-    i32x4 kd[kOzKDigits];
-    int eK = 0;
-    double mu = 0.0;
-    kstar_digits<true>(koz + (int64_t)t * kOzC, T2, g, xq, yq, cexp, kd, eK, mu);
-    mu += __shfl_xor(mu, 16);
-    mu += __shfl_xor(mu, 32);
-    char *out = kzt + (qb * nkt + t) * (int64_t)kKzt;
+    for (int64_t qb = blockIdx.y; qb < nq; qb += gridDim.y) {   // (grid.y capped at kMaxGridY)
+        const int64_t q = qb * kBN + wave * 16 + r;
+        const double xq = (double)qx[q < m ? q : m - 1], yq = (double)qy[q < m ? q : m - 1];
+        i32x4 kd[kOzKDigits];
+        int eK = 0;
+        double mu = 0.0;
+        kstar_digits<true>(koz + (int64_t)t * kOzC, T2, g, xq, yq, cexp, kd, eK, mu);
+        mu += __shfl_xor(mu, 16);
+        mu += __shfl_xor(mu, 32);
+        char *out = kzt + (qb * nkt + t) * (int64_t)kKzt;
 #pragma unroll
-    for (int u = 0; u < kOzKDigits; ++u)
-        *reinterpret_cast<i32x4 *>(out + wave * 4096 + u * 1024 + lane * 16) = kd[u];
-    if (g == 0) {
-        reinterpret_cast<int *>(out + kKztE)[wave * 16 + r] = eK;
-        reinterpret_cast<double *>(out + kKztMu)[wave * 16 + r] = mu;
+        for (int u = 0; u < kOzKDigits; ++u)
+            *reinterpret_cast<i32x4 *>(out + wave * 4096 + u * 1024 + lane * 16) = kd[u];
+        if (g == 0) {
+            reinterpret_cast<int *>(out + kKztE)[wave * 16 + r] = eK;
+            reinterpret_cast<double *>(out + kKztMu)[wave * 16 + r] = mu;
+        }
     }
 }
 
@@ -576,6 +592,429 @@ __global__ void pack_koz_kernel(const float *__restrict__ x, const float *__rest
     reinterpret_cast<float *>(c + kBK * 28)[o] = in ? y[k] : y[0];
 }
 
+// ---------------------------------------------------------------------------
+// Pair mode (SBO_OPT_PRECISE_KERNEL 4, round 5): A's and
+// K*'s exponents shared by a PAIR of k-tiles (2p, 2p + 1), so every level's
+// int32 sum chains over 128 k before the f64 combination.  The kernel is
+// issue-bound on that combination (profiles/r5_pmc_oz_table.txt: VALU
+// instructions 25.8 % of wave cycles against 6.2 % MFMA, matrix pipe 48 %);
+// chaining two tiles halves its VALU per MFMA.  Exact integer sums still:
+// per level per tile |sum| <= (pairs at the level) 64 2^14, over two tiles
+// h23 = l2 256 + l3 + [l4 / 256] < 6 2^28 + 2^23 + 2^15 < 2^31.  The price is
+// precision where a pair's two tiles differ in scale (the smaller one keeps
+// fewer of its own bits): emulated on the lpsc box at N = 8192
+// (tools/r5_emulate_pairs.py, profiles/r5_emulate_pairs.log) the variance
+// moves 3.9e-8 -> 6.1e-8 (sn2 0.01: 9.9e-7 -> 1.3e-6; l 0.8: 9.4e-8 -> 1.5e-7).
+// Layout: pair (I, p) of a row block = its tiles 2p, 2p + 1 (80 KiB each, the
+// same bytes as two kernel-1 tiles) holding four stages of 40 KiB, one per
+// quarter of the rows (64 rows = four 16-row blocks): stage piece ((s 2 + e) 4
+// + b) = digit s of tile e of block b, 1 KiB in kernel 1's lane order; the
+// pair's 16 block exponents at tile 2p's 64 B of eoz.  The K* table per
+// (query block, pair): [wave][tile e][digit u][lane][16 B] (64 KiB), eK per
+// query (512 B), the pair's mean terms per query (1 KiB).
+// Walk: an item's list entries are merged into pairs (entry t and t + 1 for
+// t even: one pair; a lone tile of a pair runs with its partner, whose K*
+// terms are then included although the plan dropped them -- more work, never
+// less accuracy); four stages per pair, double buffered; the pair's table in a
+// slot of its own, read into registers at quarter 0 and refilled for the next
+// pair at quarter 3.
+constexpr int kOz2RB = 4;                                    // 16-row blocks per stage
+constexpr int kOz2A = kOzDigits * 2 * kOz2RB * 1024;         // 40 KiB of digits per stage
+constexpr int kOz2E = 64;                                    // the pair's 16 block exponents
+constexpr int kOz2Slot = kOz2A + kOz2E;
+constexpr int kKzt2Digits = kOzWaves * 2 * kOzKDigits * 1024;   // 64 KiB
+constexpr int kKzt2E = kKzt2Digits;
+constexpr int kKzt2Mu = kKzt2E + kBN * 4;
+constexpr int kKzt2 = kKzt2Mu + kBN * 8;                     // 67072 B per (query block, pair)
+constexpr int kOz2Smem = 2 * kOz2Slot + kKzt2 + 4096;        // two stage slots, the table, the windows
+static_assert(kOz2Smem <= 160 * 1024, "pair-mode LDS");
+static_assert(kOz2A == 2 * kOzA / 2 && 4 * kOz2A == 2 * kOzTileBytes, "a pair is two kernel-1 tiles");
+
+// The 28 digit products of one 16x16 block over the pair (tile 0 then tile 1,
+// chained per level), combined once: T = (l0 256 + l1) 2^16 + l2 256 + l3 +
+// floor((l4 + 128) / 256), the +128 from level 4's initial accumulator.
+__device__ __forceinline__ void block_products2(const i32x4 *__restrict__ pa, int b, const i32x4 (&kd)[2][kOzKDigits],
+                                                double S, f64x4 &acc) {
+    const i32x4 z = {0, 0, 0, 0}, c128 = {128, 128, 128, 128};
+    i32x4 l0 = z, l1 = z, l2 = z, l3 = z, l4 = c128;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        i32x4 ad[kOzDigits];
+#pragma unroll
+        for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[((s * 2 + e) * kOz2RB + b) * 64];
+        l0 = mfma_i8(ad[0], kd[e][0], l0);
+        l1 = mfma_i8(ad[0], kd[e][1], l1);
+        l2 = mfma_i8(ad[0], kd[e][2], l2);
+        l3 = mfma_i8(ad[0], kd[e][3], l3);
+        l1 = mfma_i8(ad[1], kd[e][0], l1);
+        l2 = mfma_i8(ad[1], kd[e][1], l2);
+        l3 = mfma_i8(ad[1], kd[e][2], l3);
+        l4 = mfma_i8(ad[1], kd[e][3], l4);
+        l2 = mfma_i8(ad[2], kd[e][0], l2);
+        l3 = mfma_i8(ad[2], kd[e][1], l3);
+        l4 = mfma_i8(ad[2], kd[e][2], l4);
+        l3 = mfma_i8(ad[3], kd[e][0], l3);
+        l4 = mfma_i8(ad[3], kd[e][1], l4);
+        l4 = mfma_i8(ad[4], kd[e][0], l4);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const int h01 = l0[v] * 256 + l1[v];                  // |.| < 2^30
+        const int h23 = l2[v] * 256 + l3[v] + (l4[v] >> 8);   // |.| < 2^31 (above)
+        const double t = fma((double)h01, 65536.0, (double)h23);
+        acc[v] = fma(t, S, acc[v]);
+    }
+}
+
+// One stage: quarter QQ's four 16-row blocks into this row half's eight
+// accumulators (acc[(QQ & 1) 4 + b]).
+template <int QQ>
+__device__ __forceinline__ void stage_blocks2(const char *__restrict__ slot, int lane, const i32x4 (&kd)[2][kOzKDigits],
+                                              int eK, f64x4 (&acc)[kOzHalfRB]) {
+    const int *eA = reinterpret_cast<const int *>(slot + kOz2A);
+    const i32x4 *pa = reinterpret_cast<const i32x4 *>(slot) + lane;
+#pragma unroll
+    for (int b = 0; b < kOz2RB; ++b) {
+        const double S = ldexp(1.0, __builtin_amdgcn_readfirstlane(eA[QQ * kOz2RB + b]) + eK - kOzScale);
+        block_products2(pa, b, kd, S, acc[(QQ & 1) * kOz2RB + b]);
+    }
+}
+
+// The sweep walks each item TWICE, once per 128-row half (quarters 0-1, then
+// 2-3 of every pair), so that a wave holds eight f64 accumulator blocks, not
+// sixteen: with sixteen, the pair's two digit sets and the chained levels
+// spilled 72 registers.  The K* table piece is staged once per (pair, half).
+__global__ __launch_bounds__(kOzThreads, 1) void predict_oz2_kernel(
+    const char *__restrict__ aoz, const int *__restrict__ eoz, const int4 *__restrict__ desc,
+    const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P, int n_items, int nI,
+    int64_t m, int64_t ldp, double m0, double *__restrict__ part, double *__restrict__ mean,
+    const char *__restrict__ kzt) {
+    __shared__ __attribute__((aligned(16))) char smem[kOz2Smem];
+    const int bid = blockIdx.x;
+    const int rng = (P % 8 == 0) ? (bid % 8) * (P / 8) + bid / 8 : bid;
+    const int k0 = max(seg[rng], 0), k1 = min(seg[rng + 1], n_items);
+    if (k0 >= k1) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int r = lane & 15;
+    const int g = lane >> 4;
+    const int4 *dwin = reinterpret_cast<const int4 *>(smem + 2 * kOz2Slot + kKzt2);
+    const unsigned short *lwin = reinterpret_cast<const unsigned short *>(smem + 2 * kOz2Slot + kKzt2 + 2048);
+    const char *tz = smem + 2 * kOz2Slot;   // the (pair, half)'s K* table piece
+
+    typedef __attribute__((address_space(3))) char lds_char;
+    const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
+    const uint32_t lds_wave = lds_smem + (uint32_t)__builtin_amdgcn_readfirstlane(wave) * 1024u;
+    const uint32_t lds_tz = lds_smem + 2u * kOz2Slot;
+    const uint32_t lds_dwin = lds_tz + (uint32_t)kKzt2;
+    const uint32_t lds_lwin = lds_dwin + 2048u;
+    const char *gA = aoz + wave * 1024 + lane * 16;
+    const char *gE = reinterpret_cast<const char *>(eoz) + lane * 16;
+    const char *gD = reinterpret_cast<const char *>(desc) + lane * 16;
+    const char *gL = reinterpret_cast<const char *>(tl) + lane * 16;
+    const char *gZ = kzt + lane * 16;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const int npr = kTilesPerRowBlockStep * nI / 2;   // pairs per query block in the table
+#define SBO_OZ_DMA16(gsrc, ldst)                                                                         \
+    do {                                                                                                 \
+        uint32_t keep_;                                                                                  \
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t" \
+                     "s_mov_b32 m0, %0"                                                                  \
+                     : "=&s"(keep_)                                                                      \
+                     : "v"(gsrc), "s"(ldst)                                                              \
+                     : "memory");                                                                        \
+    } while (0)
+    // quarter q_ of pair (first packed tile Tp_) into slot buf
+#define SBO_OZ2_STAGE(Tp_, q_, buf)                                                                      \
+    do {                                                                                                 \
+        const char *s_ = gA + (int64_t)(Tp_) * kOzTileBytes + (q_) * kOz2A;                              \
+        const uint32_t d_ = __builtin_amdgcn_readfirstlane(lds_wave + (uint32_t)(buf) * kOz2Slot);       \
+        _Pragma("unroll") for (int j_ = 0; j_ < kOz2A / (1024 * kOzWaves); ++j_)                         \
+            SBO_OZ_DMA16(s_ + j_ * kOzWaves * 1024, d_ + (uint32_t)(j_ * kOzWaves * 1024));              \
+        if (wave == 0 && lane < 4)                                                                       \
+            SBO_OZ_DMA16(gE + (int64_t)(Tp_) * 64,                                                       \
+                         __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOz2Slot + kOz2A)));    \
+    } while (0)
+    // the table piece of (query block qb_, pair pr_)
+#define SBO_OZ2_TABLE(qb_, pr_)                                                                          \
+    do {                                                                                                 \
+        const char *z_ = gZ + ((int64_t)(qb_) * npr + (pr_)) * kKzt2;                                    \
+        _Pragma("unroll") for (int u_ = 0; u_ < 2 * kOzKDigits; ++u_)                                    \
+            SBO_OZ_DMA16(z_ + wave * 8192 + u_ * 1024, lds_tz + (uint32_t)(wave_u * 8192 + u_ * 1024));  \
+        if (wave == 0 && lane < 32) SBO_OZ_DMA16(z_ + kKzt2E, lds_tz + (uint32_t)kKzt2E);               \
+        if (wave == 1) SBO_OZ_DMA16(z_ + kKzt2Mu, lds_tz + (uint32_t)kKzt2Mu);                           \
+    } while (0)
+#define SBO_OZ_DESC_WINDOW(w_)                                                                           \
+    do {                                                                                                 \
+        if (wave == 1) SBO_OZ_DMA16(gD + (int64_t)(w_) * 1024, lds_dwin + (uint32_t)((w_) & 1) * 1024u); \
+    } while (0)
+#define SBO_OZ_LIST_WINDOW(w_)                                                                           \
+    do {                                                                                                 \
+        if (wave == 2) SBO_OZ_DMA16(gL + (int64_t)(w_) * 1024, lds_lwin + (uint32_t)((w_) & 1) * 1024u); \
+    } while (0)
+    auto desc_at = [&](int k) {
+        const int4 d = dwin[((k / kOzDescWin) & 1) * kOzDescWin + k % kOzDescWin];
+        const int I = min(max(__builtin_amdgcn_readfirstlane(d.x), 0), nI - 1);
+        return make_int4(I, __builtin_amdgcn_readfirstlane(d.y), __builtin_amdgcn_readfirstlane(d.z),
+                         __builtin_amdgcn_readfirstlane(d.w));
+    };
+    auto entry_off = [](const int4 &d) {
+        return (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
+    };
+    auto list_at = [&](uint64_t e, int I) {
+        const int t = __builtin_amdgcn_readfirstlane((int)lwin[((e / kOzListWin) & 1) * kOzListWin + e % kOzListWin]) &
+                      ((1 << kLevelShift) - 1);
+        return min(t, kTilesPerRowBlockStep * (I + 1) - 1);
+    };
+    // the pair of list entry e (the item's j-th of cnt): its index, and how
+    // many entries it takes (2 when entry e + 1 is the partner)
+    auto pair_at = [&](uint64_t e, int I, int j, int cnt, int &ne) {
+        const int t0 = list_at(e, I);
+        ne = 1;
+        if ((t0 & 1) == 0 && j + 1 < cnt && list_at(e + 1, I) == t0 + 1) ne = 2;
+        return t0 >> 1;
+    };
+
+    // ---- prologue
+    SBO_OZ_DESC_WINDOW(k0 / kOzDescWin);
+    SBO_OZ_DESC_WINDOW(k0 / kOzDescWin + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int4 dc = desc_at(k0);
+    uint64_t e = entry_off(dc);
+    SBO_OZ_LIST_WINDOW(e / kOzListWin);
+    SBO_OZ_LIST_WINDOW(e / kOzListWin + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int ne = 1;
+    int pr = pair_at(e, dc.x, 0, dc.w & 0xffff, ne);
+    int pr0 = pr, ne0 = ne;      // the item's first pair (the second half starts there again)
+    SBO_OZ2_STAGE(tile_start(dc.x) + 2 * pr, 0, 0);
+    SBO_OZ2_TABLE(dc.y, pr);
+    int64_t q = (int64_t)dc.y * kBN + wave * 16 + r;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    f64x4 acc[kOzHalfRB];
+#pragma unroll
+    for (int rb = 0; rb < kOzHalfRB; ++rb) acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    i32x4 kd[2][kOzKDigits];
+    int eK = 0;
+    double mu = 0.0, vsum = 0.0;
+    // k item, hp row half, j entries of the item before the current pair, sq
+    // stage of the pair in this half, cur slot
+    int k = k0, hp = 0, j = 0, sq = 0, cur = 0;
+    for (;;) {
+        const int cnt = dc.w & 0xffff;
+        // the next stage: the pair's other quarter of this half, the next pair
+        // of this half, the item's first pair again for the second half, or
+        // the first pair of item k + 1
+        int kn = k, hn = hp, jn = j, sn = sq + 1, prn = pr, nen = ne;
+        uint64_t en = e;
+        bool restart = false;
+        if (sn == 2) {
+            sn = 0;
+            jn = j + ne;
+            en = e + ne;
+            if (jn >= cnt) {
+                jn = 0;
+                if (hp == 0) {
+                    hn = 1;
+                    en = entry_off(dc);
+                    restart = true;
+                } else {
+                    hn = 0;
+                    kn = k + 1;
+                }
+            }
+        }
+        const bool more = kn < k1;
+        int4 dn = dc;
+        if (more) {
+            if (kn != k) {
+                dn = desc_at(kn);
+                if (kn % kOzDescWin == 0) SBO_OZ_DESC_WINDOW(kn / kOzDescWin + 1);
+            }
+            if (restart) {
+                // the item's entries again: its first pair from registers, the
+                // list windows reloaded for the pairs after it
+                prn = pr0;
+                nen = ne0;
+                SBO_OZ_LIST_WINDOW(en / kOzListWin);
+                SBO_OZ_LIST_WINDOW(en / kOzListWin + 1);
+            } else if (sn == 0) {
+                if (en / kOzListWin != e / kOzListWin) SBO_OZ_LIST_WINDOW(en / kOzListWin + 1);
+                prn = pair_at(en, dn.x, jn, dn.w & 0xffff, nen);
+            }
+            SBO_OZ2_STAGE(tile_start(dn.x) + 2 * prn, 2 * hn + sn, cur ^ 1);
+            if (sn == 0) SBO_OZ2_TABLE(dn.y, prn);   // (the current piece was read at this pair-half's first stage)
+        }
+        const char *slot = smem + cur * kOz2Slot;
+        const int I = dc.x;
+        const int qq = 2 * hp + sq;
+        if (sq == 0) {
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                for (int u = 0; u < kOzKDigits; ++u)
+                    kd[t2][u] = *reinterpret_cast<const i32x4 *>(tz + wave * 8192 + (t2 * kOzKDigits + u) * 1024 +
+                                                                 lane * 16);
+            eK = *reinterpret_cast<const int *>(tz + kKzt2E + (wave * 16 + r) * 4);
+            if (hp == 0 && I == nI - 1 && g == 0)
+                mu += *reinterpret_cast<const double *>(tz + kKzt2Mu + (wave * 16 + r) * 8);
+        }
+        if (qq == 0) stage_blocks2<0>(slot, lane, kd, eK, acc);
+        else if (qq == 1) stage_blocks2<1>(slot, lane, kd, eK, acc);
+        else if (qq == 2) stage_blocks2<2>(slot, lane, kd, eK, acc);
+        else stage_blocks2<3>(slot, lane, kd, eK, acc);
+        if (sq == 1 && j + ne >= cnt) {
+            // the half is done: its rows' V^2 into vsum; after the second
+            // half the column sums of the item's 256 rows
+#pragma unroll
+            for (int rb = 0; rb < kOzHalfRB; ++rb) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) vsum = fma(acc[rb][c], acc[rb][c], vsum);
+                acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
+            }
+            if (hp == 1) {
+                double sum = vsum;
+                sum += __shfl_xor(sum, 16);
+                sum += __shfl_xor(sum, 32);
+                vsum = 0.0;
+                const bool writer = lane < 16 && q < m;
+                if (writer) part[(int64_t)I * ldp + q] = sum;
+                if (I == nI - 1) {
+                    mu += __shfl_xor(mu, 16);
+                    mu += __shfl_xor(mu, 32);
+                    if (writer) mean[q] = m0 + mu;
+                    mu = 0.0;
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (!more) break;
+        if (kn != k) {
+            k = kn;
+            dc = dn;
+            q = (int64_t)dc.y * kBN + wave * 16 + r;
+        }
+        if (sn == 0) {
+            e = en;
+            pr = prn;
+            ne = nen;
+            if (jn == 0 && hn == 0) {   // a new item: remember its first pair
+                pr0 = prn;
+                ne0 = nen;
+            }
+        }
+        hp = hn;
+        j = jn;
+        sq = sn;
+        cur ^= 1;
+    }
+#undef SBO_OZ2_STAGE
+#undef SBO_OZ2_TABLE
+#undef SBO_OZ_DESC_WINDOW
+#undef SBO_OZ_LIST_WINDOW
+#undef SBO_OZ_DMA16
+}
+
+// The pair-mode K* table (SBO_OPT_PRECISE_KERNEL 4): one workgroup per (pair,
+// query block), eK from the smaller distance of the pair's two tiles, then
+// each tile's digits under it (kstar_digits' arithmetic), the pair's mean
+// terms.  grid = (pairs, query blocks).
+__global__ __launch_bounds__(kOzThreads) void kstar_table2_kernel(const char *__restrict__ koz,
+                                                                  const float *__restrict__ qx,
+                                                                  const float *__restrict__ qy, int64_t m, int npr,
+                                                                  int64_t nq, double cexp, char *__restrict__ kzt) {
+    __shared__ double T2[64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r = lane & 15;
+    if (tid < 64) T2[tid] = exp2((double)tid * 0.015625);
+    __syncthreads();
+    const int p = blockIdx.x;
+    const char *pc0 = koz + (int64_t)(2 * p) * kOzC, *pc1 = pc0 + kOzC;
+    for (int64_t qb = blockIdx.y; qb < nq; qb += gridDim.y) {
+        const int64_t q = qb * kBN + wave * 16 + r;
+        const double xq = (double)qx[q < m ? q : m - 1], yq = (double)qy[q < m ? q : m - 1];
+        const int eK = kstar_exp(fminf(kstar_dmin(pc0, g, xq, yq), kstar_dmin(pc1, g, xq, yq)), cexp);
+        char *out = kzt + (qb * npr + p) * (int64_t)kKzt2;
+        double mu = 0.0;
+#pragma unroll 1
+        for (int t2 = 0; t2 < 2; ++t2) {
+            i32x4 kd[kOzKDigits];
+            kstar_digits_e<true>(t2 ? pc1 : pc0, T2, g, xq, yq, cexp, eK, kd, mu);
+#pragma unroll
+            for (int u = 0; u < kOzKDigits; ++u)
+                *reinterpret_cast<i32x4 *>(out + wave * 8192 + (t2 * kOzKDigits + u) * 1024 + lane * 16) = kd[u];
+        }
+        mu += __shfl_xor(mu, 16);
+        mu += __shfl_xor(mu, 32);
+        if (g == 0) {
+            reinterpret_cast<int *>(out + kKzt2E)[wave * 16 + r] = eK;
+            reinterpret_cast<double *>(out + kKzt2Mu)[wave * 16 + r] = mu;
+        }
+    }
+}
+
+// A = sf2 L^-1 into pair-mode digit tiles for row blocks I >= I0 (the layout
+// above): one workgroup per (pair, row block), one thread per row; the 16-row
+// block's exponent from the pair's 128 k, then each tile's 64 values as
+// pack_oz_kernel cuts them.  grid.x = pairs of the longest row block, grid.y
+// = row block I - I0.
+__global__ __launch_bounds__(256) void pack_oz2_kernel(const double *__restrict__ Linv, int64_t ld, int64_t n,
+                                                       double sf2, int64_t I0, char *__restrict__ aoz,
+                                                       int *__restrict__ eoz) {
+    const int64_t I = I0 + blockIdx.y;
+    const int64_t p = blockIdx.x;
+    if (p >= (I + 1) * kTilesPerRowBlockStep / 2) return;
+    const int64_t Tp = tile_start(I) + 2 * p;
+    const int rr = threadIdx.x;
+    const int64_t row = I * kBM + rr;
+    auto val = [&](int64_t col) { return (row < n && col < n && col <= row) ? sf2 * Linv[row + col * ld] : 0.0; };
+    double amax = 0.0;
+    for (int c = 0; c < 2 * kBK; ++c) amax = fmax(amax, fabs(val(p * 2 * kBK + c)));
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) amax = fmax(amax, __shfl_xor(amax, o));
+    int eA = -900;
+    if (amax > 0.0) {
+        int ex;
+        (void)frexp(amax * 1.01, &ex);
+        eA = ex;
+    }
+    const int sub = rr >> 4, qq = sub >> 2, b = sub & 3;
+    if ((rr & 15) == 0) eoz[Tp * 16 + sub] = eA;
+    char *base = aoz + Tp * (int64_t)kOzTileBytes + qq * kOz2A;
+    for (int t2 = 0; t2 < 2; ++t2) {
+        double v[kBK];
+#pragma unroll
+        for (int c = 0; c < kBK; ++c) v[c] = val((2 * p + t2) * kBK + c);
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+            uint32_t w[kOzDigits][4];
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                const int64_t xa = eA > -900 ? (int64_t)rint(ldexp(v[16 * gg + jj], 39 - eA)) : 0;
+                const uint64_t yv = (uint64_t)(xa + 0x80808080ll);
+#pragma unroll
+                for (int s = 0; s < kOzDigits; ++s) {
+                    const uint32_t bt = (uint32_t)(yv >> (8 * (kOzDigits - 1 - s))) & 0xFFu;
+                    const uint32_t d = s == 0 ? bt : (bt ^ 0x80u);
+                    if ((jj & 3) == 0) w[s][jj >> 2] = d;
+                    else w[s][jj >> 2] |= d << (8 * (jj & 3));
+                }
+            }
+            const int l = (rr & 15) + 16 * gg;
+#pragma unroll
+            for (int s = 0; s < kOzDigits; ++s) {
+                uint4 *dst = reinterpret_cast<uint4 *>(base + ((s * 2 + t2) * kOz2RB + b) * 1024 + l * 16);
+                *dst = make_uint4(w[s][0], w[s][1], w[s][2], w[s][3]);
+            }
+        }
+    }
+}
+
 }  // namespace
 
 size_t oz_operand_bytes(int64_t npad) { return (size_t)kOzTileBytes * (size_t)total_tiles(npad / kBM); }
@@ -584,9 +1023,12 @@ size_t oz_coord_bytes(int64_t npad) { return (size_t)kOzC * (size_t)(npad / kBK)
 
 hipError_t launch_pack_oz(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
                           double sf2, const float *x, const float *y, const double *alpha, char *aoz, int *eoz,
-                          char *koz) {
+                          char *koz, bool pairs) {
     const int64_t nI = npad / kBM;
-    if (I0 < nI) {
+    if (I0 < nI && pairs) {
+        hipLaunchKernelGGL(pack_oz2_kernel, dim3((unsigned)(nI * kTilesPerRowBlockStep / 2), (unsigned)(nI - I0)),
+                           dim3(256), 0, s, Linv, ld, n, sf2, I0, aoz, eoz);
+    } else if (I0 < nI) {
         hipLaunchKernelGGL(pack_oz_kernel, dim3((unsigned)(nI * kTilesPerRowBlockStep), (unsigned)(nI - I0)),
                            dim3(256), 0, s, Linv, ld, n, sf2, I0, aoz, eoz);
     }
@@ -608,6 +1050,12 @@ hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, con
         return hipGetLastError();
     }
 #endif
+    if (variant == 4) {   // pair mode, K*'s digits from the pair table
+        if (!kzt) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(predict_oz2_kernel, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, desc, tl, seg, P,
+                           n_items, nI, m, ldp, m0, part, mean, kzt);
+        return hipGetLastError();
+    }
     if (variant == 3) {   // K*'s digits from the table
         if (!kzt) return hipErrorInvalidValue;
         hipLaunchKernelGGL(predict_oz_kernel<2>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc,
@@ -622,15 +1070,22 @@ hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, con
 }  // namespace sbo
 
 namespace sbo {
-size_t oz_table_bytes(int64_t npad) { return (size_t)kKzt * (size_t)(npad / kBK); }   // per query block
+size_t oz_table_bytes(int64_t npad, bool pairs) {   // per query block
+    return pairs ? (size_t)kKzt2 * (size_t)(npad / kBK / 2) : (size_t)kKzt * (size_t)(npad / kBK);
+}
 
 hipError_t launch_kstar_table(hipStream_t s, const char *koz, const float *qx, const float *qy, int64_t m,
-                              int64_t npad, double ell, int64_t nq, char *kzt) {
+                              int64_t npad, double ell, int64_t nq, char *kzt, bool pairs) {
     if (m <= 0 || nq <= 0) return hipSuccess;
     const double cexp = -1.0 / (2.0 * ell * ell * 0.69314718055994530942);
     const int nkt = (int)(npad / kBK);
-    hipLaunchKernelGGL(kstar_table_kernel, dim3((unsigned)nkt, (unsigned)nq), dim3(kOzThreads), 0, s, koz, qx, qy, m,
-                       nkt, cexp, kzt);
+    if (pairs) {
+        hipLaunchKernelGGL(kstar_table2_kernel, dim3((unsigned)(nkt / 2), (unsigned)std::min<int64_t>(nq, kMaxGridY)),
+                           dim3(kOzThreads), 0, s, koz, qx, qy, m, nkt / 2, nq, cexp, kzt);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(kstar_table_kernel, dim3((unsigned)nkt, (unsigned)std::min<int64_t>(nq, kMaxGridY)),
+                       dim3(kOzThreads), 0, s, koz, qx, qy, m, nkt, nq, cexp, kzt);
     return hipGetLastError();
 }
 }  // namespace sbo

@@ -129,7 +129,13 @@ sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_
 // 2048 level's products stay dgemms
 constexpr int64_t kInvOzMinSplit = 4096;
 bool oz_level(const sbo_ctx *ctx, int64_t h, int64_t m) {
-    return ctx->inv_oz != 0 && h >= kInvOzMinSplit && h <= 16384 && m <= 16384;
+    return ctx->inv_oz != 0 && !ctx->inv_oz_off && h >= kInvOzMinSplit && h <= 16384 && m <= 16384;
+}
+// does the recursive inverse of n columns slice any of its products?
+bool inverse_sliced(const sbo_ctx *ctx, int64_t n) {
+    if (n <= ctx->inv_base) return false;
+    const int64_t h = ((n + ctx->inv_base - 1) / ctx->inv_base + 1) / 2 * ctx->inv_base, m = n - h;
+    return oz_level(ctx, h, m) || inverse_sliced(ctx, h) || inverse_sliced(ctx, m);
 }
 
 // A^-1 (recursion scratch scr), then S = B A^-1
@@ -525,6 +531,21 @@ bool probe_due(const sbo_ctx *ctx) {
            (ctx->n - ctx->probe_n) * 100 >= ctx->probe_n * (int64_t)ctx->reprobe_pct;
 }
 
+// The precise operand's buffers for npad rows, keeping the row blocks below
+// I0 (grow_keep copies on `stream` and waits for it: the fit reserves them
+// before it forks work onto aux_stream, so that the fork is not serialised).
+sbo_status reserve_precise(sbo_ctx *ctx, int64_t npad, int64_t I0) {
+    if (ctx->precise_kernel >= 1) {
+        SBO_HIP(grow_keep(ctx, ctx->aoz, sbo::oz_operand_bytes(npad), sbo::oz_operand_bytes(I0 * sbo::kBM)));
+        SBO_HIP(grow_keep(ctx, ctx->eoz, sbo::oz_exp_bytes(npad), sbo::oz_exp_bytes(I0 * sbo::kBM)));
+        SBO_HIP(ctx->koz.reserve(sbo::oz_coord_bytes(npad)));
+    } else {
+        SBO_HIP(grow_keep(ctx, ctx->a64, sbo::f64_operand_bytes(npad), sbo::f64_operand_bytes(I0 * sbo::kBM)));
+        SBO_HIP(ctx->kc64.reserve(sbo::f64_coord_bytes(npad)));
+    }
+    return SBO_OK;
+}
+
 // The precise sweep's operand (SBO_OPT_PRECISE_KERNEL: f64 tiles or int8
 // digit tiles) for row blocks >= I0 of npad rows, from the f64 inverse and
 // alpha64, on stream s (the buffers grow keeping the row blocks below I0).
@@ -536,7 +557,7 @@ sbo_status pack_precise(sbo_ctx *ctx, hipStream_t s, int64_t npad, int64_t I0) {
         SBO_HIP(ctx->koz.reserve(sbo::oz_coord_bytes(npad)));
         SBO_HIP(sbo::launch_pack_oz(s, ctx->Linv.as<double>(), ctx->cap, ctx->n, npad, I0, sf2, ctx->x.as<float>(),
                                     ctx->y.as<float>(), ctx->alpha64.as<double>(), ctx->aoz.as<char>(),
-                                    ctx->eoz.as<int>(), ctx->koz.as<char>()));
+                                    ctx->eoz.as<int>(), ctx->koz.as<char>(), ctx->precise_kernel == 4));
     } else {
         SBO_HIP(grow_keep(ctx, ctx->a64, sbo::f64_operand_bytes(npad), sbo::f64_operand_bytes(I0 * sbo::kBM)));
         SBO_HIP(ctx->kc64.reserve(sbo::f64_coord_bytes(npad)));
@@ -544,6 +565,98 @@ sbo_status pack_precise(sbo_ctx *ctx, hipStream_t s, int64_t npad, int64_t I0) {
                                      ctx->y.as<float>(), ctx->alpha64.as<double>(), ctx->a64.as<double>(),
                                      ctx->kc64.as<double>()));
     }
+    return SBO_OK;
+}
+
+// The inverse's accuracy guard (SBO_OPT_INV_CHECK; inv_check.hip).  Launch:
+// on chk_stream once `stream` has finished the inverse, beside the operand
+// packs that follow it (it only reads L and L^-1).  The guard set: a 4 x 4
+// lattice over the training box (its corners included: the largest
+// variances, which the contract normalises by) and kChkTrain training
+// locations, every (n / kChkTrain)-th stored point (the k-d order spreads
+// them over the data in proportion to its density; where the data is dense
+// the variance is smallest and sf2 - |V|^2 cancels hardest).
+// kInvCheckTol = 5e-7: a twentieth of the 1e-5 contract -- the inverse's share
+// adds to the sweeps' own errors, which the probe holds to 5e-6 x the largest
+// whole-grid / probe ratio measured.
+constexpr int kChkGrid = 4, kChkTrain = sbo::kChkQ - kChkGrid * kChkGrid;
+constexpr double kInvCheckTol = 5e-7;
+sbo_status inverse_check_launch(sbo_ctx *ctx) {
+    const int64_t n = ctx->n;
+    if (!ctx->chk_stream) {
+        SBO_HIP(hipStreamCreateWithFlags(&ctx->chk_stream, hipStreamNonBlocking));
+        SBO_HIP(hipEventCreate(&ctx->ev_chk0));
+        SBO_HIP(hipEventCreate(&ctx->ev_chk1));
+    }
+    SBO_HIP(ctx->chk.reserve(sbo::inv_check_bytes(n)));
+    float *q = nullptr;
+    double *cs = nullptr;
+    SBO_HIP(sbo::launch_inv_check(ctx->chk_stream, nullptr, nullptr, 0, n, nullptr, nullptr, 0.0, 0.0,
+                                  ctx->chk.as<void>(), &q, &cs));
+    static thread_local std::vector<float> hq;   // (lives until the copy below has run)
+    hq.assign(2 * kChkGrid * kChkGrid, 0.0f);
+    for (int i = 0; i < kChkGrid; ++i)
+        for (int j = 0; j < kChkGrid; ++j) {
+            hq[i * kChkGrid + j] = ctx->bbox[0] + (ctx->bbox[1] - ctx->bbox[0]) * (float)j / (float)(kChkGrid - 1);
+            hq[kChkGrid * kChkGrid + i * kChkGrid + j] =
+                ctx->bbox[2] + (ctx->bbox[3] - ctx->bbox[2]) * (float)i / (float)(kChkGrid - 1);
+        }
+    SBO_HIP(hipEventRecord(ctx->ev_panel, ctx->stream));   // the inverse is done
+    SBO_HIP(hipStreamWaitEvent(ctx->chk_stream, ctx->ev_panel, 0));
+    SBO_HIP(hipEventRecord(ctx->ev_chk0, ctx->chk_stream));
+    constexpr int G = kChkGrid * kChkGrid, Q = sbo::kChkQ;
+    SBO_HIP(hipMemcpyAsync(q, hq.data(), sizeof(float) * G, hipMemcpyHostToDevice, ctx->chk_stream));
+    SBO_HIP(hipMemcpyAsync(q + Q, hq.data() + G, sizeof(float) * G, hipMemcpyHostToDevice, ctx->chk_stream));
+    // training locations: every stride-th stored point (n > kChkTrain here;
+    // fewer points repeat the last one)
+    const int64_t stride = std::max<int64_t>(1, n / kChkTrain);
+    const int64_t mt = std::min<int64_t>(kChkTrain, (n - stride / 2 + stride - 1) / stride);
+    SBO_HIP(hipMemcpy2DAsync(q + G, sizeof(float), ctx->x.as<float>() + stride / 2, sizeof(float) * stride,
+                             sizeof(float), (size_t)mt, hipMemcpyDeviceToDevice, ctx->chk_stream));
+    SBO_HIP(hipMemcpy2DAsync(q + Q + G, sizeof(float), ctx->y.as<float>() + stride / 2, sizeof(float) * stride,
+                             sizeof(float), (size_t)mt, hipMemcpyDeviceToDevice, ctx->chk_stream));
+    for (int64_t c = G + mt; c < Q; ++c) {
+        SBO_HIP(hipMemcpyAsync(q + c, q + G + mt - 1, sizeof(float), hipMemcpyDeviceToDevice, ctx->chk_stream));
+        SBO_HIP(hipMemcpyAsync(q + Q + c, q + Q + G + mt - 1, sizeof(float), hipMemcpyDeviceToDevice,
+                               ctx->chk_stream));
+    }
+    const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
+    SBO_HIP(sbo::launch_inv_check(ctx->chk_stream, ctx->Linv.as<double>(), ctx->L.as<float>(), ctx->cap, n,
+                                  ctx->x.as<float>(), ctx->y.as<float>(), sf2, ctx->hyper.length_scale,
+                                  ctx->chk.as<void>(), nullptr, nullptr));
+    SBO_HIP(hipEventRecord(ctx->ev_chk1, ctx->chk_stream));
+    return SBO_OK;
+}
+// Wait for the launched check and fill r (err, err_grid, err_train, var_max, ms).
+sbo_status inverse_check_read(sbo_ctx *ctx, sbo_inv_check &r) {
+    float *q = nullptr;
+    double *cs = nullptr;
+    SBO_HIP(sbo::launch_inv_check(ctx->chk_stream, nullptr, nullptr, 0, ctx->n, nullptr, nullptr, 0.0, 0.0,
+                                  ctx->chk.as<void>(), &q, &cs));
+    constexpr int G = kChkGrid * kChkGrid, Q = sbo::kChkQ;
+    double h[2 * Q];
+    SBO_HIP(hipMemcpyAsync(h, cs, sizeof(h), hipMemcpyDeviceToHost, ctx->chk_stream));
+    SBO_HIP(hipStreamSynchronize(ctx->chk_stream));
+    float ms = 0.0f;
+    SBO_HIP(hipEventElapsedTime(&ms, ctx->ev_chk0, ctx->ev_chk1));
+    const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
+    double dmax[2] = {0.0, 0.0}, vmax[2] = {0.0, 0.0};
+    bool finite = true;
+    for (int c = 0; c < Q; ++c) {
+        const int part = c < G ? 0 : 1;
+        finite = finite && std::isfinite(h[2 * c]) && std::isfinite(h[2 * c + 1]);
+        dmax[part] = std::max(dmax[part], std::fabs(h[2 * c]));        // |d var| = ||V1|^2 - |V0|^2|
+        vmax[part] = std::max(vmax[part], sf2 - h[2 * c + 1]);          // var from the refined V1
+    }
+    auto rel = [](double d, double v) { return v > 0.0 ? d / v : (d > 0.0 ? HUGE_VAL : 0.0); };
+    r.ran = 1;
+    r.m = Q;
+    r.err = finite ? rel(std::max(dmax[0], dmax[1]), std::max(vmax[0], vmax[1])) : HUGE_VAL;
+    r.err_grid = finite ? rel(dmax[0], vmax[0]) : HUGE_VAL;
+    r.err_train = finite ? rel(dmax[1], vmax[1]) : HUGE_VAL;
+    r.var_max = std::max(vmax[0], vmax[1]);
+    r.tol = kInvCheckTol;
+    r.ms = ms;
     return SBO_OK;
 }
 
@@ -578,7 +691,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                       sizeof(float) * old_tiles * sbo::kTileFloats));
     SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
     rocblas_int hinfo = 0;
-    bool alpha_aux = false, kcoord_pending = false, x3_planes_aux = false, packs_aux = false;
+    bool alpha_aux = false, kcoord_pending = false, x3_planes_aux = false, packs_aux = false, chk_pending = false;
     // the inverse's first half ran beside the Cholesky (blocked_potrf): its
     // info slots 1 .. inv_slot stay, the rest are cleared
     const bool early = ctx->inverse_bits == 64 && ctx->inverse_rec && !incr && ctx->early_inv_n == n;
@@ -665,6 +778,16 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             }
         }
         ctx->linv_n = n;
+        // the inverse's accuracy guard, on its own stream beside what follows
+        if (!incr && (ctx->inv_check == 2 || ctx->inv_oz_off ||
+                      (ctx->inv_check == 1 && ctx->inverse_rec && !early && inverse_sliced(ctx, n)))) {
+            ctx->chk_res = sbo_inv_check{};
+            ctx->chk_res.digits = (ctx->inverse_rec && !early && inverse_sliced(ctx, n)) ? ctx->inv_oz : 0;
+            if (sbo_status st = inverse_check_launch(ctx)) return st;
+            chk_pending = true;
+        } else if (!incr) {
+            ctx->chk_res = sbo_inv_check{};
+        }
         // alpha = K^-1 (y - m0) = L^-T L^-1 (y - m0), in f64 from the f64
         // inverse: two triangular matrix-vector products (bandwidth-bound and
         // parallel, unlike the two sequential triangular solves of spotrs),
@@ -731,6 +854,8 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             ctx->x3_I0 = xI0;
         }
 
+        if (eager_f64)   // (before the fork: a growing operand copies and waits on `stream`)
+            if (sbo_status st = reserve_precise(ctx, npad, std::max<int64_t>(ctx->a64_I0, 0))) return st;
         SBO_HIP(sbo::launch_pack_tiles(ctx->stream, Li, ld, n, npad, I0, sf2, ctx->aug.as<float>()));
         if (eager_x3 || eager_f64) {
             SBO_HIP(hipEventRecord(ctx->ev_panel, ctx->stream));
@@ -839,6 +964,25 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     } else {
         ctx->x3_I0 = std::min(ctx->x3_I0, I0);  // the split operand is derived lazily (run_tick)
         if (!incr && ctx->a64_I0 != INT64_MAX) ctx->a64_I0 = 0;
+    }
+    if (chk_pending) {
+        sbo_inv_check r = ctx->chk_res;
+        if (sbo_status st = inverse_check_read(ctx, r)) return st;
+        r.err_fallback = -1.0;
+        ctx->chk_res = r;
+        if (!(r.err <= r.tol) && r.digits != 0 && !ctx->inv_oz_off) {
+            // the sliced inverse misses the guard's bound: the fit again with
+            // dgemm products (checked too), reported as fired
+            ctx->inv_oz_off = true;
+            const sbo_status st = refresh_operand(ctx, 0);
+            ctx->inv_oz_off = false;
+            const sbo_inv_check f = ctx->chk_res;
+            ctx->chk_res = r;
+            ctx->chk_res.fired = 1;
+            ctx->chk_res.err_fallback = f.ran ? f.err : -1.0;
+            ctx->chk_res.ms = r.ms + f.ms;
+            return st;
+        }
     }
     ctx->fitted = true;
     return probe_precision(ctx);
@@ -1352,7 +1496,8 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     }
     SBO_HIP(ctx->plan_work.reserve(sbo::predict_work_bytes(ctx->npad, ms, P)));
     // (the K* table's precise sweep plans each chunk of query blocks itself)
-    const bool chunked = precise && ctx->precise_kernel == 3 && !cost;
+    const bool chunked = precise && (ctx->precise_kernel == 3 || ctx->precise_kernel == 4) && !cost;
+    const bool pairs = ctx->precise_kernel == 4;
     if (!chunked)
         SBO_HIP(sbo::launch_plan(ctx->stream, ctx->kbox.as<float4>(), ctx->npad, qx, qy, ms, ldp,
                                  (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan,
@@ -1383,7 +1528,7 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
             // 33 chunks of 244 query blocks).  An item's result does not
             // depend on the chunking (plans are per query block).
             const int64_t nQ = (ms + sbo::kBN - 1) / sbo::kBN;
-            const size_t per_qb = sbo::oz_table_bytes(ctx->npad);
+            const size_t per_qb = sbo::oz_table_bytes(ctx->npad, pairs);
             size_t budget = (size_t)ctx->table_mb << 20;
             if (budget == 0) {
                 // auto: 1/32 of the free device memory, within [256 MiB, 8 GiB]
@@ -1405,12 +1550,13 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
                                          ctx->prof ? ctx->counters.as<unsigned long long>() : nullptr, P,
                                          ctx->plan_work.as<void>(), ctx->plan_work.capacity()));
                 SBO_HIP(sbo::launch_kstar_table(ctx->stream, ctx->koz.as<char>(), qx + c0, qy + c0, mc, ctx->npad,
-                                                ctx->hyper.length_scale, nq, ctx->kzt.as<char>()));
+                                                ctx->hyper.length_scale, nq, ctx->kzt.as<char>(), pairs));
                 sbo::plan_views(ctx->npad, mc, P, ctx->plan_work.as<void>(), &desc, &tl, &seg);
                 SBO_HIP(sbo::launch_predict_oz(ctx->stream, ctx->aoz.as<char>(), ctx->eoz.as<int>(),
                                                ctx->koz.as<char>(), desc, tl, seg, P, (int)(nIc * nq), (int)nIc,
                                                qx + c0, qy + c0, mc, ldp, ctx->hyper.length_scale,
-                                               ctx->hyper.prior_mean, pd + c0, md + c0, 3, ctx->kzt.as<char>()));
+                                               ctx->hyper.prior_mean, pd + c0, md + c0, ctx->precise_kernel,
+                                               ctx->kzt.as<char>()));
             }
         } else {
         sbo::plan_views(ctx->npad, ms, P, ctx->plan_work.as<void>(), &desc, &tl, &seg);
@@ -1572,6 +1718,10 @@ SBO_API void sbo_destroy(sbo_ctx *ctx) {
     if (ctx->ev_inv) (void)hipEventDestroy(ctx->ev_inv);
     if (ctx->blas_inv) rocblas_destroy_handle(ctx->blas_inv);
     if (ctx->inv_stream) (void)hipStreamDestroy(ctx->inv_stream);
+    if (ctx->chk_stream) (void)hipStreamSynchronize(ctx->chk_stream);
+    if (ctx->ev_chk0) (void)hipEventDestroy(ctx->ev_chk0);
+    if (ctx->ev_chk1) (void)hipEventDestroy(ctx->ev_chk1);
+    if (ctx->chk_stream) (void)hipStreamDestroy(ctx->chk_stream);
     if (ctx->blas) rocblas_destroy_handle(ctx->blas);
     if (ctx->host_key) (void)hipHostFree(ctx->host_key);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
@@ -2159,18 +2309,27 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             return SBO_OK;
         case SBO_OPT_PRECISE_KERNEL:
 #ifdef SBO_DIAG
-            SBO_CHECK(value == 0 || value == 1 || value == 3 || value == 9, SBO_E_INVAL,
-                      "SBO_OPT_PRECISE_KERNEL: 0, 1, 3 or 9 (diagnostic)");
+            SBO_CHECK(value == 0 || value == 1 || value == 3 || value == 4 || value == 9, SBO_E_INVAL,
+                      "SBO_OPT_PRECISE_KERNEL: 0, 1, 3, 4 or 9 (diagnostic)");
 #else
-            SBO_CHECK(value == 0 || value == 1 || value == 3, SBO_E_INVAL,
-                      "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA), 1 (int8) or 3 (int8, K* table)");
+            SBO_CHECK(value == 0 || value == 1 || value == 3 || value == 4, SBO_E_INVAL,
+                      "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA), 1 (int8), 3 (int8, K* table) or 4 (int8, "
+                      "k-tile pairs)");
 #endif
-            if ((ctx->precise_kernel == 0) != (value == 0)) ctx->a64_I0 = 0;   // the other operand: derive it all
+            {
+                // the operand layout each kernel reads: f64 tiles, int8 tiles, int8 pairs
+                auto layout = [](int64_t k) { return k == 0 ? 0 : k == 4 ? 2 : 1; };
+                if (layout(ctx->precise_kernel) != layout(value)) ctx->a64_I0 = 0;   // derive it all
+            }
             ctx->precise_kernel = (int)value;
             return SBO_OK;
         case SBO_OPT_INV_OZ:
             SBO_CHECK(value == 0 || value == 5 || value == 6, SBO_E_INVAL, "SBO_OPT_INV_OZ must be 0, 5 or 6");
             ctx->inv_oz = (int)value;
+            return SBO_OK;
+        case SBO_OPT_INV_CHECK:
+            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_INV_CHECK must be 0, 1 or 2");
+            ctx->inv_check = (int)value;
             return SBO_OK;
         case SBO_OPT_TABLE_MB:
             SBO_CHECK(value >= 0 && value <= (int64_t(1) << 20), SBO_E_INVAL,
@@ -2221,6 +2380,25 @@ SBO_API sbo_status sbo_get_precision(const sbo_ctx *ctx, int *precise, double *p
     if (probe_err) *probe_err = ctx->probe_n ? ctx->probe_err : -1.0;
     if (probe_var_min) *probe_var_min = ctx->probe_n ? ctx->probe_vmin : -1.0;
     if (probe_var_max) *probe_var_max = ctx->probe_n ? ctx->probe_vmax : -1.0;
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_trim(sbo_ctx *ctx) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_HIP(hipSetDevice(ctx->device));
+    SBO_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->aux_stream) SBO_HIP(hipStreamSynchronize(ctx->aux_stream));
+    if (ctx->inv_stream) SBO_HIP(hipStreamSynchronize(ctx->inv_stream));
+    if (ctx->chk_stream) SBO_HIP(hipStreamSynchronize(ctx->chk_stream));
+    for (sbo::DevBuf *b : {&ctx->scratch, &ctx->gzws, &ctx->gzws_aux, &ctx->chk, &ctx->restage, &ctx->kzt, &ctx->qcost})
+        b->release();
+    return SBO_OK;
+}
+
+SBO_API sbo_status sbo_get_inverse_check(const sbo_ctx *ctx, sbo_inv_check *out) {
+    if (!ctx || !out) return SBO_E_INVAL;
+    if (!ctx->fitted) return SBO_E_STATE;
+    *out = ctx->chk_res;
     return SBO_OK;
 }
 

@@ -25,6 +25,9 @@ constexpr int kBK = 64;
 constexpr int kTileFloats = kBM * kBK;           // one packed [BK][BM] tile
 constexpr int kTilesPerRowBlockStep = kBM / kBK;  // k-tiles added per row block
 constexpr int kAcqThreads = 256;
+// grid.y / grid.z of a launch stay below the device limit (65535 on gfx950);
+// kernels that index columns by blockIdx.y loop over j += gridDim.y
+constexpr int64_t kMaxGridY = 65535;
 
 __host__ __device__ inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
@@ -112,6 +115,14 @@ struct sbo_ctx {
     int64_t inv_base = 2048;     // SBO_OPT_INV_BASE: dtrtri base case of the recursive inverse
     int64_t inv_panels = 16;     // SBO_OPT_INV_PANELS: dgemm panels per product of the recursion
     int inv_oz = 6;              // SBO_OPT_INV_OZ: digits of the int8-sliced top-level products (0: dgemm)
+    bool inv_oz_off = false;     // (set while a fit redoes its inverse with dgemm products: the guard fired)
+    // the inverse's accuracy guard (SBO_OPT_INV_CHECK, inv_check.hip): its
+    // stream, workspace, timing events and the last result
+    int inv_check = 1;           // SBO_OPT_INV_CHECK: 0 off, 1 after sliced inverses, 2 after every full inverse
+    hipStream_t chk_stream = nullptr;
+    hipEvent_t ev_chk0 = nullptr, ev_chk1 = nullptr;
+    sbo::DevBuf chk;
+    sbo_inv_check chk_res{};     // (ran = 0: none since the last fit)
     int64_t early_inv_n = 0;     // n of a factor whose inverse's first half is done (refresh_operand finishes it)
     int inv_slot = 0;            // info slots the first half used (1 .. inv_slot)
     std::string err;
@@ -396,26 +407,28 @@ hipError_t launch_predict_f64(hipStream_t s, const double *a64, const double *kc
                               const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
                               double *mean);
 // The int8 sliced precise sweep (predict_oz.hip, SBO_OPT_PRECISE_KERNEL 1):
-// A = sf2 L^-1 from the fit's f64 inverse as five base-128 int8 digit slices
-// per 16-row block and k-tile (80 KiB per packed tile) with a power-of-two
-// exponent per block (oz_exp_bytes: 16 int32 per tile), per k-tile x, y (f32)
-// and sf2 alpha (f64).  The sweep reads the same plan as launch_predict_f64 and
+// A = sf2 L^-1 from the fit's f64 inverse as five balanced base-256 int8
+// digit slices per 16-row block and k-tile (80 KiB per packed tile) with a
+// power-of-two exponent per block (oz_exp_bytes: 16 int32 per tile), per
+// k-tile x, y (f64 and f32) and sf2 alpha (f64).  The sweep reads the same plan as launch_predict_f64 and
 // writes the same f64 partials and mean.
 size_t oz_operand_bytes(int64_t npad);
 size_t oz_exp_bytes(int64_t npad);
 size_t oz_coord_bytes(int64_t npad);
 hipError_t launch_pack_oz(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
                           double sf2, const float *x, const float *y, const double *alpha, char *aoz, int *eoz,
-                          char *koz);
+                          char *koz, bool pairs = false);
 hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, const char *koz, const int4 *desc,
                              const unsigned short *tl, const int *seg, int P, int n_items, int nI, const float *qx,
                              const float *qy, int64_t m, int64_t ldp, double ell, double m0, double *part,
                              double *mean, int variant = 1, const char *kzt = nullptr);
 // The K* table (SBO_OPT_PRECISE_KERNEL 3): bytes per query block, and the
 // table of nq query blocks of the queries qx/qy (m of them) for every k-tile.
-size_t oz_table_bytes(int64_t npad);
+// pairs (SBO_OPT_PRECISE_KERNEL 4): exponents shared by k-tile pairs (2p,
+// 2p + 1) -- the operand (launch_pack_oz), the table and the sweep (variant 4)
+size_t oz_table_bytes(int64_t npad, bool pairs = false);
 hipError_t launch_kstar_table(hipStream_t s, const char *koz, const float *qx, const float *qy, int64_t m,
-                              int64_t npad, double ell, int64_t nq, char *kzt);
+                              int64_t npad, double ell, int64_t nq, char *kzt, bool pairs = false);
 // The int8-sliced f64 GEMM (ozgemm.hip): C (m x n, ldc) = alpha op(A) op(B)
 // (+ C), column-major f64, op(A) m x K (A itself K x m with kGzTransA), op(B)
 // K x n (n x K with kGzTransB); a triangular operand's zero part is not read;
@@ -433,6 +446,18 @@ size_t gz_workspace_bytes(int64_t m, int64_t n, int64_t K, int nd);
 hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, const double *B, int64_t ldb,
                           int64_t m, int64_t n, int64_t K, double alpha, double *C, int64_t ldc, unsigned flags,
                           char *ws);
+// The fit's accuracy guard of the f64 inverse (inv_check.hip): on kChkQ
+// queries (coordinates at *qxy: x[kChkQ] then y[kChkQ], filled by the caller
+// before the launch) V0 = Linv Kq and one refinement against the f32 factor
+// L, dV = Linv (Kq - L V0), both lower-triangular column-major with lda ld;
+// *colsums = per column (sum dV (2 V0 + dV), sum (V0 + dV)^2).  work:
+// inv_check_bytes(n); with Linv null only the pointers are set.
+constexpr int kChkQ = 64;
+int64_t inv_check_rows(int64_t n);
+size_t inv_check_bytes(int64_t n);
+hipError_t launch_inv_check(hipStream_t s, const double *Linv, const float *L, int64_t ld, int64_t n,
+                            const float *x, const float *y, double sf2, double ell, void *work, float **qxy,
+                            double **colsums);
 // Morton ordering of the queries (query_order.hip): workspace of
 // query_order_bytes(m); returns the permutation and the gathered coordinates
 // (all inside the workspace).

@@ -146,10 +146,15 @@ def allreduce_key_dev(key_dev, reduce_fn, out=None, group=None):
     """The same exchange with the combine left on the device (VERDICT r3
     weak-6: no per-tick D2H sync and host combine): one all-gather of the
     16-byte keys into a device buffer, then ``reduce_fn(gathered, out)``
-    (``Context.reduce_keys``: one workgroup on the library's stream, ordered
-    after the all-gather by syncing the streams) writes the combined key to a
-    (2,) int64 device tensor, which is returned.  Read it (key_tensor_to_pairs)
-    only when the caller needs the index on the host."""
+    (``Context.reduce_keys``: one workgroup on the library's stream) writes
+    the combined key to a (2,) int64 device tensor, which is returned.  The
+    all-gather leaves ``gathered`` on torch's current stream; reduce_keys makes
+    the library's stream wait for it (an event wait when the context runs on
+    another torch stream, a host sync of the current stream when it runs on
+    its own), records ``gathered`` on the library stream for the caching
+    allocator, and orders the current stream after the reduce.  Read the
+    result (key_tensor_to_pairs) only when the caller needs the index on the
+    host."""
     import torch
     import torch.distributed as dist
     world = _group_size(group)

@@ -73,11 +73,16 @@ class Context:
         N.check(self._lib.sbo_create(int(device), ctypes.byref(h)))
         self.handle = h
         self.device = device
+        self._torch_stream = None   # the torch stream the context runs on (set_stream), None: its own
 
     def set_stream(self, stream) -> None:
         """Bind to a HIP stream (a torch.cuda.Stream, a raw handle int, or None)."""
         raw = getattr(stream, "cuda_stream", stream)
         N.check(self._lib.sbo_set_stream(self.handle, ctypes.c_void_p(raw) if raw else None), self.handle)
+        if raw and not hasattr(stream, "cuda_stream"):
+            import torch
+            stream = torch.cuda.ExternalStream(int(raw), device=f"cuda:{self.device}")
+        self._torch_stream = stream if raw else None
 
     # ------------------------------------------------- frontier, 8(f)1
     def frontier(self, Dx, Dy, safe, width: int, height: int) -> np.ndarray:
@@ -118,7 +123,24 @@ class Context:
             if out is None:
                 out = torch.empty(2, dtype=torch.int64, device=keys.device)
             fl = N.SBO_DEVICE_PTRS | (N.SBO_ASYNC if async_ else 0)
+            # keys / out live on torch's current stream (an all-gather wrote
+            # keys there): order the library's stream after it, keep keys
+            # alive for the allocator until the reduce ran, and order the
+            # current stream after the reduce for whoever reads out
+            cur = torch.cuda.current_stream(keys.device)
+            lib_s = self._torch_stream
+            if lib_s is None:
+                # the library's own stream, which torch cannot wait on: sync
+                # the current stream before and the library's after (no async)
+                cur.synchronize()
+                fl = N.SBO_DEVICE_PTRS
+            elif lib_s.cuda_stream != cur.cuda_stream:
+                lib_s.wait_stream(cur)
             self.check(self._lib.sbo_keys_reduce(self.handle, _ptr(keys), n, _ptr(out), fl))
+            if lib_s is not None and lib_s.cuda_stream != cur.cuda_stream:
+                keys.record_stream(lib_s)
+                out.record_stream(lib_s)
+                cur.wait_stream(lib_s)
             return out
         k = np.ascontiguousarray(np.asarray(keys, np.int64).reshape(-1))
         r = N.sbo_key()
@@ -275,6 +297,19 @@ class TerrainMapper:
         p = sbo_probe()
         self.ctx.check(self._lib.sbo_get_probe(self.ctx.handle, ctypes.byref(p)))
         return {f: getattr(p, f) for f, _ in sbo_probe._fields_}
+
+    def inverse_check(self) -> dict:
+        """The fit's inverse accuracy guard (sbo_get_inverse_check,
+        SBO_OPT_INV_CHECK): its normwise variance effect, whether it fired and
+        recomputed the inverse with dgemm products, and its device time."""
+        from ._native import sbo_inv_check
+        r = sbo_inv_check()
+        self.ctx.check(self._lib.sbo_get_inverse_check(self.ctx.handle, ctypes.byref(r)))
+        return {f: getattr(r, f) for f, _ in sbo_inv_check._fields_}
+
+    def trim(self) -> None:
+        """Release the workspaces kept between calls (sbo_trim)."""
+        self.ctx.check(self._lib.sbo_trim(self.ctx.handle))
 
     def set_option(self, option: int, value: int) -> None:
         self.ctx.check(self._lib.sbo_set_option(self.ctx.handle, int(option), int(value)))

@@ -1,0 +1,175 @@
+"""The fit's run-time accuracy guard of its f64 inverse (SBO_OPT_INV_CHECK,
+round 5) and the posterior on ill-conditioned K where the int8-sliced inverse
+runs (N > 4096: csrc/ozgemm.hip at the recursion's splits >= 4096; N = 16384
+slices both top levels).
+
+The sliced GEMM's error is relative to row and column maxima, so its effect
+grows with cond(K), which the mapper's configuration sets
+(config/lpsc.yaml:35-37: noise_level, length_scale).  The precision probe
+cannot see it (its fast and precise sweeps read the same inverse); the guard
+measures it on 64 queries by one f64 refinement against the f32 factor and
+falls back to dgemm products above 5e-7.  Contract: mu and var within 1e-5
+normwise of the fp64 oracle given the device factor (alpha solved in f64 from
+it), under default options -- whichever sweep the probe picks.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O  # noqa: E402
+from safe_bayesian_optimization_amd import TerrainMapper, synthetic  # noqa: E402
+from safe_bayesian_optimization_amd import _native as N  # noqa: E402
+from safe_bayesian_optimization_amd.terrain import Hyper, synthetic_box  # noqa: E402
+
+REL_TOL = 1e-5
+CHECK_TOL = 5e-7
+
+
+@pytest.fixture(scope="module")
+def mapper():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    O.set_threads(16)
+    gm = TerrainMapper(0)
+    yield gm
+    gm.close()
+
+
+def f32(a):
+    return np.ascontiguousarray(a, np.float32)
+
+
+def nrel(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def oracle64(gm, wl):
+    """fp64 posterior of the device's own f32 factor, alpha solved from it in f64."""
+    from scipy.linalg import solve_triangular
+    L, _ = gm.factor()
+    o = gm.order()
+    L64 = L.astype(np.float64)
+    del L
+    h = wl.hyper
+    r = f32(wl.obs)[o].astype(np.float64) - h.prior_mean
+    alpha = solve_triangular(L64.T, solve_triangular(L64, r, lower=True), lower=False)
+    Lcm = O.colmajor_from_lower(L64)
+    del L64
+    return O.predict(Lcm, alpha, f32(wl.x)[o], f32(wl.y)[o], f32(wl.qx), f32(wl.qy), h.length_scale, h.sf2,
+                     h.prior_mean)
+
+
+def workload(n, box, hyper):
+    """The domain and data of the default hyper-parameters (l = 0.4: the box,
+    or a square of ~8 points per 0.4^2), fitted with `hyper` -- l = 1.6 there
+    holds 128 points per l^2; a 32 x 16 query grid (the oracle costs N^2 per
+    query)."""
+    wl = synthetic_box(n, 32, 16, seed=n) if box else synthetic(n, 32, 16, seed=n + 5)
+    wl.hyper = hyper
+    return wl
+
+
+CASES = [
+    ("l1.6", 8192, False, Hyper(length_scale=1.6)),
+    ("l1.6", 16384, False, Hyper(length_scale=1.6)),
+    ("box_sn0.01", 8192, True, Hyper(noise_level=0.01)),
+    ("box_sn0.01", 16384, True, Hyper(noise_level=0.01)),
+    ("box_sn0.001", 16384, True, Hyper(noise_level=0.001)),
+    ("box", 12288, True, Hyper()),
+]
+
+
+@pytest.mark.parametrize("name,n,box,hyper", CASES, ids=[f"{c[0]}-{c[1]}" for c in CASES])
+def test_ill_conditioned_sliced_inverse(mapper, name, n, box, hyper):
+    """Default options (six-digit sliced inverse, the guard on, the probe
+    picking the sweep): the guard ran on the sliced inverse, and mu / var meet
+    the contract against the oracle whatever it decided."""
+    wl = workload(n, box, hyper)
+    gm = TerrainMapper(0, hyper, ctx=mapper.ctx)
+    gm.fit(wl.x, wl.y, wl.obs)
+    chk = gm.inverse_check()
+    precise, perr, _, _ = gm.precision()
+    mu, sd = gm.predict(wl.qx, wl.qy)
+    omu, ovar = oracle64(gm, wl)
+    emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
+    print(f"{name} n={n}: check err {chk['err']:.2e} (grid {chk['err_grid']:.2e} train {chk['err_train']:.2e}) "
+          f"fired {chk['fired']} fallback {chk['err_fallback']:.2e} {chk['ms']:.2f} ms; probe {perr:.2e} "
+          f"precise {precise}; mu {emu:.2e} var {evar:.2e}")
+    assert chk["ran"] == 1 and chk["digits"] == 6 and chk["m"] == 64
+    assert chk["tol"] == CHECK_TOL
+    assert chk["fired"] == (0 if chk["err"] <= CHECK_TOL else 1)
+    if chk["fired"]:
+        assert chk["err_fallback"] <= CHECK_TOL
+    assert emu < REL_TOL and evar < REL_TOL
+
+
+def test_guard_fires_on_five_digits(mapper):
+    """SBO_OPT_INV_OZ = 5 on the lpsc box at N = 16384 moved the variance by
+    3.7e-6 in round 4 (profiles/r4_inv_oz_ab.log): the guard must see it, redo
+    the inverse with dgemm products (err_fallback: that inverse's own measure,
+    orders below), and the posterior must then meet the contract; with the
+    guard off the five-digit inverse stays and the posterior moves."""
+    wl = workload(16384, True, Hyper())
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    try:
+        gm.set_option(N.SBO_OPT_INV_OZ, 5)
+        gm.fit(wl.x, wl.y, wl.obs)
+        chk = gm.inverse_check()
+        mu, sd = gm.predict(wl.qx, wl.qy)
+        omu, ovar = oracle64(gm, wl)
+        emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
+        print(f"five digits: check err {chk['err']:.2e} fired {chk['fired']} fallback {chk['err_fallback']:.2e} "
+              f"{chk['ms']:.2f} ms; mu {emu:.2e} var {evar:.2e}")
+        assert chk["ran"] == 1 and chk["digits"] == 5
+        assert chk["err"] > CHECK_TOL and chk["fired"] == 1
+        assert 0.0 <= chk["err_fallback"] < CHECK_TOL / 10
+        assert emu < REL_TOL and evar < REL_TOL
+        # the guard off: the five-digit inverse is kept (and is visibly worse)
+        gm.set_option(N.SBO_OPT_INV_CHECK, 0)
+        gm.fit(wl.x, wl.y, wl.obs)
+        off = gm.inverse_check()
+        assert off["ran"] == 0 and off["fired"] == 0
+        mu5, sd5 = gm.predict(wl.qx, wl.qy)
+        evar5 = nrel(sd5.astype(np.float64) ** 2, ovar)
+        print(f"five digits, guard off: var {evar5:.2e}")
+        assert evar5 > evar
+    finally:
+        gm.set_option(N.SBO_OPT_INV_OZ, 6)
+        gm.set_option(N.SBO_OPT_INV_CHECK, 1)
+
+
+def test_guard_on_dgemm_inverse_and_appends(mapper):
+    """SBO_OPT_INV_CHECK = 2 checks every full inverse: the dgemm one measures
+    orders below the bound (the guard's own floor); with 1 and SBO_OPT_INV_OZ
+    = 0 it does not run; appends keep the fit's result; below the slicing
+    size (N <= 4096) the default does not run it."""
+    wl = workload(8192, True, Hyper())
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    try:
+        gm.set_option(N.SBO_OPT_INV_OZ, 0)
+        gm.set_option(N.SBO_OPT_INV_CHECK, 2)
+        gm.fit(wl.x, wl.y, wl.obs)
+        chk = gm.inverse_check()
+        print(f"dgemm inverse: check err {chk['err']:.2e} {chk['ms']:.2f} ms")
+        assert chk["ran"] == 1 and chk["digits"] == 0 and chk["fired"] == 0
+        assert chk["err"] < CHECK_TOL / 100
+        gm.set_option(N.SBO_OPT_INV_CHECK, 1)
+        gm.fit(wl.x, wl.y, wl.obs)
+        assert gm.inverse_check()["ran"] == 0
+        gm.set_option(N.SBO_OPT_INV_OZ, 6)
+        gm.fit(wl.x, wl.y, wl.obs)
+        first = gm.inverse_check()
+        assert first["ran"] == 1 and first["digits"] == 6
+        extra = synthetic_box(8, 2, 2, seed=77)
+        gm.append(extra.x, extra.y, extra.obs)
+        assert gm.inverse_check() == first
+        small = workload(4096, True, Hyper())
+        gm.fit(small.x, small.y, small.obs)
+        assert gm.inverse_check()["ran"] == 0
+    finally:
+        gm.set_option(N.SBO_OPT_INV_OZ, 6)
+        gm.set_option(N.SBO_OPT_INV_CHECK, 1)
+    with pytest.raises(N.SboError):
+        gm.set_option(N.SBO_OPT_INV_CHECK, 3)

@@ -96,6 +96,12 @@ def main():
         out["int8_vs_f64_whole_grid_var"] = nrel(v1, v0)
         out["int8_vs_f64_whole_grid_mu"] = nrel(res["kernel1"]["mu"], res["kernel0"]["mu"].astype(np.float64))
         out["speedup"] = out["kernel0"]["sweep_ms"] / out["kernel1"]["sweep_ms"]
+    if "kernel3" in res and "kernel4" in res:   # round 5: the k-tile pair sweep against the table sweep
+        v3 = res["kernel3"]["sd"].astype(np.float64) ** 2
+        v4 = res["kernel4"]["sd"].astype(np.float64) ** 2
+        out["pair_vs_table_whole_grid_var"] = nrel(v4, v3)
+        out["pair_vs_table_whole_grid_mu"] = nrel(res["kernel4"]["mu"], res["kernel3"]["mu"].astype(np.float64))
+        out["pair_speedup"] = out["kernel3"]["sweep_ms"] / out["kernel4"]["sweep_ms"]
     print(json.dumps(out), flush=True)
 
 
