@@ -482,6 +482,17 @@ SBO_API sbo_status sbo_get_inverse_check(const sbo_ctx *ctx, sbo_inv_check *out)
  * the context's streams. */
 SBO_API sbo_status sbo_trim(sbo_ctx *ctx);
 
+/* Startup warm-up for the node's first map (no reference counterpart: the
+ * node pays its first request_terrain_map, node.cpp:568-623, on a cold
+ * process): fits n_cap synthetic points with `hyper` and the context's
+ * options, then sweeps an m_cap-point raster grid with the fast and the
+ * precise sweep, so that every code object a fit and a tick load (the
+ * library's kernels, rocBLAS / rocSOLVER / Tensile) is loaded and the
+ * workspaces are sized for fits of up to n_cap points and ticks of up to
+ * m_cap queries.  The context is left unfitted (as after sbo_create); its
+ * options are unchanged.  Synchronous. */
+SBO_API sbo_status sbo_warmup(sbo_ctx *ctx, int64_t n_cap, int64_t m_cap, sbo_hyper hyper);
+
 /* The sweep the ticks run (precise = 1: the f64 sweep) and the last probe
  * (SBO_OPT_PRECISION): the fast sweep's normwise variance error against the
  * precise one on the 32 x 32 probe grid and that grid's smallest and largest

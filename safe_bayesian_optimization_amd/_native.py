@@ -33,7 +33,7 @@ EXPORTS = (
     "sbo_get_order", "sbo_profile_work", "sbo_profile_mfma", "sbo_debug_x3_stamps", "sbo_get_skip", "sbo_frontier", "sbo_subgoal",
     "sbo_get_bounds", "sbo_get_jitter", "sbo_get_tile_bounds", "sbo_state_bytes", "sbo_export_state", "sbo_import_state", "sbo_query_cost",
     "sbo_polygon_correct", "sbo_polydist", "sbo_point_within", "sbo_project_subgoal", "sbo_get_precision",
-    "sbo_kd_order", "sbo_get_probe", "sbo_keys_reduce", "sbo_get_inverse_check", "sbo_trim",
+    "sbo_kd_order", "sbo_get_probe", "sbo_keys_reduce", "sbo_get_inverse_check", "sbo_trim", "sbo_warmup",
 )
 SBO_OPT_INVERSE_BITS = 1
 SBO_OPT_SPATIAL_ORDER = 2
@@ -189,6 +189,8 @@ def lib():
     L.sbo_get_inverse_check.restype = st
     L.sbo_trim.argtypes = [vp]
     L.sbo_trim.restype = st
+    L.sbo_warmup.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, sbo_hyper]
+    L.sbo_warmup.restype = st
     L.sbo_get_order.argtypes = [vp, vp]
     L.sbo_get_order.restype = st
     L.sbo_kd_order.argtypes = [vp, vp, i64, i64, vp]

@@ -627,6 +627,7 @@ constexpr int kKzt2E = kKzt2Digits;
 constexpr int kKzt2Mu = kKzt2E + kBN * 4;
 constexpr int kKzt2 = kKzt2Mu + kBN * 8;                     // 67072 B per (query block, pair)
 constexpr int kOz2Smem = 2 * kOz2Slot + kKzt2 + 4096;        // two stage slots, the table, the windows
+constexpr int kOz2TableDma = 2 * kOzKDigits + 2;            // DMA instructions per wave per table piece
 static_assert(kOz2Smem <= 160 * 1024, "pair-mode LDS");
 static_assert(kOz2A == 2 * kOzA / 2 && 4 * kOz2A == 2 * kOzTileBytes, "a pair is two kernel-1 tiles");
 
@@ -684,6 +685,9 @@ __device__ __forceinline__ void stage_blocks2(const char *__restrict__ slot, int
 // 2-3 of every pair), so that a wave holds eight f64 accumulator blocks, not
 // sixteen: with sixteen, the pair's two digit sets and the chained levels
 // spilled 72 registers.  The K* table piece is staged once per (pair, half).
+// NOTABLE (diagnostic build only, wrong results): the pair tables after the
+// first are not staged -- the bound on what the table traffic costs.
+template <bool NOTABLE>
 __global__ __launch_bounds__(kOzThreads, 1) void predict_oz2_kernel(
     const char *__restrict__ aoz, const int *__restrict__ eoz, const int4 *__restrict__ desc,
     const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P, int n_items, int nI,
@@ -736,14 +740,17 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz2_kernel(
             SBO_OZ_DMA16(gE + (int64_t)(Tp_) * 64,                                                       \
                          __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kOz2Slot + kOz2A)));    \
     } while (0)
-    // the table piece of (query block qb_, pair pr_)
+    // the table piece of (query block qb_, pair pr_): each wave moves exactly
+    // what it reads itself (its digits, its 16 queries' eK and mean terms) --
+    // kSbo2TableDma instructions -- so a wave may refill the piece as soon
+    // as it has read it, whatever the other waves are doing
 #define SBO_OZ2_TABLE(qb_, pr_)                                                                          \
     do {                                                                                                 \
         const char *z_ = gZ + ((int64_t)(qb_) * npr + (pr_)) * kKzt2;                                    \
         _Pragma("unroll") for (int u_ = 0; u_ < 2 * kOzKDigits; ++u_)                                    \
             SBO_OZ_DMA16(z_ + wave * 8192 + u_ * 1024, lds_tz + (uint32_t)(wave_u * 8192 + u_ * 1024));  \
-        if (wave == 0 && lane < 32) SBO_OZ_DMA16(z_ + kKzt2E, lds_tz + (uint32_t)kKzt2E);               \
-        if (wave == 1) SBO_OZ_DMA16(z_ + kKzt2Mu, lds_tz + (uint32_t)kKzt2Mu);                           \
+        if (lane < 4) SBO_OZ_DMA16(z_ + kKzt2E + wave * 64, lds_tz + (uint32_t)(kKzt2E + wave_u * 64));  \
+        if (lane < 8) SBO_OZ_DMA16(z_ + kKzt2Mu + wave * 128, lds_tz + (uint32_t)(kKzt2Mu + wave_u * 128)); \
     } while (0)
 #define SBO_OZ_DESC_WINDOW(w_)                                                                           \
     do {                                                                                                 \
@@ -805,6 +812,7 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz2_kernel(
     // k item, hp row half, j entries of the item before the current pair, sq
     // stage of the pair in this half, cur slot
     int k = k0, hp = 0, j = 0, sq = 0, cur = 0;
+    bool table_ahead = false;
     for (;;) {
         const int cnt = dc.w & 0xffff;
         // the next stage: the pair's other quarter of this half, the next pair
@@ -848,7 +856,6 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz2_kernel(
                 prn = pair_at(en, dn.x, jn, dn.w & 0xffff, nen);
             }
             SBO_OZ2_STAGE(tile_start(dn.x) + 2 * prn, 2 * hn + sn, cur ^ 1);
-            if (sn == 0) SBO_OZ2_TABLE(dn.y, prn);   // (the current piece was read at this pair-half's first stage)
         }
         const char *slot = smem + cur * kOz2Slot;
         const int I = dc.x;
@@ -863,6 +870,30 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz2_kernel(
             eK = *reinterpret_cast<const int *>(tz + kKzt2E + (wave * 16 + r) * 4);
             if (hp == 0 && I == nI - 1 && g == 0)
                 mu += *reinterpret_cast<const double *>(tz + kKzt2Mu + (wave * 16 + r) * 8);
+            // the NEXT pair-half's piece, two stages ahead (its latency, not
+            // the A stage's, was what the pair sweep waited on: the same sweep
+            // without table traffic ran 1538 against 1907 ms,
+            // profiles/r5_oz_bounds.log): the next pair of this half, this
+            // item's first pair for its second half, or item k + 1's first
+            if (!NOTABLE) {
+                int qbN = -1, prN = 0, neN = 1;
+                if (j + ne < cnt) {
+                    prN = pair_at(e + ne, I, j + ne, cnt, neN);
+                    qbN = dc.y;
+                } else if (hp == 0) {
+                    prN = pr0;
+                    qbN = dc.y;
+                } else if (k + 1 < k1) {
+                    const int4 d2 = desc_at(k + 1);
+                    prN = pair_at(entry_off(d2), d2.x, 0, d2.w & 0xffff, neN);
+                    qbN = d2.y;
+                }
+                if (qbN >= 0) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the piece are done
+                    SBO_OZ2_TABLE(qbN, prN);
+                    table_ahead = true;
+                }
+            }
         }
         if (qq == 0) stage_blocks2<0>(slot, lane, kd, eK, acc);
         else if (qq == 1) stage_blocks2<1>(slot, lane, kd, eK, acc);
@@ -892,7 +923,13 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz2_kernel(
                 }
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // the next stage's A must have landed; the table piece issued this
+        // step may stay in flight until the end of the next one
+        if (table_ahead)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOz2TableDma) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        table_ahead = false;
         __syncthreads();
         if (!more) break;
         if (kn != k) {
@@ -1050,10 +1087,17 @@ hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, con
         return hipGetLastError();
     }
 #endif
+#ifdef SBO_DIAG
+    if (variant == 10) {   // timing bound: pair mode without the table traffic (wrong results)
+        hipLaunchKernelGGL(predict_oz2_kernel<true>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, desc, tl,
+                           seg, P, n_items, nI, m, ldp, m0, part, mean, kzt);
+        return hipGetLastError();
+    }
+#endif
     if (variant == 4) {   // pair mode, K*'s digits from the pair table
         if (!kzt) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(predict_oz2_kernel, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, desc, tl, seg, P,
-                           n_items, nI, m, ldp, m0, part, mean, kzt);
+        hipLaunchKernelGGL(predict_oz2_kernel<false>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, desc, tl,
+                           seg, P, n_items, nI, m, ldp, m0, part, mean, kzt);
         return hipGetLastError();
     }
     if (variant == 3) {   // K*'s digits from the table

@@ -557,7 +557,8 @@ sbo_status pack_precise(sbo_ctx *ctx, hipStream_t s, int64_t npad, int64_t I0) {
         SBO_HIP(ctx->koz.reserve(sbo::oz_coord_bytes(npad)));
         SBO_HIP(sbo::launch_pack_oz(s, ctx->Linv.as<double>(), ctx->cap, ctx->n, npad, I0, sf2, ctx->x.as<float>(),
                                     ctx->y.as<float>(), ctx->alpha64.as<double>(), ctx->aoz.as<char>(),
-                                    ctx->eoz.as<int>(), ctx->koz.as<char>(), ctx->precise_kernel == 4));
+                                    ctx->eoz.as<int>(), ctx->koz.as<char>(),
+                                    ctx->precise_kernel == 4 || ctx->precise_kernel == 10));
     } else {
         SBO_HIP(grow_keep(ctx, ctx->a64, sbo::f64_operand_bytes(npad), sbo::f64_operand_bytes(I0 * sbo::kBM)));
         SBO_HIP(ctx->kc64.reserve(sbo::f64_coord_bytes(npad)));
@@ -1496,8 +1497,8 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     }
     SBO_HIP(ctx->plan_work.reserve(sbo::predict_work_bytes(ctx->npad, ms, P)));
     // (the K* table's precise sweep plans each chunk of query blocks itself)
-    const bool chunked = precise && (ctx->precise_kernel == 3 || ctx->precise_kernel == 4) && !cost;
-    const bool pairs = ctx->precise_kernel == 4;
+    const bool chunked = precise && ctx->precise_kernel >= 3 && ctx->precise_kernel != 9 && !cost;
+    const bool pairs = ctx->precise_kernel == 4 || ctx->precise_kernel == 10;
     if (!chunked)
         SBO_HIP(sbo::launch_plan(ctx->stream, ctx->kbox.as<float4>(), ctx->npad, qx, qy, ms, ldp,
                                  (float)ctx->hyper.length_scale, (float)ctx->hyper.prior_mean, plan,
@@ -2309,8 +2310,8 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             return SBO_OK;
         case SBO_OPT_PRECISE_KERNEL:
 #ifdef SBO_DIAG
-            SBO_CHECK(value == 0 || value == 1 || value == 3 || value == 4 || value == 9, SBO_E_INVAL,
-                      "SBO_OPT_PRECISE_KERNEL: 0, 1, 3, 4 or 9 (diagnostic)");
+            SBO_CHECK(value == 0 || value == 1 || value == 3 || value == 4 || value == 9 || value == 10, SBO_E_INVAL,
+                      "SBO_OPT_PRECISE_KERNEL: 0, 1, 3, 4, 9 or 10 (diagnostics)");
 #else
             SBO_CHECK(value == 0 || value == 1 || value == 3 || value == 4, SBO_E_INVAL,
                       "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA), 1 (int8), 3 (int8, K* table) or 4 (int8, "
@@ -2318,7 +2319,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
 #endif
             {
                 // the operand layout each kernel reads: f64 tiles, int8 tiles, int8 pairs
-                auto layout = [](int64_t k) { return k == 0 ? 0 : k == 4 ? 2 : 1; };
+                auto layout = [](int64_t k) { return k == 0 ? 0 : (k == 4 || k == 10) ? 2 : 1; };
                 if (layout(ctx->precise_kernel) != layout(value)) ctx->a64_I0 = 0;   // derive it all
             }
             ctx->precise_kernel = (int)value;
@@ -2393,6 +2394,77 @@ SBO_API sbo_status sbo_trim(sbo_ctx *ctx) {
     for (sbo::DevBuf *b : {&ctx->scratch, &ctx->gzws, &ctx->gzws_aux, &ctx->chk, &ctx->restage, &ctx->kzt, &ctx->qcost})
         b->release();
     return SBO_OK;
+}
+
+SBO_API sbo_status sbo_warmup(sbo_ctx *ctx, int64_t n_cap, int64_t m_cap, sbo_hyper hyper) {
+    if (!ctx) return SBO_E_INVAL;
+    SBO_CHECK(n_cap > 0 && m_cap > 0, SBO_E_EMPTY, "sbo_warmup: n_cap and m_cap must be > 0");
+    SBO_CHECK(n_cap < (int64_t)1 << 30 && m_cap < (int64_t)1 << 31, SBO_E_INVAL, "sbo_warmup: sizes too large");
+    if (sbo_status st = check_hyper(ctx, hyper)) return st;
+    SBO_HIP(hipSetDevice(ctx->device));
+    // n_cap points uniform over a square of about 8 points per l^2 (the C2-C5
+    // density: a well-conditioned fit), a smooth field as observations
+    const double side = hyper.length_scale * std::sqrt((double)n_cap / 8.0);
+    std::vector<float> hx((size_t)n_cap), hy((size_t)n_cap), ho((size_t)n_cap);
+    uint64_t z = 0x9E3779B97F4A7C15ull;
+    auto next = [&z]() {   // SplitMix64 -> [0, 1)
+        uint64_t v = (z += 0x9E3779B97F4A7C15ull);
+        v = (v ^ (v >> 30)) * 0xBF58476D1CE4E5B9ull;
+        v = (v ^ (v >> 27)) * 0x94D049BB133111EBull;
+        return (double)((v ^ (v >> 31)) >> 11) * 0x1.0p-53;
+    };
+    for (int64_t i = 0; i < n_cap; ++i) {
+        hx[(size_t)i] = (float)(next() * side);
+        hy[(size_t)i] = (float)(next() * side);
+        ho[(size_t)i] = (float)(std::sin(hx[(size_t)i] / hyper.length_scale) +
+                                std::cos(0.7 * hy[(size_t)i] / hyper.length_scale));
+    }
+    sbo_status st = sbo_fit(ctx, hx.data(), hy.data(), ho.data(), n_cap, hyper, 0);
+    // an m_cap-point raster over the square (the grid-patch query path), swept
+    // with both sweeps; device buffers so that the tick's own workspaces are
+    // what gets sized
+    const int64_t w = std::max<int64_t>(1, (int64_t)std::ceil(std::sqrt((double)m_cap)));
+    const int64_t h = (m_cap + w - 1) / w, m = w * h;
+    DevBuf dq, dk;
+    if (st == SBO_OK) {
+        std::vector<float> gq(2 * (size_t)m);
+        for (int64_t i = 0; i < h; ++i)
+            for (int64_t j = 0; j < w; ++j) {
+                gq[(size_t)(i * w + j)] = (float)(side * (double)j / (double)std::max<int64_t>(w - 1, 1));
+                gq[(size_t)(m + i * w + j)] = (float)(side * (double)i / (double)std::max<int64_t>(h - 1, 1));
+            }
+        if (dq.reserve(sizeof(float) * 2 * (size_t)m) != hipSuccess || dk.reserve(sizeof(sbo_key)) != hipSuccess ||
+            hipMemcpy(dq.as<float>(), gq.data(), sizeof(float) * 2 * (size_t)m, hipMemcpyHostToDevice) != hipSuccess)
+            st = SBO_E_OOM;
+    }
+    const int popt = ctx->precision_opt;
+    for (int prec = 0; prec <= 1 && st == SBO_OK; ++prec) {
+        if (prec == 1 && !(ctx->inverse_bits == 64 && ctx->linv_n == ctx->n)) break;
+        ctx->precision_opt = prec;
+        if ((st = probe_precision(ctx)) != SBO_OK) break;
+        st = sbo_tick(ctx, dq.as<float>(), dq.as<float>() + m, m, 2.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, nullptr,
+                      nullptr, nullptr, nullptr, dk.as<sbo_key>(), SBO_DEVICE_PTRS);
+    }
+    ctx->precision_opt = popt;
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    // unfitted again; the workspaces keep their sizes (the query buffers go:
+    // forget the grid layout cached by their addresses)
+    ctx->fitted = false;
+    ctx->has_factor = false;
+    ctx->n = 0;
+    ctx->linv_n = 0;
+    ctx->z_n = 0;
+    ctx->probe_n = 0;
+    ctx->precise = false;
+    ctx->n_sorted = 0;
+    ctx->widened_n = 0;
+    ctx->early_inv_n = 0;
+    ctx->order.clear();
+    ctx->chk_res = sbo_inv_check{};
+    ctx->qgrid_x = ctx->qgrid_y = nullptr;
+    ctx->qgrid_m = -1;
+    ctx->hyper = sbo_hyper{0.4, 1.0, 0.1, 0.0};
+    return st;
 }
 
 SBO_API sbo_status sbo_get_inverse_check(const sbo_ctx *ctx, sbo_inv_check *out) {

@@ -307,6 +307,12 @@ class TerrainMapper:
         self.ctx.check(self._lib.sbo_get_inverse_check(self.ctx.handle, ctypes.byref(r)))
         return {f: getattr(r, f) for f, _ in sbo_inv_check._fields_}
 
+    def warmup(self, n_cap: int, m_cap: int) -> None:
+        """Load every code object a fit and a tick need and size the
+        workspaces for up to n_cap points / m_cap queries (sbo_warmup); the
+        mapper is left unfitted."""
+        self.ctx.check(self._lib.sbo_warmup(self.ctx.handle, int(n_cap), int(m_cap), _to_hyper(self.hyper)))
+
     def trim(self) -> None:
         """Release the workspaces kept between calls (sbo_trim)."""
         self.ctx.check(self._lib.sbo_trim(self.ctx.handle))

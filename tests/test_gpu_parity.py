@@ -1584,3 +1584,55 @@ def test_pair_sweep_chunks_and_lone_tiles(mapper):
         gm.set_option(N.SBO_OPT_TABLE_MB, 0)
         gm.set_option(N.SBO_OPT_PRECISION, -1)
         gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 3)
+
+
+def test_warmup_and_trim(dev):
+    """sbo_warmup (round 5): a fit of n_cap synthetic points
+    and both sweeps over an m_cap grid, then the context is unfitted (tick and
+    append refuse) -- and a fit after it gives bitwise the outputs of a fresh
+    context; sbo_trim releases the workspaces without touching the fitted
+    state (a tick after it: bitwise the same)."""
+    wl = synthetic(3000, 70, 60, seed=21)
+    q = (torch.tensor(f32(wl.qx), device=dev), torch.tensor(f32(wl.qy), device=dev))
+    fresh = TerrainMapper(0, wl.hyper)
+    fresh.fit(wl.x, wl.y, wl.obs)
+    ref = fresh.predict(*q)
+    fresh.close()
+    gm = TerrainMapper(0, wl.hyper)
+    try:
+        gm.warmup(6000, 100000)
+        assert gm.n == 0
+        with pytest.raises(N.SboError):
+            gm.predict(*q)
+        gm.fit(wl.x, wl.y, wl.obs)
+        out = gm.predict(*q)
+        assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
+        gm.trim()
+        again = gm.predict(*q)
+        assert torch.equal(again[0], ref[0]) and torch.equal(again[1], ref[1])
+        gm.append(wl.x[:5] + 0.01, wl.y[:5], wl.obs[:5])
+        assert gm.n == 3005
+    finally:
+        gm.close()
+
+
+def test_product_matches_diagnostic_build():
+    """The diagnostic build (lib/libsbo_diag.so: csrc/diag/predict_x3_diag.hip,
+    a hand-kept twin of the product's split sweep with its A/B and timing
+    variants) must stay bitwise the product at variant 3 -- tools/compare_libs.py
+    on C2 and a box workload (VERDICT r4 hygiene: only a by-hand run kept
+    the two in step).  Each library runs in a child process of its own."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prod = os.path.join(root, "safe_bayesian_optimization_amd", "lib", "libsbo.so")
+    diag = os.path.join(root, "safe_bayesian_optimization_amd", "lib", "libsbo_diag.so")
+    if not os.path.exists(diag):
+        pytest.skip("lib/libsbo_diag.so not built (make -C safe_bayesian_optimization_amd diag)")
+    if os.path.getmtime(diag) < os.path.getmtime(prod) - 3600:
+        pytest.fail("lib/libsbo_diag.so is older than libsbo.so: rebuild it (make diag)")
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "compare_libs.py"), prod, diag,
+                        "--configs", "C2", "box"], capture_output=True, text=True, timeout=600)
+    print(r.stdout[-2000:])
+    assert r.returncode == 0 and "ALL BITWISE EQUAL" in r.stdout, r.stderr[-2000:]

@@ -32,6 +32,10 @@ def main(d, cus=256, kernel=None):
         for c in sorted(e):
             if c.startswith("SQ_") and c not in ("SQ_WAVE_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES") and "SQ_WAVE_CYCLES" in e:
                 line += f"  {c} {e[c] / e['SQ_WAVE_CYCLES'] * 100:.1f}%"
+            elif c.startswith("TCC_") or c.startswith("TCP_") or c.startswith("TA_"):
+                line += f"  {c} {e[c]:.4g}"
+        if "TCC_HIT_sum" in e and "TCC_MISS_sum" in e:
+            line += f"  L2 hit rate {e['TCC_HIT_sum'] / max(e['TCC_HIT_sum'] + e['TCC_MISS_sum'], 1) * 100:.1f}%"
         print(line)
 
 

@@ -34,6 +34,7 @@ def main():
     dev = torch.device("cuda:0")
     f32 = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
     gm = TerrainMapper(0, wl.hyper)
+    gm.ctx.set_stream(torch.cuda.current_stream(dev))
     gm.fit(f32(wl.x), f32(wl.y), f32(wl.obs))
     m_total = wl.qx.size
     base = None
@@ -54,11 +55,23 @@ def main():
                             lo=torch.empty(m, dtype=torch.float64, device=dev),
                             hi=torch.empty(m, dtype=torch.float64, device=dev),
                             safe=torch.empty(m, dtype=torch.uint8, device=dev))
-                gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs)
+                # the bench's step on this rank: the tick (async, device key)
+                # and the device combine of the P gathered 16-byte keys
+                # (sbo_keys_reduce; the all-gather itself, P x 16 B over xGMI,
+                # is not emulated)
+                key = torch.empty(2, dtype=torch.int64, device=dev)
+                gathered = torch.zeros(2 * P, dtype=torch.int64, device=dev)
+                best = torch.empty(2, dtype=torch.int64, device=dev)
+
+                def step():
+                    gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs, key_out=key, async_=True)
+                    gathered[:2].copy_(key)
+                    gm.ctx.reduce_keys(gathered, best)
+                step()
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for _ in range(a.reps):
-                    gm.tick(qx, qy, wl.beta, wl.f_min, outputs=outs)
+                    step()
                 torch.cuda.synchronize()
                 ms.append((time.perf_counter() - t0) * 1e3 / a.reps)
             value = m_total / (max(ms) * 1e-3)
