@@ -445,8 +445,8 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * precise regime).  The SBO_OPT_INV_OVERLAP fit keeps the dgemm products. */
 #define SBO_OPT_INV_OZ 24
 /* SBO_OPT_INV_CHECK (default 1; 0 off; 2 after every full inverse): the
- * fit's run-time accuracy guard of its f64 inverse X.  On 64 queries (a 4 x 4
- * lattice over the training box and 48 training locations) it forms V0 = X k
+ * fit's run-time accuracy guard of its f64 inverse X.  On 32 queries (a 4 x 4
+ * lattice over the training box and 16 training locations) it forms V0 = X k
  * and one refinement against the f32 factor, V1 = V0 + X (k - L V0), in f64,
  * and takes err = max |(sf2 - |V0|^2) - (sf2 - |V1|^2)| / max (sf2 - |V1|^2):
  * the inverse's own share of the variance error, which the precision probe
@@ -456,6 +456,17 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * dgemm products and checks it again (sbo_get_inverse_check).  Runs on a
  * stream of its own beside the fit's operand packs. */
 #define SBO_OPT_INV_CHECK 25
+/* SBO_OPT_PLAN_BLOCK (0 = row-block-major; bi << 8 | bq): the item order of
+ * the precise sweep's plans -- blocks of bi row blocks x bq query blocks, so
+ * that the sweep workgroups of one XCD share the K* table pieces of a query
+ * block in their L2 as well as the A tiles of a row block.  Results do not
+ * depend on it (items are computed independently). */
+#define SBO_OPT_PLAN_BLOCK 26
+/* SBO_OPT_PROBE_SIZE (grid << 16 | train; default 32 << 16 | 512): the
+ * precision probe's query set -- a grid x grid lattice over the training box
+ * and `train` training locations (SBO_OPT_PRECISION); the next fit or append
+ * probes again. */
+#define SBO_OPT_PROBE_SIZE 27
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The last inverse check (SBO_OPT_INV_CHECK) of the current fit: ran = 1 if

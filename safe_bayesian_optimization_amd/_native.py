@@ -60,6 +60,8 @@ SBO_OPT_PRECISE_KERNEL = 22
 SBO_OPT_TABLE_MB = 23
 SBO_OPT_INV_OZ = 24
 SBO_OPT_INV_CHECK = 25
+SBO_OPT_PLAN_BLOCK = 26
+SBO_OPT_PROBE_SIZE = 27
 
 
 class SboError(RuntimeError):

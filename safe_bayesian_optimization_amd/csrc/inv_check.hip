@@ -10,13 +10,13 @@
 // six-digit margin without a signal.
 //
 // What: on a guard set of kChkQ queries (a 4 x 4 lattice over the training
-// box and 48 training locations) the posterior's V = L^-1 k_q is formed with
+// box and 16 training locations) the posterior's V = L^-1 k_q is formed with
 // the computed inverse X, V0 = X Kq, and refined once against the f32 factor
 // itself, V1 = V0 + X (Kq - L V0), all in f64.  With X = L^-1 (I + E), V1's
 // error is O(E^2), so |V1|^2 - |V0|^2 is the inverse's own effect on the
 // latent variance sf2 - |V|^2 at those queries (to first order in E), and
 // the fit compares its normwise size with the contract (sbo_api.cpp,
-// inverse_check).  Cost: three triangular products with 64 right-hand sides
+// inverse_check).  Cost: three triangular products with 32 right-hand sides
 // (two over the f64 inverse, one over the f32 factor) -- one read of each
 // lower triangle -- on a stream of their own beside the fit's operand packs.
 //
@@ -38,7 +38,10 @@ namespace {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kChkRows = 64;              // rows per workgroup: four waves of 16
+constexpr int kChkWaves = 8;
+constexpr int kChkRows = 16 * kChkWaves;  // rows per workgroup: eight waves of 16
+constexpr int kChkThreads = 64 * kChkWaves;
+constexpr int kChkCB = kChkQ / 16;        // 16-column blocks per wave
 constexpr int kChkKC = 1024;              // k per workgroup (split-k chunk)
 constexpr int kChkStage = 64;             // k staged in LDS per step
 constexpr int kChkLd = kChkQ + 16;        // LDS row stride (doubles): the four
@@ -72,13 +75,15 @@ __device__ __forceinline__ int chk_chunks(int64_t rb, int64_t n) {
 }
 
 // grid (row blocks, chunks); wave w owns rows 16 w .. 16 w + 15 of the row
-// block and all kChkQ columns (four 16 x 16 f64 accumulators).  A fragment
+// block and all kChkQ columns (kChkCB 16 x 16 f64 accumulators).  A fragment
 // (lane l): T[row r0 + (l & 15)][k + (l >> 4)], B: X[k + (l >> 4)][16 j + (l & 15)];
 // D: row (l >> 4) + 4 v, column l & 15 (cdna_hip_programming.md, f64 MFMA).
+// The stage's A fragments are loaded before the X stage is waited for, so
+// the triangle's stream (the bound: one read of it) overlaps the staging.
 template <class T>
-__global__ __launch_bounds__(256) void chk_trimul_kernel(const T *__restrict__ Tm, int64_t ld, int64_t n,
-                                                          int64_t rows, const double *__restrict__ X,
-                                                          double *__restrict__ P) {
+__global__ __launch_bounds__(kChkThreads) void chk_trimul_kernel(const T *__restrict__ Tm, int64_t ld, int64_t n,
+                                                                  int64_t rows, const double *__restrict__ X,
+                                                                  double *__restrict__ P) {
     __shared__ double xs[kChkStage * kChkLd];
     const int64_t rb = blockIdx.x;
     const int kc = blockIdx.y;
@@ -91,16 +96,22 @@ __global__ __launch_bounds__(256) void chk_trimul_kernel(const T *__restrict__ T
     const int64_t rend = (rb + 1) * kChkRows;
     if (ke > rend) ke = rend;
     if (ke > n) ke = n;
-    f64x4 acc[4];
+    f64x4 acc[kChkCB];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < kChkCB; ++j) acc[j] = f64x4{0.0, 0.0, 0.0, 0.0};
     for (int64_t k0 = kb; k0 < ke; k0 += kChkStage) {
-        __syncthreads();
-        // stage X[k0 .. k0 + 63][0 .. 63]: 64 x 64 doubles, 16 per thread
-        // (rows past `rows` read as zero)
+        // the A fragments of the stage's 16 k steps (lower triangle, k < ke)
+        double a[kChkStage / 4];
 #pragma unroll
-        for (int e = 0; e < kChkStage * kChkQ / 256; e += 2) {
-            const int f = (int)threadIdx.x * 2 + e * 256;  // element pair index
+        for (int s = 0; s < kChkStage / 4; ++s) {
+            const int64_t k = k0 + 4 * s + (lane >> 4);
+            a[s] = (k < ke && k <= row && row < n) ? (double)Tm[row + k * ld] : 0.0;
+        }
+        __syncthreads();
+        // stage X[k0 .. k0 + 63][0 .. kChkQ - 1] (rows past `rows` read as zero)
+#pragma unroll
+        for (int e = 0; e < kChkStage * kChkQ / kChkThreads; e += 2) {
+            const int f = (int)threadIdx.x * 2 + e * kChkThreads;  // element pair index
             const int kr = f / kChkQ, cc = f % kChkQ;
             const int64_t k = k0 + kr;
             double2 v = {0.0, 0.0};
@@ -108,23 +119,16 @@ __global__ __launch_bounds__(256) void chk_trimul_kernel(const T *__restrict__ T
             *reinterpret_cast<double2 *>(xs + kr * kChkLd + cc) = v;
         }
         __syncthreads();
-        // the A fragments of the stage's 16 k steps, lower triangle and k < ke only
-        double a[kChkStage / 4];
-#pragma unroll
-        for (int s = 0; s < kChkStage / 4; ++s) {
-            const int64_t k = k0 + 4 * s + (lane >> 4);
-            a[s] = (k < ke && k <= row && row < n) ? (double)Tm[row + k * ld] : 0.0;
-        }
 #pragma unroll
         for (int s = 0; s < kChkStage / 4; ++s) {
             const double *xb = xs + (4 * s + (lane >> 4)) * kChkLd + (lane & 15);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[j] = mfma_f64(a[s], xb[16 * j], acc[j]);
+            for (int j = 0; j < kChkCB; ++j) acc[j] = mfma_f64(a[s], xb[16 * j], acc[j]);
         }
     }
     double *out = P + ((int64_t)kc * rows + r0) * kChkQ;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < kChkCB; ++j)
 #pragma unroll
         for (int v = 0; v < 4; ++v) out[((lane >> 4) + 4 * v) * kChkQ + 16 * j + (lane & 15)] = acc[j][v];
 }
@@ -179,8 +183,8 @@ hipError_t trimul(hipStream_t s, const T *Tm, int64_t ld, int64_t n, int64_t row
                   double *Y, const double *sub) {
     const int64_t nrb = rows / kChkRows;
     const int64_t nkc = (rows + kChkKC - 1) / kChkKC;
-    hipLaunchKernelGGL(chk_trimul_kernel<T>, dim3((unsigned)nrb, (unsigned)nkc), dim3(256), 0, s, Tm, ld, n, rows, X,
-                       P);
+    hipLaunchKernelGGL(chk_trimul_kernel<T>, dim3((unsigned)nrb, (unsigned)nkc), dim3(kChkThreads), 0, s, Tm, ld, n,
+                       rows, X, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int64_t tot = rows * kChkQ;

@@ -1552,8 +1552,34 @@ __device__ QBox plan_setup(const float *__restrict__ qx, const float *__restrict
 }
 
 // Item index of (I, qb): row-block major, heaviest (last) row block first.
-__device__ __forceinline__ int64_t plan_item(int I, int nI, int64_t nQ, int64_t qb) {
-    return (int64_t)(nI - 1 - I) * nQ + qb;
+// Item order (round 5): row-block-major, heaviest row block first; with
+// blk = bi << 8 | bq (> 0, the precise sweep's SBO_OPT_PLAN_BLOCK) in blocks
+// of bi row blocks x bq query blocks, so that the sweep workgroups of one XCD,
+// which run consecutive items at once, share the K* table pieces of a query
+// block (bi of them) as well as the A tiles of a row block (bq of them) in
+// their L2 -- instead of 32-fold A sharing and no table sharing.  A bijection
+// of [0, nI nQ); plan_item_inv inverts it.
+__device__ __forceinline__ int64_t plan_item(int I, int nI, int64_t nQ, int64_t qb, int blk = 0) {
+    const int64_t r = nI - 1 - I;
+    if (blk == 0) return r * nQ + qb;
+    const int64_t bi = blk >> 8, bq = blk & 255;
+    const int64_t IB = r / bi, ii = r % bi, QB = qb / bq, qq = qb % bq;
+    const int64_t bie = min(bi, (int64_t)nI - IB * bi), bqe = min(bq, nQ - QB * bq);
+    return IB * bi * nQ + QB * bie * bq + ii * bqe + qq;
+}
+__device__ __forceinline__ void plan_item_inv(int64_t item, int nI, int64_t nQ, int blk, int &I, int64_t &qb) {
+    if (blk == 0) {
+        I = nI - 1 - (int)(item / nQ);
+        qb = item % nQ;
+        return;
+    }
+    const int64_t bi = blk >> 8, bq = blk & 255;
+    const int64_t IB = item / (bi * nQ), r0 = item - IB * bi * nQ;
+    const int64_t bie = min(bi, (int64_t)nI - IB * bi);
+    const int64_t QB = r0 / (bie * bq), r1 = r0 - QB * bie * bq;
+    const int64_t bqe = min(bq, nQ - QB * bq);
+    I = nI - 1 - (int)(IB * bi + r1 / bqe);
+    qb = QB * bq + r1 % bqe;
 }
 // 64-tile chunks of the longest item (the code bitmap's stride per item)
 __host__ __device__ __forceinline__ int plan_chunks(int nI) { return (kTilesPerRowBlockStep * nI + 63) / 64; }
@@ -1569,7 +1595,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, float cexp, float skip_d2,
     float skip_d2_mean, float lg_tau, float m0, int64_t ldp, float *__restrict__ part, float *__restrict__ mean,
     unsigned long long *__restrict__ key, unsigned char *__restrict__ thr, unsigned long long *__restrict__ wkey,
-    unsigned long long *__restrict__ bits, int wide) {
+    unsigned long long *__restrict__ bits, int wide, int blk) {
     // dynamic LDS: the increment-bin cache [kPlanWaves][kPlanBinCache], then
     // the distance and |k|_2 caches of min(nkt, kPlanD2) tiles each
     extern __shared__ unsigned plan_dyn[];
@@ -1627,7 +1653,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
         const unsigned long long bud = !fill ? (unsigned long long)floor(4294967296.0 / sqrt((double)nI))
                                        : (wtot[I] <= budget_exp ? ~0ull : budget_exp);
         const int drop_max = R.threshold(I, bins[wave], lane, bud, bc);
-        const int64_t item = plan_item(I, nI, nQ, qb);
+        const int64_t item = plan_item(I, nI, nQ, qb, blk);
         // the item's codes, 64 tiles per chunk: kept / level 1 / level 2 masks (read by plan_write)
         unsigned long long *ib = bits + item * (int64_t)plan_chunks(nI) * 3;
         int cnt = 0;
@@ -1677,7 +1703,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
 __global__ __launch_bounds__(256) void plan_write_kernel(
     int nI, int64_t nQ, const unsigned long long *__restrict__ key, const unsigned long long *__restrict__ scan,
     const unsigned long long *__restrict__ bits, int4 *__restrict__ desc, unsigned short *__restrict__ tl,
-    int prod_full, unsigned long long *__restrict__ partial) {
+    int prod_full, unsigned long long *__restrict__ partial, int blk) {
     // partial (may be null): per wave [MFMA products, tiles at level 1, at level 2]
     // (summed by plan_counts_reduce_kernel: no contended global atomics)
     const int lane = threadIdx.x & 63;
@@ -1688,8 +1714,9 @@ __global__ __launch_bounds__(256) void plan_write_kernel(
         const unsigned long long k = key[item];
         const int cnt = (int)(k & kPlanCountMask);
         if (cnt > 0) {
-            const int I = nI - 1 - (int)(item / nQ);
-            const int64_t qb = item % nQ;
+            int I;
+            int64_t qb;
+            plan_item_inv(item, nI, nQ, blk, I, qb);
             const unsigned long long ex = scan[item] - k;
             const uint64_t off = ex & kPlanCountMask;
             const int64_t ne = (int64_t)(ex >> kPlanKeyShift);
@@ -1756,7 +1783,7 @@ __global__ __launch_bounds__(256) void plan_counts_reduce_kernel(const unsigned 
 __global__ void plan_seg_kernel(const unsigned long long *__restrict__ scan, int64_t n_items,
                                 const int4 *__restrict__ desc, int P, int *__restrict__ seg,
                                 unsigned long long *__restrict__ tiles_done, const unsigned long long *__restrict__ wkey,
-                                const unsigned long long *__restrict__ wscan, int nI, int64_t nQ) {
+                                const unsigned long long *__restrict__ wscan, int nI, int64_t nQ, int blk) {
     const unsigned long long last = scan[n_items - 1];
     const uint64_t total = last & kPlanCountMask;
     const uint64_t wtotal = wscan[n_items - 1];
@@ -1771,7 +1798,7 @@ __global__ void plan_seg_kernel(const unsigned long long *__restrict__ scan, int
         while (lo < hi) {
             const int64_t mid = (lo + hi) >> 1;
             const int4 d = desc[mid];
-            const int64_t it = plan_item(d.x, nI, nQ, d.y);
+            const int64_t it = plan_item(d.x, nI, nQ, d.y, blk);
             const uint64_t off = wscan[it] - wkey[it];
             if (off < target) lo = mid + 1; else hi = mid;
         }
@@ -2486,6 +2513,8 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
         return hipErrorInvalidValue;
     const PlanLayout L = plan_layout(nI, nQ, P);
     if (work_bytes < L.total) return hipErrorInvalidValue;
+    if (skip.order_blk != 0 && ((skip.order_blk >> 8) < 1 || (skip.order_blk & 255) < 1 || (skip.order_blk >> 16) != 0))
+        return hipErrorInvalidValue;
     char *w = static_cast<char *>(work);
     auto *key = reinterpret_cast<unsigned long long *>(w + L.key);
     auto *scan = reinterpret_cast<unsigned long long *>(w + L.scan);
@@ -2519,7 +2548,7 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
                        levels, make_float2(skip.lvl_key[0], skip.lvl_key[1]), nI,
                        nQ, qx, qy,
                        m, cexp, skip_d2, skip_d2_mean, skip.lg_tau_v, m0, ldp, part, mean, key, thr, wkey, bits,
-                       skip.wide ? 1 : 0);
+                       skip.wide ? 1 : 0, skip.order_blk);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t tb = L.temp_bytes;
@@ -2530,14 +2559,15 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     if (e != hipSuccess) return e;
     const int64_t wblocks = std::min<int64_t>((items + 3) / 4, kPlanWriteBlocks);
     hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)wblocks), dim3(256), 0, s, nI, nQ, key, scan, bits,
-                       desc, tl, skip.prod_full, tiles_done ? reinterpret_cast<unsigned long long *>(w + L.lvcnt) : nullptr);
+                       desc, tl, skip.prod_full, tiles_done ? reinterpret_cast<unsigned long long *>(w + L.lvcnt) : nullptr,
+                       skip.order_blk);
     if (tiles_done)
         hipLaunchKernelGGL(plan_counts_reduce_kernel, dim3(1), dim3(256), 0, s,
                            reinterpret_cast<const unsigned long long *>(w + L.lvcnt), wblocks * 4, tiles_done + 1);
     auto *rec = reinterpret_cast<int4 *>(w + L.rec);
     if (!L.xcd) {
         hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, P, seg, tiles_done, wkey,
-                           wscan, nI, nQ);
+                           wscan, nI, nQ, skip.order_blk);
         if (skip.records)
             hipLaunchKernelGGL(plan_rec_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, scan, items, desc,
                                tl, rec);
@@ -2555,7 +2585,7 @@ hipError_t launch_plan(hipStream_t s, const float4 *kbox, int64_t npad, const fl
     e = hipMemsetAsync(cnt2, 0, 8 * (size_t)items, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(plan_seg_kernel, dim3(1), dim3(256), 0, s, scan, items, desc, 8, xseg, tiles_done, wkey, wscan,
-                       nI, nQ);
+                       nI, nQ, skip.order_blk);
     hipLaunchKernelGGL(plan_perm_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, scan, items, desc,
                        xseg, G, pos_of, cnt2);
     e = hipGetLastError();

@@ -631,54 +631,86 @@ constexpr int kOz2TableDma = 2 * kOzKDigits + 2;            // DMA instructions 
 static_assert(kOz2Smem <= 160 * 1024, "pair-mode LDS");
 static_assert(kOz2A == 2 * kOzA / 2 && 4 * kOz2A == 2 * kOzTileBytes, "a pair is two kernel-1 tiles");
 
-// The 28 digit products of one 16x16 block over the pair (tile 0 then tile 1,
-// chained per level), combined once: T = (l0 256 + l1) 2^16 + l2 256 + l3 +
-// floor((l4 + 128) / 256), the +128 from level 4's initial accumulator.
-__device__ __forceinline__ void block_products2(const i32x4 *__restrict__ pa, int b, const i32x4 (&kd)[2][kOzKDigits],
-                                                double S, f64x4 &acc) {
+// One stage: quarter QQ's four 16-row blocks into this row half's eight
+// accumulators (acc[(QQ & 1) 4 + b]), software-pipelined by hand (round 5):
+// the stage is eight sub-blocks (block b, tile e), each five digit reads and
+// fourteen MFMAs; sub-block i + 1's reads are issued among sub-block i's
+// MFMAs, and block b - 1's f64 combination among block b's first sub-block's
+// MFMAs (its level sums held in a second register set).  The compiler's own
+// schedule issued each sub-block's reads just before their MFMAs and waited
+// on them at once (s_waitcnt lgkmcnt(4) right after the reads), and combined
+// every block after its last MFMA: the LDS latency and the combination were
+// exposed in both waves of a SIMD at the same time.
+__device__ __forceinline__ void oz2_read(const i32x4 *__restrict__ pa, int i, i32x4 (&ad)[kOzDigits]) {
+    const int b = i >> 1, e = i & 1;
+#pragma unroll
+    for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[((s * 2 + e) * kOz2RB + b) * 64];
+}
+struct Oz2Levels {
+    i32x4 l0, l1, l2, l3, l4;
+};
+__device__ __forceinline__ void oz2_products(const i32x4 (&ad)[kOzDigits], const i32x4 (&kd)[kOzKDigits], bool first,
+                                             Oz2Levels &L) {
     const i32x4 z = {0, 0, 0, 0}, c128 = {128, 128, 128, 128};
-    i32x4 l0 = z, l1 = z, l2 = z, l3 = z, l4 = c128;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        i32x4 ad[kOzDigits];
-#pragma unroll
-        for (int s = 0; s < kOzDigits; ++s) ad[s] = pa[((s * 2 + e) * kOz2RB + b) * 64];
-        l0 = mfma_i8(ad[0], kd[e][0], l0);
-        l1 = mfma_i8(ad[0], kd[e][1], l1);
-        l2 = mfma_i8(ad[0], kd[e][2], l2);
-        l3 = mfma_i8(ad[0], kd[e][3], l3);
-        l1 = mfma_i8(ad[1], kd[e][0], l1);
-        l2 = mfma_i8(ad[1], kd[e][1], l2);
-        l3 = mfma_i8(ad[1], kd[e][2], l3);
-        l4 = mfma_i8(ad[1], kd[e][3], l4);
-        l2 = mfma_i8(ad[2], kd[e][0], l2);
-        l3 = mfma_i8(ad[2], kd[e][1], l3);
-        l4 = mfma_i8(ad[2], kd[e][2], l4);
-        l3 = mfma_i8(ad[3], kd[e][0], l3);
-        l4 = mfma_i8(ad[3], kd[e][1], l4);
-        l4 = mfma_i8(ad[4], kd[e][0], l4);
-    }
+    L.l0 = mfma_i8(ad[0], kd[0], first ? z : L.l0);
+    L.l1 = mfma_i8(ad[0], kd[1], first ? z : L.l1);
+    L.l2 = mfma_i8(ad[0], kd[2], first ? z : L.l2);
+    L.l3 = mfma_i8(ad[0], kd[3], first ? z : L.l3);
+    L.l1 = mfma_i8(ad[1], kd[0], L.l1);
+    L.l2 = mfma_i8(ad[1], kd[1], L.l2);
+    L.l3 = mfma_i8(ad[1], kd[2], L.l3);
+    L.l4 = mfma_i8(ad[1], kd[3], first ? c128 : L.l4);
+    L.l2 = mfma_i8(ad[2], kd[0], L.l2);
+    L.l3 = mfma_i8(ad[2], kd[1], L.l3);
+    L.l4 = mfma_i8(ad[2], kd[2], L.l4);
+    L.l3 = mfma_i8(ad[3], kd[0], L.l3);
+    L.l4 = mfma_i8(ad[3], kd[1], L.l4);
+    L.l4 = mfma_i8(ad[4], kd[0], L.l4);
+}
+__device__ __forceinline__ void oz2_combine(const Oz2Levels &L, double S, f64x4 &acc) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-        const int h01 = l0[v] * 256 + l1[v];                  // |.| < 2^30
-        const int h23 = l2[v] * 256 + l3[v] + (l4[v] >> 8);   // |.| < 2^31 (above)
+        const int h01 = L.l0[v] * 256 + L.l1[v];                  // |.| < 2^30
+        const int h23 = L.l2[v] * 256 + L.l3[v] + (L.l4[v] >> 8);   // |.| < 2^31 (above)
         const double t = fma((double)h01, 65536.0, (double)h23);
         acc[v] = fma(t, S, acc[v]);
     }
 }
-
-// One stage: quarter QQ's four 16-row blocks into this row half's eight
-// accumulators (acc[(QQ & 1) 4 + b]).
+// interleave: each of the 14 MFMAs followed by up to three VALU (a pending
+// combination)
+__device__ __forceinline__ void oz2_interleave(bool combine) {
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // MFMA
+        if (combine) __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);     // VALU
+    }
+}
 template <int QQ>
 __device__ __forceinline__ void stage_blocks2(const char *__restrict__ slot, int lane, const i32x4 (&kd)[2][kOzKDigits],
                                               int eK, f64x4 (&acc)[kOzHalfRB]) {
     const int *eA = reinterpret_cast<const int *>(slot + kOz2A);
     const i32x4 *pa = reinterpret_cast<const i32x4 *>(slot) + lane;
+    double S[kOz2RB];
 #pragma unroll
-    for (int b = 0; b < kOz2RB; ++b) {
-        const double S = ldexp(1.0, __builtin_amdgcn_readfirstlane(eA[QQ * kOz2RB + b]) + eK - kOzScale);
-        block_products2(pa, b, kd, S, acc[(QQ & 1) * kOz2RB + b]);
+    for (int b = 0; b < kOz2RB; ++b)
+        S[b] = ldexp(1.0, __builtin_amdgcn_readfirstlane(eA[QQ * kOz2RB + b]) + eK - kOzScale);
+    i32x4 ad[2][kOzDigits];
+    Oz2Levels L[2];
+    oz2_read(pa, 0, ad[0]);
+#pragma unroll
+    for (int i = 0; i < 2 * kOz2RB; ++i) {
+        const int b = i >> 1, e = i & 1;
+        // the next sub-block's reads stay above this one's MFMAs (a
+        // scheduling barrier each side), so their latency hides under them
+        if (i + 1 < 2 * kOz2RB) oz2_read(pa, i + 1, ad[(i + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        oz2_products(ad[i & 1], kd[e], e == 0, L[b & 1]);
+        const bool comb = e == 0 && b > 0;
+        if (comb) oz2_combine(L[(b - 1) & 1], S[b - 1], acc[(QQ & 1) * kOz2RB + b - 1]);
+        oz2_interleave(comb);
+        __builtin_amdgcn_sched_barrier(0);
     }
+    oz2_combine(L[(kOz2RB - 1) & 1], S[kOz2RB - 1], acc[(QQ & 1) * kOz2RB + kOz2RB - 1]);
 }
 
 // The sweep walks each item TWICE, once per 128-row half (quarters 0-1, then

@@ -1017,8 +1017,8 @@ void precise_budget(sbo_ctx *ctx) {
 // the fast sweep's normwise variance error against it, max |d var| / max var
 // (the contract's metric); above kPreciseTol the context's ticks use the
 // precise sweep.  The query set (round 4): a 32 x 32 grid
-// over the training box AND up to kProbeTrain training locations (every
-// (n / kProbeTrain)-th point of the k-d order, so dense clusters are sampled in
+// over the training box AND up to 512 training locations (every (n / 512)-th
+// point of the k-d order, so dense clusters are sampled in
 // proportion to their points): where the data is dense the variance is
 // smallest and sf2 - |V|^2 cancels hardest, and a narrow dense path (the
 // publisher's data, turtlesim_spatial_publisher.py:151-183) falls between the
@@ -1039,7 +1039,6 @@ void precise_budget(sbo_ctx *ctx) {
 // inverse (SBO_OPT_INVERSE_BITS 64) and a factor (not an imported state).
 constexpr double kPreciseTol = 5e-6;
 constexpr int kProbeRefBits = 24;
-constexpr int kProbeTrain = 512;
 sbo_status probe_precision(sbo_ctx *ctx) {
     const bool avail = ctx->inverse_bits == 64 && ctx->has_factor && ctx->linv_n == ctx->n;
     if (!avail || ctx->precision_opt == 0) {
@@ -1049,9 +1048,9 @@ sbo_status probe_precision(sbo_ctx *ctx) {
     }
     const bool fresh = probe_due(ctx);
     if (fresh) {
-        constexpr int G = 32, MG = G * G;
+        const int G = ctx->probe_grid, MG = G * G;
         const int64_t n = ctx->n;
-        const int MT = (int)std::min<int64_t>(n, kProbeTrain), M = MG + MT;
+        const int MT = (int)std::min<int64_t>(n, ctx->probe_train), M = MG + MT;
         const int64_t stride = n / MT;     // >= 1
         std::vector<float> h(2 * (size_t)M);
         for (int i = 0; i < G; ++i)
@@ -1442,6 +1441,7 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
     plan.prod_full = !precise && ctx->kernel_variant >= 2 ? 6 : 1;
     plan.records = !precise && ctx->kernel_variant >= 2;
     plan.wide = precise;
+    plan.order_blk = precise && !cost ? ctx->plan_block : 0;   // (the query-cost plan reads its keys row-block-major)
 #ifdef SBO_DIAG
     // timing diagnostic (diagnostic build only): the drop-only plan
     // with every kept tile at level SBO_LVL_FORCE -- outside the error budget
@@ -2327,6 +2327,19 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
         case SBO_OPT_INV_OZ:
             SBO_CHECK(value == 0 || value == 5 || value == 6, SBO_E_INVAL, "SBO_OPT_INV_OZ must be 0, 5 or 6");
             ctx->inv_oz = (int)value;
+            return SBO_OK;
+        case SBO_OPT_PROBE_SIZE:
+            SBO_CHECK(value >= 0 && (value >> 16) >= 4 && (value >> 16) <= 256 && (value & 0xffff) >= 1 &&
+                          (value & 0xffff) <= 16384,
+                      SBO_E_INVAL, "SBO_OPT_PROBE_SIZE must be grid << 16 | train (grid 4..256, train 1..16384)");
+            ctx->probe_grid = (int)(value >> 16);
+            ctx->probe_train = (int)(value & 0xffff);
+            ctx->probe_n = 0;   // probe again at the next refresh
+            return SBO_OK;
+        case SBO_OPT_PLAN_BLOCK:
+            SBO_CHECK(value == 0 || ((value >> 8) >= 1 && (value >> 8) <= 64 && (value & 255) >= 1), SBO_E_INVAL,
+                      "SBO_OPT_PLAN_BLOCK must be 0 or bi << 8 | bq with 1 <= bi <= 64, 1 <= bq <= 255");
+            ctx->plan_block = (int)value;
             return SBO_OK;
         case SBO_OPT_INV_CHECK:
             SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_INV_CHECK must be 0, 1 or 2");

@@ -202,6 +202,8 @@ struct sbo_ctx {
     double probe_err_grid = -1.0, probe_err_train = -1.0, probe_vmax_grid = 0.0, probe_vmax_train = 0.0;
     int probe_m_grid = 0, probe_m_train = 0;
     int64_t table_mb = 0;        // SBO_OPT_TABLE_MB: the K* table's memory budget (SBO_OPT_PRECISE_KERNEL 3; 0: auto)
+    int probe_grid = 32, probe_train = 512;  // SBO_OPT_PROBE_SIZE: the probe's grid side and training locations
+    int plan_block = 0;          // SBO_OPT_PLAN_BLOCK: the precise plans' item blocks (bi << 8 | bq; 0: row-block-major)
     int reprobe_pct = 25;        // SBO_OPT_REPROBE: appends re-probe once N grew by this share (0: every append)
     bool inv_batched = true;      // SBO_OPT_INV_LEAVES: the recursion's base cases in one batched dtrtri
     bool inv_leaves_done = false; // (set while a recursion runs whose base cases are already inverted)
@@ -279,6 +281,7 @@ struct SkipPlan {
     int prod_full = 1;  // MFMA products per full-precision tile (6: split sweep), for the counter
     bool records = false;  // also write the split sweep's step records (plan_views' rec)
     bool wide = false;     // empty items' outputs as f64 (the precise sweep's partials and mean)
+    int order_blk = 0;     // item order: 0 row-block-major, else blocks of (bi << 8 | bq) -- plan_item
     // rank of a tile's two level increments against drops: log2(time a drop
     // saves / time the level step saves), per-tile sweep time at C4 of six,
     // three, one product(s) 18.6, 12.9, 9.9 ns (variants 22, 20, 21)
@@ -452,7 +455,7 @@ hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, c
 // L, dV = Linv (Kq - L V0), both lower-triangular column-major with lda ld;
 // *colsums = per column (sum dV (2 V0 + dV), sum (V0 + dV)^2).  work:
 // inv_check_bytes(n); with Linv null only the pointers are set.
-constexpr int kChkQ = 64;
+constexpr int kChkQ = 32;
 int64_t inv_check_rows(int64_t n);
 size_t inv_check_bytes(int64_t n);
 hipError_t launch_inv_check(hipStream_t s, const double *Linv, const float *L, int64_t ld, int64_t n,

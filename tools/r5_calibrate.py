@@ -18,6 +18,7 @@ GPU diagnostic, one JSON line per workload:
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -31,6 +32,9 @@ from safe_bayesian_optimization_amd.terrain import Hyper, path_workload, synthet
 
 def nrel(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+PROBE_SIZES = [(48, 1024), (64, 2048)]
 
 
 def main():
@@ -52,6 +56,20 @@ def main():
                     continue
                 pi = gm.probe_info()
                 chk = gm.inverse_check()
+                # the probe at other sizes on the same data (SBO_OPT_PROBE_SIZE: grid side, training points)
+                probe_sizes, fit_ms = {}, {}
+                X, Y, OB = t(base.x), t(base.y), t(base.obs)
+                for pg, pt in [(32, 512)] + PROBE_SIZES:
+                    gm.set_option(N.SBO_OPT_PROBE_SIZE, (pg << 16) | pt)
+                    gm.fit(X, Y, OB)
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    gm.fit(X, Y, OB)
+                    torch.cuda.synchronize()
+                    fit_ms[f"{pg}x{pg}+{pt}"] = (time.perf_counter() - t0) * 1e3
+                    probe_sizes[f"{pg}x{pg}+{pt}"] = gm.probe_info()["err"]
+                gm.set_option(N.SBO_OPT_PROBE_SIZE, (32 << 16) | 512)
+                gm.fit(X, Y, OB)
                 qx, qy = t(base.qx), t(base.qy)
                 v = {}
                 for prec in (0, 1):
@@ -77,7 +95,9 @@ def main():
                        "guard_ms": chk["ms"],
                        "sliced_vs_dgemm_whole_grid_var": inv_eff,
                        "ratio_grid_over_guard": inv_eff / max(chk["err"], 1e-30) if chk["ran"] else None,
-                       "grid_var_min": float(v[1].min()), "grid_var_max": float(v[1].max())}
+                       "grid_var_min": float(v[1].min()), "grid_var_max": float(v[1].max()),
+                       "probe_err_by_size": probe_sizes, "fit_ms_by_probe_size": fit_ms,
+                       "ratio_by_probe_size": {k: err_fast / max(e, 1e-30) for k, e in probe_sizes.items()}}
                 print(json.dumps(res), flush=True)
                 gm.close()
 
