@@ -261,7 +261,9 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     const int4 *__restrict__ desc, const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P,
     int n_items, int nI, const float *__restrict__ qx, const float *__restrict__ qy, int64_t m, int64_t ldp,
     double cexp, double m0, double *__restrict__ part, double *__restrict__ mean, const char *__restrict__ kzt) {
-    constexpr bool NOKSTAR = MODE == 1, TABLE = MODE == 2;
+    // (diagnostic build only, wrong results: MODE 3 = TABLE without any stage
+    // DMA -- the compute bound; 4 = TABLE without the table's DMA)
+    constexpr bool NOKSTAR = MODE == 1, TABLE = MODE >= 2, DMA_A = MODE != 3, DMA_T = MODE == 2;
     constexpr int kSlot = TABLE ? kOzSlotT : kOzSlot;
     __shared__ __attribute__((aligned(16))) char smem[TABLE ? kOzSmemT : kOzSmem];
     const int bid = blockIdx.x;
@@ -311,13 +313,14 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
     do {                                                                                                 \
         const char *s_ = gA + (int64_t)(T_) * kOzTileBytes + (h_) * kOzA;                                \
         const uint32_t d_ = __builtin_amdgcn_readfirstlane(lds_wave + (uint32_t)(buf) * kSlot);          \
-        _Pragma("unroll") for (int j_ = 0; j_ < kOzA / (1024 * kOzWaves); ++j_)                          \
-            SBO_OZ_DMA16(s_ + j_ * kOzWaves * 1024, d_ + (uint32_t)(j_ * kOzWaves * 1024));              \
-        if (wave == 0 && lane < 2)                                                                       \
+        if (DMA_A)                                                                                       \
+            _Pragma("unroll") for (int j_ = 0; j_ < kOzA / (1024 * kOzWaves); ++j_)                      \
+                SBO_OZ_DMA16(s_ + j_ * kOzWaves * 1024, d_ + (uint32_t)(j_ * kOzWaves * 1024));          \
+        if (DMA_A && wave == 0 && lane < 2)                                                              \
             SBO_OZ_DMA16(gE + (int64_t)(T_) * 64 + (h_) * 32,                                            \
                          __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kSlot + kOzA)));       \
         if (TABLE) {                                                                                     \
-            if ((kt_) >= 0) {                                                                            \
+            if (DMA_T && (kt_) >= 0) {                                                                   \
                 const char *z_ = gZ + ((int64_t)(qb_) * nkt + (kt_)) * kKzt;                              \
                 const uint32_t zd_ = __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((buf) * kSlot + kOzA + kOzE)); \
                 _Pragma("unroll") for (int u_ = 0; u_ < kOzKDigits; ++u_)                                \
@@ -474,6 +477,230 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
 #undef SBO_OZ_DESC_WINDOW
 #undef SBO_OZ_LIST_WINDOW
 #undef SBO_OZ_DMA16
+}
+
+// SBO_OPT_PRECISE_KERNEL 5 (round 5): kernel 3 with a deeper stream.  Kernel
+// 3 stages one half-tile ahead (two slots of A + the K* table piece, 150 KiB),
+// so each 40 KiB stage has one stage of MFMA time (~1.7 us) to arrive -- at
+// 114 KiB per tile a CU needs ~38 GB/s for that, beyond what the L2-missing
+// part of the stream delivers per CU (MI355X_MICROARCH.md, gather rates: 23-34
+// GB/s per CU from HBM / the Infinity Cache at ~72 KiB in flight).  Here A is
+// staged a whole TILE ahead in three slots (the stage s + 2 into the slot stage
+// s - 1 read), and the K* table piece -- read into registers once per tile at
+// its first half -- is single-buffered per wave: each wave DMAs its own
+// digits, eK (lanes < 4) and mean terms (lanes < 8) of the next tile right
+// after reading the current one, two stages before use.  3 x 41 KiB + 33.5
+// KiB + windows = 158 KiB of LDS.  The waits are counted: at the end of a
+// first-half stage vmcnt(A group + table group) leaves the next tile's
+// pieces in flight, at the end of a second-half stage vmcnt(A group); anything
+// issued earlier (windows, the previous stage's groups) is complete there.
+// Products, digits and sums are kernel 3's: results bitwise equal.
+constexpr int kOz3Slot = kOzA + kOzE;                       // A digits + block exponents
+constexpr int kOz3Table = 3 * kOz3Slot;                     // the K* table piece (per-wave parts)
+constexpr int kOz3Win = kOz3Table + kKzt;                   // descriptor + list windows
+constexpr int kOz3Smem = kOz3Win + 4096;
+constexpr int kOz3AGroup = kOzA / (1024 * kOzWaves) + 1;    // A DMA instructions per wave per stage (5 + exponents)
+constexpr int kOz3TGroup = kOzKDigits + 2;                  // table DMA instructions per wave per tile (6)
+static_assert(kOz3Smem <= 160 * 1024, "three A slots and one table piece must fit the LDS");
+static_assert(kOz3AGroup == 6 && kOz3TGroup == 6, "the vmcnt immediates below");
+
+__global__ __launch_bounds__(kOzThreads, 1) void predict_oz3_kernel(
+    const char *__restrict__ aoz, const int *__restrict__ eoz, const int4 *__restrict__ desc,
+    const unsigned short *__restrict__ tl, const int *__restrict__ seg, int P, int n_items, int nI, int64_t m,
+    int64_t ldp, double m0, double *__restrict__ part, double *__restrict__ mean, const char *__restrict__ kzt) {
+    __shared__ __attribute__((aligned(16))) char smem[kOz3Smem];
+    const int bid = blockIdx.x;
+    const int rng = (P % 8 == 0) ? (bid % 8) * (P / 8) + bid / 8 : bid;
+    const int k0 = max(seg[rng], 0), k1 = min(seg[rng + 1], n_items);
+    if (k0 >= k1) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int r = lane & 15;
+    const int g = lane >> 4;
+    const int4 *dwin = reinterpret_cast<const int4 *>(smem + kOz3Win);
+    const unsigned short *lwin = reinterpret_cast<const unsigned short *>(smem + kOz3Win + 2048);
+    typedef __attribute__((address_space(3))) char lds_char;
+    const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const uint32_t lds_wave = lds_smem + (uint32_t)wave_u * 1024u;
+    const uint32_t lds_dwin = lds_smem + kOz3Win;
+    const uint32_t lds_lwin = lds_dwin + 2048u;
+    const uint32_t lds_tab = lds_smem + kOz3Table;
+    const char *gA = aoz + wave * 1024 + lane * 16;
+    const char *gE = reinterpret_cast<const char *>(eoz) + lane * 16;
+    const char *gD = reinterpret_cast<const char *>(desc) + lane * 16;
+    const char *gL = reinterpret_cast<const char *>(tl) + lane * 16;
+    const char *gZ = kzt + lane * 16;
+    const int nkt = kTilesPerRowBlockStep * nI;
+#define SBO_OZ3_DMA16(gsrc, ldst)                                                                        \
+    do {                                                                                                 \
+        uint32_t keep_;                                                                                  \
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t" \
+                     "s_mov_b32 m0, %0"                                                                  \
+                     : "=&s"(keep_)                                                                      \
+                     : "v"(gsrc), "s"(ldst)                                                              \
+                     : "memory");                                                                        \
+    } while (0)
+    // half h_ of packed tile T_ into A slot sl_ (the exponents by every wave's
+    // lanes 0-1: the same 32 B, so the per-wave group counts are uniform)
+#define SBO_OZ3_A(T_, h_, sl_)                                                                           \
+    do {                                                                                                 \
+        const char *s_ = gA + (int64_t)(T_) * kOzTileBytes + (h_) * kOzA;                                \
+        const uint32_t d_ = __builtin_amdgcn_readfirstlane(lds_wave + (uint32_t)(sl_) * kOz3Slot);       \
+        _Pragma("unroll") for (int j_ = 0; j_ < kOz3AGroup - 1; ++j_)                                    \
+            SBO_OZ3_DMA16(s_ + j_ * kOzWaves * 1024, d_ + (uint32_t)(j_ * kOzWaves * 1024));             \
+        if (lane < 2)                                                                                    \
+            SBO_OZ3_DMA16(gE + (int64_t)(T_) * 64 + (h_) * 32,                                           \
+                          __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((sl_) * kOz3Slot + kOzA))); \
+    } while (0)
+    // this wave's part of the K* table piece of (query block qb_, k-tile kt_)
+#define SBO_OZ3_TABLE(kt_, qb_)                                                                          \
+    do {                                                                                                 \
+        const char *z_ = gZ + ((int64_t)(qb_) * nkt + (kt_)) * kKzt;                                      \
+        _Pragma("unroll") for (int u_ = 0; u_ < kOzKDigits; ++u_)                                        \
+            SBO_OZ3_DMA16(z_ + wave * 4096 + u_ * 1024, lds_tab + (uint32_t)(wave_u * 4096 + u_ * 1024)); \
+        if (lane < 4) SBO_OZ3_DMA16(z_ + kKztE + wave * 64, lds_tab + (uint32_t)(kKztE + wave_u * 64));   \
+        if (lane < 8) SBO_OZ3_DMA16(z_ + kKztMu + wave * 128, lds_tab + (uint32_t)(kKztMu + wave_u * 128)); \
+    } while (0)
+#define SBO_OZ3_DESC_WINDOW(w_)                                                                          \
+    do {                                                                                                 \
+        if (wave == 1) SBO_OZ3_DMA16(gD + (int64_t)(w_) * 1024, lds_dwin + (uint32_t)((w_) & 1) * 1024u); \
+    } while (0)
+#define SBO_OZ3_LIST_WINDOW(w_)                                                                          \
+    do {                                                                                                 \
+        if (wave == 2) SBO_OZ3_DMA16(gL + (int64_t)(w_) * 1024, lds_lwin + (uint32_t)((w_) & 1) * 1024u); \
+    } while (0)
+    auto desc_at = [&](int k) {
+        const int4 d = dwin[((k / kOzDescWin) & 1) * kOzDescWin + k % kOzDescWin];
+        const int I = min(max(__builtin_amdgcn_readfirstlane(d.x), 0), nI - 1);
+        return make_int4(I, __builtin_amdgcn_readfirstlane(d.y), __builtin_amdgcn_readfirstlane(d.z),
+                         __builtin_amdgcn_readfirstlane(d.w));
+    };
+    auto entry_off = [](const int4 &d) {
+        return (uint64_t)(uint32_t)d.z | ((uint64_t)((uint32_t)d.w >> 16) << 32);
+    };
+    auto list_at = [&](uint64_t e, int I) {
+        const int t = __builtin_amdgcn_readfirstlane((int)lwin[((e / kOzListWin) & 1) * kOzListWin + e % kOzListWin]) &
+                      ((1 << kLevelShift) - 1);
+        return min(t, kTilesPerRowBlockStep * (I + 1) - 1);
+    };
+
+    // ---- prologue: windows, the first tile (both halves and its table piece)
+    SBO_OZ3_DESC_WINDOW(k0 / kOzDescWin);
+    SBO_OZ3_DESC_WINDOW(k0 / kOzDescWin + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // the current tile (k, j: item and its j-th tile; e: its tile-list entry)
+    int4 dc = desc_at(k0);
+    uint64_t e = entry_off(dc);
+    SBO_OZ3_LIST_WINDOW(e / kOzListWin);
+    SBO_OZ3_LIST_WINDOW(e / kOzListWin + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int j = 0;
+    const int t = list_at(e, dc.x);
+    SBO_OZ3_TABLE(t, dc.y);
+    SBO_OZ3_A(tile_start(dc.x) + t, 0, 0);
+    SBO_OZ3_A(tile_start(dc.x) + t, 1, 1);
+    // the next tile (kN, jN, eN, tN, dN), valid while kN < k1; its windows are
+    // requested as it enters them (each is read only after a later barrier)
+    int kN = k0, jN = 1, tN = 0;
+    uint64_t eN = e + 1;
+    int4 dN = dc;
+    auto advance = [&]() {
+        if (jN >= (dN.w & 0xffff)) {
+            ++kN;
+            jN = 0;
+            if (kN < k1) {
+                dN = desc_at(kN);
+                if (kN % kOzDescWin == 0) SBO_OZ3_DESC_WINDOW(kN / kOzDescWin + 1);
+            }
+        }
+        if (kN < k1) {
+            if (eN % kOzListWin == 0) SBO_OZ3_LIST_WINDOW(eN / kOzListWin + 1);
+            tN = list_at(eN, dN.x);
+        }
+    };
+    advance();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    f64x4 acc[kOzRB];
+#pragma unroll
+    for (int rb = 0; rb < kOzRB; ++rb) acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    i32x4 kd[kOzKDigits];
+    int eK = 0;
+    double mu = 0.0;
+    int64_t q = (int64_t)dc.y * kBN + wave * 16 + r;
+    int sl = 0, h = 0;
+    for (;;) {
+        const bool more = kN < k1;
+        const char *slot = smem + sl * kOz3Slot;
+        const int sl2 = sl == 0 ? 2 : sl - 1;   // (sl + 2) % 3: the slot stage s - 1 read
+        const int I = dc.x;
+        if (more) SBO_OZ3_A(tile_start(dN.x) + tN, h, sl2);
+        if (h == 0) {
+            // this tile's K* digits into registers, then (the wave's reads
+            // done) the next tile's table piece into the same bytes
+            const char *tz = smem + kOz3Table;
+#pragma unroll
+            for (int u = 0; u < kOzKDigits; ++u)
+                kd[u] = *reinterpret_cast<const i32x4 *>(tz + wave * 4096 + u * 1024 + lane * 16);
+            eK = *reinterpret_cast<const int *>(tz + kKztE + (wave * 16 + r) * 4);
+            if (I == nI - 1 && g == 0) mu += *reinterpret_cast<const double *>(tz + kKztMu + (wave * 16 + r) * 8);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (more) SBO_OZ3_TABLE(tN, dN.y);
+            stage_blocks<0>(slot, lane, kd, eK, acc);
+        } else {
+            stage_blocks<1>(slot, lane, kd, eK, acc);
+        }
+        if (h == 1 && j == (dc.w & 0xffff) - 1) {
+            // item done: column sums of V^2 over its 256 rows
+            double sum = 0.0;
+#pragma unroll
+            for (int rb = 0; rb < kOzRB; ++rb) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) sum = fma(acc[rb][c], acc[rb][c], sum);
+                acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
+            }
+            sum += __shfl_xor(sum, 16);
+            sum += __shfl_xor(sum, 32);
+            const bool writer = lane < 16 && q < m;
+            if (writer) part[(int64_t)I * ldp + q] = sum;
+            if (I == nI - 1) {
+                mu += __shfl_xor(mu, 16);
+                mu += __shfl_xor(mu, 32);
+                if (writer) mean[q] = m0 + mu;
+                mu = 0.0;
+            }
+        }
+        // the next tile's pieces issued in this stage may stay in flight; what
+        // was issued before them (the stage after this one) has landed
+        if (!more)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (h == 0)
+            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // kOz3AGroup + kOz3TGroup
+        else
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");    // kOz3AGroup
+        __syncthreads();
+        if (h == 1) {
+            if (!more) break;
+            j = jN;
+            q = (int64_t)dN.y * kBN + wave * 16 + r;
+            dc = dN;
+            ++jN;
+            ++eN;
+            advance();
+        }
+        h ^= 1;
+        sl = sl == 2 ? 0 : sl + 1;
+    }
+#undef SBO_OZ3_A
+#undef SBO_OZ3_TABLE
+#undef SBO_OZ3_DESC_WINDOW
+#undef SBO_OZ3_LIST_WINDOW
+#undef SBO_OZ3_DMA16
 }
 
 // The K* table of nq query blocks (SBO_OPT_PRECISE_KERNEL 3): one workgroup per
@@ -1120,6 +1347,16 @@ hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, con
     }
 #endif
 #ifdef SBO_DIAG
+    if (variant == 11 || variant == 12) {   // timing bounds: kernel 3 without any stage DMA / the table's
+        if (!kzt) return hipErrorInvalidValue;
+        if (variant == 11)
+            hipLaunchKernelGGL(predict_oz_kernel<3>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc,
+                               tl, seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean, kzt);
+        else
+            hipLaunchKernelGGL(predict_oz_kernel<4>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc,
+                               tl, seg, P, n_items, nI, qx, qy, m, ldp, cexp, m0, part, mean, kzt);
+        return hipGetLastError();
+    }
     if (variant == 10) {   // timing bound: pair mode without the table traffic (wrong results)
         hipLaunchKernelGGL(predict_oz2_kernel<true>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, desc, tl,
                            seg, P, n_items, nI, m, ldp, m0, part, mean, kzt);
@@ -1130,6 +1367,12 @@ hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, con
         if (!kzt) return hipErrorInvalidValue;
         hipLaunchKernelGGL(predict_oz2_kernel<false>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, desc, tl,
                            seg, P, n_items, nI, m, ldp, m0, part, mean, kzt);
+        return hipGetLastError();
+    }
+    if (variant == 5) {   // K*'s digits from the table, A staged a tile ahead
+        if (!kzt) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(predict_oz3_kernel, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, desc, tl, seg, P,
+                           n_items, nI, m, ldp, m0, part, mean, kzt);
         return hipGetLastError();
     }
     if (variant == 3) {   // K*'s digits from the table

@@ -2310,12 +2310,12 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             return SBO_OK;
         case SBO_OPT_PRECISE_KERNEL:
 #ifdef SBO_DIAG
-            SBO_CHECK(value == 0 || value == 1 || value == 3 || value == 4 || value == 9 || value == 10, SBO_E_INVAL,
-                      "SBO_OPT_PRECISE_KERNEL: 0, 1, 3, 4, 9 or 10 (diagnostics)");
+            SBO_CHECK(value == 0 || value == 1 || (value >= 3 && value <= 5) || (value >= 9 && value <= 12),
+                      SBO_E_INVAL, "SBO_OPT_PRECISE_KERNEL: 0, 1, 3, 4, 5 or 9-12 (diagnostics)");
 #else
-            SBO_CHECK(value == 0 || value == 1 || value == 3 || value == 4, SBO_E_INVAL,
-                      "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA), 1 (int8), 3 (int8, K* table) or 4 (int8, "
-                      "k-tile pairs)");
+            SBO_CHECK(value == 0 || value == 1 || (value >= 3 && value <= 5), SBO_E_INVAL,
+                      "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA), 1 (int8), 3 (int8, K* table), 4 (int8, "
+                      "k-tile pairs) or 5 (int8, K* table, A a tile ahead)");
 #endif
             {
                 // the operand layout each kernel reads: f64 tiles, int8 tiles, int8 pairs

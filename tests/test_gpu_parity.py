@@ -1390,10 +1390,10 @@ def test_precision_levels(mapper):
 # the precise kernels' tolerances against the fp64 oracle: the f64 sweep to
 # f64 rounding (f32 outputs: 1e-6), the int8 sliced sweep to its slicing
 # (emulated 1.2e-6 on the lpsc box at N = 8192, tools/r4_emulate_ozaki.py)
-PRECISE_TOL = {0: (1e-6, 1e-6), 1: (1e-6, 4e-6), 3: (1e-6, 4e-6), 4: (1e-6, 4e-6)}
+PRECISE_TOL = {0: (1e-6, 1e-6), 1: (1e-6, 4e-6), 3: (1e-6, 4e-6), 4: (1e-6, 4e-6), 5: (1e-6, 4e-6)}
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 3, 4])
+@pytest.mark.parametrize("kernel", [0, 1, 3, 4, 5])
 @pytest.mark.parametrize("n,gw,gh,box", [(2048, 64, 48, False), (3000, 90, 70, True), (700, 40, 30, True)])
 def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box, kernel):
     """SBO_OPT_PRECISION = 1: the f64 sweep (SBO_OPT_PRECISE_KERNEL 0: A =
@@ -1449,7 +1449,7 @@ def test_int8_mfma_k_layout(mapper):
     for n in (64, 65, 130):
         wl = synthetic_box(n, 7, 5, seed=n)
         outs = {}
-        for kernel in (0, 1, 3):
+        for kernel in (0, 1, 3, 5):
             gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
             gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
             gm.set_option(N.SBO_OPT_PRECISION, 1)
@@ -1458,7 +1458,7 @@ def test_int8_mfma_k_layout(mapper):
         gm.set_option(N.SBO_OPT_PRECISION, -1)
         gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 3)
         omu, ovar = oracle_given_factor64(gm, wl)
-        for kernel in (0, 1, 3):
+        for kernel in (0, 1, 3, 5):
             mu, sd = outs[kernel]
             emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
             print(f"N={n} kernel {kernel}: mu {emu:.2e} var {evar:.2e}")
@@ -1509,7 +1509,8 @@ def test_kstar_table_chunks(mapper):
     is bitwise kernel 1's (the mean sums its per-tile terms in another order:
     within 1e-12); bitwise the same for any chunking (1 MiB: one query block
     per chunk on this N) and sweep partition, on the lpsc box with a ragged
-    last query block."""
+    last query block.  Kernel 5 (A staged a tile ahead, round 5) is bitwise
+    kernel 3 under every chunking and partition."""
     from safe_bayesian_optimization_amd.terrain import synthetic_box
     wl = synthetic_box(3000, 61, 29, seed=5)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
@@ -1517,7 +1518,8 @@ def test_kstar_table_chunks(mapper):
     try:
         gm.fit(wl.x, wl.y, wl.obs)
         res = {}
-        for kernel, mb, groups in ((1, 2048, 0), (3, 2048, 0), (3, 0, 0), (3, 1, 0), (3, 1, 7), (3, 3, 1000)):
+        for kernel, mb, groups in ((1, 2048, 0), (3, 2048, 0), (3, 0, 0), (3, 1, 0), (3, 1, 7), (3, 3, 1000),
+                                   (5, 2048, 0), (5, 1, 0), (5, 1, 7), (5, 3, 1000), (5, 2, 31)):
             gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
             gm.set_option(N.SBO_OPT_TABLE_MB, mb)
             gm.set_option(N.SBO_OPT_SWEEP_GROUPS, groups)
@@ -1525,7 +1527,7 @@ def test_kstar_table_chunks(mapper):
         base = res[(3, 2048, 0)]
         for k, (mu, sd) in res.items():
             assert np.array_equal(sd, res[(1, 2048, 0)][1]), k
-            if k[0] == 3:
+            if k[0] in (3, 5):
                 assert np.array_equal(mu, base[0]) and np.array_equal(sd, base[1]), k
         assert nrel(base[0], res[(1, 2048, 0)][0].astype(np.float64)) < 1e-6
         omu, ovar = oracle_given_factor64(gm, wl)

@@ -3,7 +3,8 @@ box at N (default 16384) and the bench's 1000 x 1000 grid: for each precise
 kernel (OZ_KERNELS, default "3 4") and each block shape (BLOCKS, bi:bq pairs,
 "0" = row-block-major), ms per tick (HIP events of the sweep launches,
 sbo_profile) and whether mu / sd are bitwise those of the row-block-major
-order (they must be: items are independent).  GPU diagnostic, one JSON line.
+order (they must be: items are independent); REF_ACROSS=1 compares every
+kernel with the first one's output instead.  GPU diagnostic, one JSON line.
     python tools/r5_plan_block_ab.py [n]"""
 import ctypes
 import json
@@ -31,11 +32,14 @@ def main():
     kernels = [int(k) for k in os.environ.get("OZ_KERNELS", "3 4").split()]
     blocks = os.environ.get("BLOCKS", "0 4:8 2:16 8:4 1:32").split()
     out = {"n": n}
+    across = os.environ.get("REF_ACROSS") == "1"   # compare every kernel with the first one's output
+    ref = None
     for kernel in kernels:
         gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
         gm.fit(t(wl.x), t(wl.y), t(wl.obs))
         qx, qy = t(wl.qx), t(wl.qy)
-        ref = None
+        if not across:
+            ref = None
         for b in blocks:
             v = 0 if b == "0" else (int(b.split(":")[0]) << 8) | int(b.split(":")[1])
             gm.set_option(N.SBO_OPT_PLAN_BLOCK, v)
