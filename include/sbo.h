@@ -467,6 +467,10 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * and `train` training locations (SBO_OPT_PRECISION); the next fit or append
  * probes again. */
 #define SBO_OPT_PROBE_SIZE 27
+/* SBO_OPT_INV_OZ_MIN (2048, 4096 default, 8192): the smallest split of the
+ * recursive inverse whose two products run as the int8-sliced GEMM
+ * (SBO_OPT_INV_OZ); the levels below keep dgemm products. */
+#define SBO_OPT_INV_OZ_MIN 28
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The last inverse check (SBO_OPT_INV_CHECK) of the current fit: ran = 1 if

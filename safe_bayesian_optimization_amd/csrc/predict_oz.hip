@@ -495,6 +495,13 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
 // pieces in flight, at the end of a second-half stage vmcnt(A group); anything
 // issued earlier (windows, the previous stage's groups) is complete there.
 // Products, digits and sums are kernel 3's: results bitwise equal.
+// a wave-uniform pointer the compiler cannot prove uniform, into SGPRs
+__device__ __forceinline__ const char *sgpr_ptr(const char *p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const char *>((uintptr_t)(((uint64_t)hi << 32) | lo));
+}
 constexpr int kOz3Slot = kOzA + kOzE;                       // A digits + block exponents
 constexpr int kOz3Table = 3 * kOz3Slot;                     // the K* table piece (per-wave parts)
 constexpr int kOz3Win = kOz3Table + kKzt;                   // descriptor + list windows
@@ -527,50 +534,58 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz3_kernel(
     const uint32_t lds_dwin = lds_smem + kOz3Win;
     const uint32_t lds_lwin = lds_dwin + 2048u;
     const uint32_t lds_tab = lds_smem + kOz3Table;
-    const char *gA = aoz + wave * 1024 + lane * 16;
-    const char *gE = reinterpret_cast<const char *>(eoz) + lane * 16;
-    const char *gD = reinterpret_cast<const char *>(desc) + lane * 16;
-    const char *gL = reinterpret_cast<const char *>(tl) + lane * 16;
-    const char *gZ = kzt + lane * 16;
     const int nkt = kTilesPerRowBlockStep * nI;
-#define SBO_OZ3_DMA16(gsrc, ldst)                                                                        \
+    // LDS-DMA with an SGPR base (global_load_lds_dwordx4 v_off, s_base), as in
+    // predict_x3.hip: the only per-lane operand is the byte offset lane * 16,
+    // so no 64-bit per-lane address competes with the accumulators for VGPRs
+    // (a spilled address's reload waits for vmcnt(0), which would drain the
+    // stream this kernel keeps in flight); the partial pieces run under a
+    // wave-uniform EXEC mask, so every wave issues the same count.
+    const uint32_t voff = (uint32_t)lane * 16u;
+    const char *sA = aoz + (int64_t)wave_u * 1024;
+    const char *sE = reinterpret_cast<const char *>(eoz);
+    const char *sD = reinterpret_cast<const char *>(desc);
+    const char *sL = reinterpret_cast<const char *>(tl);
+    // (the windows: wave 1 the descriptors, wave 2 the list; masks in SGPRs)
+    const uint64_t win_mask1 = (uint64_t)0 - (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(wave == 1 ? 1 : 0);
+    const uint64_t win_mask2 = (uint64_t)0 - (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(wave == 2 ? 1 : 0);
+#define SBO_OZ3_DMA16(sbase, ldst)                                                                       \
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"((const void *)sgpr_ptr(sbase)), \
+                 "{m0}"(ldst)                                                                           \
+                 : "memory")
+#define SBO_OZ3_DMA16M(sbase, ldst, mask)                                                                \
     do {                                                                                                 \
-        uint32_t keep_;                                                                                  \
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t" \
-                     "s_mov_b32 m0, %0"                                                                  \
-                     : "=&s"(keep_)                                                                      \
-                     : "v"(gsrc), "s"(ldst)                                                              \
-                     : "memory");                                                                        \
+        uint64_t sv_;                                                                                    \
+        asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %4\n\ts_nop 0\n\t"                     \
+                     "global_load_lds_dwordx4 %1, %2\n\ts_mov_b64 exec, %0"                              \
+                     : "=&s"(sv_)                                                                        \
+                     : "v"(voff), "s"((const void *)sgpr_ptr(sbase)), "{m0}"(ldst), "s"((uint64_t)(mask)) \
+                     : "memory", "scc");                                                                 \
     } while (0)
     // half h_ of packed tile T_ into A slot sl_ (the exponents by every wave's
     // lanes 0-1: the same 32 B, so the per-wave group counts are uniform)
 #define SBO_OZ3_A(T_, h_, sl_)                                                                           \
     do {                                                                                                 \
-        const char *s_ = gA + (int64_t)(T_) * kOzTileBytes + (h_) * kOzA;                                \
+        const char *s_ = sA + (int64_t)(T_) * kOzTileBytes + (h_) * kOzA;                                \
         const uint32_t d_ = __builtin_amdgcn_readfirstlane(lds_wave + (uint32_t)(sl_) * kOz3Slot);       \
         _Pragma("unroll") for (int j_ = 0; j_ < kOz3AGroup - 1; ++j_)                                    \
             SBO_OZ3_DMA16(s_ + j_ * kOzWaves * 1024, d_ + (uint32_t)(j_ * kOzWaves * 1024));             \
-        if (lane < 2)                                                                                    \
-            SBO_OZ3_DMA16(gE + (int64_t)(T_) * 64 + (h_) * 32,                                           \
-                          __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((sl_) * kOz3Slot + kOzA))); \
+        SBO_OZ3_DMA16M(sE + (int64_t)(T_) * 64 + (h_) * 32,                                              \
+                       __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)((sl_) * kOz3Slot + kOzA)), 0x3ull); \
     } while (0)
     // this wave's part of the K* table piece of (query block qb_, k-tile kt_)
 #define SBO_OZ3_TABLE(kt_, qb_)                                                                          \
     do {                                                                                                 \
-        const char *z_ = gZ + ((int64_t)(qb_) * nkt + (kt_)) * kKzt;                                      \
+        const char *z_ = kzt + ((int64_t)(qb_) * nkt + (kt_)) * kKzt;                                     \
         _Pragma("unroll") for (int u_ = 0; u_ < kOzKDigits; ++u_)                                        \
-            SBO_OZ3_DMA16(z_ + wave * 4096 + u_ * 1024, lds_tab + (uint32_t)(wave_u * 4096 + u_ * 1024)); \
-        if (lane < 4) SBO_OZ3_DMA16(z_ + kKztE + wave * 64, lds_tab + (uint32_t)(kKztE + wave_u * 64));   \
-        if (lane < 8) SBO_OZ3_DMA16(z_ + kKztMu + wave * 128, lds_tab + (uint32_t)(kKztMu + wave_u * 128)); \
+            SBO_OZ3_DMA16(z_ + wave_u * 4096 + u_ * 1024, lds_tab + (uint32_t)(wave_u * 4096 + u_ * 1024)); \
+        SBO_OZ3_DMA16M(z_ + kKztE + wave_u * 64, lds_tab + (uint32_t)(kKztE + wave_u * 64), 0xfull);     \
+        SBO_OZ3_DMA16M(z_ + kKztMu + wave_u * 128, lds_tab + (uint32_t)(kKztMu + wave_u * 128), 0xffull); \
     } while (0)
 #define SBO_OZ3_DESC_WINDOW(w_)                                                                          \
-    do {                                                                                                 \
-        if (wave == 1) SBO_OZ3_DMA16(gD + (int64_t)(w_) * 1024, lds_dwin + (uint32_t)((w_) & 1) * 1024u); \
-    } while (0)
+    SBO_OZ3_DMA16M(sD + (int64_t)(w_) * 1024, lds_dwin + (uint32_t)((w_) & 1) * 1024u, win_mask1)
 #define SBO_OZ3_LIST_WINDOW(w_)                                                                          \
-    do {                                                                                                 \
-        if (wave == 2) SBO_OZ3_DMA16(gL + (int64_t)(w_) * 1024, lds_lwin + (uint32_t)((w_) & 1) * 1024u); \
-    } while (0)
+    SBO_OZ3_DMA16M(sL + (int64_t)(w_) * 1024, lds_lwin + (uint32_t)((w_) & 1) * 1024u, win_mask2)
     auto desc_at = [&](int k) {
         const int4 d = dwin[((k / kOzDescWin) & 1) * kOzDescWin + k % kOzDescWin];
         const int I = min(max(__builtin_amdgcn_readfirstlane(d.x), 0), nI - 1);
@@ -701,6 +716,7 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz3_kernel(
 #undef SBO_OZ3_DESC_WINDOW
 #undef SBO_OZ3_LIST_WINDOW
 #undef SBO_OZ3_DMA16
+#undef SBO_OZ3_DMA16M
 }
 
 // The K* table of nq query blocks (SBO_OPT_PRECISE_KERNEL 3): one workgroup per

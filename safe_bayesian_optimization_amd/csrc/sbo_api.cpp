@@ -125,11 +125,10 @@ int inverse_base_cases(int64_t n, int64_t base) {
 sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
                              int &slot, sbo::DevBuf *ozws = nullptr);
 // SBO_OPT_INV_OZ: a level of the recursion whose split is at least
-// kInvOzMinSplit runs its two products as the sliced GEMM (K <= 16384); the
-// 2048 level's products stay dgemms
-constexpr int64_t kInvOzMinSplit = 4096;
+// SBO_OPT_INV_OZ_MIN (default 4096) runs its two products as the sliced GEMM
+// (K <= 16384); the levels below keep dgemms
 bool oz_level(const sbo_ctx *ctx, int64_t h, int64_t m) {
-    return ctx->inv_oz != 0 && !ctx->inv_oz_off && h >= kInvOzMinSplit && h <= 16384 && m <= 16384;
+    return ctx->inv_oz != 0 && !ctx->inv_oz_off && h >= ctx->inv_oz_min && h <= 16384 && m <= 16384;
 }
 // does the recursive inverse of n columns slice any of its products?
 bool inverse_sliced(const sbo_ctx *ctx, int64_t n) {
@@ -2327,6 +2326,11 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
         case SBO_OPT_INV_OZ:
             SBO_CHECK(value == 0 || value == 5 || value == 6, SBO_E_INVAL, "SBO_OPT_INV_OZ must be 0, 5 or 6");
             ctx->inv_oz = (int)value;
+            return SBO_OK;
+        case SBO_OPT_INV_OZ_MIN:
+            SBO_CHECK(value == 2048 || value == 4096 || value == 8192, SBO_E_INVAL,
+                      "SBO_OPT_INV_OZ_MIN must be 2048, 4096 or 8192");
+            ctx->inv_oz_min = value;
             return SBO_OK;
         case SBO_OPT_PROBE_SIZE:
             SBO_CHECK(value >= 0 && (value >> 16) >= 4 && (value >> 16) <= 256 && (value & 0xffff) >= 1 &&

@@ -3,7 +3,9 @@
 csrc/ozgemm.hip): warm fit time, the precision probe's verdict and error,
 and the posterior over the whole grid against the dgemm fit's (normwise
 max |d| / max |ref| of mu and of var).  Workloads: C4 (synthetic, N = 16384,
-1000 x 1000) and the lpsc box (N = 16384, 1000 x 1000).  GPU diagnostic.
+1000 x 1000) and the lpsc box (N = 16384, 1000 x 1000).  INV_OZ_MIN (round
+5): the smallest sliced splits to try (SBO_OPT_INV_OZ_MIN, default "4096");
+the guard's measure (sbo_get_inverse_check) is printed.  GPU diagnostic.
     python tools/r4_inv_oz_ab.py [n] [digits ...]"""
 import os
 import sys
@@ -26,9 +28,11 @@ def main():
     t = lambda a: torch.tensor(np.ascontiguousarray(a, np.float32), device=dev)  # noqa: E731
     for name, wl in (("C4", synthetic(n, 1000, 1000, seed=0)), ("lpsc box", synthetic_box(n, 1000, 1000, seed=0))):
         ref = None
-        for oz in [0] + digits:
+        mins = [int(v) for v in os.environ.get("INV_OZ_MIN", "4096").split()]
+        for oz, omin in [(0, 4096)] + [(d, m) for d in digits for m in mins]:
             gm = TerrainMapper(0, wl.hyper)
             gm.set_option(N.SBO_OPT_INV_OZ, oz)
+            gm.set_option(N.SBO_OPT_INV_OZ_MIN, omin)
             X, Y, O = t(wl.x), t(wl.y), t(wl.obs)
             ts = []
             for _ in range(4):
@@ -41,8 +45,10 @@ def main():
             mu, sd = gm.predict(t(wl.qx), t(wl.qy))
             mu = mu.cpu().numpy().astype(np.float64)
             var = sd.cpu().numpy().astype(np.float64) ** 2
-            line = (f"{name} N={n} inv_oz={oz}: warm fits {', '.join(f'{v:.1f}' for v in ts[1:])} ms, "
-                    f"precise={precise} probe_err={perr:.3e}")
+            chk = gm.inverse_check()
+            line = (f"{name} N={n} inv_oz={oz} min={omin}: warm fits {', '.join(f'{v:.1f}' for v in ts[1:])} ms, "
+                    f"precise={precise} probe_err={perr:.3e} guard ran={chk['ran']} err={chk['err']:.2e} "
+                    f"fired={chk['fired']} {chk['ms']:.2f} ms")
             if ref is None:
                 ref = (mu, var)
             else:

@@ -12,4 +12,5 @@ REF_ACROSS=1 OZ_KERNELS="3 5" BLOCKS="0" step k5_ab 300 python -u tools/r5_plan_
 step guard_tests 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests/test_gpu_invcheck.py
 step bench 300 python -u bench.py --no-cpu --no-regimes --steps 5 --warmup 2
 SBO_LIB=safe_bayesian_optimization_amd/lib/libsbo_diag.so OZ_KERNELS="3 11 12" step bounds 600 python -u tools/r4_oz_ab.py 16384 256
-step probe_design 900 python -u tools/r5_probe_design.py 8192 500
+INV_OZ_MIN="4096 2048" step inv_oz_min 600 python -u tools/r4_inv_oz_ab.py 16384 6
+step probe_design 600 python -u tools/r5_probe_design.py 8192 500
