@@ -400,7 +400,13 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * sgemm / ssyrk (0) or by the library's f32 matrix-core kernel -- 2 all of
  * them, 1 the trailing updates of at most 8192 rows, where it measured faster
  * than ssyrk (the fit's time is the same: those run beside the chain).  All
- * compute in f32 with exact f32 products; the factors agree to f32 rounding. */
+ * compute in f32 with exact f32 products; the factors agree to f32 rounding.
+ * 3: the outer panels' rank-512 updates on the bf16 matrix cores with each
+ * f32 operand split into three bf16 pieces (six products per f32 product,
+ * f32 accumulation): C4 fit 46.1 -> 43.8 ms, but the factor's backward error
+ * grows 1.3x (synthetic) to 2.6x (the lpsc box), which on the box moves the
+ * posterior 1.9e-4 from the exact one against 4.8e-6 -- not for the precise
+ * regime, hence not the default. */
 #define SBO_OPT_CHOL_GEMM 17
 /* SBO_OPT_INV_BASE (default 2048, in [1024, 8192], rounded down to a multiple
  * of 128) and SBO_OPT_INV_PANELS (default 16, in [1, 64]): the recursive f64

@@ -1241,6 +1241,8 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
     // tools/r3_gemm_probe.cpp); the upper triangle it also writes is never read
     constexpr int64_t kSmallTrail = 6144;
     bool trail_pending = false;
+    if (ctx->chol_gemm_own == 3 && n > NB2)   // both plane buffers at the first panel's size, up front
+        for (sbo::DevBuf &pb : ctx->cholx3) SBO_HIP(pb.reserve(sbo::chol_x3_bytes(n - NB2, NB2)));
     sbo_status st = SBO_OK;
     for (int64_t K = 0; K < n && st == SBO_OK; K += NB2) {
         const int64_t W = std::min(NB2, n - K);
@@ -1302,10 +1304,26 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         const float *P = L + (K + W) + K * ld;   // the panel's rows below it: m3 x W
         float *C1 = L + (K + W) + (K + W) * ld;
         const int64_t W2 = std::min(NB2, m3);    // the next outer panel
+        // SBO_OPT_CHOL_GEMM 3: the panel split into bf16 planes once, read by
+        // the look-ahead here and the trailing update on aux_stream (two
+        // buffers: this panel's trailing update may still read the previous
+        // buffer's twin until the next look-ahead has waited for it)
+        const bool x3 = ctx->chol_gemm_own == 3 && W % 32 == 0;
+        char *planes = nullptr;
+        if (x3) {
+            sbo::DevBuf &pb = ctx->cholx3[(K / NB2) & 1];
+            if (pb.reserve(sbo::chol_x3_bytes(m3, W)) != hipSuccess ||
+                sbo::launch_chol_split(ctx->stream, P, ld, m3, W, pb.as<char>()) != hipSuccess) {
+                st = SBO_E_DEVICE;
+                break;
+            }
+            planes = pb.as<char>();
+        }
         if (hipEventRecord(ctx->ev_panel, ctx->stream) != hipSuccess ||
             (trail_pending && hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0) != hipSuccess)) { st = SBO_E_DEVICE; break; }
         const bool la_ok =
-            ctx->chol_gemm_own == 2
+            x3 ? sbo::launch_chol_update_x3(ctx->stream, planes, m3, W, 0, m3, 0, W2, false, C1, ld) == hipSuccess
+            : ctx->chol_gemm_own == 2
                 ? sbo::launch_chol_update(ctx->stream, P, P, ld, m3, W2, W, false, C1) == hipSuccess
                 : rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m3,
                                 (rocblas_int)W2, (rocblas_int)W, &minus_one, P, (rocblas_int)ld, P, (rocblas_int)ld,
@@ -1318,7 +1336,10 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
             // (1: the own kernel only where it measured faster than rocBLAS,
             // the lower update of m4 <= 8192; 2: every update)
             bool ok;
-            if (ctx->chol_gemm_own == 2 || (ctx->chol_gemm_own == 1 && m4 <= 8192))
+            if (x3)
+                ok = sbo::launch_chol_update_x3(ctx->aux_stream, planes, m3, W, W2, m4, W2, m4, true,
+                                                C1 + W2 + W2 * ld, ld) == hipSuccess;
+            else if (ctx->chol_gemm_own == 2 || (ctx->chol_gemm_own == 1 && m4 <= 8192))
                 ok = sbo::launch_chol_update(ctx->aux_stream, P + W2, P + W2, ld, m4, m4, W, true,
                                              C1 + W2 + W2 * ld) == hipSuccess;
             else
@@ -2285,7 +2306,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->inv_panels = value;
             return SBO_OK;
         case SBO_OPT_CHOL_GEMM:
-            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_CHOL_GEMM must be 0, 1 or 2");
+            SBO_CHECK(value >= 0 && value <= 3, SBO_E_INVAL, "SBO_OPT_CHOL_GEMM must be 0, 1, 2 or 3");
             ctx->chol_gemm_own = (int)value;
             return SBO_OK;
         case SBO_OPT_CHOL_DIAG:
@@ -2408,7 +2429,8 @@ SBO_API sbo_status sbo_trim(sbo_ctx *ctx) {
     if (ctx->aux_stream) SBO_HIP(hipStreamSynchronize(ctx->aux_stream));
     if (ctx->inv_stream) SBO_HIP(hipStreamSynchronize(ctx->inv_stream));
     if (ctx->chk_stream) SBO_HIP(hipStreamSynchronize(ctx->chk_stream));
-    for (sbo::DevBuf *b : {&ctx->scratch, &ctx->gzws, &ctx->gzws_aux, &ctx->chk, &ctx->restage, &ctx->kzt, &ctx->qcost})
+    for (sbo::DevBuf *b : {&ctx->scratch, &ctx->gzws, &ctx->gzws_aux, &ctx->chk, &ctx->restage, &ctx->kzt, &ctx->qcost,
+                           &ctx->cholx3[0], &ctx->cholx3[1]})
         b->release();
     return SBO_OK;
 }

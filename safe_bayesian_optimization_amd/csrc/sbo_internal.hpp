@@ -193,6 +193,7 @@ struct sbo_ctx {
     sbo::DevBuf aoz, eoz, koz;   // int8 digit operand, its block exponents, coordinates (predict_oz.hip)
     sbo::DevBuf gzws;            // the int8-sliced GEMM's packed operands (SBO_OPT_INV_OZ)
     sbo::DevBuf gzws_aux;        //   and those of the products on aux_stream (the inverse's second half)
+    sbo::DevBuf cholx3[2];       // the Cholesky's outer panels split into bf16 planes (SBO_OPT_CHOL_GEMM 3), alternating
     sbo::DevBuf kzt;             // the int8 sweep's K* table of one chunk of query blocks (SBO_OPT_PRECISE_KERNEL 3)
     int precise_kernel = 3;      // SBO_OPT_PRECISE_KERNEL: 0 the f64 MFMA sweep, 1 the int8 sliced sweep, 3 the same reading the K* table
     int64_t a64_I0 = 0;          // first row block whose precise operand (of precise_kernel) is stale
@@ -363,6 +364,15 @@ hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t
 // C -= P Q^T over 128 x 128 tiles (lower: the tiles on and below the diagonal of an m x m C), f32, lda ld, K columns
 hipError_t launch_chol_update(hipStream_t s, const float *P, const float *Q, int64_t ld, int64_t m, int64_t nc,
                               int64_t K, bool lower, float *C);
+// SBO_OPT_CHOL_GEMM 3 (csrc/chol_x3.hip): the outer panel P (m x K f32, lda ld,
+// K a multiple of 32) into three bf16 planes in MFMA fragment order
+// (chol_x3_bytes), then C (rows x cols, lda ld) -= P[r0 ..] P[c0 ..]^T on the bf16
+// matrix cores with six split products per f32 product (lower: the tiles on and
+// below the diagonal of a square region with r0 == c0)
+size_t chol_x3_bytes(int64_t m, int64_t K);
+hipError_t launch_chol_split(hipStream_t s, const float *P, int64_t ld, int64_t m, int64_t K, char *planes);
+hipError_t launch_chol_update_x3(hipStream_t s, const char *planes, int64_t m, int64_t K, int64_t r0, int64_t rows,
+                                 int64_t c0, int64_t cols, bool lower, float *C, int64_t ld);
 // The panel below it: A21 (m2 x kb, lda ld) := A21 L11^-T (forward substitution, f32).
 // version 1: chol_trsm_mfma_kernel (MFMA updates of the later columns; default), 0: chol_trsm_kernel (bitwise equal)
 hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb, float *A21, int64_t m2, int version = 1);
