@@ -285,6 +285,123 @@ __global__ __launch_bounds__(256, 1) void gz_gemm_kernel(const char *__restrict_
     }
 }
 
+// Round 5: the same product with more waves per SIMD -- NW = 16 (the
+// default): sixteen waves of 16 x 32 (one A block and two B blocks each,
+// ND x 2 int32 accumulator blocks, 95 VGPRs, four waves per SIMD); NW = 8
+// (built with SBO_GZ_8WAVE): eight of 16 x 64 -- so that one wave's products
+// run while the others wait on their LDS reads or the stage barrier; the
+// stage and its 1 KiB LDS-DMA pieces are the four-wave kernel's.  The inverse's
+// top-level products at 8192^3 (tools/ozgemm_bench.hip, packs included,
+// profiles/r5_ozgemm_waves.log): 5.93 / 5.88 ms with four waves (one per
+// SIMD), 5.00 / 5.06 with eight, 4.68 / 4.73 with sixteen.  Bitwise the
+// four-wave kernel's results (the int32 level sums are exact in any order;
+// the combination is the same code).
+template <int ND, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void gz_gemm8_kernel(const char *__restrict__ Ad, const int *__restrict__ eA,
+                                                              const char *__restrict__ Bd, const int *__restrict__ eB,
+                                                              int64_t m, int64_t n, int Kb, int tilesM,
+                                                              double *__restrict__ C, int64_t ldc, double alpha,
+                                                              unsigned flags) {
+    // NW = 8: wave w = A block w, all four B blocks; NW = 16: A block w & 7,
+    // B blocks 2 (w >> 3) .. + 1
+    constexpr int kBW = (kGzTN / 16) * 8 / NW;   // B blocks per wave
+    const bool triA = flags & kGzTriA, beta1 = flags & kGzBeta1, transC = flags & kGzTransC;
+    constexpr int kPieces = (kGzTM / 16 + kGzTN / 16) * ND;   // 1 KiB pieces per stage
+    constexpr int kStage = kPieces * 1024;
+    constexpr int kPerWave = (kPieces + NW - 1) / NW;
+    __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+    const int tilesN = (int)(gridDim.x / tilesM);
+    const int tm = blockIdx.x % tilesM;
+    const int tn = (flags & kGzTriBUpper) ? tilesN - 1 - (int)(blockIdx.x / tilesM) : (int)(blockIdx.x / tilesM);
+    const int64_t i0 = (int64_t)tm * kGzTM, j0 = (int64_t)tn * kGzTN;
+    int kb0 = 0, kb1 = Kb;
+    if (flags & kGzTriBLower) kb0 = (int)(j0 / kGzBK);
+    if (flags & kGzTriBUpper) kb1 = min(Kb, (int)((j0 + kGzTN - 1) / kGzBK) + 1);
+    if (triA) kb1 = min(kb1, (int)((i0 + kGzTM - 1) / kGzBK) + 1);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wa = wave & 7, wb0 = (wave >> 3) * kBW;
+
+    typedef __attribute__((address_space(3))) char lds_char;
+    const uint32_t lds_smem = (uint32_t)(uintptr_t)(lds_char *)(smem);
+    const char *gA = Ad + (i0 / 16) * (int64_t)Kb * ND * 1024 + lane * 16;
+    const char *gB = Bd + (j0 / 16) * (int64_t)Kb * ND * 1024 + lane * 16;
+#define SBO_GZ_DMA16(gsrc, ldst)                                                                         \
+    do {                                                                                                 \
+        uint32_t keep_;                                                                                  \
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t" \
+                     "s_mov_b32 m0, %0"                                                                  \
+                     : "=&s"(keep_)                                                                      \
+                     : "v"(gsrc), "s"(ldst)                                                              \
+                     : "memory");                                                                        \
+    } while (0)
+    auto stage = [&](int kb_, int buf_) {
+#pragma unroll
+        for (int q = 0; q < kPerWave; ++q) {
+            const int p = wave + NW * q;
+            if (kPieces % NW != 0 && p >= kPieces) break;   // (uniform per wave)
+            const int pa = p < (kGzTM / 16) * ND ? p : p - (kGzTM / 16) * ND;
+            const int blk = pa / ND, s = pa % ND;
+            const char *src = (p < (kGzTM / 16) * ND ? gA : gB) + ((int64_t)blk * Kb + kb_) * ND * 1024 + s * 1024;
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_smem + (uint32_t)(buf_ * kStage + p * 1024));
+            SBO_GZ_DMA16(src, dst);
+        }
+    };
+
+    i32x4 acc[kBW][ND];
+#pragma unroll
+    for (int c = 0; c < kBW; ++c)
+#pragma unroll
+        for (int L = 0; L < ND; ++L) acc[c][L] = i32x4{0, 0, 0, 0};
+
+    if (kb0 < kb1) {
+        stage(kb0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    int cur = 0;
+    for (int kb = kb0; kb < kb1; ++kb) {
+        if (kb + 1 < kb1) stage(kb + 1, cur ^ 1);
+        const i32x4 *sA = reinterpret_cast<const i32x4 *>(smem + cur * kStage) + lane;
+        const i32x4 *sB = sA + (kGzTM / 16) * ND * 64;
+        i32x4 ad[ND];
+#pragma unroll
+        for (int s = 0; s < ND; ++s) ad[s] = sA[(wa * ND + s) * 64];
+#pragma unroll
+        for (int c = 0; c < kBW; ++c) {
+            i32x4 bd[ND];
+#pragma unroll
+            for (int u = 0; u < ND; ++u) bd[u] = sB[((wb0 + c) * ND + u) * 64];
+#pragma unroll
+            for (int u = 0; u < ND; ++u)
+#pragma unroll
+                for (int s = 0; s + u < ND; ++s) acc[c][s + u] = mfma_i8(ad[s], bd[u], acc[c][s + u]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        cur ^= 1;
+    }
+#undef SBO_GZ_DMA16
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int c = 0; c < kBW; ++c) {
+        const int64_t j = j0 + 16 * (wb0 + c) + cl;
+        if (j >= n) continue;
+        const int ej = eB[j];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int64_t i = i0 + 16 * wa + 4 * g + v;
+            if (i >= m) continue;
+            double t = (double)acc[c][ND - 1][v];
+#pragma unroll
+            for (int L = ND - 2; L >= 0; --L) t = fma((double)acc[c][L][v], ldexp(1.0, 8 * (ND - 1 - L)), t);
+            const double val = alpha * ldexp(t, eA[i] + ej - 8 * ND - 6);
+            double *dst = transC ? C + j + i * ldc : C + i + j * ldc;
+            *dst = beta1 ? *dst + val : val;
+        }
+    }
+}
+
 template <int ND>
 hipError_t gz_run(hipStream_t s, const double *A, int64_t lda, const double *B, int64_t ldb, int64_t m, int64_t n,
                   int64_t K, double alpha, double *C, int64_t ldc, unsigned flags, char *ws) {
@@ -321,8 +438,16 @@ hipError_t gz_run(hipStream_t s, const double *A, int64_t lda, const double *B, 
         hipLaunchKernelGGL((gz_digits_kernel<ND, false>), db, dim3(256), 0, s, B, ldb, n, K, Kb, tb, mb, pb, eb);
     }
     const int tilesM = (int)(mp / kGzTM), tilesN = (int)(np / kGzTN);
+#ifdef SBO_GZ_4WAVE
     hipLaunchKernelGGL((gz_gemm_kernel<ND>), dim3((unsigned)(tilesM * tilesN)), dim3(256), 0, s, pa, ea, pb, eb, m,
                        n, Kb, tilesM, C, ldc, alpha, flags);
+#elif defined(SBO_GZ_8WAVE)
+    hipLaunchKernelGGL((gz_gemm8_kernel<ND, 8>), dim3((unsigned)(tilesM * tilesN)), dim3(512), 0, s, pa, ea, pb, eb, m,
+                       n, Kb, tilesM, C, ldc, alpha, flags);
+#else
+    hipLaunchKernelGGL((gz_gemm8_kernel<ND, 16>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s, pa, ea, pb, eb,
+                       m, n, Kb, tilesM, C, ldc, alpha, flags);
+#endif
     return hipGetLastError();
 }
 

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 5: the sixteen-wave sliced GEMM in the fit: the inverse tests, the
+# guard tests, fit timing (C2 / C3-size / C4 / box).
+export TMPDIR=/tmp
+O=gpurun_out/r5gz16; mkdir -p $O
+step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -3 $O/$name.log | cut -c1-400; [ $rc -eq 0 ] || exit $rc; }
+step tests 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "sliced_inverse or recursive_inverse or inverse_overlap or small_append or lpsc_stress"
+step guard 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests/test_gpu_invcheck.py
+step timing 300 python -u tools/fit_timing.py --n 2048 8192 16384 --reps 4 --oz 6
+step timing_box 300 python -u tools/fit_timing.py --n 16384 --reps 3 --oz 6 --box
