@@ -473,9 +473,10 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * and `train` training locations (SBO_OPT_PRECISION); the next fit or append
  * probes again. */
 #define SBO_OPT_PROBE_SIZE 27
-/* SBO_OPT_INV_OZ_MIN (2048, 4096 default, 8192): the smallest split of the
- * recursive inverse whose two products run as the int8-sliced GEMM
- * (SBO_OPT_INV_OZ); the levels below keep dgemm products. */
+/* SBO_OPT_INV_OZ_MIN (0 automatic, default; 2048, 4096, 8192): the smallest
+ * split of the recursive inverse whose two products run as the int8-sliced
+ * GEMM (SBO_OPT_INV_OZ); the levels below keep dgemm products.  Automatic:
+ * 2048 for N >= 12288, else 4096. */
 #define SBO_OPT_INV_OZ_MIN 28
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 

@@ -125,10 +125,14 @@ int inverse_base_cases(int64_t n, int64_t base) {
 sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *S,
                              int &slot, sbo::DevBuf *ozws = nullptr);
 // SBO_OPT_INV_OZ: a level of the recursion whose split is at least
-// SBO_OPT_INV_OZ_MIN (default 4096) runs its two products as the sliced GEMM
-// (K <= 16384); the levels below keep dgemms
+// SBO_OPT_INV_OZ_MIN runs its two products as the sliced GEMM (K <= 16384);
+// the levels below keep dgemms.  Automatic (0, default): 2048 in the inverses
+// of N >= 12288 (C4: fit 42.0 -> 41.3 ms, profiles/r5_inv_oz_min_gz16.log),
+// else 4096 (below that the 2048 level's products are too small to pay for
+// their packs, and a sliced inverse brings the guard's check)
 bool oz_level(const sbo_ctx *ctx, int64_t h, int64_t m) {
-    return ctx->inv_oz != 0 && !ctx->inv_oz_off && h >= ctx->inv_oz_min && h <= 16384 && m <= 16384;
+    const int64_t mn = ctx->inv_oz_min > 0 ? ctx->inv_oz_min : (ctx->n >= 12288 ? 2048 : 4096);
+    return ctx->inv_oz != 0 && !ctx->inv_oz_off && h >= mn && h <= 16384 && m <= 16384;
 }
 // does the recursive inverse of n columns slice any of its products?
 bool inverse_sliced(const sbo_ctx *ctx, int64_t n) {
@@ -2349,8 +2353,8 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->inv_oz = (int)value;
             return SBO_OK;
         case SBO_OPT_INV_OZ_MIN:
-            SBO_CHECK(value == 2048 || value == 4096 || value == 8192, SBO_E_INVAL,
-                      "SBO_OPT_INV_OZ_MIN must be 2048, 4096 or 8192");
+            SBO_CHECK(value == 0 || value == 2048 || value == 4096 || value == 8192, SBO_E_INVAL,
+                      "SBO_OPT_INV_OZ_MIN must be 0 (automatic), 2048, 4096 or 8192");
             ctx->inv_oz_min = value;
             return SBO_OK;
         case SBO_OPT_PROBE_SIZE:

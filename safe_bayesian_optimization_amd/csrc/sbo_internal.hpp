@@ -115,7 +115,7 @@ struct sbo_ctx {
     int64_t inv_base = 2048;     // SBO_OPT_INV_BASE: dtrtri base case of the recursive inverse
     int64_t inv_panels = 16;     // SBO_OPT_INV_PANELS: dgemm panels per product of the recursion
     int inv_oz = 6;              // SBO_OPT_INV_OZ: digits of the int8-sliced top-level products (0: dgemm)
-    int64_t inv_oz_min = 4096;   // SBO_OPT_INV_OZ_MIN: the smallest sliced split
+    int64_t inv_oz_min = 0;      // SBO_OPT_INV_OZ_MIN: the smallest sliced split (0: 2048 at N >= 12288, else 4096)
     bool inv_oz_off = false;     // (set while a fit redoes its inverse with dgemm products: the guard fired)
     // the inverse's accuracy guard (SBO_OPT_INV_CHECK, inv_check.hip): its
     // stream, workspace, timing events and the last result
