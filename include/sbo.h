@@ -396,17 +396,20 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * them -- with their inner updates on the matrix cores (1) or on the VALU (0);
  * the factor is bitwise the same. */
 #define SBO_OPT_CHOL_DIAG 16
-/* SBO_OPT_CHOL_GEMM (default 0): the blocked Cholesky's updates by rocBLAS
- * sgemm / ssyrk (0) or by the library's f32 matrix-core kernel -- 2 all of
- * them, 1 the trailing updates of at most 8192 rows, where it measured faster
- * than ssyrk (the fit's time is the same: those run beside the chain).  All
- * compute in f32 with exact f32 products; the factors agree to f32 rounding.
- * 3: the outer panels' rank-512 updates on the bf16 matrix cores with each
- * f32 operand split into three bf16 pieces (six products per f32 product,
- * f32 accumulation): C4 fit 46.1 -> 43.8 ms, but the factor's backward error
- * grows 1.3x (synthetic) to 2.6x (the lpsc box), which on the box moves the
- * posterior 1.9e-4 from the exact one against 4.8e-6 -- not for the precise
- * regime, hence not the default. */
+/* SBO_OPT_CHOL_GEMM (default 4): the blocked Cholesky's updates.  4 / 5: the
+ * outer panels' two big updates (the look-ahead block column and the lower
+ * trailing triangle, k = 512) as the int8-sliced GEMM of csrc/ozgemm.hip with
+ * 4 / 5 base-256 digits per row (exact int32 digit products, one f64
+ * combination per element, f32 out), from one pack of the panel per outer
+ * step; the chain's small updates by rocBLAS.  C4 fit 41.3 -> 37.3 ms (5
+ * digits: 39.0); the factor's backward error 1.64e-7 -> 1.38e-7 (synthetic,
+ * N = 8192) and 2.51e-7 -> 8.7e-8 on the lpsc box against rocBLAS's f32
+ * GEMMs.  0: rocBLAS sgemm / ssyrk; 1 / 2: the library's f32 matrix-core
+ * kernel for the small trailing updates / every update (exact f32 products;
+ * the factors agree to f32 rounding); 3: the outer updates on the bf16
+ * matrix cores with each operand split in three (faster than rocBLAS, but
+ * the factor's backward error 2.6x worse on the box -- not for the precise
+ * regime). */
 #define SBO_OPT_CHOL_GEMM 17
 /* SBO_OPT_INV_BASE (default 2048, in [1024, 8192], rounded down to a multiple
  * of 128) and SBO_OPT_INV_PANELS (default 16, in [1, 64]): the recursive f64

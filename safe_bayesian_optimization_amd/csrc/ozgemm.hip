@@ -28,6 +28,7 @@
 // (12 ND KiB), double buffered, one barrier per k-block.  Lower-triangular
 // operands start / stop the k loop at the tile's diagonal.
 #include <cstdint>
+#include <type_traits>
 
 #include "sbo_internal.hpp"
 
@@ -35,6 +36,8 @@ namespace sbo {
 namespace {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+constexpr unsigned kGzVec4 = 1u << 30;   // (internal) the f32 epilogue may use 16-B accesses
 
 constexpr int kGzTM = 128;   // rows of A per workgroup
 constexpr int kGzTN = 64;    // columns of B per workgroup
@@ -49,19 +52,19 @@ __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
 // column-major matrix, A) or M[k + i ld] (its columns, B); tri 1 keeps only
 // k <= i (A lower triangular), 2 only k >= i (B lower triangular); rows >=
 // rows and k >= K are zero.
-template <bool ROWS_OF_COLMAJOR>
-__device__ __forceinline__ double gz_at(const double *__restrict__ M, int64_t ld, int64_t rows, int64_t K, int tri,
+template <bool ROWS_OF_COLMAJOR, class T>
+__device__ __forceinline__ double gz_at(const T *__restrict__ M, int64_t ld, int64_t rows, int64_t K, int tri,
                                         int64_t i, int64_t k) {
     if (i >= rows || k >= K) return 0.0;
     if ((tri == 1 && k > i) || (tri == 2 && k < i)) return 0.0;
-    return ROWS_OF_COLMAJOR ? M[i + k * ld] : M[k + i * ld];
+    return (double)(ROWS_OF_COLMAJOR ? M[i + k * ld] : M[k + i * ld]);
 }
 
 // Pass 1: each row's max |entry| over a chunk of 1024 k (16 rows x 1024 k per
 // workgroup, grid = row blocks x chunks), combined across chunks by a 64-bit
 // atomic max on the (non-negative) double's bits.  rmax zeroed beforehand.
-template <bool ROWS_OF_COLMAJOR>
-__global__ __launch_bounds__(256) void gz_max_kernel(const double *__restrict__ M, int64_t ld, int64_t rows,
+template <bool ROWS_OF_COLMAJOR, class T>
+__global__ __launch_bounds__(256) void gz_max_kernel(const T *__restrict__ M, int64_t ld, int64_t rows,
                                                      int64_t K, int tri, unsigned long long *__restrict__ rmax) {
     __shared__ double red[4][16];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -105,8 +108,8 @@ __global__ __launch_bounds__(256) void gz_max_kernel(const double *__restrict__ 
 // = row blocks x ceil(Kb / 4)); thread (r, g) cuts row r's k = 16 g .. 16 g +
 // 15 of its k-block into ND bytes each and stores them as one 16-B word per
 // digit.  ex[i]: the row's exponent (-900: an all-zero row).
-template <int ND, bool ROWS_OF_COLMAJOR>
-__global__ __launch_bounds__(256) void gz_digits_kernel(const double *__restrict__ M, int64_t ld, int64_t rows,
+template <int ND, bool ROWS_OF_COLMAJOR, class T>
+__global__ __launch_bounds__(256) void gz_digits_kernel(const T *__restrict__ M, int64_t ld, int64_t rows,
                                                         int64_t K, int Kb, int tri,
                                                         const unsigned long long *__restrict__ rmax,
                                                         char *__restrict__ out, int *__restrict__ ex) {
@@ -296,11 +299,11 @@ __global__ __launch_bounds__(256, 1) void gz_gemm_kernel(const char *__restrict_
 // SIMD), 5.00 / 5.06 with eight, 4.68 / 4.73 with sixteen.  Bitwise the
 // four-wave kernel's results (the int32 level sums are exact in any order;
 // the combination is the same code).
-template <int ND, int NW>
+template <int ND, int NW, class TO>
 __global__ __launch_bounds__(64 * NW, 1) void gz_gemm8_kernel(const char *__restrict__ Ad, const int *__restrict__ eA,
                                                               const char *__restrict__ Bd, const int *__restrict__ eB,
                                                               int64_t m, int64_t n, int Kb, int tilesM,
-                                                              double *__restrict__ C, int64_t ldc, double alpha,
+                                                              TO *__restrict__ C, int64_t ldc, double alpha,
                                                               unsigned flags) {
     // NW = 8: wave w = A block w, all four B blocks; NW = 16: A block w & 7,
     // B blocks 2 (w >> 3) .. + 1
@@ -318,6 +321,9 @@ __global__ __launch_bounds__(64 * NW, 1) void gz_gemm8_kernel(const char *__rest
     if (flags & kGzTriBLower) kb0 = (int)(j0 / kGzBK);
     if (flags & kGzTriBUpper) kb1 = min(Kb, (int)((j0 + kGzTN - 1) / kGzBK) + 1);
     if (triA) kb1 = min(kb1, (int)((i0 + kGzTM - 1) / kGzBK) + 1);
+    // kGzLowerC: only C's lower triangle is wanted -- a tile wholly above the
+    // diagonal does nothing (the diagonal tiles are written whole)
+    if ((flags & kGzLowerC) && i0 + kGzTM - 1 < j0) return;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wa = wave & 7, wb0 = (wave >> 3) * kBW;
@@ -388,23 +394,41 @@ __global__ __launch_bounds__(64 * NW, 1) void gz_gemm8_kernel(const char *__rest
         const int64_t j = j0 + 16 * (wb0 + c) + cl;
         if (j >= n) continue;
         const int ej = eB[j];
+        const int64_t ib = i0 + 16 * wa + 4 * g;   // the lane's four consecutive rows of column j
+        if constexpr (std::is_same_v<TO, float>) {
+            // (kGzVec4: C 16-B aligned with ldc % 4 == 0 -- the four rows in one
+            // 16-B load and store; 16 lanes of a quarter cover a column's 64 B)
+            if ((flags & kGzVec4) && !transC && ib + 3 < m) {
+                f32x4v *dst = reinterpret_cast<f32x4v *>(C + ib + j * ldc);
+                f32x4v o = beta1 ? *dst : f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    double t = (double)acc[c][ND - 1][v];
+#pragma unroll
+                    for (int L = ND - 2; L >= 0; --L) t = fma((double)acc[c][L][v], ldexp(1.0, 8 * (ND - 1 - L)), t);
+                    o[v] = (float)((double)o[v] + alpha * ldexp(t, eA[ib + v] + ej - 8 * ND - 6));
+                }
+                *dst = o;
+                continue;
+            }
+        }
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-            const int64_t i = i0 + 16 * wa + 4 * g + v;
+            const int64_t i = ib + v;
             if (i >= m) continue;
             double t = (double)acc[c][ND - 1][v];
 #pragma unroll
             for (int L = ND - 2; L >= 0; --L) t = fma((double)acc[c][L][v], ldexp(1.0, 8 * (ND - 1 - L)), t);
             const double val = alpha * ldexp(t, eA[i] + ej - 8 * ND - 6);
-            double *dst = transC ? C + j + i * ldc : C + i + j * ldc;
-            *dst = beta1 ? *dst + val : val;
+            TO *dst = transC ? C + j + i * ldc : C + i + j * ldc;
+            *dst = (TO)(beta1 ? (double)*dst + val : val);
         }
     }
 }
 
-template <int ND>
-hipError_t gz_run(hipStream_t s, const double *A, int64_t lda, const double *B, int64_t ldb, int64_t m, int64_t n,
-                  int64_t K, double alpha, double *C, int64_t ldc, unsigned flags, char *ws) {
+template <int ND, class TI, class TO>
+hipError_t gz_run(hipStream_t s, const TI *A, int64_t lda, const TI *B, int64_t ldb, int64_t m, int64_t n,
+                  int64_t K, double alpha, TO *C, int64_t ldc, unsigned flags, char *ws) {
     const int Kb = (int)((K + kGzBK - 1) / kGzBK);
     const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, np = (n + kGzTN - 1) / kGzTN * kGzTN;
     char *pa = ws;
@@ -424,29 +448,34 @@ hipError_t gz_run(hipStream_t s, const double *A, int64_t lda, const double *B, 
     const dim3 ga((unsigned)(mp / 16), chunks), gb((unsigned)(np / 16), chunks);
     const dim3 da((unsigned)(mp / 16), kq), db((unsigned)(np / 16), kq);
     if (flags & kGzTransA) {
-        hipLaunchKernelGGL((gz_max_kernel<false>), ga, dim3(256), 0, s, A, lda, m, K, ta, ma);
-        hipLaunchKernelGGL((gz_digits_kernel<ND, false>), da, dim3(256), 0, s, A, lda, m, K, Kb, ta, ma, pa, ea);
+        hipLaunchKernelGGL((gz_max_kernel<false, TI>), ga, dim3(256), 0, s, A, lda, m, K, ta, ma);
+        hipLaunchKernelGGL((gz_digits_kernel<ND, false, TI>), da, dim3(256), 0, s, A, lda, m, K, Kb, ta, ma, pa, ea);
     } else {
-        hipLaunchKernelGGL((gz_max_kernel<true>), ga, dim3(256), 0, s, A, lda, m, K, ta, ma);
-        hipLaunchKernelGGL((gz_digits_kernel<ND, true>), da, dim3(256), 0, s, A, lda, m, K, Kb, ta, ma, pa, ea);
+        hipLaunchKernelGGL((gz_max_kernel<true, TI>), ga, dim3(256), 0, s, A, lda, m, K, ta, ma);
+        hipLaunchKernelGGL((gz_digits_kernel<ND, true, TI>), da, dim3(256), 0, s, A, lda, m, K, Kb, ta, ma, pa, ea);
     }
     if (flags & kGzTransB) {
-        hipLaunchKernelGGL((gz_max_kernel<true>), gb, dim3(256), 0, s, B, ldb, n, K, tb, mb);
-        hipLaunchKernelGGL((gz_digits_kernel<ND, true>), db, dim3(256), 0, s, B, ldb, n, K, Kb, tb, mb, pb, eb);
+        hipLaunchKernelGGL((gz_max_kernel<true, TI>), gb, dim3(256), 0, s, B, ldb, n, K, tb, mb);
+        hipLaunchKernelGGL((gz_digits_kernel<ND, true, TI>), db, dim3(256), 0, s, B, ldb, n, K, Kb, tb, mb, pb, eb);
     } else {
-        hipLaunchKernelGGL((gz_max_kernel<false>), gb, dim3(256), 0, s, B, ldb, n, K, tb, mb);
-        hipLaunchKernelGGL((gz_digits_kernel<ND, false>), db, dim3(256), 0, s, B, ldb, n, K, Kb, tb, mb, pb, eb);
+        hipLaunchKernelGGL((gz_max_kernel<false, TI>), gb, dim3(256), 0, s, B, ldb, n, K, tb, mb);
+        hipLaunchKernelGGL((gz_digits_kernel<ND, false, TI>), db, dim3(256), 0, s, B, ldb, n, K, Kb, tb, mb, pb, eb);
     }
     const int tilesM = (int)(mp / kGzTM), tilesN = (int)(np / kGzTN);
 #ifdef SBO_GZ_4WAVE
-    hipLaunchKernelGGL((gz_gemm_kernel<ND>), dim3((unsigned)(tilesM * tilesN)), dim3(256), 0, s, pa, ea, pb, eb, m,
-                       n, Kb, tilesM, C, ldc, alpha, flags);
-#elif defined(SBO_GZ_8WAVE)
-    hipLaunchKernelGGL((gz_gemm8_kernel<ND, 8>), dim3((unsigned)(tilesM * tilesN)), dim3(512), 0, s, pa, ea, pb, eb, m,
-                       n, Kb, tilesM, C, ldc, alpha, flags);
+    if constexpr (std::is_same_v<TO, double>) {
+        if (flags & kGzLowerC) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((gz_gemm_kernel<ND>), dim3((unsigned)(tilesM * tilesN)), dim3(256), 0, s, pa, ea, pb, eb,
+                           m, n, Kb, tilesM, C, ldc, alpha, flags);
+        return hipGetLastError();
+    }
+#endif
+#ifdef SBO_GZ_8WAVE
+    hipLaunchKernelGGL((gz_gemm8_kernel<ND, 8, TO>), dim3((unsigned)(tilesM * tilesN)), dim3(512), 0, s, pa, ea, pb,
+                       eb, m, n, Kb, tilesM, C, ldc, alpha, flags);
 #else
-    hipLaunchKernelGGL((gz_gemm8_kernel<ND, 16>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s, pa, ea, pb, eb,
-                       m, n, Kb, tilesM, C, ldc, alpha, flags);
+    hipLaunchKernelGGL((gz_gemm8_kernel<ND, 16, TO>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s, pa, ea,
+                       pb, eb, m, n, Kb, tilesM, C, ldc, alpha, flags);
 #endif
     return hipGetLastError();
 }
@@ -464,9 +493,74 @@ hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, c
                           char *ws) {
     if (m <= 0 || n <= 0) return hipSuccess;
     if (K <= 0 || K > kGzMaxK) return hipErrorInvalidValue;
+    if (flags & kGzLowerC) return hipErrorInvalidValue;
     switch (nd) {
         case 5: return gz_run<5>(s, A, lda, B, ldb, m, n, K, alpha, C, ldc, flags, ws);
         case 6: return gz_run<6>(s, A, lda, B, ldb, m, n, K, alpha, C, ldc, flags, ws);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// The Cholesky's panel packed once (rows padded to 128: digits, then the
+// row exponents, then the row maxima) and its products read from the pack:
+// op(A) = rows a0 .. a0 + m of the pack, op(B)^T = rows b0 .. b0 + n (a0, b0
+// multiples of 128), K = the pack's.
+size_t gz_pack_bytes(int64_t m, int64_t K, int nd) {
+    const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, Kp = (K + kGzBK - 1) / kGzBK * kGzBK;
+    return (size_t)(mp * Kp * nd + 12 * mp) + 256;
+}
+
+hipError_t launch_gz_pack_f32(hipStream_t s, int nd, const float *P, int64_t ld, int64_t m, int64_t K, char *pack) {
+    if (m <= 0 || K <= 0 || K > kGzMaxK || (nd != 4 && nd != 5)) return hipErrorInvalidValue;
+    const int Kb = (int)((K + kGzBK - 1) / kGzBK);
+    const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM;
+    char *pd = pack;
+    int *ex = reinterpret_cast<int *>(pd + mp * (int64_t)Kb * kGzBK * nd);
+    unsigned long long *mx = reinterpret_cast<unsigned long long *>(
+        pd + mp * (int64_t)Kb * kGzBK * nd + ((sizeof(int) * mp + 7) / 8) * 8);
+    hipError_t err = hipMemsetAsync(mx, 0, sizeof(unsigned long long) * (size_t)mp, s);
+    if (err != hipSuccess) return err;
+    const dim3 ga((unsigned)(mp / 16), (unsigned)((K + 1023) / 1024)), da((unsigned)(mp / 16), (unsigned)((Kb + 3) / 4));
+    hipLaunchKernelGGL((gz_max_kernel<true, float>), ga, dim3(256), 0, s, P, ld, m, K, 0, mx);
+    if (nd == 4)
+        hipLaunchKernelGGL((gz_digits_kernel<4, true, float>), da, dim3(256), 0, s, P, ld, m, K, Kb, 0, mx, pd, ex);
+    else
+        hipLaunchKernelGGL((gz_digits_kernel<5, true, float>), da, dim3(256), 0, s, P, ld, m, K, Kb, 0, mx, pd, ex);
+    return hipGetLastError();
+}
+
+hipError_t launch_gz_gemm_packed_f32(hipStream_t s, int nd, const char *pack, int64_t mpack, int64_t K, int64_t a0,
+                                     int64_t m, int64_t b0, int64_t n, double alpha, float *C, int64_t ldc,
+                                     unsigned flags) {
+    if (m <= 0 || n <= 0) return hipSuccess;
+    if (K <= 0 || K > kGzMaxK || (nd != 4 && nd != 5) || a0 % kGzTM != 0 || b0 % kGzTM != 0 || a0 + m > mpack ||
+        b0 + n > mpack || (flags & (kGzTransC | kGzTriA | kGzTriBLower | kGzTriBUpper)))
+        return hipErrorInvalidValue;
+    const int Kb = (int)((K + kGzBK - 1) / kGzBK);
+    const int64_t mp = (mpack + kGzTM - 1) / kGzTM * kGzTM;
+    const int *ex = reinterpret_cast<const int *>(pack + mp * (int64_t)Kb * kGzBK * nd);
+    const int64_t blk = (int64_t)Kb * nd * 1024;   // one 16-row block of the pack
+    const char *pa = pack + (a0 / 16) * blk, *pb = pack + (b0 / 16) * blk;
+    const int tilesM = (int)((m + kGzTM - 1) / kGzTM), tilesN = (int)((n + kGzTN - 1) / kGzTN);
+    if (((uintptr_t)C % 16) == 0 && ldc % 4 == 0) flags |= kGzVec4;
+    if (nd == 4)
+        hipLaunchKernelGGL((gz_gemm8_kernel<4, 16, float>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s, pa,
+                           ex + a0, pb, ex + b0, m, n, Kb, tilesM, C, ldc, alpha, flags);
+    else
+        hipLaunchKernelGGL((gz_gemm8_kernel<5, 16, float>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s, pa,
+                           ex + a0, pb, ex + b0, m, n, Kb, tilesM, C, ldc, alpha, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_gz_gemm_f32(hipStream_t s, int nd, const float *A, int64_t lda, const float *B, int64_t ldb,
+                              int64_t m, int64_t n, int64_t K, double alpha, float *C, int64_t ldc, unsigned flags,
+                              char *ws) {
+    if (m <= 0 || n <= 0) return hipSuccess;
+    if (K <= 0 || K > kGzMaxK) return hipErrorInvalidValue;
+    if ((flags & kGzLowerC) && (flags & kGzTransC)) return hipErrorInvalidValue;
+    switch (nd) {
+        case 4: return gz_run<4>(s, A, lda, B, ldb, m, n, K, alpha, C, ldc, flags, ws);
+        case 5: return gz_run<5>(s, A, lda, B, ldb, m, n, K, alpha, C, ldc, flags, ws);
         default: return hipErrorInvalidValue;
     }
 }

@@ -1247,6 +1247,15 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
     bool trail_pending = false;
     if (ctx->chol_gemm_own == 3 && n > NB2)   // both plane buffers at the first panel's size, up front
         for (sbo::DevBuf &pb : ctx->cholx3) SBO_HIP(pb.reserve(sbo::chol_x3_bytes(n - NB2, NB2)));
+    // SBO_OPT_CHOL_GEMM 4 / 5: the two big updates as the int8-sliced GEMM
+    // with 4 / 5 digits (csrc/ozgemm.hip, f32 in and out) from ONE pack of the
+    // outer panel per step (the look-ahead's both operands and the trailing
+    // update's are row ranges of it), two packs alternating across steps (the
+    // trailing update on aux_stream may still read the previous one), sized up
+    // front for the first outer panel
+    const int oz_nd = (ctx->chol_gemm_own == 4 || ctx->chol_gemm_own == 5) ? ctx->chol_gemm_own : 0;
+    if (oz_nd && n > NB2)
+        for (sbo::DevBuf &pb : ctx->cholx3) SBO_HIP(pb.reserve(sbo::gz_pack_bytes(n - NB2, NB2, oz_nd)));
     sbo_status st = SBO_OK;
     for (int64_t K = 0; K < n && st == SBO_OK; K += NB2) {
         const int64_t W = std::min(NB2, n - K);
@@ -1314,7 +1323,14 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         // buffer's twin until the next look-ahead has waited for it)
         const bool x3 = ctx->chol_gemm_own == 3 && W % 32 == 0;
         char *planes = nullptr;
-        if (x3) {
+        const bool ozp = oz_nd && W % 64 == 0 && W2 % 128 == 0;   // (the last panels: rocBLAS)
+        if (ozp) {
+            planes = ctx->cholx3[(K / NB2) & 1].as<char>();
+            if (sbo::launch_gz_pack_f32(ctx->stream, oz_nd, P, ld, m3, W, planes) != hipSuccess) {
+                st = SBO_E_DEVICE;
+                break;
+            }
+        } else if (x3) {
             sbo::DevBuf &pb = ctx->cholx3[(K / NB2) & 1];
             if (pb.reserve(sbo::chol_x3_bytes(m3, W)) != hipSuccess ||
                 sbo::launch_chol_split(ctx->stream, P, ld, m3, W, pb.as<char>()) != hipSuccess) {
@@ -1326,7 +1342,9 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         if (hipEventRecord(ctx->ev_panel, ctx->stream) != hipSuccess ||
             (trail_pending && hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0) != hipSuccess)) { st = SBO_E_DEVICE; break; }
         const bool la_ok =
-            x3 ? sbo::launch_chol_update_x3(ctx->stream, planes, m3, W, 0, m3, 0, W2, false, C1, ld) == hipSuccess
+            ozp ? sbo::launch_gz_gemm_packed_f32(ctx->stream, oz_nd, planes, m3, W, 0, m3, 0, W2, -1.0, C1, ld,
+                                                 sbo::kGzBeta1) == hipSuccess
+            : x3 ? sbo::launch_chol_update_x3(ctx->stream, planes, m3, W, 0, m3, 0, W2, false, C1, ld) == hipSuccess
             : ctx->chol_gemm_own == 2
                 ? sbo::launch_chol_update(ctx->stream, P, P, ld, m3, W2, W, false, C1) == hipSuccess
                 : rocblas_sgemm(ctx->blas, rocblas_operation_none, rocblas_operation_transpose, (rocblas_int)m3,
@@ -1340,7 +1358,11 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
             // (1: the own kernel only where it measured faster than rocBLAS,
             // the lower update of m4 <= 8192; 2: every update)
             bool ok;
-            if (x3)
+            if (ozp)
+                ok = sbo::launch_gz_gemm_packed_f32(ctx->aux_stream, oz_nd, planes, m3, W, W2, m4, W2, m4, -1.0,
+                                                    C1 + W2 + W2 * ld, ld,
+                                                    sbo::kGzBeta1 | sbo::kGzLowerC) == hipSuccess;
+            else if (x3)
                 ok = sbo::launch_chol_update_x3(ctx->aux_stream, planes, m3, W, W2, m4, W2, m4, true,
                                                 C1 + W2 + W2 * ld, ld) == hipSuccess;
             else if (ctx->chol_gemm_own == 2 || (ctx->chol_gemm_own == 1 && m4 <= 8192))
@@ -2310,7 +2332,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->inv_panels = value;
             return SBO_OK;
         case SBO_OPT_CHOL_GEMM:
-            SBO_CHECK(value >= 0 && value <= 3, SBO_E_INVAL, "SBO_OPT_CHOL_GEMM must be 0, 1, 2 or 3");
+            SBO_CHECK(value >= 0 && value <= 5, SBO_E_INVAL, "SBO_OPT_CHOL_GEMM must be in [0, 5]");
             ctx->chol_gemm_own = (int)value;
             return SBO_OK;
         case SBO_OPT_CHOL_DIAG:

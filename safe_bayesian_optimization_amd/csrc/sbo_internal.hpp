@@ -103,7 +103,7 @@ struct sbo_ctx {
     int aux_reserved = 0;        // the mask the current aux stream was created with
     hipEvent_t ev_panel = nullptr, ev_trail = nullptr;
     hipEvent_t ev_pack = nullptr;  // the fit's operand packs on aux_stream (refresh_operand)
-    int chol_gemm_own = 0;       // SBO_OPT_CHOL_GEMM: 2 every factorization update by chol_update_kernel, 1 the small trailing ones, 0 rocBLAS
+    int chol_gemm_own = 4;       // SBO_OPT_CHOL_GEMM: 4 (default) / 5 the outer panels' updates int8-sliced, 3 split bf16, 2 every update by chol_update_kernel, 1 the small trailing ones, 0 rocBLAS
     int chol_diag = 1;           // SBO_OPT_CHOL_DIAG: 1 the MFMA chain kernels (diagonal block, panel), 0 the VALU ones (bitwise equal)
     int chol_outer = 512;        // SBO_OPT_CHOL_OUTER: outer panel width of the two-level Cholesky (128: one level)
     // the recursive inverse's first half beside the Cholesky's last steps
@@ -456,10 +456,23 @@ constexpr unsigned kGzTriBUpper = 8;   // op(B) upper triangular: b_kj = 0 for k
 constexpr unsigned kGzTransB = 16;
 constexpr unsigned kGzTransC = 32;
 constexpr unsigned kGzBeta1 = 64;      // C += instead of C =
+constexpr unsigned kGzLowerC = 128;    // (f32 form) only tiles that meet C's lower triangle
 size_t gz_workspace_bytes(int64_t m, int64_t n, int64_t K, int nd);
 hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, const double *B, int64_t ldb,
                           int64_t m, int64_t n, int64_t K, double alpha, double *C, int64_t ldc, unsigned flags,
                           char *ws);
+// The same product on f32 operands and an f32 C (4 or 5 digits: the Cholesky's
+// updates, SBO_OPT_CHOL_GEMM 4 / 5); kGzLowerC skips the tiles above C's diagonal.
+hipError_t launch_gz_gemm_f32(hipStream_t s, int nd, const float *A, int64_t lda, const float *B, int64_t ldb,
+                              int64_t m, int64_t n, int64_t K, double alpha, float *C, int64_t ldc, unsigned flags,
+                              char *ws);
+// ... and with one pack of the panel's m rows shared by every product of an
+// outer step: op(A) its rows a0 .., op(B)^T its rows b0 .. (multiples of 128)
+size_t gz_pack_bytes(int64_t m, int64_t K, int nd);
+hipError_t launch_gz_pack_f32(hipStream_t s, int nd, const float *P, int64_t ld, int64_t m, int64_t K, char *pack);
+hipError_t launch_gz_gemm_packed_f32(hipStream_t s, int nd, const char *pack, int64_t mpack, int64_t K, int64_t a0,
+                                     int64_t m, int64_t b0, int64_t n, double alpha, float *C, int64_t ldc,
+                                     unsigned flags);
 // The fit's accuracy guard of the f64 inverse (inv_check.hip): on kChkQ
 // queries (coordinates at *qxy: x[kChkQ] then y[kChkQ], filled by the caller
 // before the launch) V0 = Linv Kq and one refinement against the f32 factor

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 5: the Cholesky's updates as the int8-sliced GEMM (SBO_OPT_CHOL_GEMM
+# 4 / 5): tests, factor quality against the exact posterior, fit timing.
+export TMPDIR=/tmp
+O=gpurun_out/r5cholgz; mkdir -p $O
+step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -6 $O/$name.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc; }
+step tests 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "cholesky"
+CHOL_GEMMS="0 4 5" step exact 600 python -u tools/r5_cholx3_exact.py 8192 1024
+step timing 300 python -u tools/fit_timing.py --n 8192 16384 --reps 3 --oz 6 --gemm 0 4 5

@@ -36,7 +36,7 @@ def main():
         sel = np.sort(rng.choice(wl.qx.size, ns, replace=False))
         qx, qy = f32(wl.qx[sel]), f32(wl.qy[sel])
         exact = None
-        for g in (0, 3):
+        for g in [int(v) for v in os.environ.get("CHOL_GEMMS", "0 3").split()]:
             gm = TerrainMapper(0, h)
             gm.set_option(N.SBO_OPT_CHOL_GEMM, g)
             gm.fit(wl.x, wl.y, wl.obs)
