@@ -104,6 +104,22 @@ __global__ __launch_bounds__(256) void gz_max_kernel(const T *__restrict__ M, in
     }
 }
 
+// Pass 1 for the Cholesky's f32 panel (the rows of a column-major m x K
+// matrix): one thread per row and 128 k per workgroup, so a wave's loads are
+// 64 consecutive rows (256 B) of one column -- the 16-row form above reads
+// 64-B pieces and was latency-bound there (~35 us per C4 panel).
+__global__ __launch_bounds__(256) void gz_rowmax_f32_kernel(const float *__restrict__ M, int64_t ld, int64_t rows,
+                                                            int64_t K, unsigned long long *__restrict__ rmax) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= rows) return;
+    const int64_t k0 = (int64_t)blockIdx.y * 128, k1 = min(K, k0 + 128);
+    const float *p = M + i;
+    float amax = 0.0f;
+#pragma unroll 16
+    for (int64_t k = k0; k < k1; ++k) amax = fmaxf(amax, fabsf(p[k * ld]));
+    if (amax > 0.0f) atomicMax(rmax + i, (unsigned long long)__double_as_longlong((double)amax));
+}
+
 // Pass 2: the digits, 16 rows x 4 k-blocks per workgroup (one per wave; grid
 // = row blocks x ceil(Kb / 4)); thread (r, g) cuts row r's k = 16 g .. 16 g +
 // 15 of its k-block into ND bytes each and stores them as one 16-B word per
@@ -299,27 +315,27 @@ __global__ __launch_bounds__(256, 1) void gz_gemm_kernel(const char *__restrict_
 // SIMD), 5.00 / 5.06 with eight, 4.68 / 4.73 with sixteen.  Bitwise the
 // four-wave kernel's results (the int32 level sums are exact in any order;
 // the combination is the same code).
-template <int ND, int NW, class TO>
+template <int ND, int NW, class TO, int TN = kGzTN>
 __global__ __launch_bounds__(64 * NW, 1) void gz_gemm8_kernel(const char *__restrict__ Ad, const int *__restrict__ eA,
                                                               const char *__restrict__ Bd, const int *__restrict__ eB,
                                                               int64_t m, int64_t n, int Kb, int tilesM,
                                                               TO *__restrict__ C, int64_t ldc, double alpha,
                                                               unsigned flags) {
-    // NW = 8: wave w = A block w, all four B blocks; NW = 16: A block w & 7,
-    // B blocks 2 (w >> 3) .. + 1
-    constexpr int kBW = (kGzTN / 16) * 8 / NW;   // B blocks per wave
+    // NW = 8: wave w = A block w, all TN / 16 B blocks; NW = 16: A block
+    // w & 7, half of them (TN = 64: two; 128: four)
+    constexpr int kBW = (TN / 16) * 8 / NW;      // B blocks per wave
     const bool triA = flags & kGzTriA, beta1 = flags & kGzBeta1, transC = flags & kGzTransC;
-    constexpr int kPieces = (kGzTM / 16 + kGzTN / 16) * ND;   // 1 KiB pieces per stage
+    constexpr int kPieces = (kGzTM / 16 + TN / 16) * ND;      // 1 KiB pieces per stage
     constexpr int kStage = kPieces * 1024;
     constexpr int kPerWave = (kPieces + NW - 1) / NW;
     __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
     const int tilesN = (int)(gridDim.x / tilesM);
     const int tm = blockIdx.x % tilesM;
     const int tn = (flags & kGzTriBUpper) ? tilesN - 1 - (int)(blockIdx.x / tilesM) : (int)(blockIdx.x / tilesM);
-    const int64_t i0 = (int64_t)tm * kGzTM, j0 = (int64_t)tn * kGzTN;
+    const int64_t i0 = (int64_t)tm * kGzTM, j0 = (int64_t)tn * TN;
     int kb0 = 0, kb1 = Kb;
     if (flags & kGzTriBLower) kb0 = (int)(j0 / kGzBK);
-    if (flags & kGzTriBUpper) kb1 = min(Kb, (int)((j0 + kGzTN - 1) / kGzBK) + 1);
+    if (flags & kGzTriBUpper) kb1 = min(Kb, (int)((j0 + TN - 1) / kGzBK) + 1);
     if (triA) kb1 = min(kb1, (int)((i0 + kGzTM - 1) / kGzBK) + 1);
     // kGzLowerC: only C's lower triangle is wanted -- a tile wholly above the
     // diagonal does nothing (the diagonal tiles are written whole)
@@ -521,7 +537,9 @@ hipError_t launch_gz_pack_f32(hipStream_t s, int nd, const float *P, int64_t ld,
     hipError_t err = hipMemsetAsync(mx, 0, sizeof(unsigned long long) * (size_t)mp, s);
     if (err != hipSuccess) return err;
     const dim3 ga((unsigned)(mp / 16), (unsigned)((K + 1023) / 1024)), da((unsigned)(mp / 16), (unsigned)((Kb + 3) / 4));
-    hipLaunchKernelGGL((gz_max_kernel<true, float>), ga, dim3(256), 0, s, P, ld, m, K, 0, mx);
+    (void)ga;
+    hipLaunchKernelGGL(gz_rowmax_f32_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)((K + 127) / 128)), dim3(256),
+                       0, s, P, ld, m, K, mx);
     if (nd == 4)
         hipLaunchKernelGGL((gz_digits_kernel<4, true, float>), da, dim3(256), 0, s, P, ld, m, K, Kb, 0, mx, pd, ex);
     else
@@ -541,14 +559,19 @@ hipError_t launch_gz_gemm_packed_f32(hipStream_t s, int nd, const char *pack, in
     const int *ex = reinterpret_cast<const int *>(pack + mp * (int64_t)Kb * kGzBK * nd);
     const int64_t blk = (int64_t)Kb * nd * 1024;   // one 16-row block of the pack
     const char *pa = pack + (a0 / 16) * blk, *pb = pack + (b0 / 16) * blk;
-    const int tilesM = (int)((m + kGzTM - 1) / kGzTM), tilesN = (int)((n + kGzTN - 1) / kGzTN);
+    // 128 x 128 tiles (four B blocks per wave): twice the products per
+    // staged k-block and per prologue / epilogue of the short k = 512 loop
+    // (two 64 / 80 KiB stages fit the LDS at 4 / 5 digits)
+    constexpr int TN = 128;
+    const int tilesM = (int)((m + kGzTM - 1) / kGzTM), tilesN = (int)((n + TN - 1) / TN);
+    if (b0 + (n + TN - 1) / TN * TN > (mpack + kGzTM - 1) / kGzTM * kGzTM) return hipErrorInvalidValue;
     if (((uintptr_t)C % 16) == 0 && ldc % 4 == 0) flags |= kGzVec4;
     if (nd == 4)
-        hipLaunchKernelGGL((gz_gemm8_kernel<4, 16, float>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s, pa,
-                           ex + a0, pb, ex + b0, m, n, Kb, tilesM, C, ldc, alpha, flags);
+        hipLaunchKernelGGL((gz_gemm8_kernel<4, 16, float, TN>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s,
+                           pa, ex + a0, pb, ex + b0, m, n, Kb, tilesM, C, ldc, alpha, flags);
     else
-        hipLaunchKernelGGL((gz_gemm8_kernel<5, 16, float>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s, pa,
-                           ex + a0, pb, ex + b0, m, n, Kb, tilesM, C, ldc, alpha, flags);
+        hipLaunchKernelGGL((gz_gemm8_kernel<5, 16, float, TN>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s,
+                           pa, ex + a0, pb, ex + b0, m, n, Kb, tilesM, C, ldc, alpha, flags);
     return hipGetLastError();
 }
 
