@@ -108,16 +108,21 @@ __global__ __launch_bounds__(256) void gz_max_kernel(const T *__restrict__ M, in
 // matrix): one thread per row and 128 k per workgroup, so a wave's loads are
 // 64 consecutive rows (256 B) of one column -- the 16-row form above reads
 // 64-B pieces and was latency-bound there (~35 us per C4 panel).
-__global__ __launch_bounds__(256) void gz_rowmax_f32_kernel(const float *__restrict__ M, int64_t ld, int64_t rows,
-                                                            int64_t K, unsigned long long *__restrict__ rmax) {
+// (the f64 operands of the inverse's products too, tri as gz_at's: 1 keeps
+// k <= i, 2 keeps k >= i)
+template <class T>
+__global__ __launch_bounds__(256) void gz_rowmax_kernel(const T *__restrict__ M, int64_t ld, int64_t rows, int64_t K,
+                                                        int tri, unsigned long long *__restrict__ rmax) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= rows) return;
-    const int64_t k0 = (int64_t)blockIdx.y * 128, k1 = min(K, k0 + 128);
-    const float *p = M + i;
-    float amax = 0.0f;
+    int64_t k0 = (int64_t)blockIdx.y * 128, k1 = min(K, k0 + 128);
+    if (tri == 1) k1 = min(k1, i + 1);
+    if (tri == 2) k0 = max(k0, i);
+    const T *p = M + i;
+    double amax = 0.0;
 #pragma unroll 16
-    for (int64_t k = k0; k < k1; ++k) amax = fmaxf(amax, fabsf(p[k * ld]));
-    if (amax > 0.0f) atomicMax(rmax + i, (unsigned long long)__double_as_longlong((double)amax));
+    for (int64_t k = k0; k < k1; ++k) amax = fmax(amax, fabs((double)p[k * ld]));
+    if (amax > 0.0) atomicMax(rmax + i, (unsigned long long)__double_as_longlong(amax));
 }
 
 // Pass 2: the digits, 16 rows x 4 k-blocks per workgroup (one per wave; grid
@@ -463,15 +468,17 @@ hipError_t gz_run(hipStream_t s, const TI *A, int64_t lda, const TI *B, int64_t 
     const int tb = (flags & kGzTriBLower) ? 2 : (flags & kGzTriBUpper) ? 1 : 0;
     const dim3 ga((unsigned)(mp / 16), chunks), gb((unsigned)(np / 16), chunks);
     const dim3 da((unsigned)(mp / 16), kq), db((unsigned)(np / 16), kq);
+    const dim3 rga((unsigned)((m + 255) / 256), (unsigned)((K + 127) / 128)),
+        rgb((unsigned)((n + 255) / 256), (unsigned)((K + 127) / 128));
     if (flags & kGzTransA) {
         hipLaunchKernelGGL((gz_max_kernel<false, TI>), ga, dim3(256), 0, s, A, lda, m, K, ta, ma);
         hipLaunchKernelGGL((gz_digits_kernel<ND, false, TI>), da, dim3(256), 0, s, A, lda, m, K, Kb, ta, ma, pa, ea);
     } else {
-        hipLaunchKernelGGL((gz_max_kernel<true, TI>), ga, dim3(256), 0, s, A, lda, m, K, ta, ma);
+        hipLaunchKernelGGL(gz_rowmax_kernel<TI>, rga, dim3(256), 0, s, A, lda, m, K, ta, ma);
         hipLaunchKernelGGL((gz_digits_kernel<ND, true, TI>), da, dim3(256), 0, s, A, lda, m, K, Kb, ta, ma, pa, ea);
     }
     if (flags & kGzTransB) {
-        hipLaunchKernelGGL((gz_max_kernel<true, TI>), gb, dim3(256), 0, s, B, ldb, n, K, tb, mb);
+        hipLaunchKernelGGL(gz_rowmax_kernel<TI>, rgb, dim3(256), 0, s, B, ldb, n, K, tb, mb);
         hipLaunchKernelGGL((gz_digits_kernel<ND, true, TI>), db, dim3(256), 0, s, B, ldb, n, K, Kb, tb, mb, pb, eb);
     } else {
         hipLaunchKernelGGL((gz_max_kernel<false, TI>), gb, dim3(256), 0, s, B, ldb, n, K, tb, mb);
@@ -538,8 +545,8 @@ hipError_t launch_gz_pack_f32(hipStream_t s, int nd, const float *P, int64_t ld,
     if (err != hipSuccess) return err;
     const dim3 ga((unsigned)(mp / 16), (unsigned)((K + 1023) / 1024)), da((unsigned)(mp / 16), (unsigned)((Kb + 3) / 4));
     (void)ga;
-    hipLaunchKernelGGL(gz_rowmax_f32_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)((K + 127) / 128)), dim3(256),
-                       0, s, P, ld, m, K, mx);
+    hipLaunchKernelGGL(gz_rowmax_kernel<float>, dim3((unsigned)((m + 255) / 256), (unsigned)((K + 127) / 128)),
+                       dim3(256), 0, s, P, ld, m, K, 0, mx);
     if (nd == 4)
         hipLaunchKernelGGL((gz_digits_kernel<4, true, float>), da, dim3(256), 0, s, P, ld, m, K, Kb, 0, mx, pd, ex);
     else
