@@ -138,7 +138,7 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
     wl = synthetic(n, 24, 20, seed=n + 3)
     res = {}
     for ch in (0, 2, (1, 128), (1, 256), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 3), (1, 256, 3), (1, 512, 4),
-               (1, 512, 5), 1):
+               (1, 512, 5), (1, 128, 4), (1, 256, 4), (1, 1024, 4), 1):
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
         outer = ch[1] if isinstance(ch, tuple) else 512
         gm.set_option(N.SBO_OPT_CHOL_OUTER, outer)
@@ -156,7 +156,7 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
     gm.set_option(N.SBO_OPT_CHOL_OUTER, 512)
     gm.set_option(N.SBO_OPT_CHOL_GEMM, 0)
     for ch in (1, 2, (1, 128), (1, 256), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 3), (1, 256, 3), (1, 512, 4),
-               (1, 512, 5)):   # own panel solve (default), rocBLAS strsm panels, one / two levels, against spotrf
+               (1, 512, 5), (1, 128, 4), (1, 256, 4), (1, 1024, 4)):   # own panel solve (default), rocBLAS strsm panels, one / two levels, against spotrf
         assert np.abs(res[0][0] - res[ch][0]).max() <= 1e-4 * np.abs(res[0][0]).max()
         assert nrel(res[ch][1][0], res[0][1][0].astype(np.float64)) < REL_TOL
         assert nrel(res[ch][1][1].astype(np.float64) ** 2, res[0][1][1].astype(np.float64) ** 2) < REL_TOL
