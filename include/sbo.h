@@ -406,10 +406,10 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * N = 8192) and 2.51e-7 -> 8.7e-8 on the lpsc box against rocBLAS's f32
  * GEMMs.  0: rocBLAS sgemm / ssyrk; 1 / 2: the library's f32 matrix-core
  * kernel for the small trailing updates / every update (exact f32 products;
- * the factors agree to f32 rounding); 3: the outer updates on the bf16
- * matrix cores with each operand split in three (faster than rocBLAS, but
- * the factor's backward error 2.6x worse on the box -- not for the precise
- * regime). */
+ * the factors agree to f32 rounding).  (3, the outer updates on the bf16
+ * matrix cores with each operand split in three -- faster than rocBLAS, but
+ * the factor's backward error 2.6x worse on the box -- exists only in the
+ * diagnostic build; SBO_E_INVAL here.) */
 #define SBO_OPT_CHOL_GEMM 17
 /* SBO_OPT_INV_BASE (default 2048, in [1024, 8192], rounded down to a multiple
  * of 128) and SBO_OPT_INV_PANELS (default 16, in [1, 64]): the recursive f64

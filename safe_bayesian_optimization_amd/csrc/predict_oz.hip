@@ -479,7 +479,9 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz_kernel(
 #undef SBO_OZ_DMA16
 }
 
-// SBO_OPT_PRECISE_KERNEL 5 (round 5): kernel 3 with a deeper stream.  Kernel
+#ifdef SBO_DIAG
+// SBO_OPT_PRECISE_KERNEL 5 (round 5; diagnostic build only -- measured no
+// faster than kernel 3): kernel 3 with a deeper stream.  Kernel
 // 3 stages one half-tile ahead (two slots of A + the K* table piece, 150 KiB),
 // so each 40 KiB stage has one stage of MFMA time (~1.7 us) to arrive -- at
 // 114 KiB per tile a CU needs ~38 GB/s for that, beyond what the L2-missing
@@ -718,6 +720,8 @@ __global__ __launch_bounds__(kOzThreads, 1) void predict_oz3_kernel(
 #undef SBO_OZ3_DMA16
 #undef SBO_OZ3_DMA16M
 }
+
+#endif  // SBO_DIAG
 
 // The K* table of nq query blocks (SBO_OPT_PRECISE_KERNEL 3): one workgroup per
 // (k-tile t, query block), each wave its 16 queries' digit operands exactly as
@@ -1385,12 +1389,14 @@ hipError_t launch_predict_oz(hipStream_t s, const char *aoz, const int *eoz, con
                            seg, P, n_items, nI, m, ldp, m0, part, mean, kzt);
         return hipGetLastError();
     }
+#ifdef SBO_DIAG
     if (variant == 5) {   // K*'s digits from the table, A staged a tile ahead
         if (!kzt) return hipErrorInvalidValue;
         hipLaunchKernelGGL(predict_oz3_kernel, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, desc, tl, seg, P,
                            n_items, nI, m, ldp, m0, part, mean, kzt);
         return hipGetLastError();
     }
+#endif
     if (variant == 3) {   // K*'s digits from the table
         if (!kzt) return hipErrorInvalidValue;
         hipLaunchKernelGGL(predict_oz_kernel<2>, dim3((unsigned)P), dim3(kOzThreads), 0, s, aoz, eoz, koz, desc,

@@ -2332,7 +2332,14 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->inv_panels = value;
             return SBO_OK;
         case SBO_OPT_CHOL_GEMM:
-            SBO_CHECK(value >= 0 && value <= 5, SBO_E_INVAL, "SBO_OPT_CHOL_GEMM must be in [0, 5]");
+#ifdef SBO_DIAG
+            SBO_CHECK(value >= 0 && value <= 5, SBO_E_INVAL, "SBO_OPT_CHOL_GEMM must be in [0, 5] (diagnostics)");
+#else
+            // (3, the split-bf16 updates, only in the diagnostic build: a worse
+            // factor on ill-conditioned K)
+            SBO_CHECK(value >= 0 && value <= 5 && value != 3, SBO_E_INVAL,
+                      "SBO_OPT_CHOL_GEMM must be 0, 1, 2, 4 or 5");
+#endif
             ctx->chol_gemm_own = (int)value;
             return SBO_OK;
         case SBO_OPT_CHOL_DIAG:
@@ -2359,9 +2366,9 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             SBO_CHECK(value == 0 || value == 1 || (value >= 3 && value <= 5) || (value >= 9 && value <= 12),
                       SBO_E_INVAL, "SBO_OPT_PRECISE_KERNEL: 0, 1, 3, 4, 5 or 9-12 (diagnostics)");
 #else
-            SBO_CHECK(value == 0 || value == 1 || (value >= 3 && value <= 5), SBO_E_INVAL,
-                      "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA), 1 (int8), 3 (int8, K* table), 4 (int8, "
-                      "k-tile pairs) or 5 (int8, K* table, A a tile ahead)");
+            SBO_CHECK(value == 0 || value == 1 || value == 3 || value == 4, SBO_E_INVAL,
+                      "SBO_OPT_PRECISE_KERNEL must be 0 (f64 MFMA), 1 (int8), 3 (int8, K* table) or 4 (int8, "
+                      "k-tile pairs)");
 #endif
             {
                 // the operand layout each kernel reads: f64 tiles, int8 tiles, int8 pairs

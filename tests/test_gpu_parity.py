@@ -132,13 +132,12 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
     factorization in one level (SBO_OPT_CHOL_OUTER = 128) and in two (256,
     1024; 512 default), with its own matrix-core updates for every update
     (SBO_OPT_CHOL_GEMM 2), for the small trailing ones (1) or none (0), and
-    with the outer panels' updates on the bf16 matrix cores with split
-    operands (3, round 5) or as the int8-sliced GEMM with 4 / 5 digits (4 / 5,
-    round 5), too."""
+    with the outer panels' updates as the int8-sliced GEMM with 4 / 5 digits
+    (4, the default since round 5 / 5) at four outer panel widths, too."""
     wl = synthetic(n, 24, 20, seed=n + 3)
     res = {}
-    for ch in (0, 2, (1, 128), (1, 256), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 3), (1, 256, 3), (1, 512, 4),
-               (1, 512, 5), (1, 128, 4), (1, 256, 4), (1, 1024, 4), 1):
+    for ch in (0, 2, (1, 128), (1, 256), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 4), (1, 512, 5), (1, 128, 4),
+               (1, 256, 4), (1, 1024, 4), 1):
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
         outer = ch[1] if isinstance(ch, tuple) else 512
         gm.set_option(N.SBO_OPT_CHOL_OUTER, outer)
@@ -155,8 +154,8 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
     gm.set_option(N.SBO_OPT_CHOLESKY, 1)
     gm.set_option(N.SBO_OPT_CHOL_OUTER, 512)
     gm.set_option(N.SBO_OPT_CHOL_GEMM, 0)
-    for ch in (1, 2, (1, 128), (1, 256), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 3), (1, 256, 3), (1, 512, 4),
-               (1, 512, 5), (1, 128, 4), (1, 256, 4), (1, 1024, 4)):   # own panel solve (default), rocBLAS strsm panels, one / two levels, against spotrf
+    for ch in (1, 2, (1, 128), (1, 256), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 4), (1, 512, 5), (1, 128, 4),
+               (1, 256, 4), (1, 1024, 4)):   # own panel solve (default), rocBLAS strsm panels, one / two levels, against spotrf
         assert np.abs(res[0][0] - res[ch][0]).max() <= 1e-4 * np.abs(res[0][0]).max()
         assert nrel(res[ch][1][0], res[0][1][0].astype(np.float64)) < REL_TOL
         assert nrel(res[ch][1][1].astype(np.float64) ** 2, res[0][1][1].astype(np.float64) ** 2) < REL_TOL
@@ -1394,10 +1393,10 @@ def test_precision_levels(mapper):
 # the precise kernels' tolerances against the fp64 oracle: the f64 sweep to
 # f64 rounding (f32 outputs: 1e-6), the int8 sliced sweep to its slicing
 # (emulated 1.2e-6 on the lpsc box at N = 8192, tools/r4_emulate_ozaki.py)
-PRECISE_TOL = {0: (1e-6, 1e-6), 1: (1e-6, 4e-6), 3: (1e-6, 4e-6), 4: (1e-6, 4e-6), 5: (1e-6, 4e-6)}
+PRECISE_TOL = {0: (1e-6, 1e-6), 1: (1e-6, 4e-6), 3: (1e-6, 4e-6), 4: (1e-6, 4e-6)}
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 3, 4, 5])
+@pytest.mark.parametrize("kernel", [0, 1, 3, 4])
 @pytest.mark.parametrize("n,gw,gh,box", [(2048, 64, 48, False), (3000, 90, 70, True), (700, 40, 30, True)])
 def test_precise_sweep_matches_oracle(mapper, n, gw, gh, box, kernel):
     """SBO_OPT_PRECISION = 1: the f64 sweep (SBO_OPT_PRECISE_KERNEL 0: A =
@@ -1453,7 +1452,7 @@ def test_int8_mfma_k_layout(mapper):
     for n in (64, 65, 130):
         wl = synthetic_box(n, 7, 5, seed=n)
         outs = {}
-        for kernel in (0, 1, 3, 5):
+        for kernel in (0, 1, 3):
             gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
             gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
             gm.set_option(N.SBO_OPT_PRECISION, 1)
@@ -1462,7 +1461,7 @@ def test_int8_mfma_k_layout(mapper):
         gm.set_option(N.SBO_OPT_PRECISION, -1)
         gm.set_option(N.SBO_OPT_PRECISE_KERNEL, 3)
         omu, ovar = oracle_given_factor64(gm, wl)
-        for kernel in (0, 1, 3, 5):
+        for kernel in (0, 1, 3):
             mu, sd = outs[kernel]
             emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
             print(f"N={n} kernel {kernel}: mu {emu:.2e} var {evar:.2e}")
@@ -1513,8 +1512,7 @@ def test_kstar_table_chunks(mapper):
     is bitwise kernel 1's (the mean sums its per-tile terms in another order:
     within 1e-12); bitwise the same for any chunking (1 MiB: one query block
     per chunk on this N) and sweep partition, on the lpsc box with a ragged
-    last query block.  Kernel 5 (A staged a tile ahead, round 5) is bitwise
-    kernel 3 under every chunking and partition."""
+    last query block."""
     from safe_bayesian_optimization_amd.terrain import synthetic_box
     wl = synthetic_box(3000, 61, 29, seed=5)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
@@ -1522,8 +1520,7 @@ def test_kstar_table_chunks(mapper):
     try:
         gm.fit(wl.x, wl.y, wl.obs)
         res = {}
-        for kernel, mb, groups in ((1, 2048, 0), (3, 2048, 0), (3, 0, 0), (3, 1, 0), (3, 1, 7), (3, 3, 1000),
-                                   (5, 2048, 0), (5, 1, 0), (5, 1, 7), (5, 3, 1000), (5, 2, 31)):
+        for kernel, mb, groups in ((1, 2048, 0), (3, 2048, 0), (3, 0, 0), (3, 1, 0), (3, 1, 7), (3, 3, 1000)):
             gm.set_option(N.SBO_OPT_PRECISE_KERNEL, kernel)
             gm.set_option(N.SBO_OPT_TABLE_MB, mb)
             gm.set_option(N.SBO_OPT_SWEEP_GROUPS, groups)
@@ -1531,7 +1528,7 @@ def test_kstar_table_chunks(mapper):
         base = res[(3, 2048, 0)]
         for k, (mu, sd) in res.items():
             assert np.array_equal(sd, res[(1, 2048, 0)][1]), k
-            if k[0] in (3, 5):
+            if k[0] == 3:
                 assert np.array_equal(mu, base[0]) and np.array_equal(sd, base[1]), k
         assert nrel(base[0], res[(1, 2048, 0)][0].astype(np.float64)) < 1e-6
         omu, ovar = oracle_given_factor64(gm, wl)
@@ -1642,3 +1639,55 @@ def test_product_matches_diagnostic_build():
                         "--configs", "C2", "box"], capture_output=True, text=True, timeout=600)
     print(r.stdout[-2000:])
     assert r.returncode == 0 and "ALL BITWISE EQUAL" in r.stdout, r.stderr[-2000:]
+
+
+def test_diagnostic_only_variants(mapper):
+    """Round 5's measured-and-rejected variants live in the diagnostic build
+    only: the product rejects SBO_OPT_PRECISE_KERNEL 5 and
+    SBO_OPT_CHOL_GEMM 3; in lib/libsbo_diag.so (a child process, SBO_LIB)
+    kernel 5 is bitwise kernel 3 on the lpsc box and the split-bf16 Cholesky
+    updates keep the backward-error bound at N = 4100."""
+    import os
+    import subprocess
+    import sys
+    g = TerrainMapper(0, ctx=mapper.ctx)
+    with pytest.raises(N.SboError):
+        g.set_option(N.SBO_OPT_PRECISE_KERNEL, 5)
+    with pytest.raises(N.SboError):
+        g.set_option(N.SBO_OPT_CHOL_GEMM, 3)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    diag = os.path.join(root, "safe_bayesian_optimization_amd", "lib", "libsbo_diag.so")
+    if not os.path.exists(diag):
+        pytest.skip("lib/libsbo_diag.so not built (make -C safe_bayesian_optimization_amd diag)")
+    child = r"""
+import sys, numpy as np
+sys.path.insert(0, %r)
+from oracle import oracle as O
+from safe_bayesian_optimization_amd import TerrainMapper, synthetic
+from safe_bayesian_optimization_amd import _native as N
+from safe_bayesian_optimization_amd.terrain import synthetic_box
+wl = synthetic_box(3000, 61, 29, seed=5)
+gm = TerrainMapper(0, wl.hyper)
+gm.set_option(N.SBO_OPT_PRECISION, 1)
+gm.fit(wl.x, wl.y, wl.obs)
+res = {}
+for k in (3, 5):
+    gm.set_option(N.SBO_OPT_PRECISE_KERNEL, k)
+    res[k] = gm.predict(wl.qx, wl.qy)
+assert np.array_equal(res[3][0], res[5][0]) and np.array_equal(res[3][1], res[5][1])
+w2 = synthetic(4100, 24, 20, seed=4103)
+g2 = TerrainMapper(0, w2.hyper)
+g2.set_option(N.SBO_OPT_CHOL_GEMM, 3)
+g2.fit(w2.x, w2.y, w2.obs)
+L, _ = g2.factor()
+o = g2.order()
+K = O.rbf_fill_f32in(np.float32(w2.x)[o], np.float32(w2.y)[o])
+L64 = L.astype(np.float64)
+be = np.linalg.norm(L64 @ L64.T - K) / np.linalg.norm(K)
+assert be <= 10 * 4100 * 2.0 ** -24, be
+print("DIAG VARIANTS OK", be)
+""" % root
+    env = dict(os.environ, SBO_LIB=diag)
+    r = subprocess.run([sys.executable, "-c", child], capture_output=True, text=True, timeout=600, env=env)
+    print(r.stdout[-1000:])
+    assert r.returncode == 0 and "DIAG VARIANTS OK" in r.stdout, r.stderr[-2000:]
