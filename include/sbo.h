@@ -442,7 +442,7 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * SBO_OPT_PRECISE_KERNEL 3 sweeps through (the queries run in chunks of as
  * many 128-query blocks as fit it; at least one). */
 #define SBO_OPT_TABLE_MB 23
-/* SBO_OPT_INV_OZ (default 6; 5; 0: rocBLAS dgemm): the recursive f64
+/* SBO_OPT_INV_OZ (default 6; 5, 4; 0: rocBLAS dgemm): the recursive f64
  * inverse's products at splits of 4096 and more (S = L21 A^-1, X21 = -C^-1 S;
  * N <= 32768)
  * as an f64 GEMM emulated on the int8 matrix cores -- each row / column cut
@@ -451,7 +451,8 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * error is relative to a row's and a column's largest entries (2^-40 / 2^-48
  * of them for 5 / 6 digits), not to each product's: six digits move the
  * posterior by < 5e-7 against the dgemm fit, five by up to 4e-6 (not for the
- * precise regime).  The SBO_OPT_INV_OVERLAP fit keeps the dgemm products. */
+ * precise regime).  With SBO_OPT_INV_OZ_ADAPT the value is the most digits a
+ * fit uses.  The SBO_OPT_INV_OVERLAP fit keeps the dgemm products. */
 #define SBO_OPT_INV_OZ 24
 /* SBO_OPT_INV_CHECK (default 1; 0 off; 2 after every full inverse): the
  * fit's run-time accuracy guard of its f64 inverse X.  On 32 queries (a 4 x 4
@@ -481,6 +482,19 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * GEMM (SBO_OPT_INV_OZ); the levels below keep dgemm products.  Automatic:
  * 2048 for N >= 12288, else 4096. */
 #define SBO_OPT_INV_OZ_MIN 28
+/* SBO_OPT_INV_OZ_ADAPT (default 1; 0 off): the sliced inverse's digits per
+ * fit from the guard's last reading (SBO_OPT_INV_CHECK must be on).  Its
+ * measure grows ~256x per digit dropped (200-1000x measured), so a fit at d
+ * digits with err e lets the next fit -- same hyper-parameters, N within
+ * [0.8, 1.25] of it -- take five digits when e 256^(d - 5) <= tol / 1000
+ * (never four: the guard watches the variance, and at four digits the mean
+ * moved 2.9e-6 at C4 while the guard read 1.2e-8).  That fit is checked as
+ * any other: if the data moved and it fires (dgemm products), the data keeps
+ * SBO_OPT_INV_OZ digits from then on.  The first fit after sbo_create /
+ * sbo_warmup, after an option change or a hyper-parameter change takes
+ * SBO_OPT_INV_OZ digits.  sbo_get_inverse_check's digits say which ran:
+ * C4's warm refits take five (fit -2 ms), the lpsc box stays at six. */
+#define SBO_OPT_INV_OZ_ADAPT 29
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
 /* The last inverse check (SBO_OPT_INV_CHECK) of the current fit: ran = 1 if

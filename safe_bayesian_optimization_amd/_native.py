@@ -63,6 +63,7 @@ SBO_OPT_INV_CHECK = 25
 SBO_OPT_PLAN_BLOCK = 26
 SBO_OPT_PROBE_SIZE = 27
 SBO_OPT_INV_OZ_MIN = 28
+SBO_OPT_INV_OZ_ADAPT = 29
 
 
 class SboError(RuntimeError):

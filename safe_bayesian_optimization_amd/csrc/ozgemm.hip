@@ -518,6 +518,7 @@ hipError_t launch_gz_gemm(hipStream_t s, int nd, const double *A, int64_t lda, c
     if (K <= 0 || K > kGzMaxK) return hipErrorInvalidValue;
     if (flags & kGzLowerC) return hipErrorInvalidValue;
     switch (nd) {
+        case 4: return gz_run<4>(s, A, lda, B, ldb, m, n, K, alpha, C, ldc, flags, ws);
         case 5: return gz_run<5>(s, A, lda, B, ldb, m, n, K, alpha, C, ldc, flags, ws);
         case 6: return gz_run<6>(s, A, lda, B, ldb, m, n, K, alpha, C, ldc, flags, ws);
         default: return hipErrorInvalidValue;

@@ -134,6 +134,62 @@ bool oz_level(const sbo_ctx *ctx, int64_t h, int64_t m) {
     const int64_t mn = ctx->inv_oz_min > 0 ? ctx->inv_oz_min : (ctx->n >= 12288 ? 2048 : 4096);
     return ctx->inv_oz != 0 && !ctx->inv_oz_off && h >= mn && h <= 16384 && m <= 16384;
 }
+// The digits of the current fit's sliced products (SBO_OPT_INV_OZ_ADAPT:
+// chosen per fit by choose_inv_digits)
+int inv_digits(const sbo_ctx *ctx) { return ctx->inv_oz_cur > 0 ? ctx->inv_oz_cur : ctx->inv_oz; }
+// SBO_OPT_INV_OZ_ADAPT: the guard's measure of a sliced inverse (its
+// variance effect on 32 queries) grows ~256x per digit dropped -- the
+// digits' truncation and the dropped digit products are 2^-8 coarser each;
+// measured 200x (C4) to 1000x (lpsc box) from six digits to five,
+// tools/r5_inv_adapt.py -- so the last reading at d digits predicts the next
+// fit's at d' as err 256^(d - d').  The guard watches the variance only, and
+// the mean moves more (four digits at C4: mean 2.9e-6 against the guard's
+// 1.2e-8; five: the mean at six digits' 7.5e-8), so the next fit takes five
+// digits only when the prediction for five is within a thousandth of the
+// guard's bound, never four, and only for the same hyper-parameters and N
+// within [0.8, 1.25] of the measured fit's; the guard checks that fit as
+// any other (if the data moved and it fires: dgemm products, and six digits
+// from then on for this data).  C4: 5.6e-13 at six digits -> five (1.1e-10);
+// the lpsc box: 3.8e-9 -> stays at six.
+constexpr int kInvOzAdaptMin = 5;
+constexpr double kInvOzMargin = 1000.0;
+// the fit's data is "the same" as the last guarded fit's: the same
+// hyper-parameters, N within [0.8, 1.25] of it
+bool inv_same_data(const sbo_ctx *ctx) {
+    const sbo_hyper &a = ctx->hyper, &b = ctx->inv_oz_hist_hyper;
+    return ctx->inv_oz_hist_n > 0 && a.length_scale == b.length_scale && a.sigma_f == b.sigma_f &&
+           a.noise_level == b.noise_level && 5 * ctx->n >= 4 * ctx->inv_oz_hist_n &&
+           4 * ctx->n <= 5 * ctx->inv_oz_hist_n;
+}
+int choose_inv_digits(const sbo_ctx *ctx) {
+    if (!ctx->inv_oz_adapt || ctx->inv_check == 0 || ctx->inv_oz == 0 || ctx->inv_oz_next <= 0 ||
+        !inv_same_data(ctx))
+        return ctx->inv_oz;
+    return std::min(ctx->inv_oz, ctx->inv_oz_next);
+}
+// after the guard read a fit's inverse: the next fit's digits
+void record_inv_digits(sbo_ctx *ctx, const sbo_inv_check &r) {
+    if (!inv_same_data(ctx)) ctx->inv_oz_pinned = false;
+    ctx->inv_oz_hist_n = ctx->n;
+    ctx->inv_oz_hist_hyper = ctx->hyper;
+    ctx->inv_oz_next = 0;
+    if (!ctx->inv_oz_adapt || !r.ran || r.digits <= 0) return;
+    if (!(r.err <= r.tol)) {
+        // fired at reduced digits: this data keeps SBO_OPT_INV_OZ digits from
+        // now on (no reduced fit that fires every other time)
+        if (r.digits < ctx->inv_oz) ctx->inv_oz_pinned = true;
+        return;
+    }
+    if (ctx->inv_oz_pinned) return;
+    int nd = ctx->inv_oz;
+    for (int d = kInvOzAdaptMin; d < ctx->inv_oz; ++d)
+        if (r.err * std::ldexp(1.0, 8 * (r.digits - d)) <= r.tol / kInvOzMargin) {
+            nd = d;
+            break;
+        }
+    ctx->inv_oz_next = nd;
+}
+
 // does the recursive inverse of n columns slice any of its products?
 bool inverse_sliced(const sbo_ctx *ctx, int64_t n) {
     if (n <= ctx->inv_base) return false;
@@ -161,8 +217,8 @@ sbo_status inverse_first_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64
     if (ozws && oz_level(ctx, h, m)) {   // S = L21 A^-1 in one sliced GEMM (A^-1 lower triangular)
         hipStream_t st;
         SBO_BLAS(rocblas_get_stream(hb, &st));
-        SBO_HIP(ozws->reserve(sbo::gz_workspace_bytes(m, h, h, ctx->inv_oz)));
-        SBO_HIP(sbo::launch_gz_gemm(st, ctx->inv_oz, Li + h, ld, Li, ld, m, h, h, 1.0, S, m, sbo::kGzTriBLower,
+        SBO_HIP(ozws->reserve(sbo::gz_workspace_bytes(m, h, h, inv_digits(ctx))));
+        SBO_HIP(sbo::launch_gz_gemm(st, inv_digits(ctx), Li + h, ld, Li, ld, m, h, h, 1.0, S, m, sbo::kGzTriBLower,
                                     ozws->as<char>()));
         return SBO_OK;
     }
@@ -192,8 +248,8 @@ sbo_status inverse_second_half(sbo_ctx *ctx, rocblas_handle hb, double *Li, int6
         // form, C^-1 as a lower-triangular op(A): 7.4 vs 5.x ms at C4)
         hipStream_t st;
         SBO_BLAS(rocblas_get_stream(hb, &st));
-        SBO_HIP(ozws->reserve(sbo::gz_workspace_bytes(h, m, m, ctx->inv_oz)));
-        SBO_HIP(sbo::launch_gz_gemm(st, ctx->inv_oz, S, m, C, ld, h, m, m, -1.0, B, ld,
+        SBO_HIP(ozws->reserve(sbo::gz_workspace_bytes(h, m, m, inv_digits(ctx))));
+        SBO_HIP(sbo::launch_gz_gemm(st, inv_digits(ctx), S, m, C, ld, h, m, m, -1.0, B, ld,
                                     sbo::kGzTransA | sbo::kGzTransB | sbo::kGzTriBUpper | sbo::kGzTransC,
                                     ozws->as<char>()));
         return SBO_OK;
@@ -266,9 +322,9 @@ sbo_status inverse_lower_f64_par(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld
     // (a reserve that reallocates mid-fit would wait for the device)
     sbo::DevBuf *ozA = nullptr, *ozC = nullptr;
     if (ctx->inv_oz != 0 && oz_level(ctx, h, m)) {
-        SBO_HIP(ctx->gzws.reserve(std::max(sbo::gz_workspace_bytes(m, h, h, ctx->inv_oz),
-                                           sbo::gz_workspace_bytes(h, m, m, ctx->inv_oz))));
-        SBO_HIP(ctx->gzws_aux.reserve(sbo::gz_workspace_bytes(m, m, m, ctx->inv_oz)));
+        SBO_HIP(ctx->gzws.reserve(std::max(sbo::gz_workspace_bytes(m, h, h, inv_digits(ctx)),
+                                           sbo::gz_workspace_bytes(h, m, m, inv_digits(ctx)))));
+        SBO_HIP(ctx->gzws_aux.reserve(sbo::gz_workspace_bytes(m, m, m, inv_digits(ctx))));
         ozA = &ctx->gzws;
         ozC = &ctx->gzws_aux;
     }
@@ -786,7 +842,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         if (!incr && (ctx->inv_check == 2 || ctx->inv_oz_off ||
                       (ctx->inv_check == 1 && ctx->inverse_rec && !early && inverse_sliced(ctx, n)))) {
             ctx->chk_res = sbo_inv_check{};
-            ctx->chk_res.digits = (ctx->inverse_rec && !early && inverse_sliced(ctx, n)) ? ctx->inv_oz : 0;
+            ctx->chk_res.digits = (ctx->inverse_rec && !early && inverse_sliced(ctx, n)) ? inv_digits(ctx) : 0;
             if (sbo_status st = inverse_check_launch(ctx)) return st;
             chk_pending = true;
         } else if (!incr) {
@@ -974,6 +1030,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         if (sbo_status st = inverse_check_read(ctx, r)) return st;
         r.err_fallback = -1.0;
         ctx->chk_res = r;
+        if (!ctx->inv_oz_off) record_inv_digits(ctx, r);
         if (!(r.err <= r.tol) && r.digits != 0 && !ctx->inv_oz_off) {
             // the sliced inverse misses the guard's bound: the fit again with
             // dgemm products (checked too), reported as fired
@@ -1421,6 +1478,7 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
 
 sbo_status factor_and_refresh(sbo_ctx *ctx) {
     rocblas_int *info = ctx->info.as<rocblas_int>();
+    ctx->inv_oz_cur = choose_inv_digits(ctx);   // (before blocked_potrf: its early first half slices too)
     ctx->widened_n = 0;
     // only the factorization that runs now may hand the inverse's first half
     // to refresh_operand (blocked_potrf sets it; the rocSOLVER path never
@@ -2378,8 +2436,16 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->precise_kernel = (int)value;
             return SBO_OK;
         case SBO_OPT_INV_OZ:
-            SBO_CHECK(value == 0 || value == 5 || value == 6, SBO_E_INVAL, "SBO_OPT_INV_OZ must be 0, 5 or 6");
+            SBO_CHECK(value == 0 || (value >= 4 && value <= 6), SBO_E_INVAL, "SBO_OPT_INV_OZ must be 0, 4, 5 or 6");
             ctx->inv_oz = (int)value;
+            ctx->inv_oz_cur = ctx->inv_oz_next = 0;
+            ctx->inv_oz_pinned = false;
+            return SBO_OK;
+        case SBO_OPT_INV_OZ_ADAPT:
+            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_INV_OZ_ADAPT must be 0 or 1");
+            ctx->inv_oz_adapt = (int)value;
+            ctx->inv_oz_next = 0;
+            ctx->inv_oz_pinned = false;
             return SBO_OK;
         case SBO_OPT_INV_OZ_MIN:
             SBO_CHECK(value == 0 || value == 2048 || value == 4096 || value == 8192, SBO_E_INVAL,
@@ -2533,6 +2599,9 @@ SBO_API sbo_status sbo_warmup(sbo_ctx *ctx, int64_t n_cap, int64_t m_cap, sbo_hy
     ctx->early_inv_n = 0;
     ctx->order.clear();
     ctx->chk_res = sbo_inv_check{};
+    ctx->inv_oz_next = 0;   // (the synthetic fit's guard reading says nothing about the real data)
+    ctx->inv_oz_hist_n = 0;
+    ctx->inv_oz_pinned = false;
     ctx->qgrid_x = ctx->qgrid_y = nullptr;
     ctx->qgrid_m = -1;
     ctx->hyper = sbo_hyper{0.4, 1.0, 0.1, 0.0};

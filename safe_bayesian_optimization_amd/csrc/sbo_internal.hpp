@@ -117,6 +117,16 @@ struct sbo_ctx {
     int inv_oz = 6;              // SBO_OPT_INV_OZ: digits of the int8-sliced top-level products (0: dgemm)
     int64_t inv_oz_min = 0;      // SBO_OPT_INV_OZ_MIN: the smallest sliced split (0: 2048 at N >= 12288, else 4096)
     bool inv_oz_off = false;     // (set while a fit redoes its inverse with dgemm products: the guard fired)
+    // SBO_OPT_INV_OZ_ADAPT: the digits of the current fit's sliced products
+    // (inv_digits), those the last guard reading allows for the next fit of
+    // the same hyper-parameters and about the same N (0: inv_oz), that
+    // reading's N and hyper-parameters, and whether a reduced fit of this data
+    // fired (then it keeps inv_oz digits)
+    int inv_oz_adapt = 1;
+    int inv_oz_cur = 0, inv_oz_next = 0;
+    int64_t inv_oz_hist_n = 0;
+    sbo_hyper inv_oz_hist_hyper{};
+    bool inv_oz_pinned = false;
     // the inverse's accuracy guard (SBO_OPT_INV_CHECK, inv_check.hip): its
     // stream, workspace, timing events and the last result
     int inv_check = 1;           // SBO_OPT_INV_CHECK: 0 off, 1 after sliced inverses, 2 after every full inverse

@@ -173,3 +173,75 @@ def test_guard_on_dgemm_inverse_and_appends(mapper):
         gm.set_option(N.SBO_OPT_INV_CHECK, 1)
     with pytest.raises(N.SboError):
         gm.set_option(N.SBO_OPT_INV_CHECK, 3)
+
+
+def test_inverse_digits_adapt(mapper):
+    """SBO_OPT_INV_OZ_ADAPT (default): a refit of the same hyper-parameters and
+    about the same N takes five digits when the last guard reading predicts
+    them a thousandth of the bound (C4-like synthetic data: 5.6e-13 at six),
+    and its posterior -- the precise sweep, so that the inverse's own effect
+    shows -- stays within 2e-7 of the six-digit fit's and meets the contract;
+    the lpsc box (3.8e-9 at six) stays at six.  A reduced fit that fires (the
+    box's data under the synthetic data's reading) falls back to dgemm
+    products, and that data keeps six digits from then on; a changed
+    hyper-parameter or N, or an option change, start again at six."""
+    n = 16384
+    syn = synthetic(n, 32, 16, seed=3)
+    box = synthetic_box(n, 32, 16, seed=3)
+    gm = TerrainMapper(0, syn.hyper, ctx=mapper.ctx)
+    try:
+        gm.set_option(N.SBO_OPT_INV_OZ_ADAPT, 1)
+        gm.set_option(N.SBO_OPT_PRECISION, 1)
+        got = []
+        for _ in range(3):
+            gm.fit(syn.x, syn.y, syn.obs)
+            c = gm.inverse_check()
+            mu, sd = gm.predict(syn.qx, syn.qy)
+            got.append((c, mu.astype(np.float64), sd.astype(np.float64) ** 2))
+        print("synthetic:", [(c["digits"], f"{c['err']:.1e}", c["fired"]) for c, _, _ in got])
+        assert [c["digits"] for c, _, _ in got] == [6, 5, 5]
+        assert all(c["fired"] == 0 and c["err"] <= CHECK_TOL / 100 for c, _, _ in got)
+        dmu, dvar = nrel(got[2][1], got[0][1]), nrel(got[2][2], got[0][2])
+        print(f"five vs six digits: mu {dmu:.2e} var {dvar:.2e}")
+        assert dmu < 2e-7 and dvar < 2e-7
+        omu, ovar = oracle64(gm, syn)
+        assert nrel(got[2][1], omu) < REL_TOL and nrel(got[2][2], ovar) < REL_TOL
+        # the box's data under the synthetic data's reading: five digits fire
+        gm.fit(box.x, box.y, box.obs)
+        c = gm.inverse_check()
+        print(f"box at five: err {c['err']:.1e} fired {c['fired']} fallback {c['err_fallback']:.1e}")
+        assert c["digits"] == 5 and c["fired"] == 1 and 0.0 <= c["err_fallback"] <= CHECK_TOL
+        for wl in (box, box, syn):   # pinned at six for this data
+            gm.fit(wl.x, wl.y, wl.obs)
+            c = gm.inverse_check()
+            assert c["digits"] == 6 and c["fired"] == 0
+        # new data (another N): six, then five again; an option change: six
+        syn2 = synthetic(12288, 32, 16, seed=9)
+        ds = []
+        for k in range(3):
+            if k == 2:
+                gm.set_option(N.SBO_OPT_INV_OZ, 6)
+            gm.fit(syn2.x, syn2.y, syn2.obs)
+            ds.append(gm.inverse_check()["digits"])
+        assert ds == [6, 5, 6]
+        # another hyper-parameter: six
+        gm.fit(syn2.x, syn2.y, syn2.obs)
+        assert gm.inverse_check()["digits"] == 5
+        gm2 = TerrainMapper(0, Hyper(length_scale=0.41), ctx=mapper.ctx)
+        gm2.fit(syn2.x, syn2.y, syn2.obs)
+        assert gm2.inverse_check()["digits"] == 6
+        # the lpsc box stays at six; adaptation off: always six
+        gm.set_option(N.SBO_OPT_INV_OZ_ADAPT, 0)
+        gm.fit(syn.x, syn.y, syn.obs)
+        gm.fit(syn.x, syn.y, syn.obs)
+        assert gm.inverse_check()["digits"] == 6
+        gm.set_option(N.SBO_OPT_INV_OZ_ADAPT, 1)
+        bx = workload(16384, True, Hyper())
+        for _ in range(2):
+            gm.fit(bx.x, bx.y, bx.obs)
+            assert gm.inverse_check()["digits"] == 6
+    finally:
+        gm.set_option(N.SBO_OPT_PRECISION, -1)
+        gm.set_option(N.SBO_OPT_INV_OZ_ADAPT, 1)
+    with pytest.raises(N.SboError):
+        gm.set_option(N.SBO_OPT_INV_OZ_ADAPT, 2)

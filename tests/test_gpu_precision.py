@@ -133,12 +133,18 @@ def test_c4_whole_grid(dev):
     """C4 (the headline): the default tick against the precise sweep over all
     10^6 grid points, and the precise sweep against the oracle on a sample --
     the whole-grid error the 3072-point headline sample can only estimate, next
-    to the probe's own number (DESIGN.md 5a records the ratio)."""
+    to the probe's own number (DESIGN.md 5a records the ratio).  As in the
+    bench: a refit after the first fit, so the inverse is the one the guard's
+    reading of the first allows (SBO_OPT_INV_OZ_ADAPT: five digits)."""
     n, gw, gh = CONFIGS["C4"]
     wl = synthetic(n, gw, gh, seed=0, name="C4")
     gm = TerrainMapper(0, wl.hyper)
     t = lambda a: torch.tensor(f32(a), device=dev)  # noqa: E731
     gm.fit(t(wl.x), t(wl.y), t(wl.obs))
+    assert gm.inverse_check()["digits"] == 6
+    gm.fit(t(wl.x), t(wl.y), t(wl.obs))
+    chk = gm.inverse_check()
+    assert chk["digits"] == 5 and chk["fired"] == 0
     pi = gm.probe_info()
     assert not pi["precise"]          # the headline runs the fast sweep
     qx, qy = t(wl.qx), t(wl.qy)
