@@ -393,8 +393,10 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
 #define SBO_OPT_CHOL_OUTER 15
 /* SBO_OPT_CHOL_DIAG (default 1): the blocked Cholesky's chain kernels -- the
  * 128 x 128 diagonal blocks (16-column panels) and the panel solves below
- * them -- with their inner updates on the matrix cores (1) or on the VALU (0);
- * the factor is bitwise the same. */
+ * them -- with their inner updates on the matrix cores, left-looking (1: one
+ * MFMA chain per block from every finished column, in registers) or
+ * right-looking (2: each finished panel's update through LDS), or on the VALU
+ * (0); the factor is bitwise the same. */
 #define SBO_OPT_CHOL_DIAG 16
 /* SBO_OPT_CHOL_GEMM (default 4): the blocked Cholesky's updates.  4 / 5: the
  * outer panels' two big updates (the look-ahead block column and the lower

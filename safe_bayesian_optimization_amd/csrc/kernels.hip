@@ -486,6 +486,130 @@ __global__ __launch_bounds__(256) void chol_diag_mfma_kernel(float *__restrict__
     SBO_CSTAMP(3);
 }
 
+// The same diagonal block, left-looking (round 5; SBO_OPT_CHOL_DIAG 1, the
+// default -- 2 keeps the right-looking chol_diag_mfma_kernel): before wave 0
+// factors a 16-column panel, the four waves bring the panel's columns up to
+// date with every factored column in one MFMA chain per 16 x 16 block, the
+// accumulator in registers -- each element sees fmaf(-L[i][j], L[l][j], a)
+// for j ascending as in the right-looking kernel's per-panel updates, so the
+// factor is bitwise the same -- instead of updating the whole trailing
+// triangle through LDS after every panel.
+__global__ __launch_bounds__(256) void chol_diag_ll_kernel(float *__restrict__ A, int64_t ld, int kb, int64_t k0,
+                                                           int *__restrict__ info) {
+    static_assert(kCholNB == 128, "two panel rows per lane of wave 0, 8 x 16 blocks");
+    __shared__ __attribute__((aligned(16))) float a[kCholNB][kCholNB + 4];
+    __shared__ int s_bad;
+    if (*info != 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // thread (i, h): row i = tid & 127 of columns h, h + 2, h + 4, ... (coalesced
+    // over i), 16 loads in flight per batch
+    // (every load unconditional, from inside the kb x kb block: the rows and
+    // columns past kb read its last row / column and are replaced after)
+    const int li = tid & (kCholNB - 1), lh = tid >> 7;
+    const float *colp = A + min(li, kb - 1);
+    for (int j0 = 0; j0 < kCholNB; j0 += 32) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = colp[(int64_t)min(j0 + 2 * u + lh, kb - 1) * ld];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int j = j0 + 2 * u + lh;
+            a[li][j] = (li < kb && j < kb && li >= j) ? v[u] : (li == j ? 1.0f : 0.0f);
+        }
+    }
+    if (tid == 0) s_bad = 0;
+    __syncthreads();
+    const int fi = lane & 15, fk = lane >> 4;   // operand lane map: A[fi][fk], B[fk][fi]; C row 4 fk + v, col fi
+    for (int jb = 0; jb < kCholNB; jb += kCholPW) {
+        if (jb > 0) {
+            // the panel's columns jb .. jb + 15, rows jb .. 127, from every
+            // factored column 0 .. jb - 1: one MFMA chain per 16 x 16 block
+            for (int q = wave; q < (kCholNB - jb) / 16; q += 4) {
+                const int i0 = jb + 16 * q;
+                f32x4_t acc;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[v] = a[i0 + 4 * fk + v][jb + fi];
+                for (int k16 = 0; k16 < jb; k16 += 16) {
+                    float av[4], bv[4];
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        av[kk] = -a[i0 + fi][k16 + 4 * kk + fk];
+                        bv[kk] = a[jb + fi][k16 + 4 * kk + fk];
+                    }
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v) a[i0 + 4 * fk + v][jb + fi] = acc[v];
+            }
+            __syncthreads();
+        }
+        if (wave == 0) {
+            const int r0 = jb + lane, r1 = jb + 64 + lane;
+            const int q0 = min(r0, kCholNB - 1), q1 = min(r1, kCholNB - 1);
+            float p0[kCholPW], p1[kCholPW];
+#pragma unroll
+            for (int c4 = 0; c4 < kCholPW / 4; ++c4) {
+                const float4 u0 = reinterpret_cast<const float4 *>(&a[q0][jb])[c4];
+                const float4 u1 = reinterpret_cast<const float4 *>(&a[q1][jb])[c4];
+                p0[4 * c4] = u0.x; p0[4 * c4 + 1] = u0.y; p0[4 * c4 + 2] = u0.z; p0[4 * c4 + 3] = u0.w;
+                p1[4 * c4] = u1.x; p1[4 * c4 + 1] = u1.y; p1[4 * c4 + 2] = u1.z; p1[4 * c4 + 3] = u1.w;
+            }
+            int bad = 0;
+#pragma unroll
+            for (int c = 0; c < kCholPW; ++c) {
+                // (no early exit inside the unrolled panel: a failed pivot is
+                // recorded and the rest of the panel computes garbage that the
+                // block never stores)
+                const int j = jb + c;
+                const float djj = lane_value(p0[c], c);   // row j is lane c's first row
+                // (pivots below FLT_MIN fail too: v_rsq_f32 of a denormal may overflow)
+                if (bad == 0 && (!(djj >= 1.17549435e-38f) || !(djj < __builtin_huge_valf()))) bad = j + 1;
+                // every lane, no row tests: the lanes above the diagonal
+                // (row < column) compute values of the upper triangle that
+                // nothing reads (the lane-mask per column and row would be
+                // 136 live SGPR pairs); the diagonal lane's p0[c] is djj, so
+                // L_jj = djj * rs there
+                const float rs = __builtin_amdgcn_rsqf(djj);
+                p0[c] = p0[c] * rs;
+                p1[c] = p1[c] * rs;
+#pragma unroll
+                for (int c2 = c + 1; c2 < kCholPW; ++c2) {
+                    const float lc2 = lane_value(p0[c], c2);   // L[jb + c2][j], lane c2's (already scaled)
+                    p0[c2] = fmaf(-p0[c], lc2, p0[c2]);
+                    p1[c2] = fmaf(-p1[c], lc2, p1[c2]);
+                }
+            }
+            if (r0 < kCholNB) {
+#pragma unroll
+                for (int c = 0; c < kCholPW; ++c) a[r0][jb + c] = p0[c];
+            }
+            if (r1 < kCholNB) {
+#pragma unroll
+                for (int c = 0; c < kCholPW; ++c) a[r1][jb + c] = p1[c];
+            }
+            if (lane == 0 && bad) s_bad = bad;
+        }
+        __syncthreads();
+        if (s_bad) break;
+    }
+    if (s_bad) {
+        if (tid == 0) atomicCAS(info, 0, (int)(k0 + s_bad));
+        return;
+    }
+    float *colw = A + li + (int64_t)lh * ld;
+    for (int j0 = 0; j0 < kCholNB; j0 += 32) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = a[li][j0 + 2 * u + lh];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int j = j0 + 2 * u + lh;
+            if (li < kb && j < kb && li >= j) colw[(int64_t)(j0 + 2 * u) * ld] = v[u];
+        }
+    }
+}
+
 // The blocked Cholesky's trailing updates (a2): C[r][c] -= sum_k P[r][k] Q[c][k]
 // over 128 x 128 tiles of C (all tiles of an m x nc block, or, lower != 0,
 // the tiles on and below the diagonal of an m x m block), f32 in and out,
@@ -842,6 +966,109 @@ __global__ __launch_bounds__(256) void chol_trsm_mfma_kernel(const float *__rest
     if (in)
         for (int j = h; j < kb; j += 2) A21[row + (int64_t)j * ld] = X[j * kTrX + t];
     SBO_CSTAMP(11);
+}
+
+// The same panel solve, left-looking (round 5; SBO_OPT_CHOL_DIAG 1, the
+// default -- 2 keeps the right-looking chol_trsm_mfma_kernel): before the
+// rows solve 16-column block B, the four waves bring its columns up to date
+// with every solved column 0 .. 16B - 1 in one MFMA chain per 16 x 16 result
+// block, the accumulator in registers from X itself -- X[c][t] sees
+// fmaf(-L[c][u], x_u(t), .) for u ascending, the same terms in the same order
+// as the right-looking kernel's per-block updates (and the VALU kernel's
+// loop), so the panel is bitwise the same; the right-looking kernel read and
+// wrote every later block's accumulators through LDS after every block (56
+// 16 x 16 updates per wave, each a four-MFMA chain) where this issues 8B
+// MFMAs per wave as two interleaved chains.  Wave w owns row blocks 2w and
+// 2w + 1 (rows 32w .. 32w + 31).
+__global__ __launch_bounds__(256) void chol_trsm_ll_kernel(const float *__restrict__ L11, int64_t ld, int kb,
+                                                           float *__restrict__ A21, int64_t m2) {
+    __shared__ __attribute__((aligned(16))) float Ls[kCholNB * kTrsmLd];
+    __shared__ float X[kCholNB * kTrX];
+    __shared__ float rinv[kCholNB];
+    const int tid = threadIdx.x, t = tid & (kCholNB - 1), h = tid >> 7;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int64_t row = (int64_t)blockIdx.x * kCholNB + t;
+    const bool in = row < m2, lin = t < kb;
+    const float *lp = L11 + min(t, kb - 1);
+    const float *xp = A21 + (in ? row : 0);
+    for (int jb = 0; jb < kCholNB; jb += 64) {
+        float lv[32], xv[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            const int64_t off = (int64_t)min(jb + 2 * u + h, kb - 1) * ld;
+            lv[u] = lp[off];
+            xv[u] = xp[off];
+        }
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            const int j = jb + 2 * u + h;
+            Ls[t * kTrsmLd + j] = (j < kb && lin && t >= j) ? lv[u] : (t == j && j >= kb ? 1.0f : 0.0f);
+            X[j * kTrX + t] = (in && j < kb) ? xv[u] : 0.0f;
+        }
+    }
+    __syncthreads();
+    if (tid < kCholNB) rinv[tid] = __fdiv_rn(1.0f, Ls[tid * kTrsmLd + tid]);
+    __syncthreads();
+    const int fr = lane & 15, fg = lane >> 4;
+    const int rb0 = 32 * wave, rb1 = rb0 + 16;
+    for (int B = 0; B < kCholNB / 16; ++B) {
+        const int j0 = 16 * B;
+        if (B > 0) {
+            f32x4_t acc0, acc1;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                acc0[v] = X[(j0 + 4 * fg + v) * kTrX + rb0 + fr];
+                acc1[v] = X[(j0 + 4 * fg + v) * kTrX + rb1 + fr];
+            }
+            for (int k16 = 0; k16 < B; ++k16) {   // (16 columns at a time: operand reads batched)
+                float av[4], b0[4], b1[4];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int u = 16 * k16 + 4 * kk + fg;
+                    av[kk] = -Ls[(j0 + fr) * kTrsmLd + u];
+                    b0[kk] = X[u * kTrX + rb0 + fr];
+                    b1[kk] = X[u * kTrX + rb1 + fr];
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], b0[kk], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], b1[kk], acc1, 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                X[(j0 + 4 * fg + v) * kTrX + rb0 + fr] = acc0[v];
+                X[(j0 + 4 * fg + v) * kTrX + rb1 + fr] = acc1[v];
+            }
+            __syncthreads();
+        }
+        if (h == 0) {
+            float4 lb[16][4];
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    if (4 * v <= q) lb[q][v] = reinterpret_cast<const float4 *>(Ls + (j0 + q) * kTrsmLd + j0)[v];
+            float sb[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) sb[q] = X[(j0 + q) * kTrX + t];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                sb[q] = sb[q] * rinv[j0 + q];
+#pragma unroll
+                for (int q2 = q + 1; q2 < 16; ++q2) {
+                    const float4 l4 = lb[q2][q >> 2];
+                    const float l = (q & 3) == 0 ? l4.x : (q & 3) == 1 ? l4.y : (q & 3) == 2 ? l4.z : l4.w;
+                    sb[q2] = fmaf(-sb[q], l, sb[q2]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) X[(j0 + q) * kTrX + t] = sb[q];
+        }
+        __syncthreads();
+    }
+    if (in)
+        for (int j = h; j < kb; j += 2) A21[row + (int64_t)j * ld] = X[j * kTrX + t];
 }
 
 // Row 1-norms of the packed operand: block I, thread r sums |A[I*BM + r][:]|.
@@ -2356,6 +2583,8 @@ hipError_t launch_row_l1(hipStream_t s, const float *aug, int64_t npad, int64_t 
 hipError_t launch_chol_diag(hipStream_t s, float *A, int64_t ld, int kb, int64_t k0, int *info, int version) {
     if (kb <= 0 || kb > kCholNB) return hipErrorInvalidValue;
     if (version == 1)
+        hipLaunchKernelGGL(chol_diag_ll_kernel, dim3(1), dim3(256), 0, s, A, ld, kb, k0, info);
+    else if (version == 2)
         hipLaunchKernelGGL(chol_diag_mfma_kernel, dim3(1), dim3(256), 0, s, A, ld, kb, k0, info);
     else
         hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, s, A, ld, kb, k0, info);
@@ -2380,6 +2609,9 @@ hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb,
     if (kb <= 0 || kb > kCholNB || m2 < 0) return hipErrorInvalidValue;
     if (m2 == 0) return hipSuccess;
     if (version == 1)
+        hipLaunchKernelGGL(chol_trsm_ll_kernel, dim3((unsigned)((m2 + kCholNB - 1) / kCholNB)), dim3(2 * kCholNB), 0,
+                           s, L11, ld, kb, A21, m2);
+    else if (version == 2)
         hipLaunchKernelGGL(chol_trsm_mfma_kernel, dim3((unsigned)((m2 + kCholNB - 1) / kCholNB)), dim3(2 * kCholNB), 0,
                            s, L11, ld, kb, A21, m2);
     else

@@ -2401,7 +2401,7 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->chol_gemm_own = (int)value;
             return SBO_OK;
         case SBO_OPT_CHOL_DIAG:
-            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_CHOL_DIAG must be 0 or 1");
+            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_CHOL_DIAG must be 0, 1 or 2");
             ctx->chol_diag = (int)value;
             return SBO_OK;
         case SBO_OPT_CHOL_OUTER:

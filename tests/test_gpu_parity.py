@@ -164,19 +164,20 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
 @pytest.mark.parametrize("n", [77, 300, 4100])
 def test_chol_diag_kernels_bitwise(mapper, n):
     """The diagonal-block kernels (SBO_OPT_CHOL_DIAG 1: 16-column panels with
-    matrix-core trailing updates, 0: 8-column VALU panels) give the same
+    matrix-core trailing updates and the left-looking panel solve, 2: the same
+    with the right-looking one, 0: 8-column VALU panels) give the same
     factor bit for bit: every element sees fmaf(-L[i][j], L[l][j], a) with j
     ascending either way (an f32 MFMA is a k-ordered fmaf chain).  n = 77 and
     300 end in a partial block (the identity padding)."""
     wl = synthetic(n, 16, 12, seed=n + 5)
     got = []
-    for dv in (0, 1):
+    for dv in (0, 1, 2):
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
         gm.set_option(N.SBO_OPT_CHOL_DIAG, dv)
         gm.fit(wl.x, wl.y, wl.obs)
         got.append(gm.factor()[0])
     gm.set_option(N.SBO_OPT_CHOL_DIAG, 1)
-    assert np.array_equal(got[0], got[1])
+    assert np.array_equal(got[0], got[1]) and np.array_equal(got[0], got[2])
 
 
 def test_blocked_cholesky_not_spd_past_first_block(mapper):
