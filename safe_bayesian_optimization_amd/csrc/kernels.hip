@@ -493,7 +493,8 @@ __global__ __launch_bounds__(256) void chol_diag_mfma_kernel(float *__restrict__
 // accumulator in registers -- each element sees fmaf(-L[i][j], L[l][j], a)
 // for j ascending as in the right-looking kernel's per-panel updates, so the
 // factor is bitwise the same -- instead of updating the whole trailing
-// triangle through LDS after every panel.
+// triangle through LDS after every panel; and the panel itself on all four
+// waves (one row per lane) instead of wave 0 (two).
 __global__ __launch_bounds__(256) void chol_diag_ll_kernel(float *__restrict__ A, int64_t ld, int kb, int64_t k0,
                                                            int *__restrict__ info) {
     static_assert(kCholNB == 128, "two panel rows per lane of wave 0, 8 x 16 blocks");
@@ -544,17 +545,20 @@ __global__ __launch_bounds__(256) void chol_diag_ll_kernel(float *__restrict__ A
             }
             __syncthreads();
         }
-        if (wave == 0) {
-            const int r0 = jb + lane, r1 = jb + 64 + lane;
-            const int q0 = min(r0, kCholNB - 1), q1 = min(r1, kCholNB - 1);
-            float p0[kCholPW], p1[kCholPW];
+        {
+            // the panel on all four waves: every wave factors the panel's top
+            // 16 x 16 triangle in lanes 0-15 (the pivot rows its other lanes
+            // need) and 48 of the rows below it in lanes 16-63; wave 0 writes
+            // the triangle.  Each row sees the same operations as on one wave.
+            const int r = lane < 16 ? jb + lane : jb + 16 + 48 * wave + (lane - 16);
+            const int q = min(r, kCholNB - 1);
+            float p0[kCholPW];
 #pragma unroll
             for (int c4 = 0; c4 < kCholPW / 4; ++c4) {
-                const float4 u0 = reinterpret_cast<const float4 *>(&a[q0][jb])[c4];
-                const float4 u1 = reinterpret_cast<const float4 *>(&a[q1][jb])[c4];
+                const float4 u0 = reinterpret_cast<const float4 *>(&a[q][jb])[c4];
                 p0[4 * c4] = u0.x; p0[4 * c4 + 1] = u0.y; p0[4 * c4 + 2] = u0.z; p0[4 * c4 + 3] = u0.w;
-                p1[4 * c4] = u1.x; p1[4 * c4 + 1] = u1.y; p1[4 * c4 + 2] = u1.z; p1[4 * c4 + 3] = u1.w;
             }
+            __syncthreads();   // (every wave has read the triangle before wave 0 writes it)
             int bad = 0;
 #pragma unroll
             for (int c = 0; c < kCholPW; ++c) {
@@ -562,33 +566,22 @@ __global__ __launch_bounds__(256) void chol_diag_ll_kernel(float *__restrict__ A
                 // recorded and the rest of the panel computes garbage that the
                 // block never stores)
                 const int j = jb + c;
-                const float djj = lane_value(p0[c], c);   // row j is lane c's first row
+                const float djj = lane_value(p0[c], c);   // row j is lane c's
                 // (pivots below FLT_MIN fail too: v_rsq_f32 of a denormal may overflow)
                 if (bad == 0 && (!(djj >= 1.17549435e-38f) || !(djj < __builtin_huge_valf()))) bad = j + 1;
-                // every lane, no row tests: the lanes above the diagonal
-                // (row < column) compute values of the upper triangle that
-                // nothing reads (the lane-mask per column and row would be
-                // 136 live SGPR pairs); the diagonal lane's p0[c] is djj, so
-                // L_jj = djj * rs there
                 const float rs = __builtin_amdgcn_rsqf(djj);
                 p0[c] = p0[c] * rs;
-                p1[c] = p1[c] * rs;
 #pragma unroll
                 for (int c2 = c + 1; c2 < kCholPW; ++c2) {
                     const float lc2 = lane_value(p0[c], c2);   // L[jb + c2][j], lane c2's (already scaled)
                     p0[c2] = fmaf(-p0[c], lc2, p0[c2]);
-                    p1[c2] = fmaf(-p1[c], lc2, p1[c2]);
                 }
             }
-            if (r0 < kCholNB) {
+            if (r < kCholNB && (lane >= 16 || wave == 0)) {
 #pragma unroll
-                for (int c = 0; c < kCholPW; ++c) a[r0][jb + c] = p0[c];
+                for (int c = 0; c < kCholPW; ++c) a[r][jb + c] = p0[c];
             }
-            if (r1 < kCholNB) {
-#pragma unroll
-                for (int c = 0; c < kCholPW; ++c) a[r1][jb + c] = p1[c];
-            }
-            if (lane == 0 && bad) s_bad = bad;
+            if (tid == 0 && bad) s_bad = bad;
         }
         __syncthreads();
         if (s_bad) break;
