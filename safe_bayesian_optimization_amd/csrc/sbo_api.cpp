@@ -1131,6 +1131,7 @@ sbo_status probe_precision(sbo_ctx *ctx) {
                                  sizeof(float), (size_t)MT, hipMemcpyDeviceToDevice, ctx->stream));
         const bool prof = ctx->prof;
         ctx->prof = false;  // (the probe is not a tick: no events, no counters)
+        ctx->order_p = nullptr;
         sbo_status st = run_tick(ctx, qx, qy, M, 0.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, sdf, nullptr, nullptr,
                                  nullptr, key, nullptr, kSweepFast);
         if (st == SBO_OK) {
@@ -1149,9 +1150,14 @@ sbo_status probe_precision(sbo_ctx *ctx) {
             ctx->probe_ref_tol = std::ldexp(
                 std::clamp(std::isfinite(vf) ? vf : sf2, std::ldexp(sf2, -kProbeRefBits), sf2), -kProbeRefBits);
         }
-        if (st == SBO_OK)
+        if (st == SBO_OK) {
+            // the same queries as the fast sweep's: its Morton order again
+            // (qwork untouched in between)
+            ctx->reuse_order = true;
             st = run_tick(ctx, qx, qy, M, 0.0, 0.0, SBO_SCORE_WIDTH, 0, nullptr, sdp, nullptr, nullptr, nullptr, key,
                           nullptr, kSweepPreciseDense);
+            ctx->reuse_order = false;
+        }
         ctx->prof = prof;
         if (st != SBO_OK) return st;
         SBO_HIP(hipMemcpyAsync(h.data(), sdf, sizeof(float) * 2 * M, hipMemcpyDeviceToHost, ctx->stream));
@@ -1573,10 +1579,17 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         if (ctx->query_order == 1 && ctx->qgrid.ok) {
             SBO_HIP(sbo::launch_query_grid(ctx->stream, qx, qy, m, ctx->qgrid, ctx->qgwork.as<void>(), &p, &sx, &sy));
             ms = ctx->qgrid.ms;
+        } else if (ctx->reuse_order && ctx->order_p) {
+            p = ctx->order_p;    // (the probe's second sweep: the same queries, already ordered)
+            sx = ctx->order_sx;
+            sy = ctx->order_sy;
         } else {
             const size_t wb = sbo::query_order_bytes(m);
             SBO_HIP(ctx->qwork.reserve(wb));
             SBO_HIP(sbo::launch_query_order(ctx->stream, qx, qy, m, ctx->bbox, ctx->qwork.as<void>(), wb, &p, &sx, &sy));
+            ctx->order_p = p;
+            ctx->order_sx = sx;
+            ctx->order_sy = sy;
         }
         perm = p;
         qx = sx;

@@ -178,6 +178,11 @@ struct sbo_ctx {
     sbo::DevBuf plan_work;       // the tick's tile plan (launch_plan)
     sbo::DevBuf fwork, fowner, fimg, fpix, fout;  // device frontier (sbo_frontier / sbo_subgoal)
     sbo::DevBuf qwork;           // query ordering workspace
+    // the probe's second sweep reads the same queries: reuse the first's
+    // Morton order (pointers into qwork; valid only while reuse_order is set)
+    bool reuse_order = false;
+    int32_t *order_p = nullptr;
+    float *order_sx = nullptr, *order_sy = nullptr;
     sbo::DevBuf kbox;            // per k-tile bounding boxes (float4)
     sbo::DevBuf alpha;           // K^-1 (y - m0), length cap
     sbo::DevBuf aug;             // packed sf2 * L^-1 tiles
