@@ -227,7 +227,9 @@ def test_append_one_point_ticks(dev):
 
 
 def test_append_one_point_c4(dev):
-    """The same trigger at the headline size: C4 fit, three one-point appends,
+    """The same trigger at the headline size: C4 fit and refit (as in the
+    bench's append1 regime: the refit's inverse at five digits,
+    SBO_OPT_INV_OZ_ADAPT, which the appends extend), three one-point appends,
     a full 10^6-point tick after each; the last against the oracle."""
     n, gw, gh = CONFIGS["C4"]
     wl = synthetic(n, gw, gh, seed=0, name="C4")
@@ -239,6 +241,8 @@ def test_append_one_point_c4(dev):
     Xd, Yd, Od = t(X), t(Y), t(OBS)
     gm = TerrainMapper(0, wl.hyper)
     gm.fit(Xd[:n], Yd[:n], Od[:n])
+    gm.fit(Xd[:n], Yd[:n], Od[:n])
+    assert gm.inverse_check()["digits"] == 5
     qx, qy = t(wl.qx), t(wl.qy)
     m = qx.numel()
     outs = full_outputs(m, dev)
