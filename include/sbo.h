@@ -487,8 +487,8 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
 /* SBO_OPT_INV_OZ_ADAPT (default 1; 0 off): the sliced inverse's digits per
  * fit from the guard's last reading (SBO_OPT_INV_CHECK must be on).  Its
  * measure grows ~256x per digit dropped (200-1000x measured), so a fit at d
- * digits with err e lets the next fit -- same hyper-parameters, N within
- * [0.8, 1.25] of it -- take five digits when e 256^(d - 5) <= tol / 1000
+ * digits with err e lets the next fit -- same hyper-parameters, N and
+ * training bounding-box area within [0.8, 1.25] of its -- take five digits when e 256^(d - 5) <= tol / 1000
  * (never four: the guard watches the variance, and at four digits the mean
  * moved 2.9e-6 at C4 while the guard read 1.2e-8).  That fit is checked as
  * any other: if the data moved and it fires (dgemm products), the data keeps

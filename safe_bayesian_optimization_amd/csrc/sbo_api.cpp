@@ -146,20 +146,26 @@ int inv_digits(const sbo_ctx *ctx) { return ctx->inv_oz_cur > 0 ? ctx->inv_oz_cu
 // the mean moves more (four digits at C4: mean 2.9e-6 against the guard's
 // 1.2e-8; five: the mean at six digits' 7.5e-8), so the next fit takes five
 // digits only when the prediction for five is within a thousandth of the
-// guard's bound, never four, and only for the same hyper-parameters and N
-// within [0.8, 1.25] of the measured fit's; the guard checks that fit as
+// guard's bound, never four, and only for the same hyper-parameters, N and
+// training-box area within [0.8, 1.25] of the measured fit's; the guard checks that fit as
 // any other (if the data moved and it fires: dgemm products, and six digits
 // from then on for this data).  C4: 5.6e-13 at six digits -> five (1.1e-10);
 // the lpsc box: 3.8e-9 -> stays at six.
 constexpr int kInvOzAdaptMin = 5;
 constexpr double kInvOzMargin = 1000.0;
 // the fit's data is "the same" as the last guarded fit's: the same
-// hyper-parameters, N within [0.8, 1.25] of it
+// hyper-parameters, N and the training bounding box's area within [0.8,
+// 1.25] of its (so the same density of points per length scale -- what sets
+// cond(K) beside the noise; the bench's C4 data and the lpsc box differ 130x)
+double bbox_area(const sbo_ctx *ctx) {
+    return (double)(ctx->bbox[1] - ctx->bbox[0]) * (double)(ctx->bbox[3] - ctx->bbox[2]);
+}
 bool inv_same_data(const sbo_ctx *ctx) {
     const sbo_hyper &a = ctx->hyper, &b = ctx->inv_oz_hist_hyper;
+    const double ar = bbox_area(ctx), ah = ctx->inv_oz_hist_area;
     return ctx->inv_oz_hist_n > 0 && a.length_scale == b.length_scale && a.sigma_f == b.sigma_f &&
            a.noise_level == b.noise_level && 5 * ctx->n >= 4 * ctx->inv_oz_hist_n &&
-           4 * ctx->n <= 5 * ctx->inv_oz_hist_n;
+           4 * ctx->n <= 5 * ctx->inv_oz_hist_n && ah > 0.0 && 5.0 * ar >= 4.0 * ah && 4.0 * ar <= 5.0 * ah;
 }
 int choose_inv_digits(const sbo_ctx *ctx) {
     if (!ctx->inv_oz_adapt || ctx->inv_check == 0 || ctx->inv_oz == 0 || ctx->inv_oz_next <= 0 ||
@@ -171,6 +177,7 @@ int choose_inv_digits(const sbo_ctx *ctx) {
 void record_inv_digits(sbo_ctx *ctx, const sbo_inv_check &r) {
     if (!inv_same_data(ctx)) ctx->inv_oz_pinned = false;
     ctx->inv_oz_hist_n = ctx->n;
+    ctx->inv_oz_hist_area = bbox_area(ctx);
     ctx->inv_oz_hist_hyper = ctx->hyper;
     ctx->inv_oz_next = 0;
     if (!ctx->inv_oz_adapt || !r.ran || r.digits <= 0) return;

@@ -119,12 +119,13 @@ struct sbo_ctx {
     bool inv_oz_off = false;     // (set while a fit redoes its inverse with dgemm products: the guard fired)
     // SBO_OPT_INV_OZ_ADAPT: the digits of the current fit's sliced products
     // (inv_digits), those the last guard reading allows for the next fit of
-    // the same hyper-parameters and about the same N (0: inv_oz), that
+    // the same hyper-parameters, about the same N and box area (0: inv_oz), that
     // reading's N and hyper-parameters, and whether a reduced fit of this data
     // fired (then it keeps inv_oz digits)
     int inv_oz_adapt = 1;
     int inv_oz_cur = 0, inv_oz_next = 0;
     int64_t inv_oz_hist_n = 0;
+    double inv_oz_hist_area = 0.0;   // (the training bounding box's area: N / area the density)
     sbo_hyper inv_oz_hist_hyper{};
     bool inv_oz_pinned = false;
     // the inverse's accuracy guard (SBO_OPT_INV_CHECK, inv_check.hip): its

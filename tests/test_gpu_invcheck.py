@@ -181,10 +181,12 @@ def test_inverse_digits_adapt(mapper):
     them a thousandth of the bound (C4-like synthetic data: 5.6e-13 at six),
     and its posterior -- the precise sweep, so that the inverse's own effect
     shows -- stays within 2e-7 of the six-digit fit's and meets the contract;
-    the lpsc box (3.8e-9 at six) stays at six.  A reduced fit that fires (the
-    box's data under the synthetic data's reading) falls back to dgemm
-    products, and that data keeps six digits from then on; a changed
-    hyper-parameter or N, or an option change, start again at six."""
+    the lpsc box (3.8e-9 at six) stays at six, and after the synthetic data
+    its different box area (density) makes it new data.  A reduced fit that
+    fires (clustered data with the synthetic data's N, box and hyper-
+    parameters) falls back to dgemm products, and that data keeps six digits
+    from then on; a changed hyper-parameter, N or box, or an option change,
+    start again at six."""
     n = 16384
     syn = synthetic(n, 32, 16, seed=3)
     box = synthetic_box(n, 32, 16, seed=3)
@@ -206,13 +208,32 @@ def test_inverse_digits_adapt(mapper):
         assert dmu < 2e-7 and dvar < 2e-7
         omu, ovar = oracle64(gm, syn)
         assert nrel(got[2][1], omu) < REL_TOL and nrel(got[2][2], ovar) < REL_TOL
-        # the box's data under the synthetic data's reading: five digits fire
+        # the lpsc box: the same N and hyper-parameters but 1/130 of the area
+        # (another density): not the same data, six digits
         gm.fit(box.x, box.y, box.obs)
+        assert gm.inverse_check()["digits"] == 6
+        gm.fit(syn.x, syn.y, syn.obs)
+        assert gm.inverse_check()["digits"] == 6
+        gm.fit(syn.x, syn.y, syn.obs)
+        assert gm.inverse_check()["digits"] == 5
+        # data the same-data test cannot tell apart -- the synthetic box with
+        # 15000 of its points replaced by the lpsc box's, moved into its middle
+        # (the extreme points kept: the same N, box and hyper-parameters) --
+        # under the synthetic data's reading: five digits fire
+        cl_x, cl_y, cl_o = f32(syn.x).copy(), f32(syn.y).copy(), f32(syn.obs).copy()
+        ext = {int(np.argmin(cl_x)), int(np.argmax(cl_x)), int(np.argmin(cl_y)), int(np.argmax(cl_y))}
+        idx = np.array([i for i in range(n) if i not in ext][:15000])
+        cx = 0.5 * (cl_x.min() + cl_x.max()) - 0.5
+        cy = 0.5 * (cl_y.min() + cl_y.max()) - 1.25
+        cl_x[idx] = f32(box.x)[:15000] + cx
+        cl_y[idx] = f32(box.y)[:15000] + cy
+        cl_o[idx] = f32(box.obs)[:15000]
+        gm.fit(cl_x, cl_y, cl_o)
         c = gm.inverse_check()
-        print(f"box at five: err {c['err']:.1e} fired {c['fired']} fallback {c['err_fallback']:.1e}")
+        print(f"clustered data at five: err {c['err']:.1e} fired {c['fired']} fallback {c['err_fallback']:.1e}")
         assert c["digits"] == 5 and c["fired"] == 1 and 0.0 <= c["err_fallback"] <= CHECK_TOL
-        for wl in (box, box, syn):   # pinned at six for this data
-            gm.fit(wl.x, wl.y, wl.obs)
+        for x, y, o in ((cl_x, cl_y, cl_o), (cl_x, cl_y, cl_o), (syn.x, syn.y, syn.obs)):   # pinned at six
+            gm.fit(x, y, o)
             c = gm.inverse_check()
             assert c["digits"] == 6 and c["fired"] == 0
         # new data (another N): six, then five again; an option change: six
