@@ -168,6 +168,13 @@ bool inv_same_data(const sbo_ctx *ctx) {
            4 * ctx->n <= 5 * ctx->inv_oz_hist_n && ah > 0.0 && 5.0 * ar >= 4.0 * ah && 4.0 * ar <= 5.0 * ah;
 }
 int choose_inv_digits(const sbo_ctx *ctx) {
+#ifdef SBO_DIAG
+    // (diagnostic build: SBO_INV_OZ_FORCE = d takes d digits for every fit
+    // the pinning allows -- the pinning's test, test_diagnostic_only_variants)
+    if (const char *e = getenv("SBO_INV_OZ_FORCE");
+        e && ctx->inv_oz_adapt && ctx->inv_check != 0 && ctx->inv_oz != 0 && !(ctx->inv_oz_pinned && inv_same_data(ctx)))
+        return std::clamp(atoi(e), 4, ctx->inv_oz);
+#endif
     if (!ctx->inv_oz_adapt || ctx->inv_check == 0 || ctx->inv_oz == 0 || ctx->inv_oz_next <= 0 ||
         !inv_same_data(ctx))
         return ctx->inv_oz;

@@ -1647,7 +1647,10 @@ def test_diagnostic_only_variants(mapper):
     only: the product rejects SBO_OPT_PRECISE_KERNEL 5 and
     SBO_OPT_CHOL_GEMM 3; in lib/libsbo_diag.so (a child process, SBO_LIB)
     kernel 5 is bitwise kernel 3 on the lpsc box and the split-bf16 Cholesky
-    updates keep the backward-error bound at N = 4100."""
+    updates keep the backward-error bound at N = 4100; and with the inverse
+    forced to five digits (SBO_INV_OZ_FORCE, diagnostic only) the lpsc box's
+    fit fires the guard and its data is pinned to six digits
+    (SBO_OPT_INV_OZ_ADAPT)."""
     import os
     import subprocess
     import sys
@@ -1686,9 +1689,25 @@ K = O.rbf_fill_f32in(np.float32(w2.x)[o], np.float32(w2.y)[o])
 L64 = L.astype(np.float64)
 be = np.linalg.norm(L64 @ L64.T - K) / np.linalg.norm(K)
 assert be <= 10 * 4100 * 2.0 ** -24, be
-print("DIAG VARIANTS OK", be)
+# SBO_INV_OZ_FORCE=5 (this child's environment): the box fires at five digits,
+# and its data is pinned to six from then on; other data (another box area)
+# takes five again
+from safe_bayesian_optimization_amd.terrain import Hyper
+bx = synthetic_box(16384, 32, 16, seed=16384)
+g3 = TerrainMapper(0, Hyper())
+ds = []
+for _ in range(3):
+    g3.fit(bx.x, bx.y, bx.obs)
+    c = g3.inverse_check()
+    ds.append((c["digits"], c["fired"]))
+assert ds == [(5, 1), (6, 0), (6, 0)], ds
+sy = synthetic(16384, 32, 16, seed=3)
+g3.fit(sy.x, sy.y, sy.obs)
+c = g3.inverse_check()
+assert (c["digits"], c["fired"]) == (5, 0), c
+print("DIAG VARIANTS OK", be, ds)
 """ % root
-    env = dict(os.environ, SBO_LIB=diag)
+    env = dict(os.environ, SBO_LIB=diag, SBO_INV_OZ_FORCE="5")
     r = subprocess.run([sys.executable, "-c", child], capture_output=True, text=True, timeout=600, env=env)
     print(r.stdout[-1000:])
     assert r.returncode == 0 and "DIAG VARIANTS OK" in r.stdout, r.stderr[-2000:]
