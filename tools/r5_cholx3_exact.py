@@ -3,6 +3,7 @@ as rocBLAS's (0)?  Both fits' posteriors (default options: whichever sweep
 the probe picks) against the exact one -- the fp64 oracle over an f64
 Cholesky of K in f64 (numpy), alpha in f64 -- on a sample of the grid, with
 each factor's backward error ||L L^T - K|| / ||K||.  GPU diagnostic:
+CHOL_GEMMS / OUTERS: the SBO_OPT_CHOL_GEMM / SBO_OPT_CHOL_OUTER values.
     python tools/r5_cholx3_exact.py [n] [sample]"""
 import os
 import sys
@@ -36,9 +37,11 @@ def main():
         sel = np.sort(rng.choice(wl.qx.size, ns, replace=False))
         qx, qy = f32(wl.qx[sel]), f32(wl.qy[sel])
         exact = None
-        for g in [int(v) for v in os.environ.get("CHOL_GEMMS", "0 3").split()]:
+        for g, ou in [(int(v), int(u)) for v in os.environ.get("CHOL_GEMMS", "0 3").split()
+                      for u in os.environ.get("OUTERS", "512").split()]:
             gm = TerrainMapper(0, h)
             gm.set_option(N.SBO_OPT_CHOL_GEMM, g)
+            gm.set_option(N.SBO_OPT_CHOL_OUTER, ou)
             gm.fit(wl.x, wl.y, wl.obs)
             o = gm.order()
             L, _ = gm.factor()
@@ -58,7 +61,7 @@ def main():
                 del Le
             emu = nrel(mu[sel], exact[0])
             evar = nrel(sd[sel].astype(np.float64) ** 2, exact[1])
-            print(f"{name} N={n} chol_gemm={g}: backward error {be:.2e}; vs the exact posterior: mu {emu:.2e} "
+            print(f"{name} N={n} chol_gemm={g} outer={ou}: backward error {be:.2e}; vs the exact posterior: mu {emu:.2e} "
                   f"var {evar:.2e} (precise sweep {precise})", flush=True)
 
 
