@@ -130,7 +130,7 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
     rocSOLVER spotrf (0): all within the backward-error bound, factors equal
     to f32 rounding, the same posterior to the contract.  The own
     factorization in one level (SBO_OPT_CHOL_OUTER = 128) and in two (256,
-    512, 1024; 1024 the default since round 5), with its own matrix-core updates for every update
+    512, 1024; 512 the default), with its own matrix-core updates for every update
     (SBO_OPT_CHOL_GEMM 2), for the small trailing ones (1) or none (0), and
     with the outer panels' updates as the int8-sliced GEMM with 4 / 5 digits
     (4, the default since round 5 / 5) at four outer panel widths, too."""
@@ -152,7 +152,7 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
         assert be <= 10 * n * EPS32, (ch, be)
         res[ch] = (L64, gm.predict(wl.qx, wl.qy))
     gm.set_option(N.SBO_OPT_CHOLESKY, 1)
-    gm.set_option(N.SBO_OPT_CHOL_OUTER, 1024)
+    gm.set_option(N.SBO_OPT_CHOL_OUTER, 512)
     gm.set_option(N.SBO_OPT_CHOL_GEMM, 0)
     for ch in (1, 2, (1, 128), (1, 256), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 4), (1, 512, 5), (1, 128, 4),
                (1, 256, 4), (1, 1024, 4)):   # own panel solve (default), rocBLAS strsm panels, one / two levels, against spotrf
