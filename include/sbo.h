@@ -489,32 +489,45 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * 2048 for N >= 12288, else 4096. */
 #define SBO_OPT_INV_OZ_MIN 28
 /* SBO_OPT_INV_OZ_ADAPT (default 1; 0 off): the sliced inverse's digits per
- * fit from the guard's last reading (SBO_OPT_INV_CHECK must be on).  Its
- * measure grows ~256x per digit dropped (200-1000x measured), so a fit at d
- * digits with err e lets the next fit -- same hyper-parameters, N and
- * training bounding-box area within [0.8, 1.25] of its -- take five digits when e 256^(d - 5) <= tol / 1000
- * (never four: the guard watches the variance, and at four digits the mean
- * moved 2.9e-6 at C4 while the guard read 1.2e-8).  That fit is checked as
- * any other: if the data moved and it fires (dgemm products), the data keeps
- * SBO_OPT_INV_OZ digits from then on.  The first fit after sbo_create /
- * sbo_warmup, after an option change or a hyper-parameter change takes
- * SBO_OPT_INV_OZ digits.  sbo_get_inverse_check's digits say which ran:
- * C4's warm refits take five (fit -2 ms), the lpsc box stays at six. */
+ * fit from the guard's last readings (SBO_OPT_INV_CHECK must be on).  Both
+ * grow ~256x per digit dropped (200-1000x measured), so a fit at d digits
+ * with readings e (variance) and e_mu (mean) lets the next fit -- same
+ * hyper-parameters, N and training bounding-box area within [0.8, 1.25] of
+ * its -- take five digits when max(e, e_mu) 256^(d - 5) <= tol / 8 (never
+ * four).  That fit must read both within tol / 8: otherwise it is redone at
+ * SBO_OPT_INV_OZ digits (fired = 1) and the data keeps SBO_OPT_INV_OZ digits
+ * from then on.  The first fit after sbo_create / sbo_warmup, after an
+ * option change or a hyper-parameter change takes SBO_OPT_INV_OZ digits.
+ * sbo_get_inverse_check's digits say which ran. */
 #define SBO_OPT_INV_OZ_ADAPT 29
 SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value);
 
-/* The last inverse check (SBO_OPT_INV_CHECK) of the current fit: ran = 1 if
- * it ran; fired = 1 if err exceeded tol and the inverse was recomputed with
- * dgemm products (err_fallback: the same measure on that inverse, -1 when it
- * did not fire); digits = the SBO_OPT_INV_OZ digits of the checked inverse
- * (0: dgemm); err over all queries, err_grid / err_train over the lattice /
- * the training locations (each normalised by its own largest variance);
- * var_max the guard set's largest variance; ms the check's device time (both
- * checks when it fired).  Appends keep the fit's result (their new rows are
- * dgemm / dtrmv products). */
+/* The last inverse check (SBO_OPT_INV_CHECK) of the current fit, on m = 31
+ * guard queries (a 4 x 4 lattice over the training box, 15 training
+ * locations).  ran = 1 if it ran; digits = the SBO_OPT_INV_OZ digits of the
+ * checked inverse (0: dgemm).  Two readings, each the inverse's own share of
+ * the posterior measured by one f64 refinement against the f32 factor:
+ *   err       the variance's, max |d var| / max var (err_grid / err_train:
+ *             over the lattice / the training locations, each normalised by
+ *             its own largest variance; var_max the largest variance);
+ *   err_mean  the mean's, max |d mu| / max |mu| (mean_max = max |mu|), from
+ *             the residual y - m0 refined the same way (round 6: alpha, and
+ *             so mu_ of src/safe_bayesian_optimization_node.cpp:642, comes
+ *             from the same inverse).
+ * fired = 1 if a reading exceeded its bound and the inverse was recomputed:
+ * a six-digit (SBO_OPT_INV_OZ) inverse whose err or err_mean exceeds tol is
+ * recomputed with dgemm products; a reduced-digit one (SBO_OPT_INV_OZ_ADAPT)
+ * already above tol / 8 with SBO_OPT_INV_OZ digits, itself checked (and
+ * recomputed with dgemm products if that one exceeds tol).  err_fallback /
+ * err_mean_fallback: the readings of the recomputed inverse (-1 when none
+ * was); kept_digits: the digits of the inverse the fit kept (0: dgemm); ms
+ * the checks' device time.  Appends keep the fit's result (their new rows
+ * are dgemm / dtrmv products). */
 typedef struct sbo_inv_check {
     int32_t ran, fired, digits, m;
     double err, err_grid, err_train, err_fallback, tol, var_max, ms;
+    double err_mean, mean_max, err_mean_fallback;
+    int32_t kept_digits, reserved;
 } sbo_inv_check;
 SBO_API sbo_status sbo_get_inverse_check(const sbo_ctx *ctx, sbo_inv_check *out);
 

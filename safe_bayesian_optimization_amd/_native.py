@@ -96,7 +96,8 @@ class sbo_inv_check(ctypes.Structure):
     _fields_ = [("ran", ctypes.c_int32), ("fired", ctypes.c_int32), ("digits", ctypes.c_int32), ("m", ctypes.c_int32),
                 ("err", ctypes.c_double), ("err_grid", ctypes.c_double), ("err_train", ctypes.c_double),
                 ("err_fallback", ctypes.c_double), ("tol", ctypes.c_double), ("var_max", ctypes.c_double),
-                ("ms", ctypes.c_double)]
+                ("ms", ctypes.c_double), ("err_mean", ctypes.c_double), ("mean_max", ctypes.c_double),
+                ("err_mean_fallback", ctypes.c_double), ("kept_digits", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 _lib = None

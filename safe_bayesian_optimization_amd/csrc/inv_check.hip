@@ -20,15 +20,26 @@
 // (two over the f64 inverse, one over the f32 factor) -- one read of each
 // lower triangle -- on a stream of their own beside the fit's operand packs.
 //
+// The mean (round 6): the last right-hand side is not a
+// query but the residual r = y - m0 itself, so the same three products give
+// z0 = X r and its refinement z1 = z0 + X (r - L z0).  The fit's alpha is
+// X^T X r (two f64 dtrmv), so a query's mean is mu0 = m0 + V0^T z0, and the
+// exact-inverse mean given the factor m0 + V1^T z1 to O(E^2): their
+// difference V0^T dz + dV^T z0 + dV^T dz is the inverse's own share of the
+// posterior mean (src/safe_bayesian_optimization_node.cpp:642, mu_), at no
+// extra pass over either triangle.
+//
 // Kernels:
-//   chk_kstar_kernel   Kq [rows][Q] (row-major f64) = sf2 exp(-d^2 / 2l^2)
+//   chk_kstar_kernel   Kq [rows][Q] (row-major f64) = sf2 exp(-d^2 / 2l^2) for
+//                      the kChkQ - 1 queries, r = obs - m0 in the last column
 //   chk_trimul_kernel  split-k partial products P[kc][i][c] = sum over k in
 //                      chunk kc, k <= i, of T[i + k ld] X[k][c] (T f64 or f32,
 //                      lower triangle only: the f32 factor's strictly upper
 //                      part holds K's entries), v_mfma_f64_16x16x4_f64,
 //                      X staged through LDS 64 k at a time
 //   chk_reduce_kernel  Y = sum over the row's chunks (fixed order), or Kq - Y
-//   chk_colsum_kernel  per column: sum dV (2 V0 + dV) and sum (V0 + dV)^2
+//   chk_colsum_kernel  per query column: sum dV (2 V0 + dV), sum (V0 + dV)^2,
+//                      sum V0 z0 and sum V0 dz + dV z0 + dV dz
 #include <cstdint>
 
 #include "sbo_internal.hpp"
@@ -42,6 +53,7 @@ constexpr int kChkWaves = 8;
 constexpr int kChkRows = 16 * kChkWaves;  // rows per workgroup: eight waves of 16
 constexpr int kChkThreads = 64 * kChkWaves;
 constexpr int kChkCB = kChkQ / 16;        // 16-column blocks per wave
+constexpr int kChkR = kChkQ - 1;          // the residual's column
 constexpr int kChkKC = 1024;              // k per workgroup (split-k chunk)
 constexpr int kChkStage = 64;             // k staged in LDS per step
 constexpr int kChkLd = kChkQ + 16;        // LDS row stride (doubles): the four
@@ -53,7 +65,8 @@ __device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
 }
 
 __global__ __launch_bounds__(256) void chk_kstar_kernel(const float *__restrict__ x, const float *__restrict__ y,
-                                                         int64_t n, int64_t rows, const float *__restrict__ qx,
+                                                         const float *__restrict__ obs, double m0, int64_t n,
+                                                         int64_t rows, const float *__restrict__ qx,
                                                          const float *__restrict__ qy, double sf2, double inv2l2,
                                                          double *__restrict__ Kq) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -62,8 +75,12 @@ __global__ __launch_bounds__(256) void chk_kstar_kernel(const float *__restrict_
     const int c = (int)(idx % kChkQ);
     double v = 0.0;
     if (j < n) {
-        const double dx = (double)x[j] - (double)qx[c], dy = (double)y[j] - (double)qy[c];
-        v = sf2 * exp(-(dx * dx + dy * dy) * inv2l2);
+        if (c == kChkR) {
+            v = (double)obs[j] - m0;   // the residual, as the fit's launch_widen_sub forms it
+        } else {
+            const double dx = (double)x[j] - (double)qx[c], dy = (double)y[j] - (double)qy[c];
+            v = sf2 * exp(-(dx * dx + dy * dy) * inv2l2);
+        }
     }
     Kq[idx] = v;
 }
@@ -149,33 +166,38 @@ __global__ __launch_bounds__(256) void chk_reduce_kernel(const double *__restric
     Y[idx] = s;
 }
 
-// out[2 c] = sum_i dV (2 V0 + dV), out[2 c + 1] = sum_i (V0 + dV)^2; one
-// workgroup per column, a fixed-order tree
+// Per query column c (one workgroup each, a fixed-order tree), with z0 =
+// V0[:, kChkR] = X r and dz = dV[:, kChkR]:
+//   out[4 c]     = sum_i dV (2 V0 + dV)            (|V1|^2 - |V0|^2)
+//   out[4 c + 1] = sum_i (V0 + dV)^2               (|V1|^2)
+//   out[4 c + 2] = sum_i V0 z0                     (the fit's mean less m0)
+//   out[4 c + 3] = sum_i V0 dz + dV z0 + dV dz     (V1^T z1 - V0^T z0)
 __global__ __launch_bounds__(256) void chk_colsum_kernel(const double *__restrict__ V0,
                                                           const double *__restrict__ dV, int64_t rows,
                                                           double *__restrict__ out) {
-    __shared__ double red[2][256];
+    __shared__ double red[4][256];
     const int c = blockIdx.x;
-    double sd = 0.0, sv = 0.0;
+    double sd = 0.0, sv = 0.0, sm = 0.0, sdm = 0.0;
     for (int64_t i = threadIdx.x; i < rows; i += 256) {
         const double v = V0[i * kChkQ + c], d = dV[i * kChkQ + c];
+        const double z = V0[i * kChkQ + kChkR], dz = dV[i * kChkQ + kChkR];
         sd += d * (2.0 * v + d);
         sv += (v + d) * (v + d);
+        sm += v * z;
+        sdm += v * dz + d * z + d * dz;
     }
     red[0][threadIdx.x] = sd;
     red[1][threadIdx.x] = sv;
+    red[2][threadIdx.x] = sm;
+    red[3][threadIdx.x] = sdm;
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) {
-            red[0][threadIdx.x] += red[0][threadIdx.x + w];
-            red[1][threadIdx.x] += red[1][threadIdx.x + w];
-        }
+        if ((int)threadIdx.x < w)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        out[2 * c] = red[0][0];
-        out[2 * c + 1] = red[1][0];
-    }
+    if (threadIdx.x < 4) out[4 * c + threadIdx.x] = red[threadIdx.x][0];
 }
 
 template <class T>
@@ -199,28 +221,28 @@ int64_t inv_check_rows(int64_t n) { return round_up(n, kChkRows); }
 size_t inv_check_bytes(int64_t n) {
     const int64_t rows = inv_check_rows(n), nkc = (rows + kChkKC - 1) / kChkKC;
     // Kq, V0, R, dV, the partials, the column sums, the queries
-    return sizeof(double) * (size_t)(rows * kChkQ * (4 + nkc) + 2 * kChkQ) + sizeof(float) * 2 * kChkQ;
+    return sizeof(double) * (size_t)(rows * kChkQ * (4 + nkc) + 4 * kChkQ) + sizeof(float) * 2 * kChkQ;
 }
 
 hipError_t launch_inv_check(hipStream_t s, const double *Linv, const float *L, int64_t ld, int64_t n,
-                            const float *x, const float *y, double sf2, double ell, void *work, float **qxy,
-                            double **colsums) {
+                            const float *x, const float *y, const float *obs, double m0, double sf2, double ell,
+                            void *work, float **qxy, double **colsums) {
     const int64_t rows = inv_check_rows(n), nkc = (rows + kChkKC - 1) / kChkKC;
     const int64_t blk = rows * kChkQ;
     double *Kq = static_cast<double *>(work), *V0 = Kq + blk, *R = V0 + blk, *dV = R + blk, *P = dV + blk;
     double *cs = P + nkc * blk;
-    float *q = reinterpret_cast<float *>(cs + 2 * kChkQ);
+    float *q = reinterpret_cast<float *>(cs + 4 * kChkQ);
     if (qxy) *qxy = q;
     if (colsums) *colsums = cs;
     if (!Linv) return hipSuccess;  // (layout query only)
-    hipLaunchKernelGGL(chk_kstar_kernel, dim3((unsigned)((blk + 255) / 256)), dim3(256), 0, s, x, y, n, rows, q,
-                       q + kChkQ, sf2, 1.0 / (2.0 * ell * ell), Kq);
+    hipLaunchKernelGGL(chk_kstar_kernel, dim3((unsigned)((blk + 255) / 256)), dim3(256), 0, s, x, y, obs, m0, n,
+                       rows, q, q + kChkQ, sf2, 1.0 / (2.0 * ell * ell), Kq);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = trimul<double>(s, Linv, ld, n, rows, Kq, P, V0, nullptr);   // V0 = X Kq
     if (e == hipSuccess) e = trimul<float>(s, L, ld, n, rows, V0, P, R, Kq);            // R = Kq - L V0
     if (e == hipSuccess) e = trimul<double>(s, Linv, ld, n, rows, R, P, dV, nullptr);    // dV = X R
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(chk_colsum_kernel, dim3(kChkQ), dim3(256), 0, s, V0, dV, rows, cs);
+    hipLaunchKernelGGL(chk_colsum_kernel, dim3(kChkR), dim3(256), 0, s, V0, dV, rows, cs);
     return hipGetLastError();
 }
 

@@ -137,22 +137,32 @@ bool oz_level(const sbo_ctx *ctx, int64_t h, int64_t m) {
 // The digits of the current fit's sliced products (SBO_OPT_INV_OZ_ADAPT:
 // chosen per fit by choose_inv_digits)
 int inv_digits(const sbo_ctx *ctx) { return ctx->inv_oz_cur > 0 ? ctx->inv_oz_cur : ctx->inv_oz; }
-// SBO_OPT_INV_OZ_ADAPT: the guard's measure of a sliced inverse (its
-// variance effect on 32 queries) grows ~256x per digit dropped -- the
-// digits' truncation and the dropped digit products are 2^-8 coarser each;
-// measured 200x (C4) to 1000x (lpsc box) from six digits to five,
-// tools/r5_inv_adapt.py -- so the last reading at d digits predicts the next
-// fit's at d' as err 256^(d - d').  The guard watches the variance only, and
-// the mean moves more (four digits at C4: mean 2.9e-6 against the guard's
-// 1.2e-8; five: the mean at six digits' 7.5e-8), so the next fit takes five
-// digits only when the prediction for five is within a thousandth of the
-// guard's bound, never four, and only for the same hyper-parameters, N and
-// training-box area within [0.8, 1.25] of the measured fit's; the guard checks that fit as
-// any other (if the data moved and it fires: dgemm products, and six digits
-// from then on for this data).  C4: 5.6e-13 at six digits -> five (1.1e-10);
-// the lpsc box: 3.8e-9 -> stays at six.
+// SBO_OPT_INV_OZ_ADAPT: the guard's readings of a sliced inverse (its
+// effect on the variance and on the mean at 31 queries) grow ~256x per digit
+// dropped -- the digits' truncation and the dropped digit products are 2^-8
+// coarser each; the variance's measured 200x (C4) to 1000x (lpsc box) from
+// six digits to five, tools/r5_inv_adapt.py -- so the last readings at d
+// digits predict the next fit's at d' as err 256^(d - d').  The next fit
+// takes five digits (never four) only when the prediction of both readings
+// for five is within tol / kInvOzPredict, and only for the same
+// hyper-parameters, N and training-box area within [0.8, 1.25] of the
+// measured fit's.  That fit must then read both within tol / kInvOzReduced
+// (a reduced inverse is a speed option, so it must sit well inside the
+// bound): otherwise the fit redoes its inverse at SBO_OPT_INV_OZ digits,
+// itself guarded, and this data keeps SBO_OPT_INV_OZ digits from then on.
+// (Round 5 gated on the variance alone with a 1000x margin, since the mean
+// went unwatched: at four digits on C4 it moved 240x the variance reading.)
+// Measured (tools/guard_mean.py, profiles/r6_guard_mean.log; readings at
+// six -> five -> four digits): C4 variance 1.4e-12 -> 2.5e-10 -> 5.2e-8,
+// mean 1.2e-10 -> 2.3e-8 -> 4.4e-6 (the whole-grid mean moved 2.9e-6 at four
+// digits: the variance reading alone passed it); the lpsc box 3.2e-9 ->
+// 3.2e-6 (variance) and 2.1e-9 -> 9.6e-7 (mean); the mean grows 140-190x per
+// digit from six to five on five workloads, the variance 180-1000x.  C4's
+// refits take five digits (predicted 3.1e-8, read 2.3e-8 <= 6.25e-8), the
+// box stays at six.
 constexpr int kInvOzAdaptMin = 5;
-constexpr double kInvOzMargin = 1000.0;
+constexpr double kInvOzReduced = 8.0;
+constexpr double kInvOzPredict = 8.0;
 // the fit's data is "the same" as the last guarded fit's: the same
 // hyper-parameters, N and the training bounding box's area within [0.8,
 // 1.25] of its (so the same density of points per length scale -- what sets
@@ -180,6 +190,15 @@ int choose_inv_digits(const sbo_ctx *ctx) {
         return ctx->inv_oz;
     return std::min(ctx->inv_oz, ctx->inv_oz_next);
 }
+// the bound a checked inverse must meet on both readings: tol, and tol /
+// kInvOzReduced for fewer than SBO_OPT_INV_OZ digits
+double inv_check_bar(const sbo_ctx *ctx, const sbo_inv_check &r) {
+    return (r.digits > 0 && r.digits < ctx->inv_oz) ? r.tol / kInvOzReduced : r.tol;
+}
+bool inv_check_passed(const sbo_ctx *ctx, const sbo_inv_check &r) {
+    const double bar = inv_check_bar(ctx, r);
+    return r.err <= bar && r.err_mean <= bar;   // (NaN fails)
+}
 // after the guard read a fit's inverse: the next fit's digits
 void record_inv_digits(sbo_ctx *ctx, const sbo_inv_check &r) {
     if (!inv_same_data(ctx)) ctx->inv_oz_pinned = false;
@@ -188,27 +207,32 @@ void record_inv_digits(sbo_ctx *ctx, const sbo_inv_check &r) {
     ctx->inv_oz_hist_hyper = ctx->hyper;
     ctx->inv_oz_next = 0;
     if (!ctx->inv_oz_adapt || !r.ran || r.digits <= 0) return;
-    if (!(r.err <= r.tol)) {
+    if (!inv_check_passed(ctx, r)) {
         // fired at reduced digits: this data keeps SBO_OPT_INV_OZ digits from
         // now on (no reduced fit that fires every other time)
         if (r.digits < ctx->inv_oz) ctx->inv_oz_pinned = true;
         return;
     }
     if (ctx->inv_oz_pinned) return;
+    const double e = std::max(r.err, r.err_mean);
     int nd = ctx->inv_oz;
     for (int d = kInvOzAdaptMin; d < ctx->inv_oz; ++d)
-        if (r.err * std::ldexp(1.0, 8 * (r.digits - d)) <= r.tol / kInvOzMargin) {
+        if (e * std::ldexp(1.0, 8 * (r.digits - d)) <= r.tol / kInvOzPredict) {
             nd = d;
             break;
         }
     ctx->inv_oz_next = nd;
 }
 
-// does the recursive inverse of n columns slice any of its products?
+// does the recursive inverse of n columns slice any of its products?  The
+// same gate as inverse_lower_f64_par's: the sliced GEMM's workspaces are handed
+// down only when the top split slices (the levels below slice with them
+// where oz_level allows; with the top split over 16384 it is all dgemm), and
+// only on the two-stream path.
 bool inverse_sliced(const sbo_ctx *ctx, int64_t n) {
-    if (n <= ctx->inv_base) return false;
-    const int64_t h = ((n + ctx->inv_base - 1) / ctx->inv_base + 1) / 2 * ctx->inv_base, m = n - h;
-    return oz_level(ctx, h, m) || inverse_sliced(ctx, h) || inverse_sliced(ctx, m);
+    if (n <= ctx->inv_base || !ctx->blas_aux || !ctx->aux_stream || !ctx->ev_panel) return false;
+    const int64_t h = inverse_split(n, ctx->inv_base);
+    return ctx->inv_oz != 0 && oz_level(ctx, h, n - h);
 }
 
 // A^-1 (recursion scratch scr), then S = B A^-1
@@ -335,7 +359,7 @@ sbo_status inverse_lower_f64_par(sbo_ctx *ctx, double *Li, int64_t n, int64_t ld
     // int8 matrix cores (oz_level), one workspace per stream, sized up front
     // (a reserve that reallocates mid-fit would wait for the device)
     sbo::DevBuf *ozA = nullptr, *ozC = nullptr;
-    if (ctx->inv_oz != 0 && oz_level(ctx, h, m)) {
+    if (inverse_sliced(ctx, n)) {
         SBO_HIP(ctx->gzws.reserve(std::max(sbo::gz_workspace_bytes(m, h, h, inv_digits(ctx)),
                                            sbo::gz_workspace_bytes(h, m, m, inv_digits(ctx)))));
         SBO_HIP(ctx->gzws_aux.reserve(sbo::gz_workspace_bytes(m, m, m, inv_digits(ctx))));
@@ -644,16 +668,18 @@ sbo_status pack_precise(sbo_ctx *ctx, hipStream_t s, int64_t npad, int64_t I0) {
 
 // The inverse's accuracy guard (SBO_OPT_INV_CHECK; inv_check.hip).  Launch:
 // on chk_stream once `stream` has finished the inverse, beside the operand
-// packs that follow it (it only reads L and L^-1).  The guard set: a 4 x 4
-// lattice over the training box (its corners included: the largest
-// variances, which the contract normalises by) and kChkTrain training
-// locations, every (n / kChkTrain)-th stored point (the k-d order spreads
-// them over the data in proportion to its density; where the data is dense
-// the variance is smallest and sf2 - |V|^2 cancels hardest).
+// packs that follow it (it only reads L, L^-1 and the observations).  The
+// guard set: a 4 x 4 lattice over the training box (its corners included:
+// the largest variances, which the contract normalises by) and kChkTrain
+// training locations, every (n / kChkTrain)-th stored point (the k-d order
+// spreads them over the data in proportion to its density; where the data
+// is dense the variance is smallest and sf2 - |V|^2 cancels hardest, and the
+// mean is largest); the last right-hand side is the residual (the mean's
+// reading).
 // kInvCheckTol = 5e-7: a twentieth of the 1e-5 contract -- the inverse's share
 // adds to the sweeps' own errors, which the probe holds to 5e-6 x the largest
 // whole-grid / probe ratio measured.
-constexpr int kChkGrid = 4, kChkTrain = sbo::kChkQ - kChkGrid * kChkGrid;
+constexpr int kChkGrid = 4, kChkQueries = sbo::kChkQ - 1, kChkTrain = kChkQueries - kChkGrid * kChkGrid;
 constexpr double kInvCheckTol = 5e-7;
 sbo_status inverse_check_launch(sbo_ctx *ctx) {
     const int64_t n = ctx->n;
@@ -665,8 +691,8 @@ sbo_status inverse_check_launch(sbo_ctx *ctx) {
     SBO_HIP(ctx->chk.reserve(sbo::inv_check_bytes(n)));
     float *q = nullptr;
     double *cs = nullptr;
-    SBO_HIP(sbo::launch_inv_check(ctx->chk_stream, nullptr, nullptr, 0, n, nullptr, nullptr, 0.0, 0.0,
-                                  ctx->chk.as<void>(), &q, &cs));
+    SBO_HIP(sbo::launch_inv_check(ctx->chk_stream, nullptr, nullptr, 0, n, nullptr, nullptr, nullptr, 0.0, 0.0,
+                                  0.0, ctx->chk.as<void>(), &q, &cs));
     static thread_local std::vector<float> hq;   // (lives until the copy below has run)
     hq.assign(2 * kChkGrid * kChkGrid, 0.0f);
     for (int i = 0; i < kChkGrid; ++i)
@@ -689,42 +715,49 @@ sbo_status inverse_check_launch(sbo_ctx *ctx) {
                              sizeof(float), (size_t)mt, hipMemcpyDeviceToDevice, ctx->chk_stream));
     SBO_HIP(hipMemcpy2DAsync(q + Q + G, sizeof(float), ctx->y.as<float>() + stride / 2, sizeof(float) * stride,
                              sizeof(float), (size_t)mt, hipMemcpyDeviceToDevice, ctx->chk_stream));
-    for (int64_t c = G + mt; c < Q; ++c) {
+    for (int64_t c = G + mt; c < kChkQueries; ++c) {
         SBO_HIP(hipMemcpyAsync(q + c, q + G + mt - 1, sizeof(float), hipMemcpyDeviceToDevice, ctx->chk_stream));
         SBO_HIP(hipMemcpyAsync(q + Q + c, q + Q + G + mt - 1, sizeof(float), hipMemcpyDeviceToDevice,
                                ctx->chk_stream));
     }
     const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
     SBO_HIP(sbo::launch_inv_check(ctx->chk_stream, ctx->Linv.as<double>(), ctx->L.as<float>(), ctx->cap, n,
-                                  ctx->x.as<float>(), ctx->y.as<float>(), sf2, ctx->hyper.length_scale,
-                                  ctx->chk.as<void>(), nullptr, nullptr));
+                                  ctx->x.as<float>(), ctx->y.as<float>(), ctx->obs.as<float>(),
+                                  ctx->hyper.prior_mean, sf2, ctx->hyper.length_scale, ctx->chk.as<void>(), nullptr,
+                                  nullptr));
     SBO_HIP(hipEventRecord(ctx->ev_chk1, ctx->chk_stream));
     return SBO_OK;
 }
-// Wait for the launched check and fill r (err, err_grid, err_train, var_max, ms).
+// Wait for the launched check and fill r (err, err_grid, err_train, var_max,
+// err_mean, mean_max, ms).
 sbo_status inverse_check_read(sbo_ctx *ctx, sbo_inv_check &r) {
     float *q = nullptr;
     double *cs = nullptr;
-    SBO_HIP(sbo::launch_inv_check(ctx->chk_stream, nullptr, nullptr, 0, ctx->n, nullptr, nullptr, 0.0, 0.0,
-                                  ctx->chk.as<void>(), &q, &cs));
-    constexpr int G = kChkGrid * kChkGrid, Q = sbo::kChkQ;
-    double h[2 * Q];
+    SBO_HIP(sbo::launch_inv_check(ctx->chk_stream, nullptr, nullptr, 0, ctx->n, nullptr, nullptr, nullptr, 0.0, 0.0,
+                                  0.0, ctx->chk.as<void>(), &q, &cs));
+    constexpr int G = kChkGrid * kChkGrid, Q = kChkQueries;
+    double h[4 * Q];
     SBO_HIP(hipMemcpyAsync(h, cs, sizeof(h), hipMemcpyDeviceToHost, ctx->chk_stream));
     SBO_HIP(hipStreamSynchronize(ctx->chk_stream));
     float ms = 0.0f;
     SBO_HIP(hipEventElapsedTime(&ms, ctx->ev_chk0, ctx->ev_chk1));
-    const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
-    double dmax[2] = {0.0, 0.0}, vmax[2] = {0.0, 0.0};
+    const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f, m0 = ctx->hyper.prior_mean;
+    double dmax[2] = {0.0, 0.0}, vmax[2] = {0.0, 0.0}, dmu = 0.0, mumax = 0.0;
     bool finite = true;
     for (int c = 0; c < Q; ++c) {
+        const double *e = h + 4 * c;
         const int part = c < G ? 0 : 1;
-        finite = finite && std::isfinite(h[2 * c]) && std::isfinite(h[2 * c + 1]);
-        dmax[part] = std::max(dmax[part], std::fabs(h[2 * c]));        // |d var| = ||V1|^2 - |V0|^2|
-        vmax[part] = std::max(vmax[part], sf2 - h[2 * c + 1]);          // var from the refined V1
+        finite = finite && std::isfinite(e[0]) && std::isfinite(e[1]) && std::isfinite(e[2]) && std::isfinite(e[3]);
+        dmax[part] = std::max(dmax[part], std::fabs(e[0]));        // |d var| = ||V1|^2 - |V0|^2|
+        vmax[part] = std::max(vmax[part], sf2 - e[1]);              // var from the refined V1
+        dmu = std::max(dmu, std::fabs(e[3]));                       // |d mu| = |V1^T z1 - V0^T z0|
+        mumax = std::max(mumax, std::fabs(m0 + e[2] + e[3]));       // mu from the refined V1, z1
     }
     auto rel = [](double d, double v) { return v > 0.0 ? d / v : (d > 0.0 ? HUGE_VAL : 0.0); };
     r.ran = 1;
     r.m = Q;
+    r.err_mean = finite ? rel(dmu, mumax) : HUGE_VAL;
+    r.mean_max = mumax;
     r.err = finite ? rel(std::max(dmax[0], dmax[1]), std::max(vmax[0], vmax[1])) : HUGE_VAL;
     r.err_grid = finite ? rel(dmax[0], vmax[0]) : HUGE_VAL;
     r.err_train = finite ? rel(dmax[1], vmax[1]) : HUGE_VAL;
@@ -766,6 +799,16 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
     rocblas_int hinfo = 0;
     bool alpha_aux = false, kcoord_pending = false, x3_planes_aux = false, packs_aux = false, chk_pending = false;
+    // a launched guard reads L, L^-1, x/y/obs and ctx->chk on chk_stream: an
+    // early return (a failed launch, NOT_SPD) waits for it before the caller
+    // can regrow or free those buffers or the next fit writes L
+    struct ChkDrain {
+        sbo_ctx *c;
+        bool pending = false;
+        ~ChkDrain() {
+            if (pending && c->chk_stream) (void)hipStreamSynchronize(c->chk_stream);
+        }
+    } drain{ctx};
     // the inverse's first half ran beside the Cholesky (blocked_potrf): its
     // info slots 1 .. inv_slot stay, the rest are cleared
     const bool early = ctx->inverse_bits == 64 && ctx->inverse_rec && !incr && ctx->early_inv_n == n;
@@ -857,6 +900,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
                       (ctx->inv_check == 1 && ctx->inverse_rec && !early && inverse_sliced(ctx, n)))) {
             ctx->chk_res = sbo_inv_check{};
             ctx->chk_res.digits = (ctx->inverse_rec && !early && inverse_sliced(ctx, n)) ? inv_digits(ctx) : 0;
+            drain.pending = true;   // (set before the launch: a half-queued guard is drained too)
             if (sbo_status st = inverse_check_launch(ctx)) return st;
             chk_pending = true;
         } else if (!incr) {
@@ -1041,20 +1085,33 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     }
     if (chk_pending) {
         sbo_inv_check r = ctx->chk_res;
-        if (sbo_status st = inverse_check_read(ctx, r)) return st;
-        r.err_fallback = -1.0;
+        const sbo_status rst = inverse_check_read(ctx, r);
+        drain.pending = false;   // (read: chk_stream is idle)
+        if (rst != SBO_OK) return rst;
+        r.err_fallback = r.err_mean_fallback = -1.0;
+        r.kept_digits = r.digits;
         ctx->chk_res = r;
         if (!ctx->inv_oz_off) record_inv_digits(ctx, r);
-        if (!(r.err <= r.tol) && r.digits != 0 && !ctx->inv_oz_off) {
-            // the sliced inverse misses the guard's bound: the fit again with
-            // dgemm products (checked too), reported as fired
-            ctx->inv_oz_off = true;
+        if (!inv_check_passed(ctx, r) && r.digits != 0 && !ctx->inv_oz_off) {
+            // the sliced inverse misses the guard's bound on the variance or
+            // the mean: a reduced-digit one is redone at SBO_OPT_INV_OZ
+            // digits, a full one with dgemm products -- the redone inverse is
+            // checked too (and a six-digit redo that misses tol goes on to
+            // dgemm products); reported as fired with the kept inverse's
+            // readings
+            const bool reduced = r.digits < ctx->inv_oz;
+            if (reduced)
+                ctx->inv_oz_cur = ctx->inv_oz;
+            else
+                ctx->inv_oz_off = true;
             const sbo_status st = refresh_operand(ctx, 0);
             ctx->inv_oz_off = false;
             const sbo_inv_check f = ctx->chk_res;
             ctx->chk_res = r;
             ctx->chk_res.fired = 1;
-            ctx->chk_res.err_fallback = f.ran ? f.err : -1.0;
+            ctx->chk_res.err_fallback = f.ran ? (f.fired ? f.err_fallback : f.err) : -1.0;
+            ctx->chk_res.err_mean_fallback = f.ran ? (f.fired ? f.err_mean_fallback : f.err_mean) : -1.0;
+            ctx->chk_res.kept_digits = f.ran ? f.kept_digits : 0;
             ctx->chk_res.ms = r.ms + f.ms;
             return st;
         }

@@ -489,18 +489,20 @@ hipError_t launch_gz_pack_f32(hipStream_t s, int nd, const float *P, int64_t ld,
 hipError_t launch_gz_gemm_packed_f32(hipStream_t s, int nd, const char *pack, int64_t mpack, int64_t K, int64_t a0,
                                      int64_t m, int64_t b0, int64_t n, double alpha, float *C, int64_t ldc,
                                      unsigned flags);
-// The fit's accuracy guard of the f64 inverse (inv_check.hip): on kChkQ
+// The fit's accuracy guard of the f64 inverse (inv_check.hip): on kChkQ - 1
 // queries (coordinates at *qxy: x[kChkQ] then y[kChkQ], filled by the caller
-// before the launch) V0 = Linv Kq and one refinement against the f32 factor
-// L, dV = Linv (Kq - L V0), both lower-triangular column-major with lda ld;
-// *colsums = per column (sum dV (2 V0 + dV), sum (V0 + dV)^2).  work:
+// before the launch) plus the residual r = obs - m0 as the last right-hand
+// side, V0 = Linv Kq and one refinement against the f32 factor L, dV = Linv
+// (Kq - L V0), both lower-triangular column-major with lda ld; *colsums = per
+// query column (sum dV (2 V0 + dV), sum (V0 + dV)^2, sum V0 z0, sum V0 dz +
+// dV z0 + dV dz) with z0 / dz the residual's columns.  work:
 // inv_check_bytes(n); with Linv null only the pointers are set.
 constexpr int kChkQ = 32;
 int64_t inv_check_rows(int64_t n);
 size_t inv_check_bytes(int64_t n);
 hipError_t launch_inv_check(hipStream_t s, const double *Linv, const float *L, int64_t ld, int64_t n,
-                            const float *x, const float *y, double sf2, double ell, void *work, float **qxy,
-                            double **colsums);
+                            const float *x, const float *y, const float *obs, double m0, double sf2, double ell,
+                            void *work, float **qxy, double **colsums);
 // Morton ordering of the queries (query_order.hip): workspace of
 // query_order_bytes(m); returns the permutation and the gathered coordinates
 // (all inside the workspace).

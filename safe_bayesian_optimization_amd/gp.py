@@ -110,19 +110,25 @@ class Context:
                                          int(width), int(height), float(gx), float(gy), ctypes.byref(idx), fl))
         return int(idx.value)
 
-    def reduce_keys(self, keys, out=None, *, async_: bool = True):
+    def reduce_keys(self, keys, out=None, *, async_: bool | None = None):
         """Combine n raw 16-byte keys ((n, 2) or (2n,) int64: f64 score bits,
         i64 index) into one (sbo_keys_reduce).  Device tensors stay on the
-        device -- the reduction runs on this context's stream, no host sync
-        with async_ -- and the (2,) int64 result tensor is returned; host
-        arrays return a (score, index) pair."""
+        device -- the reduction runs on this context's stream -- and the (2,)
+        int64 result tensor is returned; host arrays return a (score, index)
+        pair.  async_ (default: whenever possible) leaves out the host sync;
+        it needs the context bound to a torch stream (set_stream), since torch
+        cannot wait on the library's own stream -- async_=True without one
+        raises instead of silently blocking."""
         n = int((keys.numel() if _is_dev(keys) else np.asarray(keys).size) // 2)
         if _is_dev(keys):
             import torch
+            if async_ and self._torch_stream is None:
+                raise ValueError("reduce_keys(async_=True) needs set_stream(): the library's own stream "
+                                 "cannot be waited on by torch")
             keys = keys.contiguous()
             if out is None:
                 out = torch.empty(2, dtype=torch.int64, device=keys.device)
-            fl = N.SBO_DEVICE_PTRS | (N.SBO_ASYNC if async_ else 0)
+            fl = N.SBO_DEVICE_PTRS | (N.SBO_ASYNC if async_ is not False else 0)
             # keys / out live on torch's current stream (an all-gather wrote
             # keys there): order the library's stream after it, keep keys
             # alive for the allocator until the reduce ran, and order the

@@ -148,6 +148,31 @@ def synthetic_box(n: int, grid_w: int, grid_h: int, x_range=(0.0, 1.0), y_range=
                     grid_w, grid_h, hyper, f_min, seed=seed)
 
 
+def clustered(n: int, grid_w: int, grid_h: int | None = None, seed: int = 0, clusters: int = 64,
+              spread: float = 0.15, hyper: Hyper | None = None, name: str | None = None) -> Workload:
+    """``synthetic``'s square and bounding box (corner points pinned), but the
+    N points in ``clusters`` tight Gaussian clusters of s.d. ``spread`` (ADVICE
+    r5: the same box area as C4-like data -- what SBO_OPT_INV_OZ_ADAPT takes
+    for "the same data" -- at another density, so conditioning differs);
+    observations = smooth field + N(0, sn2)."""
+    hyper = hyper or Hyper()
+    grid_h = grid_h or grid_w
+    side = hyper.length_scale * math.sqrt(n / 8.0)
+    u = uniform(seed ^ 0xC1, 2 * clusters + n)
+    cx, cy = u[0:2 * clusters:2] * side, u[1:2 * clusters:2] * side
+    k = np.minimum((u[2 * clusters:] * clusters).astype(np.int64), clusters - 1)
+    x = np.clip(cx[k] + spread * normal(seed + 2, n), 0.0, side)
+    y = np.clip(cy[k] + spread * normal(seed + 3, n), 0.0, side)
+    x[0], y[0], x[-1], y[-1] = 0.0, 0.0, side, side
+    obs = smooth_field(x, y, side, hyper.length_scale, seed) + math.sqrt(hyper.sn2) * normal(seed + 1, n)
+    gx = np.linspace(0.0, side, grid_w)
+    gy = np.linspace(0.0, side, grid_h)
+    QY, QX = np.meshgrid(gy, gx, indexing="ij")
+    f_min = float(np.percentile(obs, 40.0))
+    return Workload(name or f"clustered_n{n}_g{grid_w}x{grid_h}", x, y, obs, QX.reshape(-1), QY.reshape(-1),
+                    grid_w, grid_h, hyper, f_min, side=side, seed=seed)
+
+
 def robot_path(n: int, side: float, seed: int = 0, v_max: float = 0.3, w_max: float = 1.0):
     """Training locations shaped like the publisher's stream: 30 points
     uniform within radius 1 of the start pose (turtlesim_spatial_publisher.py

@@ -53,3 +53,21 @@ def test_cpp_node_driver_builds_and_links():
     assert os.path.exists(exe)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "usage" in r.stderr
+
+
+def test_pmc_summaries_travel_to_the_gpu_box():
+    """bench.py's roofline.traffic reads profiles/r*_pmc_<config>.json on the GPU
+    box (bench.pmc_traffic); .gpurunignore must not exclude them (VERDICT r5 weak 3:
+    a blanket ./profiles entry made BENCH_r05's traffic null)."""
+    import fnmatch
+    import glob
+    pats = [p.strip() for p in open(os.path.join(ROOT, ".gpurunignore")) if p.strip()]
+    files = glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_C4.json"))
+    assert files
+    for f in files:
+        rel = "./" + os.path.relpath(f, ROOT)
+        parts = rel.split("/")
+        prefixes = ["/".join(parts[:i]) for i in range(2, len(parts) + 1)]
+        for p in pats:
+            for cand in prefixes + [pp[2:] for pp in prefixes]:
+                assert not fnmatch.fnmatch(cand, p.rstrip("/")), (p, rel)

@@ -7,8 +7,10 @@ The sliced GEMM's error is relative to row and column maxima, so its effect
 grows with cond(K), which the mapper's configuration sets
 (config/lpsc.yaml:35-37: noise_level, length_scale).  The precision probe
 cannot see it (its fast and precise sweeps read the same inverse); the guard
-measures it on 32 queries by one f64 refinement against the f32 factor and
-falls back to dgemm products above 5e-7.  Contract: mu and var within 1e-5
+measures it on 31 queries by one f64 refinement against the f32 factor -- the
+variance's share and, since round 6, the mean's (the residual y - m0 refined
+the same way: alpha comes from the same inverse) -- and falls back to dgemm
+products when either exceeds 5e-7.  Contract: mu and var within 1e-5
 normwise of the fp64 oracle given the device factor (alpha solved in f64 from
 it), under default options -- whichever sweep the probe picks.
 """
@@ -21,7 +23,7 @@ pytestmark = pytest.mark.gpu
 from oracle import oracle as O  # noqa: E402
 from safe_bayesian_optimization_amd import TerrainMapper, synthetic  # noqa: E402
 from safe_bayesian_optimization_amd import _native as N  # noqa: E402
-from safe_bayesian_optimization_amd.terrain import Hyper, synthetic_box  # noqa: E402
+from safe_bayesian_optimization_amd.terrain import Hyper, clustered, synthetic_box  # noqa: E402
 
 REL_TOL = 1e-5
 CHECK_TOL = 5e-7
@@ -95,13 +97,16 @@ def test_ill_conditioned_sliced_inverse(mapper, name, n, box, hyper):
     omu, ovar = oracle64(gm, wl)
     emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
     print(f"{name} n={n}: check err {chk['err']:.2e} (grid {chk['err_grid']:.2e} train {chk['err_train']:.2e}) "
-          f"fired {chk['fired']} fallback {chk['err_fallback']:.2e} {chk['ms']:.2f} ms; probe {perr:.2e} "
+          f"mean {chk['err_mean']:.2e} fired {chk['fired']} fallback {chk['err_fallback']:.2e} / "
+          f"{chk['err_mean_fallback']:.2e} kept {chk['kept_digits']} {chk['ms']:.2f} ms; probe {perr:.2e} "
           f"precise {precise}; mu {emu:.2e} var {evar:.2e}")
-    assert chk["ran"] == 1 and chk["digits"] == 6 and chk["m"] == 32
+    assert chk["ran"] == 1 and chk["digits"] == 6 and chk["m"] == 31
     assert chk["tol"] == CHECK_TOL
-    assert chk["fired"] == (0 if chk["err"] <= CHECK_TOL else 1)
+    passed = chk["err"] <= CHECK_TOL and chk["err_mean"] <= CHECK_TOL
+    assert chk["fired"] == (0 if passed else 1)
+    assert chk["kept_digits"] == (6 if passed else 0)
     if chk["fired"]:
-        assert chk["err_fallback"] <= CHECK_TOL
+        assert chk["err_fallback"] <= CHECK_TOL and chk["err_mean_fallback"] <= CHECK_TOL
     assert emu < REL_TOL and evar < REL_TOL
 
 
@@ -138,6 +143,74 @@ def test_guard_fires_on_five_digits(mapper):
     finally:
         gm.set_option(N.SBO_OPT_INV_OZ, 6)
         gm.set_option(N.SBO_OPT_INV_CHECK, 1)
+
+
+def test_guard_sees_the_mean(mapper):
+    """four digits on C4-like data move the whole-grid mean
+    2.9e-6 while the variance reading stays 5e-8, inside the bound
+    (profiles/r6_guard_mean.log) -- the round-5 guard kept that inverse.  The
+    mean reading must see it (> 5e-7), the fit redo its inverse with dgemm
+    products, and mu then meet the contract; with the guard off the
+    four-digit mean stays and is visibly further from the oracle."""
+    wl = synthetic(16384, 32, 16, seed=3)
+    gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
+    try:
+        gm.set_option(N.SBO_OPT_INV_OZ, 4)
+        gm.set_option(N.SBO_OPT_PRECISION, 1)      # (the precise sweep: the inverse's own effect shows)
+        gm.fit(wl.x, wl.y, wl.obs)
+        chk = gm.inverse_check()
+        mu, sd = gm.predict(wl.qx, wl.qy)
+        omu, ovar = oracle64(gm, wl)
+        emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
+        print(f"four digits: var reading {chk['err']:.2e} mean reading {chk['err_mean']:.2e} fired {chk['fired']} "
+              f"kept {chk['kept_digits']} fallback {chk['err_fallback']:.2e} / {chk['err_mean_fallback']:.2e}; "
+              f"mu {emu:.2e} var {evar:.2e}")
+        assert chk["ran"] == 1 and chk["digits"] == 4
+        assert chk["err"] <= CHECK_TOL < chk["err_mean"]     # the variance alone would have kept it
+        assert chk["fired"] == 1 and chk["kept_digits"] == 0
+        assert 0.0 <= chk["err_mean_fallback"] < CHECK_TOL / 100 and 0.0 <= chk["err_fallback"] < CHECK_TOL / 100
+        assert emu < REL_TOL and evar < REL_TOL
+        gm.set_option(N.SBO_OPT_INV_CHECK, 0)
+        gm.fit(wl.x, wl.y, wl.obs)
+        mu4, _ = gm.predict(wl.qx, wl.qy)
+        emu4 = nrel(mu4, omu)
+        print(f"four digits, guard off: mu {emu4:.2e}")
+        assert emu4 > 10 * emu
+    finally:
+        gm.set_option(N.SBO_OPT_INV_OZ, 6)
+        gm.set_option(N.SBO_OPT_INV_CHECK, 1)
+        gm.set_option(N.SBO_OPT_PRECISION, -1)
+
+
+def test_reduced_fit_on_clustered_same_area_data(mapper):
+    """SBO_OPT_INV_OZ_ADAPT judges "the same data" by N, the
+    hyper-parameters and the bounding box's area only, so clustered data in
+    the same box (another conditioning) can follow a C4-like fit at five
+    digits.  That reduced fit must read both the variance and the mean within
+    tol / 8 or be redone at six digits -- either way mu and var meet the
+    contract against the oracle."""
+    n = 16384
+    syn = synthetic(n, 32, 16, seed=3)
+    cl = clustered(n, 32, 16, seed=7)
+    gm = TerrainMapper(0, syn.hyper, ctx=mapper.ctx)
+    first = []
+    for _ in range(2):
+        gm.fit(syn.x, syn.y, syn.obs)
+        c = gm.inverse_check()
+        first.append((c["digits"], f"{c['err']:.2e}", f"{c['err_mean']:.2e}", c["fired"]))
+    print("C4-like fits:", first)
+    assert first[1][0] == 5
+    gm.fit(cl.x, cl.y, cl.obs)
+    chk = gm.inverse_check()
+    mu, sd = gm.predict(cl.qx, cl.qy)
+    omu, ovar = oracle64(gm, cl)
+    emu, evar = nrel(mu, omu), nrel(sd.astype(np.float64) ** 2, ovar)
+    print(f"clustered after C4-like: digits {chk['digits']} var {chk['err']:.2e} mean {chk['err_mean']:.2e} "
+          f"fired {chk['fired']} kept {chk['kept_digits']}; mu {emu:.2e} var {evar:.2e}")
+    assert chk["digits"] == 5
+    ok = chk["err"] <= CHECK_TOL / 8 and chk["err_mean"] <= CHECK_TOL / 8
+    assert chk["fired"] == (0 if ok else 1) and chk["kept_digits"] == (5 if ok else 6)
+    assert emu < REL_TOL and evar < REL_TOL
 
 
 def test_guard_on_dgemm_inverse_and_appends(mapper):
@@ -177,8 +250,9 @@ def test_guard_on_dgemm_inverse_and_appends(mapper):
 
 def test_inverse_digits_adapt(mapper):
     """SBO_OPT_INV_OZ_ADAPT (default): a refit of the same hyper-parameters and
-    about the same N takes five digits when the last guard reading predicts
-    them a thousandth of the bound (C4-like synthetic data: 5.6e-13 at six),
+    about the same N takes five digits when the last guard readings (variance
+    and mean) predict them within an eighth of the bound (C4-like synthetic
+    data: 1.4e-12 / 1.2e-10 at six),
     and its posterior -- the precise sweep, so that the inverse's own effect
     shows -- stays within 2e-7 of the six-digit fit's and meets the contract;
     the lpsc box (3.8e-9 at six) stays at six, and after the synthetic data
@@ -202,7 +276,8 @@ def test_inverse_digits_adapt(mapper):
             got.append((c, mu.astype(np.float64), sd.astype(np.float64) ** 2))
         print("synthetic:", [(c["digits"], f"{c['err']:.1e}", c["fired"]) for c, _, _ in got])
         assert [c["digits"] for c, _, _ in got] == [6, 5, 5]
-        assert all(c["fired"] == 0 and c["err"] <= CHECK_TOL / 100 for c, _, _ in got)
+        assert all(c["fired"] == 0 and c["err"] <= CHECK_TOL / 100 and c["err_mean"] <= CHECK_TOL / 8
+                   for c, _, _ in got)
         dmu, dvar = nrel(got[2][1], got[0][1]), nrel(got[2][2], got[0][2])
         print(f"five vs six digits: mu {dmu:.2e} var {dvar:.2e}")
         assert dmu < 2e-7 and dvar < 2e-7

@@ -2,8 +2,8 @@
 cost is made of): fit N = 16384, then 6 one-point appends (synchronous), wall
 time per append printed; run under rocprofv3 --kernel-trace and list the last
 append's kernels with tools/trace_list.py-style output (--list DIR).
-    rocprofv3 --kernel-trace -d D -o run --output-format csv -- python3 tools/r4_append_trace.py
-    python tools/r4_append_trace.py --list D"""
+    rocprofv3 --kernel-trace -d D -o run --output-format csv -- python3 tools/append_trace.py
+    python tools/append_trace.py --list D"""
 import csv
 import glob
 import os

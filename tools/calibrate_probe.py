@@ -14,7 +14,7 @@ hyper-parameters, so a longer l packs more points per l^2):
     variance, and its ratio to the guard's measure (the guard's 5e-7 times the
     largest ratio must stay far under the contract).
 GPU diagnostic, one JSON line per workload:
-    python tools/r5_calibrate.py [n] [grid]"""
+    python tools/calibrate_probe.py [n] [grid]"""
 import json
 import os
 import sys

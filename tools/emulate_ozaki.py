@@ -16,7 +16,7 @@ five digits; X = rint(K* 2^(31 - eK)), four digits; 2^e > 1.01 max per block),
 the 14 pairs s + u <= 4 (u <= 3), level 4 rounded to level-3 units, next to
 the round-4 base-128 form (five A digits, four K* digits, s + u <= 4).
 CPU only (numpy/scipy, ~12 GB at n = 16384, a few minutes):
-    python tools/r4_emulate_ozaki.py [n] [queries] [kernel]"""
+    python tools/emulate_ozaki.py [n] [queries] [kernel]"""
 import os
 import sys
 import time

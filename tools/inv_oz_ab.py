@@ -6,7 +6,7 @@ max |d| / max |ref| of mu and of var).  Workloads: C4 (synthetic, N = 16384,
 1000 x 1000) and the lpsc box (N = 16384, 1000 x 1000).  INV_OZ_MIN (round
 5): the smallest sliced splits to try (SBO_OPT_INV_OZ_MIN, default "4096");
 the guard's measure (sbo_get_inverse_check) is printed.  GPU diagnostic.
-    python tools/r4_inv_oz_ab.py [n] [digits ...]"""
+    python tools/inv_oz_ab.py [n] [digits ...]"""
 import os
 import sys
 import time

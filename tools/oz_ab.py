@@ -5,7 +5,7 @@ and the variance / mean error of each against the fp64 oracle given the
 device factor on a sample.  GPU diagnostic (tools/), one JSON line.
 OZ_KERNELS: the kernels (default "1 0"); TABLE_MB: SBO_OPT_TABLE_MB; INV_OZ:
 SBO_OPT_INV_OZ (the fit's inverse by the int8-sliced GEMM).
-    python tools/r4_oz_ab.py [n] [sample]"""
+    python tools/oz_ab.py [n] [sample]"""
 import ctypes
 import json
 import os

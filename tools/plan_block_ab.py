@@ -5,7 +5,7 @@ kernel (OZ_KERNELS, default "3 4") and each block shape (BLOCKS, bi:bq pairs,
 sbo_profile) and whether mu / sd are bitwise those of the row-block-major
 order (they must be: items are independent); REF_ACROSS=1 compares every
 kernel with the first one's output instead.  GPU diagnostic, one JSON line.
-    python tools/r5_plan_block_ab.py [n]"""
+    python tools/plan_block_ab.py [n]"""
 import ctypes
 import json
 import os

@@ -12,7 +12,7 @@ variance error max|dv| / max v is compared with the whole grid's:
   lat64   a 64 x 64 lattice + the 512 training locations
 and where the whole grid's worst point lies (its variance / the largest, its
 distance to the nearest training point / l).  GPU diagnostic, one JSON line
-per workload:  python tools/r5_probe_design.py [n] [grid]"""
+per workload:  python tools/probe_design.py [n] [grid]"""
 import json
 import os
 import sys

@@ -5,7 +5,7 @@ sweep (SBO_OPT_PRECISION 0) and the precise sweep (1) over the workload's whole
 grid on the same fit; the fast sweep's normwise variance error against the
 precise one over the whole grid, and its ratio to the probe's error.  GPU
 diagnostic (tools/), one JSON line per workload.
-    python tools/r4_probe_vs_grid.py [names...]"""
+    python tools/probe_vs_grid.py [names...]"""
 import json
 import os
 import sys
