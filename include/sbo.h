@@ -385,15 +385,16 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * stream that leaves this many CUs to the factorization's latency-bound
  * chain.  Results do not depend on it (bitwise). */
 #define SBO_OPT_INV_OVERLAP 14
-/* SBO_OPT_CHOL_OUTER (columns, default 512; a multiple of 128 in [128,
- * 4096]): the blocked Cholesky's outer panel.  Each outer panel is factored
- * by the 128-column chain with its updates kept inside the panel, and the
- * rest of the trailing matrix takes one rank-512 update per outer panel; 128
- * is the one-level factorization (a rank-128 update per 128 columns).  1024
- * measured C4 fit -0.4 ms with the factor's backward error 1.38e-7 ->
- * 1.43e-7 (synthetic) and 8.7e-8 -> 9.5e-8 (lpsc box) at N = 8192, but moved
- * test_tile_skip_exact_and_bounded's skipped-tile mean past its bound: not
- * the default. */
+/* SBO_OPT_CHOL_OUTER (columns, default 1024 since round 6; a multiple of
+ * 128 in [128, 4096]): the blocked Cholesky's outer panel.  Each outer panel
+ * is factored by the 128-column chain with its updates kept inside the
+ * panel, and the rest of the trailing matrix takes one rank-1024 update per
+ * outer panel; 128 is the one-level factorization (a rank-128 update per 128
+ * columns).  1024 against 512: C4 fit -0.4 ms, the factor's backward error
+ * 1.38e-7 -> 1.43e-7 (synthetic) and 8.7e-8 -> 9.5e-8 (lpsc box) at
+ * N = 8192.  (Round 5 kept 512 when test_tile_skip_exact_and_bounded failed
+ * at 1024; that leg compared a refit taking five inverse digits with the
+ * first fit's dense sweep -- inverse drift, not the factor's -- and is fixed.) */
 #define SBO_OPT_CHOL_OUTER 15
 /* SBO_OPT_CHOL_DIAG (default 1): the blocked Cholesky's chain kernels -- the
  * 128 x 128 diagonal blocks (16-column panels) and the panel solves below

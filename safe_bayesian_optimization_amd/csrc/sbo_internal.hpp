@@ -105,7 +105,7 @@ struct sbo_ctx {
     hipEvent_t ev_pack = nullptr;  // the fit's operand packs on aux_stream (refresh_operand)
     int chol_gemm_own = 4;       // SBO_OPT_CHOL_GEMM: 4 (default) / 5 the outer panels' updates int8-sliced, 3 split bf16, 2 every update by chol_update_kernel, 1 the small trailing ones, 0 rocBLAS
     int chol_diag = 1;           // SBO_OPT_CHOL_DIAG: 1 the MFMA chain kernels (diagonal block, panel), 0 the VALU ones (bitwise equal)
-    int chol_outer = 512;        // SBO_OPT_CHOL_OUTER: outer panel width of the two-level Cholesky (128: one level)
+    int chol_outer = 1024;       // SBO_OPT_CHOL_OUTER: outer panel width of the two-level Cholesky (128: one level)
     // the recursive inverse's first half beside the Cholesky's last steps
     // (SBO_OPT_INV_OVERLAP = R > 0: on inv_stream, CU-masked to leave R CUs free)
     hipStream_t inv_stream = nullptr;

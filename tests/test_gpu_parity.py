@@ -130,16 +130,16 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
     rocSOLVER spotrf (0): all within the backward-error bound, factors equal
     to f32 rounding, the same posterior to the contract.  The own
     factorization in one level (SBO_OPT_CHOL_OUTER = 128) and in two (256,
-    512, 1024; 512 the default), with its own matrix-core updates for every update
+    512, 1024; 1024 the default since round 6), with its own matrix-core updates for every update
     (SBO_OPT_CHOL_GEMM 2), for the small trailing ones (1) or none (0), and
     with the outer panels' updates as the int8-sliced GEMM with 4 / 5 digits
     (4, the default since round 5 / 5) at four outer panel widths, too."""
     wl = synthetic(n, 24, 20, seed=n + 3)
     res = {}
-    for ch in (0, 2, (1, 128), (1, 256), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 4), (1, 512, 5), (1, 128, 4),
+    for ch in (0, 2, (1, 128), (1, 256), (1, 512), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 4), (1, 512, 5), (1, 128, 4),
                (1, 256, 4), (1, 1024, 4), 1):
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
-        outer = ch[1] if isinstance(ch, tuple) else 512
+        outer = ch[1] if isinstance(ch, tuple) else 1024
         gm.set_option(N.SBO_OPT_CHOL_OUTER, outer)
         gm.set_option(N.SBO_OPT_CHOL_GEMM, ch[2] if isinstance(ch, tuple) and len(ch) > 2 else 0)
         gm.set_option(N.SBO_OPT_CHOLESKY, ch[0] if isinstance(ch, tuple) else ch)
@@ -155,9 +155,9 @@ def test_blocked_cholesky_matches_spotrf(mapper, n):
     # CHOL_GEMM 0 here left the later tests on rocBLAS updates, not the
     # shipped int8-sliced ones)
     gm.set_option(N.SBO_OPT_CHOLESKY, 1)
-    gm.set_option(N.SBO_OPT_CHOL_OUTER, 512)
+    gm.set_option(N.SBO_OPT_CHOL_OUTER, 1024)
     gm.set_option(N.SBO_OPT_CHOL_GEMM, 4)
-    for ch in (1, 2, (1, 128), (1, 256), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 4), (1, 512, 5), (1, 128, 4),
+    for ch in (1, 2, (1, 128), (1, 256), (1, 512), (1, 1024), (1, 512, 1), (1, 512, 2), (1, 512, 4), (1, 512, 5), (1, 128, 4),
                (1, 256, 4), (1, 1024, 4)):   # own panel solve (default), rocBLAS strsm panels, one / two levels, against spotrf
         assert np.abs(res[0][0] - res[ch][0]).max() <= 1e-4 * np.abs(res[0][0]).max()
         assert nrel(res[ch][1][0], res[0][1][0].astype(np.float64)) < REL_TOL

@@ -18,7 +18,7 @@ def main():
     p.add_argument("--inv", type=int, nargs="+", default=[1], help="SBO_OPT_INVERSE values to time (1 own recursion, 0 rocSOLVER dtrtri)")
     p.add_argument("--reserve", type=int, nargs="+", default=[0], help="SBO_OPT_CHOL_RESERVE values to time")
     p.add_argument("--overlap", type=int, nargs="+", default=[0], help="SBO_OPT_INV_OVERLAP values to time")
-    p.add_argument("--outer", type=int, nargs="+", default=[512], help="SBO_OPT_CHOL_OUTER values to time")
+    p.add_argument("--outer", type=int, nargs="+", default=[1024], help="SBO_OPT_CHOL_OUTER values to time")
     p.add_argument("--gemm", type=int, nargs="+", default=[4], help="SBO_OPT_CHOL_GEMM values to time (4: the library default)")
     p.add_argument("--inv-base", type=int, nargs="+", default=[2048], help="SBO_OPT_INV_BASE values to time")
     p.add_argument("--inv-panels", type=int, nargs="+", default=[16], help="SBO_OPT_INV_PANELS values to time")
