@@ -209,9 +209,17 @@ def run_launch_check(a, world, rank):
     _, gw, gh = CONFIGS["C4"]
     m = gw * gh
     rng = np.random.default_rng(123)
-    # a C4-shaped cost: more tiles in the middle rows than at the edges, noisy
-    rows = np.repeat(np.sin(np.linspace(0.1, np.pi - 0.1, gh)), gw)
-    cost = (0.5 + rows + 0.3 * rng.uniform(size=m)).astype(np.float32)
+    # the C4 tick plan's own per-query costs (tools/dump_c4_cost.py), else a
+    # C4-shaped stand-in: more tiles in the middle rows than at the edges
+    fx = os.path.join(ROOT, "tests", "golden", "c4_query_cost.npz")
+    if os.path.exists(fx):
+        cost = np.load(fx)["cost"].astype(np.float32)
+        cost_src = "tests/golden/c4_query_cost.npz (sbo_query_cost of the C4 fit)"
+    else:
+        rows = np.repeat(np.sin(np.linspace(0.1, np.pi - 0.1, gh)), gw)
+        cost = (0.5 + rows + 0.3 * rng.uniform(size=m)).astype(np.float32)
+        cost_src = "synthetic C4-shaped stand-in"
+    assert cost.size == m
     score = np.round(rng.uniform(0.0, 4.0, m), 2)   # ties across shards
 
     class _Rank0Costs:   # only rank 0's "mapper" knows the costs: the cut must come from the broadcast
@@ -264,7 +272,7 @@ def run_launch_check(a, world, rank):
         print(json.dumps({"metric": METRIC, "value": None, "unit": "grid-points/s", "n_gpus": world,
                           "launch_check": True, "argmax_matches_global": bool(flags[0]), "cuts": cuts,
                           "cost_share_max_over_mean": max(share) / (sum(share) / len(share)),
-                          "subgoal": {"index": sub, "want": sub_want, "cuts": fcuts},
+                          "subgoal": {"index": sub, "want": sub_want, "cuts": fcuts}, "cost_source": cost_src,
                           "config": {"workload": "launch-check (C4-sized costs)", "M": m,
                                      "parallelism": f"m-shard{world}" if world > 1 else "single"}, **info}),
               flush=True)

@@ -229,3 +229,69 @@ def test_gloo_sharded_subgoal_equals_full(world):
     assert want >= 0
     for _, got_cuts, lo_ok, idx in res:
         assert got_cuts == cuts and lo_ok and idx == want
+
+
+# ------------------------------- the real C4 plan's costs
+def _c4_plan_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from safe_bayesian_optimization_amd import _native as N
+    from safe_bayesian_optimization_amd.dist import allreduce_key_dev, key_tensor_to_pairs
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cost = np.load(os.path.join(root, "tests", "golden", "c4_query_cost.npz"))["cost"]
+    m = cost.size
+    # only rank 0's "mapper" has the plan; the others must take its cut
+    gm = _FakeMapper(cost if rank == 0 else np.ones(m, np.float32))
+    qx = torch.zeros(m)
+    a, b = cost_balanced_range(gm, qx, qx, rank, world)
+    # acquisition scores of the C4 grid, ties across the cut
+    rng = np.random.default_rng(2024)
+    score = np.round(rng.uniform(0.0, 3.0, m), 3)
+    i = int(np.argmax(score[a:b]))
+    key = torch.tensor([np.array([score[a + i]]).view(np.int64)[0], a + i], dtype=torch.int64)
+    lib = N.lib()
+
+    def lib_reduce(gathered, out):
+        """The device reduce hook's contract (Context.reduce_keys) with the
+        library's own key combine (sbo_key_combine: CPU-safe), in rank order."""
+        best = N.sbo_key(0.0, -1)
+        for s, ix in key_tensor_to_pairs(gathered):
+            best = lib.sbo_key_combine(best, N.sbo_key(s, ix))
+        return torch.tensor([np.array([best.score]).view(np.int64)[0], best.idx], dtype=torch.int64)
+
+    got = key_tensor_to_pairs(allreduce_key_dev(key, lib_reduce))[0]
+    q.put((rank, (a, b), got, float(cost[a:b].sum())))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_c4_plan_costs():
+    """World 2 on the C4 tick plan's own per-query costs (tests/golden/
+    c4_query_cost.npz, sbo_query_cost of bench.py's C4 fit, dumped by
+    tools/dump_c4_cost.py): rank 0 alone holds the costs, both ranks take its
+    broadcast cut (128-aligned, the two shares within 0.1 % of each other --
+    equal-size halves differ by far more), and the key all-gather through the
+    device-path reduce hook with the library's key combine gives the global
+    argmax of all 10^6 queries."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cost = np.load(os.path.join(root, "tests", "golden", "c4_query_cost.npz"))["cost"]
+    m = cost.size
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_plan_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    (_, s0, k0, c0), (_, s1, k1, c1) = res
+    assert m == 10 ** 6 and s0[0] == 0 and s0[1] == s1[0] and s1[1] == m and s0[1] % 128 == 0
+    assert s0[1] == balanced_cuts(cost, 2)[1]
+    assert max(c0, c1) / ((c0 + c1) / 2) < 1.001
+    half = [float(cost[:m // 2].sum()), float(cost[m // 2:].sum())]
+    assert max(half) / (sum(half) / 2) > 1.05          # equal halves would be off by > 5 %
+    score = np.round(np.random.default_rng(2024).uniform(0.0, 3.0, m), 3)
+    want = int(np.argmax(score))                        # lowest index among ties
+    for s, i in (k0, k1):
+        assert i == want and s == score[want]
