@@ -135,6 +135,76 @@ __global__ __launch_bounds__(256) void row_dot_kernel(const double *__restrict__
     if (threadIdx.x == 0) out[r] = red[0];
 }
 
+// alpha = K^-1 r = X^T (X r) from the fit's f64 inverse X (lower, column-major,
+// lda ld, its strictly upper part zero), r = obs - m0 (round 6; was two
+// rocBLAS dtrmv: 0.93 + 0.48 ms at C4 for two passes over a 1 GiB triangle).
+// Pass 1, z = X r: workgroup (row block of kAlRows rows, k chunk of kAlK
+// columns), each thread two consecutive rows (one 16-B load per k: a wave
+// reads 1 KiB of a column), r's chunk in LDS; the partial sums of chunk kc go
+// to P[kc][row] and alpha_z_reduce_kernel adds them in chunk order.  Pass 2,
+// alpha_k = sum_{i >= k} X[i][k] z_i: one wave per column (a contiguous read
+// of rows k .. n-1), a fixed-order shuffle tree.  Both deterministic.
+constexpr int kAlRows = 512, kAlK = 512;
+__global__ __launch_bounds__(256) void alpha_z_kernel(const double *__restrict__ X, int64_t ld, int64_t n,
+                                                      const float *__restrict__ obs, double m0,
+                                                      double *__restrict__ P) {
+    __shared__ double rs[kAlK];
+    const int64_t r0 = (int64_t)blockIdx.x * kAlRows, k0 = (int64_t)blockIdx.y * kAlK;
+    if (k0 >= r0 + kAlRows || k0 >= n) return;                       // above the diagonal: nothing
+    for (int j = threadIdx.x; j < kAlK; j += 256) rs[j] = k0 + j < n ? (double)obs[k0 + j] - m0 : 0.0;
+    __syncthreads();
+    const int64_t row = r0 + 2 * (int64_t)threadIdx.x;
+    const int64_t kend = min(min(k0 + kAlK, n), row + 2);             // k <= row + 1 (the pair's last row)
+    double s0 = 0.0, s1 = 0.0;
+    if (row < n) {
+        const double *col = X + row;
+        // (X's strictly upper part is zero: X[row][row + 1] adds nothing).  A
+        // 16-B load per k when every (row, k) pair is 16-B aligned (ld even),
+        // else two 8-B loads
+        if (row + 1 < n && (ld & 1) == 0) {
+#pragma unroll 8
+            for (int64_t k = k0; k < kend; ++k) {
+                const double2 v = *reinterpret_cast<const double2 *>(col + k * ld);
+                s0 = fma(v.x, rs[k - k0], s0);
+                s1 = fma(v.y, rs[k - k0], s1);
+            }
+        } else {
+            const bool two = row + 1 < n;
+#pragma unroll 8
+            for (int64_t k = k0; k < kend; ++k) {
+                s0 = fma(col[k * ld], rs[k - k0], s0);
+                if (two) s1 = fma(col[k * ld + 1], rs[k - k0], s1);
+            }
+        }
+    }
+    const int64_t kc = blockIdx.y;
+    if (row < n) P[kc * n + row] = s0;
+    if (row + 1 < n) P[kc * n + row + 1] = s1;
+}
+__global__ __launch_bounds__(256) void alpha_z_reduce_kernel(const double *__restrict__ P, int64_t n,
+                                                             double *__restrict__ z) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t nkc = i / kAlK + 1;                                 // chunks at or left of the diagonal
+    double s = 0.0;
+    for (int64_t kc = 0; kc < nkc; ++kc) s += P[kc * n + i];
+    z[i] = s;
+}
+__global__ __launch_bounds__(256) void alpha_xtz_kernel(const double *__restrict__ X, int64_t ld, int64_t n,
+                                                        const double *__restrict__ z, double *__restrict__ alpha) {
+    const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= n) return;
+    const int lane = threadIdx.x & 63;
+    const double *col = X + k * ld;
+    double s = 0.0;
+    // rows k .. n-1; lane l takes rows i = k + l, k + l + 64, ... (coalesced)
+#pragma unroll 4
+    for (int64_t i = k + lane; i < n; i += 64) s = fma(col[i], z[i], s);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) alpha[k] = s;
+}
+
 // out[i + j * ldo] = (float)d[i + j * ldd] (i < m, j = blockIdx.y)
 __global__ void narrow_2d_kernel(const double *__restrict__ d, int64_t ldd, int64_t m, int64_t n,
                                  float *__restrict__ out, int64_t ldo) {
@@ -1121,7 +1191,7 @@ typedef double f64x4_t __attribute__((ext_vector_type(4)));
 // staged half-tile, held k-major ([k][row], 128 rows + 4 padding) so that
 // the staging writes (one row per lane) and the Gram's reads (four rows x 16
 // columns per MFMA operand) both fall on distinct banks
-constexpr int kTnAtLd = kBM / 2 + 4, kTnGmLd = kBK + 4;
+constexpr int kTnGmLd = kBK + 4;
 __device__ __forceinline__ f64x4_t mfma_f64(double a, double b, f64x4_t c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -1135,19 +1205,74 @@ __device__ __forceinline__ void store_sym(double *g, int bi, int bj, int lane, f
         if (bi != bj) g[(16 * bj + (lane & 15)) * kTnGmLd + 16 * bi + (lane >> 4) + 4 * v] = a[v];
     }
 }
+// Round 6: the Gram matrices from the tile's bf16 pieces on the bf16 matrix
+// cores.  A = A0 + A1 + A2 (+ r, |r| < 2^-24 |A|) exactly as pack_x3_kernel
+// splits it, so G1 = A1^T A1 and G2 = A2^T A2 are products of bf16 values --
+// exact products, f32 accumulation -- and G = A^T A is taken as A0^T A0 + A0^T
+// A1 + A1^T A0 + A0^T A2 + A2^T A0 + G1 (the dropped A1^T A2 + A2^T A1 + A2^T
+// A2 and r's terms are < 2^-22 |A|^T|A|).  One v_mfma_f32_16x16x32_bf16 covers
+// 16 x 16 x 32 where the f64 16x16x4 form needed eight at four times the
+// cycles each.  Rigour: the stored G_c is symmetrised (lower blocks mirrored)
+// and |G_c - G| <= delta |A|^T |A| entrywise with delta = 2^-16 (<= 80 f32
+// roundings of partial sums of |A|^T |A|, 4.8e-6, plus the dropped terms),
+// so ||G_c - G||_2 <= delta |A|_F^2 and, by Weyl, lambda_max(G) <=
+// lambda_max(G_c) + delta |A|_F^2: the spectral bound below adds that term
+// (at most 64 delta = 1e-3 relative, since ||A||_2^2 >= |A|_F^2 / 64).  The
+// squarings stay f64.  Row sums and |A|_F^2 come from the pieces in f64 (A0 +
+// A1 + A2 = A to 2^-24: inside the outputs' 1e-5 log2 margin).  The pieces are
+// those pack_x3_kernel cuts (the same instructions on the unscaled values),
+// each scaled by its own power of two 2^s_p (exact) so that the piece's
+// largest |entry| is in [1, 2): f32 products and sums then stay far above
+// f32's underflow (unscaled, A2^T A2 of a tile of 2^-60 entries underflowed
+// and the bound lost its rigour -- caught by comparing against the f64
+// kernel's bounds).  The cross terms of G go to accumulators of their own
+// and are combined in f64 with the exact scale factors.  What underflow
+// remains is bounded by an absolute term: 2^-110 of each accumulator's own
+// scale in ||G_c - G||_2 (64 x 264 operations below 2^-126 each).
+// The tile is staged a quarter (64 rows) at a time: the quarter's floats are
+// one contiguous 64 x 64 block in k-major order (tile_offset), and the Gram's
+// contraction runs over that storage order (any order of the rows serves).
+constexpr int kTnPq = kBK + 8;                 // bf16 per staged k row: 144 B, conflict-free b128 reads
+constexpr double kTnDelta = 1.0 / 65536.0;     // 2^-16
+typedef float f32x4_t2 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4_t2 mfma_bf16(uint4 a, uint4 b, f32x4_t2 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+// the lower part of a 16 x 16 block (bi >= bj) of plane pi's symmetric 64 x 64
+// Gram matrix, scaled 2^(2 sp[pi]), from the f32 MFMA accumulators (lane l,
+// element v: row 16 bi + 4 (l>>4) + v, column 16 bj + (l&15)), mirrored:
+// G_A = a00 + 2^(s0 - s1) a01 + 2^(s0 - s2) a02 + 2^(2 (s0 - s1)) a1 in f64
+// (exact scalings); returns the largest |entry| written
+__device__ __forceinline__ double store_sym_gram(double *g, int bi, int bj, int lane, int pi, f32x4_t2 a00,
+                                                 f32x4_t2 a01, f32x4_t2 a02, f32x4_t2 a1, f32x4_t2 a2,
+                                                 const int (&sp)[3]) {
+    const double c01 = ldexp(1.0, sp[0] - sp[1]), c02 = ldexp(1.0, sp[0] - sp[2]), c11 = c01 * c01;
+    double mx = 0.0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const int i = 16 * bi + 4 * (lane >> 4) + v, j = 16 * bj + (lane & 15);
+        if (bi != bj || i >= j) {
+            const double x = pi == 0 ? (((double)a00[v] + c01 * (double)a01[v]) + c02 * (double)a02[v]) + c11 * (double)a1[v]
+                                     : (pi == 1 ? (double)a1[v] : (double)a2[v]);
+            g[i * kTnGmLd + j] = x;
+            g[j * kTnGmLd + i] = x;
+            mx = fmax(mx, fabs(x));
+        }
+    }
+    return mx;
+}
 __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
                                                            float4 *__restrict__ lgn) {
-    // 66 KiB of LDS, two workgroups per CU: the tile (or one of its pieces)
-    // staged 128 rows at a time, the Gram matrix and its powers in place (a
-    // product is held in registers until every read of its factor is done)
-    __shared__ float at[kBK * kTnAtLd];        // half the tile, [k][row]  (33 KiB)
+    __shared__ __attribute__((aligned(16))) unsigned short pq[3][kBK * kTnPq];   // a quarter's pieces [k][c] (27 KiB)
     __shared__ double gm[kBK * kTnGmLd];       // G, then its powers (34 KiB)
-    __shared__ double rsum[kBM];               // row 1-norms
+    __shared__ double rpart[3][4][kBK];        // row-sum partials of a quarter (6 KiB)
     __shared__ double red[2][kBM / 64];
+    __shared__ double fred[3][kBM / 64], rwm[3][kBM / 64];   // per wave: |.|_F^2 sums, row-sum maxima
     const int64_t tile = t0 + blockIdx.x;
     const float *t = aug + tile * kTileFloats;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int lrow = tid & (kBM / 2 - 1), kh = tid >> 7;   // staging: row lrow of the half, k in [32 kh, 32 kh + 32)
     float out[6];                                // (rows, spectral) of A; of A1; of A2
     double lg_fro_a = -1000.0;
     // this wave's lower blocks of the 4 x 4 block grid of G: (0,0) (1,0) (1,1) |
@@ -1155,73 +1280,182 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
     const int nb = wave < 2 ? 3 : 2;
     const int tbi[3] = {wave < 2 ? 2 * wave : 3, wave < 2 ? 2 * wave + (wave == 0 ? 1 : 0) : 3, wave == 0 ? 1 : 2};
     const int tbj[3] = {wave < 3 ? 0 : 2, wave == 0 ? 0 : (wave == 1 ? 1 : (wave == 2 ? 1 : 3)), wave == 0 ? 1 : 2};
+    // the Gram accumulators: A (its five cross terms), A1, A2
+    // G_A's terms A0^T A0, A1^T A0 + A0^T A1, A2^T A0 + A0^T A2 (scaled 2^(s0 + s_p)), then G1, G2
+    f32x4_t2 acc00[3], acc01[3], acc02[3], acc1[3], acc2[3];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) acc00[b] = acc01[b] = acc02[b] = acc1[b] = acc2[b] = f32x4_t2{0.f, 0.f, 0.f, 0.f};
+    double rmax[3] = {0.0, 0.0, 0.0}, fro[3] = {0.0, 0.0, 0.0};
+    const int sk = tid >> 2, sc = 16 * (tid & 3);   // staging: k row sk, storage columns sc .. sc + 15
+    const int rc = tid & 63, rk = tid >> 6;         // row sums: column rc, k in [16 rk, 16 rk + 16)
+    // the thread's 16 floats of each quarter (a quarter is one contiguous
+    // 64 x 64 block), all in flight at once; the tile's largest |entry| sets
+    // the scale 2^sc
+    // (the tile is read twice, the second time from L2: a pass for the
+    // pieces' maxima, then the staging)
+    auto load16 = [&](int q, float (&v)[16]) {
+        const float4 *src = reinterpret_cast<const float4 *>(t + q * 64 * kBK + 16 * tid);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 f = src[j];
+            v[4 * j] = f.x;
+            v[4 * j + 1] = f.y;
+            v[4 * j + 2] = f.z;
+            v[4 * j + 3] = f.w;
+        }
+    };
+    __shared__ float pmax[3][kBM / 64];
+    {
+        float amax[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int q = 0; q < kBM / 64; ++q) {
+            float tv[16];
+            load16(q, tv);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float x = tv[j];
+                const float a0 = bf16_rn(x), r1 = x - a0, a1 = bf16_rn(r1), a2 = bf16_rn(r1 - a1);
+                amax[0] = fmaxf(amax[0], fabsf(a0));
+                amax[1] = fmaxf(amax[1], fabsf(a1));
+                amax[2] = fmaxf(amax[2], fabsf(a2));
+            }
+        }
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) amax[pc] = fmaxf(amax[pc], __shfl_xor(amax[pc], o));
+            if (lane == 0) pmax[pc][wave] = amax[pc];
+        }
+    }
+    __syncthreads();
+    int sp[3];           // the pieces' scales: 2^sp max |piece| in [1, 2)
+    float up[3];
+    double dn[3];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+        const float m = fmaxf(fmaxf(pmax[pc][0], pmax[pc][1]), fmaxf(pmax[pc][2], pmax[pc][3]));
+        sp[pc] = m > 0.0f ? -ilogbf(m) : 0;
+        up[pc] = ldexpf(1.0f, sp[pc]);
+        dn[pc] = ldexp(1.0, -sp[pc]);
+    }
+#pragma unroll 1
+    for (int q = 0; q < kBM / 64; ++q) {
+        // stage: split (as pack_x3_kernel does, unscaled), scale each piece by 2^sp (exact), store
+        {
+            float tv[16];
+            load16(q, tv);
+            uint32_t w[3][8];
+#pragma unroll
+            for (int j = 0; j < 16; j += 2) {
+                uint32_t h[3][2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const float x = tv[j + e];
+                    const float a0 = bf16_rn(x), r1 = x - a0, a1 = bf16_rn(r1), a2 = bf16_rn(r1 - a1);
+                    h[0][e] = __float_as_uint(a0 * up[0]) >> 16;
+                    h[1][e] = __float_as_uint(a1 * up[1]) >> 16;
+                    h[2][e] = __float_as_uint(a2 * up[2]) >> 16;
+                }
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc) w[pc][j / 2] = h[pc][0] | (h[pc][1] << 16);
+            }
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) {
+                uint4 *dst = reinterpret_cast<uint4 *>(pq[pc] + sk * kTnPq + sc);
+                dst[0] = make_uint4(w[pc][0], w[pc][1], w[pc][2], w[pc][3]);
+                dst[1] = make_uint4(w[pc][4], w[pc][5], w[pc][6], w[pc][7]);
+            }
+        }
+        __syncthreads();
+        // Gram: two 32-deep contraction steps over the quarter's 64 storage columns
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int co = 32 * ks + 8 * (lane >> 4);
+            uint4 fa[3][3], fb[3][3];   // [piece][block]
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+                if (b < nb)
+#pragma unroll
+                    for (int pc = 0; pc < 3; ++pc) {
+                        fa[pc][b] = *reinterpret_cast<const uint4 *>(pq[pc] + (16 * tbi[b] + (lane & 15)) * kTnPq + co);
+                        fb[pc][b] = *reinterpret_cast<const uint4 *>(pq[pc] + (16 * tbj[b] + (lane & 15)) * kTnPq + co);
+                    }
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+                if (b < nb) {
+                    acc02[b] = mfma_bf16(fa[0][b], fb[2][b], mfma_bf16(fa[2][b], fb[0][b], acc02[b]));
+                    acc01[b] = mfma_bf16(fa[0][b], fb[1][b], mfma_bf16(fa[1][b], fb[0][b], acc01[b]));
+                    acc00[b] = mfma_bf16(fa[0][b], fb[0][b], acc00[b]);
+                    acc1[b] = mfma_bf16(fa[1][b], fb[1][b], acc1[b]);
+                    acc2[b] = mfma_bf16(fa[2][b], fb[2][b], acc2[b]);
+                }
+        }
+        // row sums (the quarter's 64 rows = its 64 storage columns) and |.|_F^2,
+        // in f64 from the pieces (A = A0 + A1 + A2 to 2^-24)
+        {
+            double s[3] = {0.0, 0.0, 0.0};
+#pragma unroll 4
+            for (int k = 16 * rk; k < 16 * rk + 16; ++k) {
+                // (unscaled: exact powers of two)
+                const double b0 = (double)__uint_as_float((uint32_t)pq[0][k * kTnPq + rc] << 16) * dn[0];
+                const double b1 = (double)__uint_as_float((uint32_t)pq[1][k * kTnPq + rc] << 16) * dn[1];
+                const double b2 = (double)__uint_as_float((uint32_t)pq[2][k * kTnPq + rc] << 16) * dn[2];
+                const double a = b0 + b1 + b2;     // exact (three bf16 values of one f32's split)
+                s[0] += fabs(a);
+                s[1] += fabs(b1);
+                s[2] += fabs(b2);
+                fro[0] = fma(a, a, fro[0]);
+                fro[1] = fma(b1, b1, fro[1]);
+                fro[2] = fma(b2, b2, fro[2]);
+            }
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) rpart[pc][rk][rc] = s[pc];
+        }
+        __syncthreads();   // (pq restaged next quarter; rpart complete)
+        if (rk == 0)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc)
+                rmax[pc] = fmax(rmax[pc], ((rpart[pc][0][rc] + rpart[pc][1][rc]) + rpart[pc][2][rc]) + rpart[pc][3][rc]);
+    }
+    // the block maxima of the row sums and the sums of |.|_F^2 (fixed-order
+    // trees), unscaled (exact: powers of two)
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+        double rs = rmax[pc], fs = fro[pc];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            rs = fmax(rs, __shfl_xor(rs, o));
+            fs += __shfl_xor(fs, o);
+        }
+        if (lane == 0) {
+            red[0][wave] = 0.0;
+            fred[pc][wave] = fs;
+            rwm[pc][wave] = rs;
+        }
+    }
+    __syncthreads();
+    double rowmax_all[3];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+        rowmax_all[pc] = fmax(fmax(rwm[pc][0], rwm[pc][1]), fmax(rwm[pc][2], rwm[pc][3]));
 #pragma unroll 1
     for (int pi = 0; pi < 3; ++pi) {
         const int plane = pi == 0 ? -1 : pi;     // -1: A itself, then A1, A2
-        // G = A^T A, its lower 16 x 16 blocks (bi >= bj; G and its powers are
-        // symmetric bit for bit -- the same products summed in the same order
-        // -- so the upper blocks are written as their transposes): wave w
-        // owns blocks nb, two or three; lane l feeds A^T[i = 16 bi + (l&15)][r]
-        // and A[r][j = 16 bj + (l&15)] at r = r0 + (l>>4)
-        f64x4_t acc[3];
-#pragma unroll
-        for (int b = 0; b < 3; ++b) acc[b] = f64x4_t{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 1
-        for (int half = 0; half < 2; ++half) {
-            const int r = half * (kBM / 2) + lrow;
-            // the thread's 32 values in flight at once (a load-use chain per
-            // value was the kernel's critical path), then the piece by
-            // selects (plane is uniform, but a branch per value kept the
-            // compiler from batching the loads); the same sums in the same order
-            float v[32];
-#pragma unroll
-            for (int j = 0; j < 32; ++j) v[j] = t[tile_offset(32 * kh + j, r)];
-            double sp = 0.0;
-#pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                const float a0 = bf16_rn(v[j]), r1 = v[j] - a0, a1 = bf16_rn(r1), a2 = bf16_rn(r1 - a1);
-                const float a = plane < 0 ? v[j] : (plane == 1 ? a1 : a2);
-                at[(32 * kh + j) * kTnAtLd + lrow] = a;
-                sp += fabs((double)a);
-            }
-            if (kh == 1) rsum[r] = sp;
-            __syncthreads();
-            if (kh == 0) rsum[r] += sp;
-            for (int r0 = 0; r0 < kBM / 2; r0 += 4) {
-                const float *col = at + (lane & 15) * kTnAtLd + r0 + (lane >> 4);
-#pragma unroll
-                for (int b = 0; b < 3; ++b)
-                    if (b < nb)
-                        acc[b] = mfma_f64((double)col[16 * kTnAtLd * tbi[b]], (double)col[16 * kTnAtLd * tbj[b]], acc[b]);
-            }
-            __syncthreads();   // at is restaged for the next half
-        }
-        // G into LDS, and its largest entry (for the first squaring's rescale)
-        // from the registers
+        // the plane's symmetrised Gram into LDS, its largest entry for the
+        // first squaring's rescale
         double gmx = 0.0;
 #pragma unroll
         for (int b = 0; b < 3; ++b)
             if (b < nb) {
-                store_sym(gm, tbi[b], tbj[b], lane, acc[b]);
-#pragma unroll
-                for (int v = 0; v < 4; ++v) gmx = fmax(gmx, fabs(acc[b][v]));
+                gmx = fmax(gmx, store_sym_gram(gm, tbi[b], tbj[b], lane, pi, acc00[b], acc01[b], acc02[b], acc1[b],
+                                               acc2[b], sp));
             }
-        double s = rsum[tid];
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            s = fmax(s, __shfl_xor(s, o));
-            gmx = fmax(gmx, __shfl_xor(gmx, o));
-        }
-        if ((tid & 63) == 0) {
-            red[0][tid >> 6] = s;
-            red[1][tid >> 6] = gmx;
-        }
+        for (int o = 32; o >= 1; o >>= 1) gmx = fmax(gmx, __shfl_xor(gmx, o));
+        if (lane == 0) red[1][wave] = gmx;
         __syncthreads();
-        const double fro2 = [&] {  // trace G = |A|_F^2 (every thread reads it)
-            double tr = 0.0;
-            for (int i = 0; i < kBK; ++i) tr += gm[i * kTnGmLd + i];
-            return tr;
-        }();
+        const double fro2 = ((fred[pi][0] + fred[pi][1]) + fred[pi][2]) + fred[pi][3];
+        double s = rowmax_all[pi];
         // k squarings, G <- (G/c)^2 with c = the largest entry (exact power-of-two
         // rescale), tracking log2 of the scale: G^(2^k) = 2^e8 * gm.  The
         // rescale rides on the MFMA's A operand, (2^-2ex a) b = (2^-ex a)(2^-ex b)
@@ -1265,9 +1499,16 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
             for (int j = 0; j < kBK; ++j) rs += fabs(gm[tid * kTnGmLd + j]);
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) rs = fmax(rs, __shfl_xor(rs, o));
-        s = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
-        // log2 ||A||_2 <= (log2 ||G^(2^k)||_inf) / 2^(k+1), with a margin for the f64 rounding
-        const double lg_spec = rs > 0.0 ? (log2(rs) + e8) / (double)(2 << kGramSquarings) + 1e-4 : -1000.0;
+        // log2 ||G_c||_2 / 2 <= (log2 ||G_c^(2^k)||_inf) / 2^(k+1), with a margin
+        // for the f64 rounding of the squarings; then ||A||_2^2 <= that^2 +
+        // delta |A|_F^2 (G_c's own error, see above)
+        // (G_c and its powers are of the plane scaled by 2^sp: 2^(2 sp) G; the
+        // absolute underflow term: 2^-110 per accumulator at its own scale,
+        // five for G_A, all at most 2^(-2 sp) unscaled)
+        const int spl = sp[pi];
+        const double lg_pow = rs > 0.0 ? (log2(rs) + e8) / (double)(2 << kGramSquarings) + 1e-4 - spl : -1000.0;
+        const double spec2 = (rs > 0.0 ? exp2(2.0 * lg_pow) : 0.0) + kTnDelta * fro2 + ldexp(5.0, -110 - 2 * spl);
+        const double lg_spec = spec2 > 0.0 ? 0.5 * log2(spec2) : -1000.0;
         const double lg_fro = fro2 > 0.0 ? 0.5 * log2(fro2) : -1000.0;
         const int o = 2 * pi;                    // A: 0, A1: 2, A2: 4
         out[o] = s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f;
@@ -2628,6 +2869,21 @@ hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n,
 
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out) {
     hipLaunchKernelGGL(narrow_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, n, out);
+    return hipGetLastError();
+}
+
+size_t alpha_work_bytes(int64_t n) { return sizeof(double) * (size_t)((n + kAlK - 1) / kAlK) * (size_t)n; }
+
+hipError_t launch_alpha_f64(hipStream_t s, const double *X, int64_t ld, int64_t n, const float *obs, double m0,
+                            double *z, double *alpha, double *work) {
+    if (n <= 0) return hipSuccess;
+    const dim3 g1((unsigned)((n + kAlRows - 1) / kAlRows), (unsigned)((n + kAlK - 1) / kAlK));
+    hipLaunchKernelGGL(alpha_z_kernel, g1, dim3(256), 0, s, X, ld, n, obs, m0, work);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(alpha_z_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, work, n, z);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(alpha_xtz_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, X, ld, n, z, alpha);
     return hipGetLastError();
 }
 

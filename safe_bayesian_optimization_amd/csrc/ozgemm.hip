@@ -147,6 +147,14 @@ __global__ __launch_bounds__(256) void gz_digits_kernel(const T *__restrict__ M,
     // the bias: 0x80 in each of the ND - 1 lower bytes
     constexpr int64_t kBias = (int64_t)(((uint64_t)1 << (8 * (ND - 1))) - 1) / 255 * 128;
     uint32_t w[ND][4];
+    // x = rint(a 2^(kBits - e)) by ONE f64 FMA (round 6; was ldexp + rint +
+    // an f64 -> i64 conversion sequence per value): fma(a, 2^(kBits - e),
+    // 1.5 2^52) rounds once, to the nearest integer with ties to even (|x| <
+    // 2^47 and the sum lies in [2^52, 2^53): ulp 1, and 1.5 2^52 is even); its
+    // bit pattern is 0x4338000000000000 + x.  Bitwise the same digits.
+    static_assert(8 * ND - 1 <= 50, "the FMA rounding needs |x| < 2^51");
+    const double scale = e > -900 ? ldexp(1.0, kBits - e) : 0.0;   // (an all-zero row: x = 0)
+    constexpr double kMagic = 6755399441055744.0;                 // 1.5 2^52
     // columns of M (k contiguous): the workgroup's 16 rows x 256 k staged
     // through LDS by coalesced wave loads (a row per wave load, rows padded
     // to 257 doubles), then read back in the digit order
@@ -167,8 +175,8 @@ __global__ __launch_bounds__(256) void gz_digits_kernel(const T *__restrict__ M,
         const double a = ROWS_OF_COLMAJOR
                              ? gz_at<true>(M, ld, rows, K, tri, i, (int64_t)kb * kGzBK + 16 * g + jj)
                              : stage[r * 257 + 64 * wave + 16 * g + jj];
-        const int64_t x = e > -900 ? (int64_t)rint(ldexp(a, kBits - e)) : 0;
-        const uint64_t y = (uint64_t)(x + kBias);
+        const uint64_t y = (uint64_t)__double_as_longlong(fma(a, scale, kMagic)) - 0x4338000000000000ull +
+                           (uint64_t)kBias;
 #pragma unroll
         for (int s = 0; s < ND; ++s) {
             const uint32_t b = (uint32_t)(y >> (8 * (ND - 1 - s))) & 0xFFu;

@@ -795,23 +795,33 @@ __global__ __launch_bounds__(256) void pack_oz_kernel(const double *__restrict__
     const int sub = rr >> 4, h = sub >> 3, rb = sub & 7;
     if ((rr & 15) == 0) eoz[T * 16 + sub] = eA;
     char *base = aoz + T * (int64_t)kOzTileBytes + h * kOzA + rb * 1024;
+    // XA = rint(A 2^(39 - eA)), |XA| < 2^39 / 1.01, from ONE f64 FMA (round 6;
+    // was ldexp + rint + an f64 -> i64 conversion sequence per value, 1.4 ms
+    // at C4): fma(A, 2^(39 - eA), 1.5 2^52) is exact up to its one rounding,
+    // to the nearest integer with ties to even (the sum lies in [2^52, 2^53):
+    // ulp 1; 1.5 2^52 is even), i.e. 1.5 2^52 + rint(A 2^(39 - eA)) -- whose
+    // bit pattern is 0x4338000000000000 + XA.  Bitwise the same digits.
+    const double scale = eA > -900 ? ldexp(1.0, 39 - eA) : 0.0;   // (all-zero block: XA = 0)
+    constexpr double kMagic = 6755399441055744.0;                  // 1.5 2^52
 #pragma unroll
     for (int gg = 0; gg < 4; ++gg) {
         uint32_t w[kOzDigits][4];
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) {
-            // XA = rint(A 2^(39 - eA)), |XA| < 2^39 / 1.01; the bytes of XA +
-            // 0x80808080 are the digits (the four lower ones + 128)
-            const int64_t xa = eA > -900 ? (int64_t)rint(ldexp(v[16 * gg + jj], 39 - eA)) : 0;
-            const uint64_t yv = (uint64_t)(xa + 0x80808080ll);
+            // the bytes of XA + 0x80808080 are the digits (the four lower ones + 128)
+            const uint64_t yv = (uint64_t)__double_as_longlong(fma(v[16 * gg + jj], scale, kMagic)) -
+                                0x4338000000000000ull + 0x80808080ull;
 #pragma unroll
             for (int s = 0; s < kOzDigits; ++s) {
                 const uint32_t b = (uint32_t)(yv >> (8 * (kOzDigits - 1 - s))) & 0xFFu;
-                const uint32_t d = s == 0 ? b : (b ^ 0x80u);
-                if ((jj & 3) == 0) w[s][jj >> 2] = d;
-                else w[s][jj >> 2] |= d << (8 * (jj & 3));
+                if ((jj & 3) == 0) w[s][jj >> 2] = b;
+                else w[s][jj >> 2] |= b << (8 * (jj & 3));
             }
         }
+#pragma unroll
+        for (int s = 1; s < kOzDigits; ++s)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[s][q] ^= 0x80808080u;
         const int l = (rr & 15) + 16 * gg;
 #pragma unroll
         for (int s = 0; s < kOzDigits; ++s) {
@@ -1301,6 +1311,7 @@ __global__ __launch_bounds__(256) void pack_oz2_kernel(const double *__restrict_
     }
     const int sub = rr >> 4, qq = sub >> 2, b = sub & 3;
     if ((rr & 15) == 0) eoz[Tp * 16 + sub] = eA;
+    const double scale = eA > -900 ? ldexp(1.0, 39 - eA) : 0.0;
     char *base = aoz + Tp * (int64_t)kOzTileBytes + qq * kOz2A;
     for (int t2 = 0; t2 < 2; ++t2) {
         double v[kBK];
@@ -1311,8 +1322,9 @@ __global__ __launch_bounds__(256) void pack_oz2_kernel(const double *__restrict_
             uint32_t w[kOzDigits][4];
 #pragma unroll
             for (int jj = 0; jj < 16; ++jj) {
-                const int64_t xa = eA > -900 ? (int64_t)rint(ldexp(v[16 * gg + jj], 39 - eA)) : 0;
-                const uint64_t yv = (uint64_t)(xa + 0x80808080ll);
+                // (the one-FMA rounding of pack_oz_kernel: bitwise the same digits)
+                const uint64_t yv = (uint64_t)__double_as_longlong(fma(v[16 * gg + jj], scale, 6755399441055744.0)) -
+                                    0x4338000000000000ull + 0x80808080ull;
 #pragma unroll
                 for (int s = 0; s < kOzDigits; ++s) {
                     const uint32_t bt = (uint32_t)(yv >> (8 * (kOzDigits - 1 - s))) & 0xFFu;

@@ -628,10 +628,21 @@ bool probe_due(const sbo_ctx *ctx) {
            (ctx->n - ctx->probe_n) * 100 >= ctx->probe_n * (int64_t)ctx->reprobe_pct;
 }
 
+// Wait (host) for a precise-operand pack still running on aux_stream
+// (refresh_operand leaves it in flight past the fit's own host sync).
+sbo_status drain_poz(sbo_ctx *ctx) {
+    if (ctx->poz_pending) {
+        SBO_HIP(hipEventSynchronize(ctx->ev_poz));
+        ctx->poz_pending = false;
+    }
+    return SBO_OK;
+}
+
 // The precise operand's buffers for npad rows, keeping the row blocks below
 // I0 (grow_keep copies on `stream` and waits for it: the fit reserves them
 // before it forks work onto aux_stream, so that the fork is not serialised).
 sbo_status reserve_precise(sbo_ctx *ctx, int64_t npad, int64_t I0) {
+    if (sbo_status st = drain_poz(ctx)) return st;
     if (ctx->precise_kernel >= 1) {
         SBO_HIP(grow_keep(ctx, ctx->aoz, sbo::oz_operand_bytes(npad), sbo::oz_operand_bytes(I0 * sbo::kBM)));
         SBO_HIP(grow_keep(ctx, ctx->eoz, sbo::oz_exp_bytes(npad), sbo::oz_exp_bytes(I0 * sbo::kBM)));
@@ -647,6 +658,7 @@ sbo_status reserve_precise(sbo_ctx *ctx, int64_t npad, int64_t I0) {
 // digit tiles) for row blocks >= I0 of npad rows, from the f64 inverse and
 // alpha64, on stream s (the buffers grow keeping the row blocks below I0).
 sbo_status pack_precise(sbo_ctx *ctx, hipStream_t s, int64_t npad, int64_t I0) {
+    if (sbo_status st = drain_poz(ctx)) return st;
     const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
     if (ctx->precise_kernel >= 1) {
         SBO_HIP(grow_keep(ctx, ctx->aoz, sbo::oz_operand_bytes(npad), sbo::oz_operand_bytes(I0 * sbo::kBM)));
@@ -777,6 +789,7 @@ sbo_status inverse_check_read(sbo_ctx *ctx, sbo_inv_check &r) {
 // row blocks that hold new rows are repacked.  alpha, the per-k coordinates
 // and the tile boxes are rebuilt in full (O(n^2) and O(n)).
 sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
+    if (sbo_status st = drain_poz(ctx)) return st;
     const int64_t n = ctx->n, ld = ctx->cap;
     const double sf2 = ctx->hyper.sigma_f * ctx->hyper.sigma_f;
     float *L = ctx->L.as<float>();
@@ -943,12 +956,11 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             SBO_BLAS(rocblas_dgemv(ha, rocblas_operation_transpose, (rocblas_int)b, (rocblas_int)n, &one, Li + n_old,
                                    (rocblas_int)ld, zv + n_old, 1, &one, d, 1));
         } else {
-            SBO_HIP(sbo::launch_widen_sub(sa, ctx->obs.as<float>(), ctx->hyper.prior_mean, n, d));
-            SBO_BLAS(rocblas_dtrmv(ha, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_non_unit,
-                                   (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
-            SBO_HIP(hipMemcpyAsync(zv, d, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, sa));
-            SBO_BLAS(rocblas_dtrmv(ha, rocblas_fill_lower, rocblas_operation_transpose, rocblas_diagonal_non_unit,
-                                   (rocblas_int)n, Li, (rocblas_int)ld, d, 1));
+            // z = L^-1 r and alpha = L^-T z by the own two-pass kernels (one
+            // read of the triangle each; rocBLAS dtrmv took 1.4 ms at C4)
+            SBO_HIP(ctx->awork.reserve(sbo::alpha_work_bytes(n)));
+            SBO_HIP(sbo::launch_alpha_f64(sa, Li, ld, n, ctx->obs.as<float>(), ctx->hyper.prior_mean, zv, d,
+                                          ctx->awork.as<double>()));
         }
         ctx->z_n = n;
         SBO_HIP(sbo::launch_narrow(sa, d, n, alpha));
@@ -987,12 +999,17 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             // tile norms): the tile norms start right after the pack
             SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)npad));
             SBO_HIP(sbo::launch_row_l1(ctx->aux_stream, ctx->aug.as<float>(), npad, I0, ctx->scratch.as<double>()));
+            SBO_HIP(hipEventRecord(ctx->ev_pack, ctx->aux_stream));   // what the host reads below
+            // the precise operand after it, left running past this fit's host
+            // sync: only the probe's precise sweep reads it, on the device,
+            // after ev_poz (round 6: 1.7 ms at C4 off the fit's critical path)
             if (eager_f64) {
                 if (sbo_status st = pack_precise(ctx, ctx->aux_stream, npad, std::max<int64_t>(ctx->a64_I0, 0)))
                     return st;
                 ctx->a64_I0 = INT64_MAX;
+                SBO_HIP(hipEventRecord(ctx->ev_poz, ctx->aux_stream));
+                ctx->poz_pending = true;
             }
-            SBO_HIP(hipEventRecord(ctx->ev_pack, ctx->aux_stream));
             packs_aux = true;
         }
         kcoord_pending = true;
@@ -1344,6 +1361,7 @@ sbo_status blocked_potrf(sbo_ctx *ctx, float *L, int64_t n, int64_t ld, rocblas_
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_panel, hipEventDisableTiming));
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_trail, hipEventDisableTiming));
         SBO_HIP(hipEventCreateWithFlags(&ctx->ev_pack, hipEventDisableTiming));
+        SBO_HIP(hipEventCreateWithFlags(&ctx->ev_poz, hipEventDisableTiming));
     }
     if (!ctx->blas_aux) {
         SBO_BLAS(rocblas_create_handle(&ctx->blas_aux));
@@ -1700,6 +1718,8 @@ sbo_status run_tick(sbo_ctx *ctx, const float *qx, const float *qy, int64_t m, d
         return SBO_OK;
     }
     if (precise) {
+        // the fit's precise operand may still be packing on aux_stream
+        if (ctx->poz_pending) SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_poz, 0));
         // f64 operand of any repacked row block, derived from the f64 inverse
         const int64_t nIc = ctx->npad / sbo::kBM;
         if (ctx->a64_I0 < nIc) {
@@ -1900,6 +1920,7 @@ SBO_API void sbo_destroy(sbo_ctx *ctx) {
     if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
     if (ctx->ev_trail) (void)hipEventDestroy(ctx->ev_trail);
     if (ctx->ev_pack) (void)hipEventDestroy(ctx->ev_pack);
+    if (ctx->ev_poz) (void)hipEventDestroy(ctx->ev_poz);
     if (ctx->blas_aux) rocblas_destroy_handle(ctx->blas_aux);
     if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
     if (ctx->inv_stream) (void)hipStreamSynchronize(ctx->inv_stream);
@@ -2013,6 +2034,7 @@ SBO_API sbo_status sbo_fit(sbo_ctx *ctx, const float *x, const float *y, const f
     SBO_CHECK(n < (int64_t)1 << 30, SBO_E_INVAL, "sbo_fit: n too large");
     if (sbo_status st = check_hyper(ctx, hyper)) return st;
     SBO_HIP(hipSetDevice(ctx->device));
+    if (sbo_status st = drain_poz(ctx)) return st;   // (a precise pack may still read x, y, L^-1, alpha64)
     ctx->fitted = false;
     ctx->hyper = hyper;
     ctx->n = n;
@@ -2044,6 +2066,7 @@ SBO_API sbo_status sbo_append(sbo_ctx *ctx, const float *x, const float *y, cons
     SBO_CHECK(b >= 0, SBO_E_INVAL, "sbo_append: b must be >= 0");
     if (b == 0) return SBO_OK;
     SBO_HIP(hipSetDevice(ctx->device));
+    if (sbo_status st = drain_poz(ctx)) return st;   // (a precise pack may still read x, y, L^-1, alpha64)
     const int64_t n0 = ctx->n, n1 = n0 + b;
     SBO_CHECK(n1 < (int64_t)1 << 30, SBO_E_INVAL, "sbo_append: n too large");
     const float sf2 = (float)(ctx->hyper.sigma_f * ctx->hyper.sigma_f);
@@ -2613,6 +2636,7 @@ SBO_API sbo_status sbo_trim(sbo_ctx *ctx) {
     if (ctx->inv_stream) SBO_HIP(hipStreamSynchronize(ctx->inv_stream));
     if (ctx->chk_stream) SBO_HIP(hipStreamSynchronize(ctx->chk_stream));
     for (sbo::DevBuf *b : {&ctx->scratch, &ctx->gzws, &ctx->gzws_aux, &ctx->chk, &ctx->restage, &ctx->kzt, &ctx->qcost,
+                           &ctx->awork,
                            &ctx->cholx3[0], &ctx->cholx3[1]})
         b->release();
     return SBO_OK;
@@ -2979,6 +3003,7 @@ SBO_API sbo_status sbo_import_state(sbo_ctx *ctx, const void *dev_buf, int64_t b
     if (!ctx) return SBO_E_INVAL;
     SBO_CHECK(dev_buf && bytes >= (int64_t)sizeof(StateHeader), SBO_E_INVAL, "sbo_import_state: bad buffer");
     SBO_HIP(hipSetDevice(ctx->device));
+    if (sbo_status st = drain_poz(ctx)) return st;   // (a precise pack may still read x, y, L^-1, alpha64)
     const char *b = static_cast<const char *>(dev_buf);
     StateHeader h;
     SBO_HIP(hipMemcpyAsync(&h, b, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));

@@ -103,6 +103,11 @@ struct sbo_ctx {
     int aux_reserved = 0;        // the mask the current aux stream was created with
     hipEvent_t ev_panel = nullptr, ev_trail = nullptr;
     hipEvent_t ev_pack = nullptr;  // the fit's operand packs on aux_stream (refresh_operand)
+    // the precise operand's pack, left running on aux_stream after the fit's
+    // host sync (round 6): the precise sweep waits on it on the device, and
+    // anything that rewrites L^-1, alpha64 or the operand first on the host
+    hipEvent_t ev_poz = nullptr;
+    bool poz_pending = false;
     int chol_gemm_own = 4;       // SBO_OPT_CHOL_GEMM: 4 (default) / 5 the outer panels' updates int8-sliced, 3 split bf16, 2 every update by chol_update_kernel, 1 the small trailing ones, 0 rocBLAS
     int chol_diag = 1;           // SBO_OPT_CHOL_DIAG: 1 the MFMA chain kernels (diagonal block, panel), 0 the VALU ones (bitwise equal)
     int chol_outer = 1024;       // SBO_OPT_CHOL_OUTER: outer panel width of the two-level Cholesky (128: one level)
@@ -204,6 +209,7 @@ struct sbo_ctx {
     bool precise = false;        // the sweep ticks run in effect
     sbo::DevBuf alpha64;         // alpha from the f64 solve (length cap)
     sbo::DevBuf zvec, rvec;      // z = L^-1 (y - m0) (f64, valid for z_n points: appends update alpha from it), r scratch
+    sbo::DevBuf awork;           // launch_alpha_f64's partial sums
     int64_t z_n = 0;
     sbo::DevBuf a64, kc64;       // f64 packed operand and coordinates, derived lazily
     sbo::DevBuf aoz, eoz, koz;   // int8 digit operand, its block exponents, coordinates (predict_oz.hip)
@@ -394,6 +400,11 @@ hipError_t launch_chol_update_x3(hipStream_t s, const char *planes, int64_t m, i
 hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb, float *A21, int64_t m2, int version = 1);
 // d = (double)in - v;  out = (float)d
 hipError_t launch_widen_sub(hipStream_t s, const float *in, double v, int64_t n, double *d);
+// alpha = X^T X (obs - m0) from the f64 inverse X (lower, lda ld), z = X (obs -
+// m0) kept; work: alpha_work_bytes(n) (the first pass's per-chunk partials)
+size_t alpha_work_bytes(int64_t n);
+hipError_t launch_alpha_f64(hipStream_t s, const double *X, int64_t ld, int64_t n, const float *obs, double m0,
+                            double *z, double *alpha, double *work);
 hipError_t launch_narrow(hipStream_t s, const double *d, int64_t n, float *out);
 // out[r] = sum_c A[r + c ld] x[c] (c < n) for rows r < rows of a column-major f64 matrix
 hipError_t launch_row_dot(hipStream_t s, const double *A, int64_t ld, int64_t rows, int64_t n, const double *x,

@@ -663,12 +663,17 @@ def test_plan_beyond_the_bin_cache(mapper):
         gm.set_option(N.SBO_OPT_SKIP_BUDGET, 20)
 
 
-def test_tile_gain_bounds_are_bounds(mapper):
+@pytest.mark.parametrize("n", [1100, 4100])
+def test_tile_gain_bounds_are_bounds(mapper, n):
     """sbo_get_tile_bounds: every packed tile's log2 bounds are upper bounds
     of the exact norms of A_It = (sf2 L^-1)_It and of its bf16 pieces A1, A2
     (the same round-to-nearest split as the sweep's operand), and the
-    spectral bounds are within the ||G^8||^(1/16) slack (<= 64^(1/16) = 1.30x)."""
-    wl = synthetic(1100, 8, seed=17)
+    spectral bounds are within the ||G^8||^(1/16) slack (<= 64^(1/16) = 1.30x).
+    Round 6: the Gram matrices come from the bf16 pieces on the bf16 matrix
+    cores, each piece scaled to [1, 2) first; n = 4100 reaches tiles far
+    below the diagonal whose A2 pieces are 2^-80 and smaller, where an
+    unscaled f32 Gram underflowed and the bound fell below the norm."""
+    wl = synthetic(n, 8, seed=17)
     gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
     gm.fit(wl.x, wl.y, wl.obs)
     n = gm.n
@@ -689,6 +694,7 @@ def test_tile_gain_bounds_are_bounds(mapper):
             return -1000.0, -1000.0
         return (np.log2(16 * np.abs(T.astype(np.float64)).sum(1).max()),
                 np.log2(np.linalg.norm(T.astype(np.float64), 2)))
+    print(f"n={n}: {tiles} tiles, smallest A2 spectral bound 2^{b[:, 7][b[:, 7] > -1000].min():.1f}")
     T0 = 0
     checked = 0
     for I in range(nI):

@@ -64,8 +64,8 @@ def main():
     p.add_argument("lib_b")
     p.add_argument("--configs", nargs="+", default=["C4", "C2", "box"])
     a = p.parse_args()
-    A = run(a.lib_a, a.configs, "/tmp/cmp_a.npz")
-    B = run(a.lib_b, a.configs, "/tmp/cmp_b.npz")
+    A = run(a.lib_a, a.configs, os.environ.get("CMP_OUT", "/tmp") + "/cmp_a.npz")
+    B = run(a.lib_b, a.configs, os.environ.get("CMP_OUT", "/tmp") + "/cmp_b.npz")
     same = True
     for k in sorted(A):
         eq = np.array_equal(A[k], B[k])
