@@ -732,6 +732,22 @@ def run_regime_stress(a, gm, prof, dev, n, gw, gh):
     fast_err = float((v_fast - v_def).abs().max() / v_def.abs().max())
     fast = _regime_line(a, "lpsc_stress_box fast sweep", "SBO_OPT_PRECISION = 0 on the same fit", m, n, *fres)
     fast["variance_error_vs_precise_sweep"] = fast_err
+    # the grid the node actually receives: the mapper's own resolution [300,
+    # 120] over the same box (config/lpsc.yaml:34), the same
+    # fit and default options -- the per-tick cost of the reference's path
+    wm = synthetic_box(n, 300, 120, seed=0)
+    mqx, mqy = f32(wm.qx), f32(wm.qy)
+    mm = mqx.numel()
+    mouts = dict(mu=torch.empty(mm, dtype=torch.float32, device=dev), sd=torch.empty(mm, dtype=torch.float32, device=dev),
+                 lo=torch.empty(mm, dtype=torch.float64, device=dev), hi=torch.empty(mm, dtype=torch.float64, device=dev),
+                 safe=torch.empty(mm, dtype=torch.uint8, device=dev))
+
+    def mstep():
+        gm.tick(mqx, mqy, wm.beta, wm.f_min, score=N.SCORE_WIDTH, outputs=mouts, key_out=key, async_=True)
+    mres = _timed_ticks(prof, mstep, max(3, a.regime_steps))
+    mapper = _regime_line(a, "lpsc_mapper_grid", "the same fit, the mapper's own 300 x 120 grid over the box "
+                          "(config/lpsc.yaml:34), default options", mm, n, *mres, precise=precise, precise_kernel=pk)
+    mapper["end_to_end"] = end_to_end(mm, fit_ms, mres[0] * 1e3)
     return _regime_line(a, "lpsc_stress_box", "N points and the grid on x [0, 1] x y [0, 2.5] (config/lpsc.yaml:32-33), "
                         "default options (SBO_OPT_PRECISION = -1: the fit-time probe picks the sweep)", m, n, *res,
                         extra={"fit_ms": fit_ms, "kstar_cutoff_log2": gm.skip_info()[0],
@@ -743,6 +759,7 @@ def run_regime_stress(a, gm, prof, dev, n, gw, gh):
                                          "err_grid": pinfo["err_grid"], "err_train": pinfo["err_train"],
                                          "how": "32 x 32 grid over the training box + 512 training locations, "
                                                 "fast vs precise sweep"},
+                               "mapper_grid_300x120": mapper,
                                "other_precise_kernel": other,
                                "int8_in_sweep_kstar": others.get(1),
                                "fast_sweep": fast}, precise=precise, precise_kernel=pk)

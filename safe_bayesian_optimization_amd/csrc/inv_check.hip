@@ -116,32 +116,54 @@ __global__ __launch_bounds__(kChkThreads) void chk_trimul_kernel(const T *__rest
     f64x4 acc[kChkCB];
 #pragma unroll
     for (int j = 0; j < kChkCB; ++j) acc[j] = f64x4{0.0, 0.0, 0.0, 0.0};
-    for (int64_t k0 = kb; k0 < ke; k0 += kChkStage) {
-        // the A fragments of the stage's 16 k steps (lower triangle, k < ke)
-        double a[kChkStage / 4];
+    // software-pipelined (round 6): the next stage's A fragments and X
+    // elements are loaded into registers before this stage's MFMAs, so a
+    // wave's loads overlap its own arithmetic (the stage-by-stage form waited
+    // out a full memory latency per 64 k: ~1.1 ms per f64 product at C4,
+    // beside the fit's tail)
+    constexpr int kXe = kChkStage * kChkQ / kChkThreads;   // X doubles per thread per stage
+    auto load_a = [&](int64_t k0, double (&a)[kChkStage / 4]) {
 #pragma unroll
         for (int s = 0; s < kChkStage / 4; ++s) {
             const int64_t k = k0 + 4 * s + (lane >> 4);
             a[s] = (k < ke && k <= row && row < n) ? (double)Tm[row + k * ld] : 0.0;
         }
-        __syncthreads();
+    };
+    auto load_x = [&](int64_t k0, double2 (&xv)[kXe / 2]) {
+#pragma unroll
+        for (int e = 0; e < kXe; e += 2) {
+            const int f = (int)threadIdx.x * 2 + e * kChkThreads;  // element pair index
+            const int64_t k = k0 + f / kChkQ;
+            xv[e / 2] = k < rows ? *reinterpret_cast<const double2 *>(X + k * kChkQ + f % kChkQ) : double2{0.0, 0.0};
+        }
+    };
+    double a[kChkStage / 4], an[kChkStage / 4];
+    double2 xv[kXe / 2];
+    load_a(kb, a);
+    load_x(kb, xv);
+    for (int64_t k0 = kb; k0 < ke; k0 += kChkStage) {
+        __syncthreads();   // every wave is done reading the previous stage
         // stage X[k0 .. k0 + 63][0 .. kChkQ - 1] (rows past `rows` read as zero)
 #pragma unroll
-        for (int e = 0; e < kChkStage * kChkQ / kChkThreads; e += 2) {
-            const int f = (int)threadIdx.x * 2 + e * kChkThreads;  // element pair index
-            const int kr = f / kChkQ, cc = f % kChkQ;
-            const int64_t k = k0 + kr;
-            double2 v = {0.0, 0.0};
-            if (k < rows) v = *reinterpret_cast<const double2 *>(X + k * kChkQ + cc);
-            *reinterpret_cast<double2 *>(xs + kr * kChkLd + cc) = v;
+        for (int e = 0; e < kXe; e += 2) {
+            const int f = (int)threadIdx.x * 2 + e * kChkThreads;
+            *reinterpret_cast<double2 *>(xs + (f / kChkQ) * kChkLd + f % kChkQ) = xv[e / 2];
         }
         __syncthreads();
+        const bool more = k0 + kChkStage < ke;
+        if (more) {
+            load_a(k0 + kChkStage, an);
+            load_x(k0 + kChkStage, xv);
+        }
 #pragma unroll
         for (int s = 0; s < kChkStage / 4; ++s) {
             const double *xb = xs + (4 * s + (lane >> 4)) * kChkLd + (lane & 15);
 #pragma unroll
             for (int j = 0; j < kChkCB; ++j) acc[j] = mfma_f64(a[s], xb[16 * j], acc[j]);
         }
+        if (more)
+#pragma unroll
+            for (int s = 0; s < kChkStage / 4; ++s) a[s] = an[s];
     }
     double *out = P + ((int64_t)kc * rows + r0) * kChkQ;
 #pragma unroll

@@ -1100,6 +1100,14 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
         ctx->x3_I0 = std::min(ctx->x3_I0, I0);  // the split operand is derived lazily (run_tick)
         if (!incr && ctx->a64_I0 != INT64_MAX) ctx->a64_I0 = 0;
     }
+    // The precision probe before the guard's reading (round 6): the guard's
+    // three products on chk_stream run beside the probe's sweeps instead of
+    // ahead of them (C4: the guard finished ~0.7 ms after the tail's last
+    // kernel).  If the guard then fires, the fit's inverse is redone and the
+    // probe with it.
+    ctx->fitted = true;
+    const sbo_status pst = probe_precision(ctx);
+    if (pst != SBO_OK) return pst;   // (the drain waits for the guard)
     if (chk_pending) {
         sbo_inv_check r = ctx->chk_res;
         const sbo_status rst = inverse_check_read(ctx, r);
@@ -1133,8 +1141,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             return st;
         }
     }
-    ctx->fitted = true;
-    return probe_precision(ctx);
+    return SBO_OK;
 }
 
 // The precise sweep's budget: the same construction as the automatic cutoff
