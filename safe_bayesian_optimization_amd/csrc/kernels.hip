@@ -1183,31 +1183,12 @@ __device__ __forceinline__ float bf16_rn(float a) {
 //           plane by plane in tile_increments.
 // The plan pairs the row-sum bounds with the largest K* of the tile and the
 // spectral ones with a bound on |k|_2 from the tile's points.  One workgroup
-// per tile, f64 arithmetic; the three matrices one after the other.  The
-// Gram matrix and its squarings are f64 MFMA products
-// (v_mfma_f64_16x16x4_f64; wave w owns rows 16w .. 16w+15 of G, four 16 x 16
-// accumulators).
-typedef double f64x4_t __attribute__((ext_vector_type(4)));
-// LDS strides of the tile-norm kernel: the Gram matrix (doubles, row
-// stride padded off the 64-bank period: with 64 the squarings' column
-// reads were 16-way bank conflicts and the final row sums 64-way) and the
-// staged half-tile, held k-major ([k][row], 128 rows + 4 padding) so that
-// the staging writes (one row per lane) and the Gram's reads (four rows x 16
-// columns per MFMA operand) both fall on distinct banks
+// per tile; the three matrices one after the other.  The Gram matrices and
+// their squarings are bf16 MFMA products of split operands (below); wave w
+// owns two or three of the ten lower 16 x 16 blocks of each 64 x 64 product.
+// LDS row stride (floats) of the powers of G: 68 puts the row-sum pass's
+// 16-B reads and the mirrored stores on distinct banks
 constexpr int kTnGmLd = kBK + 4;
-__device__ __forceinline__ f64x4_t mfma_f64(double a, double b, f64x4_t c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-// a 16 x 16 block (bi, bj) of a symmetric 64 x 64 matrix from its MFMA
-// accumulator (lane l, element v: row 16 bi + (l>>4) + 4v, column 16 bj + (l&15)),
-// and its transpose at (bj, bi)
-__device__ __forceinline__ void store_sym(double *g, int bi, int bj, int lane, f64x4_t a) {
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        g[(16 * bi + (lane >> 4) + 4 * v) * kTnGmLd + 16 * bj + (lane & 15)] = a[v];
-        if (bi != bj) g[(16 * bj + (lane & 15)) * kTnGmLd + 16 * bi + (lane >> 4) + 4 * v] = a[v];
-    }
-}
 // Round 6: the Gram matrices from the tile's bf16 pieces on the bf16 matrix
 // cores.  A = A0 + A1 + A2 (+ r, |r| < 2^-24 |A|) exactly as pack_x3_kernel
 // splits it, so G1 = A1^T A1 and G2 = A2^T A2 are products of bf16 values --
@@ -1221,7 +1202,7 @@ __device__ __forceinline__ void store_sym(double *g, int bi, int bj, int lane, f
 // so ||G_c - G||_2 <= delta |A|_F^2 and, by Weyl, lambda_max(G) <=
 // lambda_max(G_c) + delta |A|_F^2: the spectral bound below adds that term
 // (at most 64 delta = 1e-3 relative, since ||A||_2^2 >= |A|_F^2 / 64).  The
-// squarings stay f64.  Row sums and |A|_F^2 come from the pieces in f64 (A0 +
+// squarings run on the bf16 matrix cores too (their bound: in the kernel).  Row sums and |A|_F^2 come from the pieces in f64 (A0 +
 // A1 + A2 = A to 2^-24: inside the outputs' 1e-5 log2 margin).  The pieces are
 // those pack_x3_kernel cuts (the same instructions on the unscaled values),
 // each scaled by its own power of two 2^s_p (exact) so that the piece's
@@ -1243,40 +1224,55 @@ __device__ __forceinline__ f32x4_t2 mfma_bf16(uint4 a, uint4 b, f32x4_t2 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
                                                    c, 0, 0, 0);
 }
-// the lower part of a 16 x 16 block (bi >= bj) of plane pi's symmetric 64 x 64
-// Gram matrix, scaled 2^(2 sp[pi]), from the f32 MFMA accumulators (lane l,
-// element v: row 16 bi + 4 (l>>4) + v, column 16 bj + (l&15)), mirrored:
-// G_A = a00 + 2^(s0 - s1) a01 + 2^(s0 - s2) a02 + 2^(2 (s0 - s1)) a1 in f64
-// (exact scalings); returns the largest |entry| written
-__device__ __forceinline__ double store_sym_gram(double *g, int bi, int bj, int lane, int pi, f32x4_t2 a00,
-                                                 f32x4_t2 a01, f32x4_t2 a02, f32x4_t2 a1, f32x4_t2 a2,
-                                                 const int (&sp)[3]) {
+// a 16 x 16 block (bi >= bj) of plane pi's symmetric 64 x 64 Gram matrix,
+// scaled 2^(2 sp[pi]), from the f32 MFMA accumulators (lane l, element v:
+// row 16 bi + 4 (l>>4) + v, column 16 bj + (l&15)): G_A = a00 + 2^(s0 - s1)
+// a01 + 2^(s0 - s2) a02 + 2^(2 (s0 - s1)) a1 in f64 (exact scalings); the
+// entries above the diagonal of a diagonal block are left 0 (the stores
+// mirror the lower ones)
+__device__ __forceinline__ void gram_values(double (&x)[4], int bi, int bj, int lane, int pi, f32x4_t2 a00,
+                                            f32x4_t2 a01, f32x4_t2 a02, f32x4_t2 a1, f32x4_t2 a2,
+                                            const int (&sp)[3]) {
     const double c01 = ldexp(1.0, sp[0] - sp[1]), c02 = ldexp(1.0, sp[0] - sp[2]), c11 = c01 * c01;
-    double mx = 0.0;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
         const int i = 16 * bi + 4 * (lane >> 4) + v, j = 16 * bj + (lane & 15);
-        if (bi != bj || i >= j) {
-            const double x = pi == 0 ? (((double)a00[v] + c01 * (double)a01[v]) + c02 * (double)a02[v]) + c11 * (double)a1[v]
-                                     : (pi == 1 ? (double)a1[v] : (double)a2[v]);
-            g[i * kTnGmLd + j] = x;
-            g[j * kTnGmLd + i] = x;
-            mx = fmax(mx, fabs(x));
-        }
+        x[v] = (bi != bj || i >= j)
+                   ? (pi == 0 ? (((double)a00[v] + c01 * (double)a01[v]) + c02 * (double)a02[v]) + c11 * (double)a1[v]
+                              : (pi == 1 ? (double)a1[v] : (double)a2[v]))
+                   : 0.0;
     }
-    return mx;
+}
+// an f32 block (bi >= bj) of a symmetric matrix into gf (stride kTnGmLd):
+// the lower entries and their mirror (a diagonal block's upper entries from
+// its lower ones, so the stored matrix is exactly symmetric); the mirror of
+// a lane's four rows is one 16-B store
+__device__ __forceinline__ void store_sym_f32(float *gf, int bi, int bj, int lane, const float (&x)[4]) {
+    const int i0 = 16 * bi + 4 * (lane >> 4), j = 16 * bj + (lane & 15);
+    if (bi != bj) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) gf[(i0 + v) * kTnGmLd + j] = x[v];
+        *reinterpret_cast<float4 *>(gf + j * kTnGmLd + i0) = make_float4(x[0], x[1], x[2], x[3]);
+    } else {
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            if (i0 + v >= j) {
+                gf[(i0 + v) * kTnGmLd + j] = x[v];
+                gf[j * kTnGmLd + i0 + v] = x[v];
+            }
+    }
 }
 __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
                                                            float4 *__restrict__ lgn) {
     __shared__ __attribute__((aligned(16))) unsigned short pq[3][kBK * kTnPq];   // a quarter's pieces [k][c] (27 KiB)
-    __shared__ double gm[kBK * kTnGmLd];       // G, then its powers (34 KiB)
+    __shared__ __attribute__((aligned(16))) float gm[kBK * kTnGmLd];   // G, then its powers, normalised f32 (17 KiB)
     __shared__ double rpart[3][4][kBK];        // row-sum partials of a quarter (6 KiB)
     __shared__ double red[2][kBM / 64];
     __shared__ double fred[3][kBM / 64], rwm[3][kBM / 64];   // per wave: |.|_F^2 sums, row-sum maxima
     const int64_t tile = t0 + blockIdx.x;
     const float *t = aug + tile * kTileFloats;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    float out[6];                                // (rows, spectral) of A; of A1; of A2
+    __shared__ float out[6];                     // (rows, spectral) of A; of A1; of A2 (LDS: a plane-indexed array)
     double lg_fro_a = -1000.0;
     // this wave's lower blocks of the 4 x 4 block grid of G: (0,0) (1,0) (1,1) |
     // (2,0) (2,1) (2,2) | (3,0) (3,1) | (3,2) (3,3)
@@ -1444,78 +1440,167 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
 #pragma unroll 1
     for (int pi = 0; pi < 3; ++pi) {
         const int plane = pi == 0 ? -1 : pi;     // -1: A itself, then A1, A2
-        // the plane's symmetrised Gram into LDS, its largest entry for the
-        // first squaring's rescale
+        // the plane's Gram matrix G_c (f64, registers), normalised by its
+        // largest entry's power of two 2^e0 and rounded to f32: M0, symmetric
+        double gv[3][4];
         double gmx = 0.0;
 #pragma unroll
         for (int b = 0; b < 3; ++b)
             if (b < nb) {
-                gmx = fmax(gmx, store_sym_gram(gm, tbi[b], tbj[b], lane, pi, acc00[b], acc01[b], acc02[b], acc1[b],
-                                               acc2[b], sp));
+                gram_values(gv[b], tbi[b], tbj[b], lane, pi, acc00[b], acc01[b], acc02[b], acc1[b], acc2[b], sp);
+#pragma unroll
+                for (int v = 0; v < 4; ++v) gmx = fmax(gmx, fabs(gv[b][v]));
             }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) gmx = fmax(gmx, __shfl_xor(gmx, o));
         if (lane == 0) red[1][wave] = gmx;
         __syncthreads();
+        const double mx0 = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+        const int e0 = mx0 > 0.0 ? ilogb(mx0) : 0;
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+            if (b < nb) {
+                float xf[4];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) xf[v] = (float)ldexp(gv[b][v], -e0);
+                store_sym_f32(gm, tbi[b], tbj[b], lane, xf);
+            }
         const double fro2 = ((fred[pi][0] + fred[pi][1]) + fred[pi][2]) + fred[pi][3];
         double s = rowmax_all[pi];
-        // k squarings, G <- (G/c)^2 with c = the largest entry (exact power-of-two
-        // rescale), tracking log2 of the scale: G^(2^k) = 2^e8 * gm.  The
-        // rescale rides on the MFMA's A operand, (2^-2ex a) b = (2^-ex a)(2^-ex b)
-        // exactly, and each power's largest entry comes from the registers
-        // that hold it (no LDS pass for either; the same powers bit for bit)
+        // Four squarings on the bf16 matrix cores (round 6; f64 MFMA before,
+        // 2.1 ms of the C4 fit's critical path): M_k is split into three bf16
+        // planes as pack_x3_kernel splits (pq, free after the Gram), S_k =
+        // M_k M_k is taken as the six products a2 b0 + a1 b1 + a0 b2 + a1 b0 + a0
+        // b1 + a0 b0 (exact products, f32 accumulation) on the ten lower
+        // blocks, and M_(k+1) = 2^-e S_k (e: S_k's largest entry's exponent,
+        // exact) is stored mirrored, so every M_k is exactly symmetric.
+        // Rigour: |S_k - M_k^2| <= eps |M_k| |M_k| entrywise with eps = 2^-15
+        // (the dropped a1 b2 + a2 b1 + a2 b2 and the split's remainder < 2^-22,
+        // <= 396 f32 roundings of partial sums of the |terms| < 2.4e-5), so
+        // ||S_k - M_k^2||_2 <= eta ||M_k||_2^2 with eta = 64 eps (||
+        // |M| |M| ||_2 <= |M|_F^2 <= 64 ||M||_2^2) and ||M_k||_2^2 <=
+        // ||S_k||_2 / (1 - eta); M0 is G_c 2^-e0 rounded to f32, ||G_c||_2 <=
+        // 2^e0 ||M0||_2 / (1 - 2^-21).  Chained: log2 ||G_c||_2 <= e0 + (T +
+        // log2 ||M4||_inf + 15 log2(1 / (1 - eta))) / 16 + log2(1 / (1 - 2^-21)),
+        // T = 8 e1 + 4 e2 + 2 e3 + e4 (||M4||_2 <= ||M4||_inf: symmetric).
+        // Underflow (entries below 2^-110 of the largest) costs < 2^-90 of
+        // ||S_k||_2 >= 1, inside eps's slack.
         constexpr int kGramSquarings = 4;
-        double e8 = 0.0;
-        for (int it = 0; it < kGramSquarings; ++it) {
-            const double mx = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
-            if (!(mx > 0.0)) break;
-            const int ex = ilogb(mx);
-            f64x4_t sq[3];
+        constexpr double kSqEta = 64.0 / 32768.0;   // 64 eps, eps = 2^-15
+        int T = 0;
+        bool live = mx0 > 0.0;
+        for (int it = 0; it < kGramSquarings && live; ++it) {
+            __syncthreads();   // M_k stored (and every read of pq by the last products done)
+            {
+                // split M_k into the planes: row sk, columns sc .. sc + 15
+                const float4 *src = reinterpret_cast<const float4 *>(gm + sk * kTnGmLd + sc);
+                uint32_t w[3][8];
 #pragma unroll
-            for (int b = 0; b < 3; ++b) sq[b] = f64x4_t{0.0, 0.0, 0.0, 0.0};
-            for (int k0 = 0; k0 < kBK; k0 += 4) {
-                const double *arow = gm + (lane & 15) * kTnGmLd + k0 + (lane >> 4);
-                const double *brow = gm + (k0 + (lane >> 4)) * kTnGmLd + (lane & 15);
+                for (int q = 0; q < 4; ++q) {
+                    const float4 f = src[q];
+                    const float xv[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+                    for (int e = 0; e < 4; e += 2) {
+                        uint32_t h[3][2];
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const float x = xv[e + u];
+                            const float a0 = bf16_rn(x), r1 = x - a0, a1 = bf16_rn(r1), a2 = bf16_rn(r1 - a1);
+                            h[0][u] = __float_as_uint(a0) >> 16;
+                            h[1][u] = __float_as_uint(a1) >> 16;
+                            h[2][u] = __float_as_uint(a2) >> 16;
+                        }
+#pragma unroll
+                        for (int pc = 0; pc < 3; ++pc) w[pc][(4 * q + e) / 2] = h[pc][0] | (h[pc][1] << 16);
+                    }
+                }
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc) {
+                    uint4 *dst = reinterpret_cast<uint4 *>(pq[pc] + sk * kTnPq + sc);
+                    dst[0] = make_uint4(w[pc][0], w[pc][1], w[pc][2], w[pc][3]);
+                    dst[1] = make_uint4(w[pc][4], w[pc][5], w[pc][6], w[pc][7]);
+                }
+            }
+            __syncthreads();
+            f32x4_t2 sq[3];
+#pragma unroll
+            for (int b = 0; b < 3; ++b) sq[b] = f32x4_t2{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int co = 32 * ks + 8 * (lane >> 4);
+                uint4 fa[3][3], fb[3][3];   // [piece][block]
 #pragma unroll
                 for (int b = 0; b < 3; ++b)
-                    if (b < nb) sq[b] = mfma_f64(ldexp(arow[16 * kTnGmLd * tbi[b]], -2 * ex), brow[16 * tbj[b]], sq[b]);
+                    if (b < nb)
+#pragma unroll
+                        for (int pc = 0; pc < 3; ++pc) {
+                            fa[pc][b] = *reinterpret_cast<const uint4 *>(pq[pc] + (16 * tbi[b] + (lane & 15)) * kTnPq + co);
+                            fb[pc][b] = *reinterpret_cast<const uint4 *>(pq[pc] + (16 * tbj[b] + (lane & 15)) * kTnPq + co);
+                        }
+#pragma unroll
+                for (int b = 0; b < 3; ++b)
+                    if (b < nb) {
+                        sq[b] = mfma_bf16(fa[2][b], fb[0][b], sq[b]);
+                        sq[b] = mfma_bf16(fa[1][b], fb[1][b], sq[b]);
+                        sq[b] = mfma_bf16(fa[0][b], fb[2][b], sq[b]);
+                        sq[b] = mfma_bf16(fa[1][b], fb[0][b], sq[b]);
+                        sq[b] = mfma_bf16(fa[0][b], fb[1][b], sq[b]);
+                        sq[b] = mfma_bf16(fa[0][b], fb[0][b], sq[b]);
+                    }
             }
-            e8 = 2.0 * (e8 + (double)ex);  // (2^e G')^2 = 2^(2e) G'^2
-            double qmx = 0.0;
+            float qmx = 0.0f;
 #pragma unroll
             for (int b = 0; b < 3; ++b)
                 if (b < nb)
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) qmx = fmax(qmx, fabs(sq[b][v]));
+                    for (int v = 0; v < 4; ++v) qmx = fmaxf(qmx, fabsf(sq[b][v]));
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) qmx = fmax(qmx, __shfl_xor(qmx, o));
-            __syncthreads();   // every read of G and of red[1] is done
+            for (int o = 32; o >= 1; o >>= 1) qmx = fmaxf(qmx, __shfl_xor(qmx, o));
+            if (lane == 0) red[0][wave] = (double)qmx;
+            __syncthreads();   // every wave's maximum (and every read of gm by the split is done)
+            const double mk = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+            live = mk > 0.0;
+            const int ek = live ? ilogb(mk) : 0;
+            T = 2 * T + ek;
 #pragma unroll
             for (int b = 0; b < 3; ++b)
-                if (b < nb) store_sym(gm, tbi[b], tbj[b], lane, sq[b]);
-            if (lane == 0) red[1][wave] = qmx;
-            __syncthreads();
+                if (b < nb) {
+                    // (the diagonal block's upper entries are computed too; only the lower are kept)
+                    const float xf[4] = {ldexpf(sq[b][0], -ek), ldexpf(sq[b][1], -ek), ldexpf(sq[b][2], -ek),
+                                         ldexpf(sq[b][3], -ek)};
+                    store_sym_f32(gm, tbi[b], tbj[b], lane, xf);
+                }
         }
-        // ||G^(2^k)||_inf: largest absolute row sum
+        __syncthreads();   // the last power stored
+        // ||M4||_inf: largest absolute row sum (f64)
         double rs = 0.0;
         if (tid < kBK)
-            for (int j = 0; j < kBK; ++j) rs += fabs(gm[tid * kTnGmLd + j]);
+            for (int j = 0; j < kBK; ++j) rs += fabs((double)gm[tid * kTnGmLd + j]);
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) rs = fmax(rs, __shfl_xor(rs, o));
-        // log2 ||G_c||_2 / 2 <= (log2 ||G_c^(2^k)||_inf) / 2^(k+1), with a margin
-        // for the f64 rounding of the squarings; then ||A||_2^2 <= that^2 +
-        // delta |A|_F^2 (G_c's own error, see above)
-        // (G_c and its powers are of the plane scaled by 2^sp: 2^(2 sp) G; the
-        // absolute underflow term: 2^-110 per accumulator at its own scale,
-        // five for G_A, all at most 2^(-2 sp) unscaled)
+        if (lane == 0) red[1][wave] = rs;
+        __syncthreads();
+        rs = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+        if (!live) rs = 0.0;   // (a zero Gram matrix)
+        // log2 ||A||_2 (the plane scaled by 2^sp: G_c = 2^(2 sp) G) from the
+        // chain above, 1e-6 for the f64 row sums and logs; then ||A||_2^2 <=
+        // that^2 + delta |A|_F^2 (G_c's own error) + the absolute underflow
+        // term: 2^-110 per accumulator at its own scale, five for G_A, all at
+        // most 2^(-2 sp) unscaled
         const int spl = sp[pi];
-        const double lg_pow = rs > 0.0 ? (log2(rs) + e8) / (double)(2 << kGramSquarings) + 1e-4 - spl : -1000.0;
+        const double lg_g = (double)e0 +
+                            ((double)T + log2(rs) - (double)((1 << kGramSquarings) - 1) * log2(1.0 - kSqEta)) /
+                                (double)(1 << kGramSquarings) -
+                            log2(1.0 - 0x1p-21);
+        const double lg_pow = rs > 0.0 ? 0.5 * lg_g + 1e-6 - spl : -1000.0;
         const double spec2 = (rs > 0.0 ? exp2(2.0 * lg_pow) : 0.0) + kTnDelta * fro2 + ldexp(5.0, -110 - 2 * spl);
         const double lg_spec = spec2 > 0.0 ? 0.5 * log2(spec2) : -1000.0;
         const double lg_fro = fro2 > 0.0 ? 0.5 * log2(fro2) : -1000.0;
         const int o = 2 * pi;                    // A: 0, A1: 2, A2: 4
-        out[o] = s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f;
-        out[o + 1] = (float)fmin(lg_spec, lg_fro) + 1e-5f;
+        if (tid == 0) {
+            out[o] = s > 0.0 ? (float)log2(16.0 * s) + 1e-5f : -1000.0f;
+            out[o + 1] = (float)fmin(lg_spec, lg_fro) + 1e-5f;
+        }
         if (plane < 0) lg_fro_a = lg_fro;
         __syncthreads();   // gm / red / rsum / at are rewritten for the next matrix
     }
