@@ -28,6 +28,8 @@ def main():
     p.add_argument("--oz", type=int, nargs="+", default=[6], help="SBO_OPT_INV_OZ values to time (0 dgemm, 5/6 sliced; 6 the library default)")
     p.add_argument("--diag", type=int, nargs="+", default=[1], help="SBO_OPT_CHOL_DIAG values to time")
     p.add_argument("--check", type=int, nargs="+", default=[1], help="SBO_OPT_INV_CHECK values to time (0: no guard)")
+    p.add_argument("--probe", type=str, nargs="+", default=["32:512"],
+                   help="SBO_OPT_PROBE_SIZE values to time, as lattice side:training points")
     p.add_argument("--box", action="store_true", help="the lpsc stress box instead of the C3/C4 synthetic layout")
     a = p.parse_args()
     import torch
@@ -35,10 +37,10 @@ def main():
     from safe_bayesian_optimization_amd.terrain import synthetic_box
     dev = torch.device("cuda:0")
     from safe_bayesian_optimization_amd import _native as N
-    for n, ch, inv, rsv, ov, ou, gg, ib, ip, lv, pr, oz, dg, ck in [
-            (n, c, i, r, o, u, g, b, q, v, e, z, d, k) for n in a.n for c in a.chol for i in a.inv for r in a.reserve
+    for n, ch, inv, rsv, ov, ou, gg, ib, ip, lv, pr, oz, dg, ck, ps in [
+            (n, c, i, r, o, u, g, b, q, v, e, z, d, k, s) for n in a.n for c in a.chol for i in a.inv for r in a.reserve
             for o in a.overlap for u in a.outer for g in a.gemm for b in a.inv_base for q in a.inv_panels
-            for v in a.leaves for e in a.prec for z in a.oz for d in a.diag for k in a.check]:
+            for v in a.leaves for e in a.prec for z in a.oz for d in a.diag for k in a.check for s in a.probe]:
         wl = synthetic_box(n, 64, 64, seed=0) if a.box else synthetic(n, 64, 64, seed=0)
         t = lambda v: torch.as_tensor(np.ascontiguousarray(v, np.float32), device=dev)  # noqa: E731
         X, Y, O = t(wl.x), t(wl.y), t(wl.obs)
@@ -56,6 +58,8 @@ def main():
         gm.set_option(N.SBO_OPT_INV_OZ, oz)
         gm.set_option(N.SBO_OPT_CHOL_DIAG, dg)
         gm.set_option(N.SBO_OPT_INV_CHECK, ck)
+        side, train = (int(v) for v in ps.split(":"))
+        gm.set_option(N.SBO_OPT_PROBE_SIZE, side << 16 | train)
         ts = []
         for _ in range(a.reps + 1):
             torch.cuda.synchronize()
@@ -63,7 +67,7 @@ def main():
             gm.fit(X, Y, O)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
-        print(f"N={n} cholesky={ch} inverse={'own recursion' if inv else 'rocSOLVER dtrtri'} reserve={rsv} overlap={ov} outer={ou} gemm={gg} inv_base={ib} inv_panels={ip} leaves={lv} precision={pr} inv_oz={oz} diag={dg} check={ck}{' box' if a.box else ''}: first fit {ts[0]:.1f} ms, warm refits {', '.join(f'{v:.1f}' for v in ts[1:])} ms", flush=True)
+        print(f"N={n} cholesky={ch} inverse={'own recursion' if inv else 'rocSOLVER dtrtri'} reserve={rsv} overlap={ov} outer={ou} gemm={gg} inv_base={ib} inv_panels={ip} leaves={lv} precision={pr} inv_oz={oz} diag={dg} check={ck} probe={ps}{' box' if a.box else ''}: first fit {ts[0]:.1f} ms, warm refits {', '.join(f'{v:.1f}' for v in ts[1:])} ms", flush=True)
         gm.close()
 
 
