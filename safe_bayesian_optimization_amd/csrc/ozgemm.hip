@@ -41,6 +41,7 @@ constexpr unsigned kGzVec4 = 1u << 30;   // (internal) the f32 epilogue may use 
 
 constexpr int kGzTM = 128;   // rows of A per workgroup
 constexpr int kGzTN = 64;    // columns of B per workgroup
+constexpr int kGzNPad = 128; // B's columns padded to (the 128-column tiles of gz_run at <= 5 digits)
 constexpr int kGzBK = 64;    // k per stage
 constexpr int kGzMaxK = 16384;
 
@@ -459,7 +460,7 @@ template <int ND, class TI, class TO>
 hipError_t gz_run(hipStream_t s, const TI *A, int64_t lda, const TI *B, int64_t ldb, int64_t m, int64_t n,
                   int64_t K, double alpha, TO *C, int64_t ldc, unsigned flags, char *ws) {
     const int Kb = (int)((K + kGzBK - 1) / kGzBK);
-    const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, np = (n + kGzTN - 1) / kGzTN * kGzTN;
+    const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, np = (n + kGzNPad - 1) / kGzNPad * kGzNPad;
     char *pa = ws;
     char *pb = pa + mp * (int64_t)Kb * kGzBK * ND;
     unsigned long long *ma = reinterpret_cast<unsigned long long *>(pb + np * (int64_t)Kb * kGzBK * ND);
@@ -492,7 +493,10 @@ hipError_t gz_run(hipStream_t s, const TI *A, int64_t lda, const TI *B, int64_t 
         hipLaunchKernelGGL((gz_max_kernel<false, TI>), gb, dim3(256), 0, s, B, ldb, n, K, tb, mb);
         hipLaunchKernelGGL((gz_digits_kernel<ND, false, TI>), db, dim3(256), 0, s, B, ldb, n, K, Kb, tb, mb, pb, eb);
     }
-    const int tilesM = (int)(mp / kGzTM), tilesN = (int)(np / kGzTN);
+    // 128-column tiles where two stages of them fit the LDS (<= 5 digits:
+    // 2 x 80 KiB): twice the products per staged A block
+    constexpr int TNr = ND <= 5 ? 128 : kGzTN;
+    const int tilesM = (int)(mp / kGzTM), tilesN = (int)(np / TNr);
 #ifdef SBO_GZ_4WAVE
     if constexpr (std::is_same_v<TO, double>) {
         if (flags & kGzLowerC) return hipErrorInvalidValue;
@@ -505,8 +509,8 @@ hipError_t gz_run(hipStream_t s, const TI *A, int64_t lda, const TI *B, int64_t 
     hipLaunchKernelGGL((gz_gemm8_kernel<ND, 8, TO>), dim3((unsigned)(tilesM * tilesN)), dim3(512), 0, s, pa, ea, pb,
                        eb, m, n, Kb, tilesM, C, ldc, alpha, flags);
 #else
-    hipLaunchKernelGGL((gz_gemm8_kernel<ND, 16, TO>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s, pa, ea,
-                       pb, eb, m, n, Kb, tilesM, C, ldc, alpha, flags);
+    hipLaunchKernelGGL((gz_gemm8_kernel<ND, 16, TO, TNr>), dim3((unsigned)(tilesM * tilesN)), dim3(1024), 0, s, pa,
+                       ea, pb, eb, m, n, Kb, tilesM, C, ldc, alpha, flags);
 #endif
     return hipGetLastError();
 }
@@ -515,7 +519,7 @@ hipError_t gz_run(hipStream_t s, const TI *A, int64_t lda, const TI *B, int64_t 
 
 size_t gz_workspace_bytes(int64_t m, int64_t n, int64_t K, int nd) {
     const int64_t Kp = (K + kGzBK - 1) / kGzBK * kGzBK;
-    const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, np = (n + kGzTN - 1) / kGzTN * kGzTN;
+    const int64_t mp = (m + kGzTM - 1) / kGzTM * kGzTM, np = (n + kGzNPad - 1) / kGzNPad * kGzNPad;
     return (size_t)((mp + np) * Kp * nd + 12 * (mp + np)) + 256;
 }
 
