@@ -423,9 +423,11 @@ SBO_API sbo_status sbo_kd_order(const float *x, const float *y, int64_t n, int64
  * inverse's base-case size (rocSOLVER dtrtri on the diagonal blocks at
  * multiples of it) and the number of dgemm panels each of its products is cut
  * into (fewer panels: larger GEMMs, more multiplied zeros).  SBO_OPT_INV_LEAVES
- * (default 1): every base case up front in one strided-batched dtrtri (0: one
- * call per base case inside the recursion).  Tuning only; the inverse agrees
- * to f64 rounding. */
+ * (default 2): every base case up front -- with four or more full base cases
+ * by doubling from 128-column blocks (one batched dtrtri, then two
+ * strided-batched dgemms per product and level), else in one strided-batched
+ * dtrtri (1: always the latter; 0: one call per base case inside the
+ * recursion).  Tuning only; the inverse agrees to f64 rounding. */
 #define SBO_OPT_INV_BASE 18
 #define SBO_OPT_INV_PANELS 19
 #define SBO_OPT_INV_LEAVES 20

@@ -64,8 +64,10 @@ sbo_status finish(sbo_ctx *ctx, uint32_t flags) {
 // splits on multiples of the base size b = SBO_OPT_INV_BASE >= 1024
 // (inverse_split), so an n-column inverse has ceil(n / b) base cases (the last
 // one possibly a single column), and ceil(n / b) + 1 <= n/512 + 2 slots
-// always suffice.
-int64_t info_slots(int64_t n) { return std::max<int64_t>(64, n / 512 + 2); }
+// always suffice.  After them, one slot per 128-column diagonal block for the
+// batched leaves by doubling (SBO_OPT_INV_LEAVES 2, inverse_leaves).
+int64_t info_leaf128(int64_t n) { return std::max<int64_t>(64, n / 512 + 2); }
+int64_t info_slots(int64_t n) { return info_leaf128(n) + n / 128 + 1; }
 
 // Appends of at most kAppendInvRows points solve their factor rows and extend
 // the inverse by matrix-vector products with the kept f64 inverse
@@ -325,10 +327,68 @@ sbo_status inverse_lower_f64(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_
 // info slots in the recursion's order (block k: slot k).  One at a time
 // inside the recursion each 2048 block took ~0.46 ms of mostly idle chip
 // (C4: eight of them; profiles/r3_fit_timeline_leaves.txt).
-sbo_status inverse_leaves(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld) {
+// SBO_OPT_INV_LEAVES 2 (b a power-of-two multiple of 128): the full leaves
+// by doubling instead -- every 128-column diagonal block of them in one
+// batched dtrtri, then per level s = 128, 256, .., b/2 all the 2s-column
+// blocks at once, [A 0; B C]^-1 from A^-1 and C^-1 by two strided-batched
+// dgemms through scratch T (T = B A^-1, X21 = -C^-1 T).  From s = 512 up
+// each product is two dgemms that leave out the triangular factor's zero
+// quarter (3/4 of the flops).  rocSOLVER's batched dtrtri runs its own
+// doubling as ~100 launches with a copy of the leaves and mostly small
+// tiles (C4: 1.74 ms for 8 leaves of 2048).  Warm fits: C4 29.1 -> 28.4 ms,
+// C3 9.7 -> 9.5; with fewer than four leaves the batches are too small to
+// fill the chip (C2's one leaf: 2.0 -> 2.3 ms) and rocSOLVER keeps them
+// (profiles/r6_inv_leaves_doubling.log).  Scratch: leaf_scratch(n) doubles.
+bool leaves_by_doubling(const sbo_ctx *ctx, int64_t n) {
+    const int64_t b = ctx->inv_base;
+    return ctx->inv_leaves_own && n / b >= 4 && b % 128 == 0 && ((b / 128) & (b / 128 - 1)) == 0;
+}
+int64_t leaf_scratch(const sbo_ctx *ctx, int64_t n) {
+    return leaves_by_doubling(ctx, n) ? (n / ctx->inv_base) * ctx->inv_base * ctx->inv_base / 4 : 0;
+}
+sbo_status leaves_doubling(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *T) {
+    const int64_t b = ctx->inv_base, nf = n / b, nb128 = nf * b / 128;
+    rocblas_int *info128 = ctx->info.as<rocblas_int>() + info_leaf128(n);
+    SBO_BLAS(rocsolver_dtrtri_strided_batched(hb, rocblas_fill_lower, rocblas_diagonal_non_unit, 128, Li,
+                                              (rocblas_int)ld, (rocblas_stride)(128 * (ld + 1)), info128,
+                                              (rocblas_int)nb128));
+    SBO_BLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
+    const double one = 1.0, minus_one = -1.0, zero = 0.0;
+    const auto N_ = rocblas_operation_none;
+    for (int64_t s = 128; s < b; s *= 2) {
+        const rocblas_int cnt = (rocblas_int)(nf * b / (2 * s)), is = (rocblas_int)s, il = (rocblas_int)ld;
+        const rocblas_stride st = (rocblas_stride)(2 * s * (ld + 1)), sT = (rocblas_stride)(s * s);
+        const double *Ainv = Li, *Cinv = Li + s * (ld + 1);
+        double *B = Li + s;
+        if (s < 512) {
+            SBO_BLAS(rocblas_dgemm_strided_batched(hb, N_, N_, is, is, is, &one, B, il, st, Ainv, il, st, &zero, T, is,
+                                                   sT, cnt));
+            SBO_BLAS(rocblas_dgemm_strided_batched(hb, N_, N_, is, is, is, &minus_one, Cinv, il, st, T, is, sT, &zero,
+                                                   B, il, st, cnt));
+            continue;
+        }
+        const int64_t h = s / 2;
+        const rocblas_int ih = (rocblas_int)h;
+        // T[:, 0:h] = B A^-1[:, 0:h]; T[:, h:s] = B[:, h:s] A^-1[h:s, h:s]
+        SBO_BLAS(rocblas_dgemm_strided_batched(hb, N_, N_, is, ih, is, &one, B, il, st, Ainv, il, st, &zero, T, is, sT,
+                                               cnt));
+        SBO_BLAS(rocblas_dgemm_strided_batched(hb, N_, N_, is, ih, ih, &one, B + h * ld, il, st, Ainv + h * (ld + 1),
+                                               il, st, &zero, T + h * s, is, sT, cnt));
+        // X21[0:h, :] = -C^-1[0:h, 0:h] T[0:h, :]; X21[h:s, :] = -C^-1[h:s, :] T
+        SBO_BLAS(rocblas_dgemm_strided_batched(hb, N_, N_, ih, is, ih, &minus_one, Cinv, il, st, T, is, sT, &zero, B,
+                                               il, st, cnt));
+        SBO_BLAS(rocblas_dgemm_strided_batched(hb, N_, N_, ih, is, is, &minus_one, Cinv + h, il, st, T, is, sT, &zero,
+                                               B + h, il, st, cnt));
+    }
+    return SBO_OK;
+}
+
+sbo_status inverse_leaves(sbo_ctx *ctx, rocblas_handle hb, double *Li, int64_t n, int64_t ld, double *T) {
     const int64_t b = ctx->inv_base, nf = n / b, r = n - nf * b;
     rocblas_int *info = ctx->info.as<rocblas_int>() + 1;
-    if (nf > 0)
+    if (leaves_by_doubling(ctx, n)) {
+        if (sbo_status st = leaves_doubling(ctx, hb, Li, n, ld, T); st != SBO_OK) return st;
+    } else if (nf > 0)
         SBO_BLAS(rocsolver_dtrtri_strided_batched(hb, rocblas_fill_lower, rocblas_diagonal_non_unit, (rocblas_int)b,
                                                   Li, (rocblas_int)ld, (rocblas_stride)(b * (ld + 1)), info,
                                                   (rocblas_int)nf));
@@ -892,12 +952,15 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             } else if (ctx->inverse_rec) {
                 if (ctx->widened_n != n) SBO_HIP(sbo::launch_widen(ctx->stream, L, ld, n, n, true, Li, ld));
                 ctx->widened_n = 0;
+                SBO_HIP(ctx->scratch.reserve(
+                    sizeof(double) *
+                    (size_t)std::max({inverse_scratch_par(n, ctx->inv_base), leaf_scratch(ctx, n), (int64_t)1})));
                 if (ctx->inv_batched) {
-                    if (sbo_status st = inverse_leaves(ctx, ctx->blas, Li, n, ld); st != SBO_OK) return st;
+                    if (sbo_status st = inverse_leaves(ctx, ctx->blas, Li, n, ld, ctx->scratch.as<double>());
+                        st != SBO_OK)
+                        return st;
                 }
                 ctx->inv_leaves_done = ctx->inv_batched;
-                SBO_HIP(ctx->scratch.reserve(sizeof(double) *
-                                             (size_t)std::max<int64_t>(inverse_scratch_par(n, ctx->inv_base), 1)));
                 const sbo_status st = inverse_lower_f64_par(ctx, Li, n, ld, ctx->scratch.as<double>());
                 ctx->inv_leaves_done = false;
                 if (st != SBO_OK) return st;
@@ -2496,8 +2559,9 @@ SBO_API sbo_status sbo_set_option(sbo_ctx *ctx, int option, int64_t value) {
             ctx->inv_base = value / 128 * 128;   // (the split lands on multiples of it: Cholesky block columns)
             return SBO_OK;
         case SBO_OPT_INV_LEAVES:
-            SBO_CHECK(value == 0 || value == 1, SBO_E_INVAL, "SBO_OPT_INV_LEAVES must be 0 or 1");
-            ctx->inv_batched = value == 1;
+            SBO_CHECK(value >= 0 && value <= 2, SBO_E_INVAL, "SBO_OPT_INV_LEAVES must be 0, 1 or 2");
+            ctx->inv_batched = value >= 1;
+            ctx->inv_leaves_own = value == 2;
             return SBO_OK;
         case SBO_OPT_INV_PANELS:
             SBO_CHECK(value >= 1 && value <= 64, SBO_E_INVAL, "SBO_OPT_INV_PANELS must be in [1, 64]");

@@ -229,7 +229,8 @@ struct sbo_ctx {
     int probe_grid = 32, probe_train = 512;  // SBO_OPT_PROBE_SIZE: the probe's grid side and training locations
     int plan_block = 0;          // SBO_OPT_PLAN_BLOCK: the precise plans' item blocks (bi << 8 | bq; 0: row-block-major)
     int reprobe_pct = 25;        // SBO_OPT_REPROBE: appends re-probe once N grew by this share (0: every append)
-    bool inv_batched = true;      // SBO_OPT_INV_LEAVES: the recursion's base cases in one batched dtrtri
+    bool inv_batched = true;      // SBO_OPT_INV_LEAVES: the recursion's base cases inverted up front, batched
+    bool inv_leaves_own = true;   // (SBO_OPT_INV_LEAVES 2, default: by doubling from 128-column blocks, inverse_leaves)
     bool inv_leaves_done = false; // (set while a recursion runs whose base cases are already inverted)
     int64_t widened_n = 0;       // blocked_potrf widened the factor into Linv (n) for refresh_operand
     double probe_ref_tol = 0.0;  // the probe reference sweep's skip budget (absolute variance)

@@ -1093,9 +1093,11 @@ def test_recursive_inverse_matches_dtrtri(mapper, n):
     gm.set_option(N.SBO_OPT_INVERSE, 1)
     assert np.abs(got[0] - got[1]).max() <= 2e-6 * np.abs(got[0]).max()
     # the recursion's tuning (base-case size -- 1100 rounds down to 1024 --,
-    # panels per product, base cases batched up front or one by one) changes
-    # f64 rounding only
-    for base, panels, leaves in ((1024, 4, 1), (1100, 16, 0), (4096, 16, 1), (2048, 16, 0)):
+    # panels per product, base cases batched up front by rocSOLVER (1) or by
+    # doubling from 128-column blocks (2), or one by one (0)) changes f64
+    # rounding only
+    for base, panels, leaves in ((1024, 4, 1), (1100, 16, 0), (4096, 16, 1), (2048, 16, 0), (2048, 16, 2),
+                                 (1024, 4, 2), (4096, 16, 2)):
         gm = TerrainMapper(0, wl.hyper, ctx=mapper.ctx)
         gm.set_option(N.SBO_OPT_INV_BASE, base)
         gm.set_option(N.SBO_OPT_INV_PANELS, panels)
@@ -1107,7 +1109,7 @@ def test_recursive_inverse_matches_dtrtri(mapper, n):
         assert not np.triu(A, 1).any()
     gm.set_option(N.SBO_OPT_INV_BASE, 2048)
     gm.set_option(N.SBO_OPT_INV_PANELS, 16)
-    gm.set_option(N.SBO_OPT_INV_LEAVES, 1)
+    gm.set_option(N.SBO_OPT_INV_LEAVES, 2)
 
 
 @pytest.mark.parametrize("n,box,digits", [(4100, False, 6), (5000, False, 6), (5000, False, 5), (6000, True, 6),
