@@ -22,7 +22,7 @@ def main():
     p.add_argument("--gemm", type=int, nargs="+", default=[4], help="SBO_OPT_CHOL_GEMM values to time (4: the library default)")
     p.add_argument("--inv-base", type=int, nargs="+", default=[2048], help="SBO_OPT_INV_BASE values to time")
     p.add_argument("--inv-panels", type=int, nargs="+", default=[16], help="SBO_OPT_INV_PANELS values to time")
-    p.add_argument("--leaves", type=int, nargs="+", default=[1], help="SBO_OPT_INV_LEAVES values to time")
+    p.add_argument("--leaves", type=int, nargs="+", default=[2], help="SBO_OPT_INV_LEAVES values to time")
     p.add_argument("--prec", type=int, nargs="+", default=[-1],
                    help="SBO_OPT_PRECISION values to time (0: no precision probe at the fit)")
     p.add_argument("--oz", type=int, nargs="+", default=[6], help="SBO_OPT_INV_OZ values to time (0 dgemm, 5/6 sliced; 6 the library default)")
