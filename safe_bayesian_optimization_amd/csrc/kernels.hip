@@ -1262,8 +1262,14 @@ __device__ __forceinline__ void store_sym_f32(float *gf, int bi, int bj, int lan
             }
     }
 }
+// FUSED (round 6): the tile is first packed here from the f64 inverse --
+// pack_operand_kernel's values, (float)(sf2 L^-1), written to aug -- so the
+// pack and the norms are one pass over L^-1 (the staging pass re-reads the
+// thread's own stores from L2).
+template <bool FUSED>
 __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restrict__ aug, int64_t t0,
-                                                           float4 *__restrict__ lgn) {
+                                                           float4 *__restrict__ lgn, const double *__restrict__ Linv,
+                                                           int64_t ld, int64_t n, double sf2, float *augw) {
     __shared__ __attribute__((aligned(16))) unsigned short pq[3][kBK * kTnPq];   // a quarter's pieces [k][c] (27 KiB)
     __shared__ __attribute__((aligned(16))) float gm[kBK * kTnGmLd];   // G, then its powers, normalised f32 (17 KiB)
     __shared__ double rpart[3][4][kBK];        // row-sum partials of a quarter (6 KiB)
@@ -1293,7 +1299,8 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
     // (the tile is read twice, the second time from L2: a pass for the
     // pieces' maxima, then the staging)
     auto load16 = [&](int q, float (&v)[16]) {
-        const float4 *src = reinterpret_cast<const float4 *>(t + q * 64 * kBK + 16 * tid);
+        const float4 *src = FUSED ? reinterpret_cast<const float4 *>(augw + tile * kTileFloats + q * 64 * kBK + 16 * tid)
+                                  : reinterpret_cast<const float4 *>(t + q * 64 * kBK + 16 * tid);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const float4 f = src[j];
@@ -1306,10 +1313,32 @@ __global__ __launch_bounds__(kBM, 2) void tile_norm_kernel(const float *__restri
     __shared__ float pmax[3][kBM / 64];
     {
         float amax[3] = {0.0f, 0.0f, 0.0f};
+        // FUSED: the tile's row block and k-tile (tile = tile_start(I) + kb)
+        int64_t fI = 0, fkb = 0;
+        if (FUSED) {
+            fI = (int64_t)((sqrt(1.0 + 2.0 * (double)tile) - 1.0) * 0.5);
+            while (fI > 0 && tile_start(fI) > tile) --fI;
+            while (tile_start(fI + 1) <= tile) ++fI;
+            fkb = tile - tile_start(fI);
+        }
 #pragma unroll
         for (int q = 0; q < kBM / 64; ++q) {
             float tv[16];
-            load16(q, tv);
+            if (FUSED) {
+                // element 16 tid + j of quarter q (tile_offset): k = tid / 4, row
+                // 64 q + 16 (j & 3) + 4 (tid & 3) + j / 4 -- pack_operand_kernel's value
+                const int64_t col = fkb * kBK + (tid >> 2);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int64_t row = fI * kBM + 64 * q + 16 * (j & 3) + 4 * (tid & 3) + (j >> 2);
+                    tv[j] = (row < n && col < n && col <= row) ? (float)(sf2 * Linv[row + col * ld]) : 0.0f;
+                }
+                float4 *dst = reinterpret_cast<float4 *>(augw + tile * kTileFloats + q * 64 * kBK + 16 * tid);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) dst[j] = make_float4(tv[4 * j], tv[4 * j + 1], tv[4 * j + 2], tv[4 * j + 3]);
+            } else {
+                load16(q, tv);
+            }
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const float x = tv[j];
@@ -2942,11 +2971,22 @@ hipError_t launch_chol_trsm(hipStream_t s, const float *L11, int64_t ld, int kb,
     return hipGetLastError();
 }
 
+hipError_t launch_pack_tile_norms(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
+                                  double sf2, float *aug, float4 *lgn) {
+    const int64_t nI = npad / kBM;
+    const int64_t t0 = tile_start(I0), t1 = tile_start(nI);
+    if (t1 <= t0) return hipSuccess;
+    hipLaunchKernelGGL(tile_norm_kernel<true>, dim3((unsigned)(t1 - t0)), dim3(kBM), 0, s, aug, t0, lgn, Linv, ld, n,
+                       sf2, aug);
+    return hipGetLastError();
+}
+
 hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float4 *lgn) {
     const int64_t nI = npad / kBM;
     const int64_t t0 = tile_start(I0), t1 = tile_start(nI);
     if (t1 <= t0) return hipSuccess;
-    hipLaunchKernelGGL(tile_norm_kernel, dim3((unsigned)(t1 - t0)), dim3(kBM), 0, s, aug, t0, lgn);
+    hipLaunchKernelGGL(tile_norm_kernel<false>, dim3((unsigned)(t1 - t0)), dim3(kBM), 0, s, aug, t0, lgn, nullptr,
+                       (int64_t)0, (int64_t)0, 0.0, nullptr);
     return hipGetLastError();
 }
 

@@ -67,6 +67,9 @@ sbo_status finish(sbo_ctx *ctx, uint32_t flags) {
 // always suffice.  After them, one slot per 128-column diagonal block for the
 // batched leaves by doubling (SBO_OPT_INV_LEAVES 2, inverse_leaves).
 int64_t info_leaf128(int64_t n) { return std::max<int64_t>(64, n / 512 + 2); }
+#ifndef SBO_FUSED_TN
+#define SBO_FUSED_TN 1
+#endif
 int64_t info_slots(int64_t n) { return info_leaf128(n) + n / 128 + 1; }
 
 // Appends of at most kAppendInvRows points solve their factor rows and extend
@@ -872,6 +875,7 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
     SBO_HIP(ctx->kcoord.reserve(sizeof(float) * (size_t)(npad / sbo::kBK) * 3 * sbo::kBK));
     rocblas_int hinfo = 0;
     bool alpha_aux = false, kcoord_pending = false, x3_planes_aux = false, packs_aux = false, chk_pending = false;
+    bool norms_done = false;   // the tile norms ran with the pack (SBO_FUSED_TN)
     // a launched guard reads L, L^-1, x/y/obs and ctx->chk on chk_stream: an
     // early return (a failed launch, NOT_SPD) waits for it before the caller
     // can regrow or free those buffers or the next fit writes L
@@ -1049,7 +1053,16 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
 
         if (eager_f64)   // (before the fork: a growing operand copies and waits on `stream`)
             if (sbo_status st = reserve_precise(ctx, npad, std::max<int64_t>(ctx->a64_I0, 0))) return st;
+#if SBO_FUSED_TN
+        // the pack and the tile norms in one pass over L^-1 (tile_norm_kernel<true>)
+        SBO_HIP(grow_keep(ctx, ctx->tile_lgn, 2 * sizeof(float4) * (size_t)sbo::total_tiles(nI),
+                          2 * sizeof(float4) * old_tiles));
+        SBO_HIP(sbo::launch_pack_tile_norms(ctx->stream, Li, ld, n, npad, I0, sf2, ctx->aug.as<float>(),
+                                            ctx->tile_lgn.as<float4>()));
+        norms_done = true;
+#else
         SBO_HIP(sbo::launch_pack_tiles(ctx->stream, Li, ld, n, npad, I0, sf2, ctx->aug.as<float>()));
+#endif
         if (eager_x3 || eager_f64) {
             SBO_HIP(hipEventRecord(ctx->ev_panel, ctx->stream));
             SBO_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_panel, 0));
@@ -1110,9 +1123,11 @@ sbo_status refresh_operand(sbo_ctx *ctx, int64_t n_old = 0) {
             SBO_HIP(ctx->scratch.reserve(sizeof(double) * (size_t)npad));
             SBO_HIP(sbo::launch_row_l1(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->scratch.as<double>()));
         }
-        SBO_HIP(grow_keep(ctx, ctx->tile_lgn, 2 * sizeof(float4) * (size_t)sbo::total_tiles(nI),
-                          2 * sizeof(float4) * old_tiles));
-        SBO_HIP(sbo::launch_tile_norms(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->tile_lgn.as<float4>()));
+        if (!norms_done) {
+            SBO_HIP(grow_keep(ctx, ctx->tile_lgn, 2 * sizeof(float4) * (size_t)sbo::total_tiles(nI),
+                              2 * sizeof(float4) * old_tiles));
+            SBO_HIP(sbo::launch_tile_norms(ctx->stream, ctx->aug.as<float>(), npad, I0, ctx->tile_lgn.as<float4>()));
+        }
         if (kcoord_pending) {
             if (alpha_aux) SBO_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_trail, 0));
             SBO_HIP(sbo::launch_pack_kcoord(ctx->stream, ctx->x.as<float>(), ctx->y.as<float>(), alpha, n, npad, sf2,

@@ -379,6 +379,9 @@ hipError_t launch_predict_x3(hipStream_t s, const char *ax3, const float *kc3, c
 // bf16 pieces A1 and A2 (f64 sums, rounded up) for row blocks I >= I0 (-1000
 // for an all-zero matrix).
 hipError_t launch_tile_norms(hipStream_t s, const float *aug, int64_t npad, int64_t I0, float4 *lgn);
+// the f64 operand's pack (launch_pack_tiles) and the tile norms in one pass
+hipError_t launch_pack_tile_norms(hipStream_t s, const double *Linv, int64_t ld, int64_t n, int64_t npad, int64_t I0,
+                                  double sf2, float *aug, float4 *lgn);
 // Blocked Cholesky: factor the kb x kb diagonal block at A (column-major,
 // lda = ld) of step k0 in place (kb <= kCholNB); info as rocSOLVER's.
 constexpr int kCholNB = 128;
